@@ -1,0 +1,283 @@
+"""Benchmark of the MI355X gradient-codec path (BASELINE.json metric).
+
+Headline workload (``value``): BASELINE.json configs[4] at one client per GPU — a 1 GiB flat fp32
+delta (268,435,456 elements) through the stacked codec: top-k 1 % (k = 2,684,354) then 8-bit
+standard dithering (s = 127, p = inf, Philox RNG) of the kept values; one step = encode + decode,
+device-resident (input already in HBM when the timed region starts).  GB/s counts the algorithmic
+bytes of SURVEY.md §8(d): 8·D + 10·K per client (read x, write dense output, write + read the
+5-byte/entry wire).  At N GPUs each rank owns its own client delta (weak scaling), no collective in
+the timed region; ``value`` = N x per-client bytes / max-over-ranks step time.
+
+Also reported (``configs``): configs[1] (8-bit dithering of 10 cnn_femmist_tiny deltas batched),
+configs[2] (top-k 1 % of a 25M delta), and at N > 1 configs[3] (codec + fused weighted
+decode-accumulate + RCCL reduce of a 25M delta per client).  ``roofline`` is the dominant kernel's
+live HIP-event duration; ``cpu_baseline`` times the numpy oracle on a bounded sample of the
+workload on this host.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--skip-extra] [--skip-cpu]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "grad-codec GB/s (device-resident encode+decode), flat fp32 delta, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+D_HEADLINE = 268_435_456
+LEVELS = 127
+
+
+def dist_setup(n_gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(v: float, world: int) -> float:
+    if world == 1:
+        return v
+    import torch.distributed as dist
+
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def stacked_bytes(D: int, K: int) -> int:
+    return 8 * D + 10 * K
+
+
+def timed(fn, steps, warmup, world, probe=None):
+    """Barrier+sync bracketed timing of `steps` calls; optional live HIP-event probe of one kernel."""
+    from fl_sim_amd import _lib
+
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if probe:
+        _lib.call("flc_probe_set", probe.encode())
+        _lib.call("flc_probe_read", None, None)  # clear
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    probe_ms = None
+    if probe:
+        import ctypes
+
+        tot = ctypes.c_double()
+        cnt = ctypes.c_int64()
+        _lib.call("flc_probe_read", ctypes.byref(tot), ctypes.byref(cnt))
+        _lib.call("flc_probe_set", None)
+        probe_ms = tot.value / max(cnt.value, 1)
+    return (t1 - t0) * 1e3 / steps, probe_ms
+
+
+def cpu_baseline(budget_s: float = 12.0):
+    """The numpy oracle (oracle/compressors_ref.py) on a bounded sample of the headline workload."""
+    from oracle import compressors_ref as ref
+
+    n = 16_777_216  # 64 MiB sample of the 1 GiB delta, same K/D ratio
+    k = n // 100
+    g = np.random.default_rng(1234)
+    x = (g.standard_normal(n) * 1e-3).astype(np.float32)
+    reps, t_tot = 0, 0.0
+    while t_tot < budget_s and reps < 20:
+        t0 = time.perf_counter()
+        u = ref.philox_uniforms(n, 1, reps)
+        ref.stacked(x, k, LEVELS, lambda i: u[i])
+        t_tot += time.perf_counter() - t0
+        reps += 1
+    per = t_tot / reps
+    return {
+        "value": round(stacked_bytes(n, k) / per / 1e9, 4),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"numpy oracle stacked top-k 1% -> 8-bit dither on D={n} (64 MiB), {reps} reps, "
+                  f"{per * 1e3:.0f} ms/rep; host has {os.cpu_count()} logical CPUs",
+    }
+
+
+def traffic_from_profiles():
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return {}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--skip-extra", action="store_true")
+    ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--probe", default="topk_filter", help="kernel timed live for the roofline entry")
+    args = ap.parse_args()
+
+    world, rank, local = dist_setup(args.gpus)
+    from fl_sim_amd import codec
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    D, K = D_HEADLINE, D_HEADLINE // 100
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.randn(D, generator=gen, device=dev) * 1e-3
+    out = torch.empty(D, dtype=torch.float32, device=dev)
+    ctr = [0]
+
+    def step():
+        ctr[0] += 1
+        pkt = codec.stacked_encode(x, K, LEVELS, seed=rank, counter=ctr[0])
+        codec.stacked_decode(pkt, out=out)
+
+    ms, probe_ms = timed(step, args.steps, args.warmup, world, probe=args.probe)
+    ms = max_over_ranks(ms, world)
+    value = world * stacked_bytes(D, K) / (ms * 1e-3) / 1e9
+
+    # dominant-kernel roofline: algorithmic bytes per launch / live average duration
+    kernel_bytes = {"topk_filter": 4 * D, "stacked_decode": 4 * D + 5 * K + 4}
+    roof = None
+    if probe_ms:
+        ach = kernel_bytes.get(args.probe, 4 * D) / (probe_ms * 1e-3) / 1e9
+        tr = traffic_from_profiles().get(args.probe)
+        roof = {
+            "kernel": args.probe,
+            "bound": "hbm",
+            "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": tr,
+            "avg_ms": round(probe_ms, 5),
+            "algorithmic_bytes": kernel_bytes.get(args.probe),
+        }
+    del x, out
+    torch.cuda.empty_cache()
+
+    extra = {}
+    if not args.skip_extra:
+        # configs[1]: 8-bit dithering, 10 clients x cnn_femmist_tiny (417,482 params), one batched launch
+        d2, b2 = 417_482, 10
+        X = torch.randn(b2, d2, generator=gen, device=dev) * 1e-3
+        c2 = [0]
+
+        def step2():
+            c2[0] += 1
+            norms = codec.quant_norm(X)
+            pkt = codec.quant_encode(X, 0, LEVELS, norms, seed=rank, counter=c2[0], want_nnz=False)
+            codec.quant_decode(pkt)
+
+        ms2, _ = timed(step2, 50, 10, world)
+        ms2 = max_over_ranks(ms2, world)
+        extra["config2_quant8_10x417482"] = {
+            "us_per_step": round(ms2 * 1e3, 2),
+            "GB_s": round(b2 * d2 * 10 / (ms2 * 1e-3) / 1e9, 1),
+            "bytes_formula": "(8 + 8/4) * D per client",
+        }
+        del X
+        # configs[2]: top-k 1% of a 25M delta (encode + dense decode)
+        d3 = 25_000_000
+        k3 = d3 // 100
+        X3 = torch.randn(d3, generator=gen, device=dev) * 1e-3
+        o3 = torch.empty(d3, dtype=torch.float32, device=dev)
+
+        def step3():
+            idx, val = codec.topk_encode(X3, k3)
+            codec.sparse_decode(idx, val, d3, out=o3)
+
+        ms3, _ = timed(step3, 20, 5, world)
+        ms3 = max_over_ranks(ms3, world)
+        extra["config3_topk1pct_25M"] = {
+            "ms_per_step": round(ms3, 4),
+            "GB_s": round((8 * d3 + 16 * k3) / (ms3 * 1e-3) / 1e9, 1),
+            "bytes_formula": "8 * D + 16 * K",
+        }
+        if world > 1:
+            import torch.distributed as dist
+
+            acc = torch.empty(d3, dtype=torch.float32, device=dev)
+            wts = [100.0 * (i + 1) for i in range(world)]
+            w_r = wts[rank] / sum(wts)
+            c4 = [0]
+
+            def step4():
+                c4[0] += 1
+                pkt = codec.stacked_encode(X3, k3, LEVELS, seed=rank, counter=c4[0])
+                codec.stacked_decode(pkt, out=acc, weight=w_r)
+                dist.reduce(acc, dst=0)
+
+            ms4, _ = timed(step4, 10, 3, world)
+            ms4 = max_over_ranks(ms4, world)
+            extra["config4_codec_plus_rccl_reduce_25M"] = {"ms_per_step": round(ms4, 4), "clients": world}
+        del X3, o3
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.skip_cpu:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": "configs[4]: 1 GiB fp32 delta per client, stacked top-k 1% -> 8-bit standard "
+                            "dithering (s=127, p=inf, philox), encode+decode, device-resident",
+                "D": D,
+                "K": K,
+                "bytes_per_step_per_client": stacked_bytes(D, K),
+                "parallelism": f"one client per GPU x{world}",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "extra": extra,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,254 @@
+"""Device-side functional API over the C ABI: torch tensors in HBM in, torch tensors out.
+
+Every function here launches hand-written gfx950 kernels from ``libflcodec.so`` on the current HIP
+stream of the tensor's device; none of them synchronises the stream.  Tensors must be fp32, on a HIP
+device and contiguous (non-contiguous or misaligned inputs are copied once).  This module is the
+plumbing under :class:`fl_sim_amd.compressors.Compressor` and :mod:`fl_sim_amd.aggregation`; bench.py
+drives it directly for the device-resident measurement.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import call
+
+_WS: Dict[Tuple[int, int, str], torch.Tensor] = {}
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _dev_f32(x: torch.Tensor, name: str = "x") -> torch.Tensor:
+    if not isinstance(x, torch.Tensor) or x.device.type != "cuda":
+        raise TypeError(f"{name} must be a torch tensor on a HIP device (got {type(x).__name__}"
+                        f"{'' if not isinstance(x, torch.Tensor) else ' on ' + str(x.device)})")
+    if x.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {x.dtype}); the codec path is fp32")
+    if not x.is_contiguous() or x.data_ptr() % 16 != 0:
+        x = x.contiguous().clone()
+    return x
+
+
+def workspace(device: torch.device, nbytes: int, kind: str) -> torch.Tensor:
+    """Zero-initialised workspace, cached per (device, stream, kind) and grown on demand."""
+    key = (device.index if device.index is not None else torch.cuda.current_device(), _stream(device), kind)
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _WS[key] = t
+    return t
+
+
+def code_bits(levels: int) -> int:
+    """Bits per element of the dithering wire: sign + ceil(log2(levels + 1)), rounded up to 2/4/8."""
+    b = 1 + int(math.ceil(math.log2(levels + 1)))
+    for c in (2, 4, 8):
+        if b <= c:
+            return c
+    raise ValueError(f"levels={levels} does not fit an 8-bit code (at most 127 levels)")
+
+
+# ----------------------------------------------------------------------------------------------- dither
+@dataclass
+class QuantPacket:
+    """Wire of the dense dithering codec: per-row fp32 norm + packed ``bits``-bit codes."""
+
+    codes: torch.Tensor
+    norms: torch.Tensor
+    rows: int
+    d: int
+    kind: int
+    levels: int
+    bits: int
+    nnz: Optional[torch.Tensor] = None
+
+    @property
+    def nbytes(self) -> int:
+        return self.codes.numel() + 4 * self.rows
+
+
+def quant_norm(x2d: torch.Tensor, p: float = math.inf) -> torch.Tensor:
+    x2d = _dev_f32(x2d)
+    rows, d = x2d.shape
+    pk = _lib.FLC_NORM_INF if math.isinf(p) else (_lib.FLC_NORM_L2 if p == 2 else None)
+    if pk is None:
+        raise ValueError(f"p must be inf or 2 (got {p})")
+    norms = torch.empty(rows, dtype=torch.float32, device=x2d.device)
+    nb = _lib.size("flc_quant_workspace_size", rows, d)
+    ws = workspace(x2d.device, nb, "quant")
+    call("flc_quant_norm", _p(x2d), rows, d, pk, _p(norms), _p(ws), ws.numel(), _stream(x2d.device))
+    return norms
+
+
+def count_consumers(x2d: torch.Tensor, norms: Optional[torch.Tensor]) -> torch.Tensor:
+    """Device int64 scalar: the number of uniforms the reference draws for this batch."""
+    x2d = _dev_f32(x2d)
+    rows, d = x2d.shape
+    out = torch.empty(1, dtype=torch.int64, device=x2d.device)
+    call("flc_count_consumers", _p(x2d), rows, d, _p(norms), _p(out), _stream(x2d.device))
+    return out
+
+
+def quant_encode(x2d: torch.Tensor, kind: int, levels: int, norms: torch.Tensor, seed: int = 0, counter: int = 0,
+                 compat_u: Optional[torch.Tensor] = None, want_nnz: bool = True) -> QuantPacket:
+    x2d = _dev_f32(x2d)
+    rows, d = x2d.shape
+    bits = code_bits(levels)
+    nbytes = (rows * d * bits + 7) // 8
+    codes = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=x2d.device)
+    nnz = torch.empty(rows, dtype=torch.int64, device=x2d.device) if want_nnz else None
+    if compat_u is not None and compat_u.dtype != torch.float64:
+        raise TypeError("compat_u must be float64")
+    nb = _lib.size("flc_quant_workspace_size", rows, d)
+    ws = workspace(x2d.device, nb, "quant")
+    call("flc_quant_encode", _p(x2d), rows, d, kind, levels, bits, _p(norms), seed, counter, _p(compat_u),
+         _p(codes), _p(nnz), _p(ws), ws.numel(), _stream(x2d.device))
+    return QuantPacket(codes, norms, rows, d, kind, levels, bits, nnz)
+
+
+def quant_decode(pkt: QuantPacket, out: Optional[torch.Tensor] = None, row_weights: Optional[torch.Tensor] = None,
+                 accumulate: bool = False) -> torch.Tensor:
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs an out tensor")
+        out = torch.empty(pkt.rows, pkt.d, dtype=torch.float32, device=pkt.codes.device)
+    call("flc_quant_decode", _p(pkt.codes), pkt.rows, pkt.d, pkt.kind, pkt.levels, pkt.bits, _p(pkt.norms),
+         _p(row_weights), int(accumulate), _p(out), _stream(out.device))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------- natural
+def natural_encode(x: torch.Tensor, seed: int = 0, counter: int = 0, compat_u: Optional[torch.Tensor] = None,
+                   want_nnz: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    x = _dev_f32(x).reshape(-1)
+    n = x.numel()
+    codes = torch.empty(n, dtype=torch.int16, device=x.device)
+    nnz = torch.empty(1, dtype=torch.int64, device=x.device) if want_nnz else None
+    nb = _lib.size("flc_natural_workspace_size", n)
+    ws = workspace(x.device, nb, "natural")
+    call("flc_natural_encode", _p(x), n, seed, counter, _p(compat_u), _p(codes), _p(nnz), _p(ws), ws.numel(),
+         _stream(x.device))
+    return codes, nnz
+
+
+def natural_decode(codes: torch.Tensor, n: int, out: Optional[torch.Tensor] = None, weight: float = 1.0,
+                   accumulate: bool = False) -> torch.Tensor:
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=codes.device)
+    call("flc_natural_decode", _p(codes), n, weight, int(accumulate), _p(out), _stream(out.device))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------ top-k
+def topk_encode(x: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Kept set of the reference Top-K (k largest signed values): (idx int32 ascending, val fp32)."""
+    x = _dev_f32(x).reshape(-1)
+    n = x.numel()
+    idx = torch.empty(k, dtype=torch.int32, device=x.device)
+    val = torch.empty(k, dtype=torch.float32, device=x.device)
+    ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
+    call("flc_topk_encode", _p(x), n, k, _p(idx), _p(val), _p(ws), ws.numel(), _stream(x.device))
+    return idx, val
+
+
+def sparse_decode(idx: torch.Tensor, val: torch.Tensor, n: int, scale: float = 1.0, out: Optional[torch.Tensor] = None,
+                  weight: float = 1.0, accumulate: bool = False) -> torch.Tensor:
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=val.device)
+    call("flc_sparse_decode", _p(idx), _p(val), idx.numel(), scale, n, weight, int(accumulate), _p(out),
+         _stream(out.device))
+    return out
+
+
+@dataclass
+class StackedPacket:
+    """Wire of the stacked codec: ascending int32 indices, 8-bit (sign | level) codes, fp32 norm."""
+
+    idx: torch.Tensor
+    codes: torch.Tensor
+    norm: torch.Tensor
+    n: int
+    levels: int
+
+    @property
+    def nbytes(self) -> int:
+        return 5 * self.idx.numel() + 4
+
+
+def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, counter: int = 0) -> StackedPacket:
+    x = _dev_f32(x).reshape(-1)
+    n = x.numel()
+    idx = torch.empty(k, dtype=torch.int32, device=x.device)
+    codes = torch.empty(max(k, 16), dtype=torch.uint8, device=x.device)
+    norm = torch.empty(1, dtype=torch.float32, device=x.device)
+    ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
+    call("flc_stacked_encode", _p(x), n, k, levels, seed, counter, None, _p(idx), _p(codes), _p(norm), _p(ws),
+         ws.numel(), _stream(x.device))
+    return StackedPacket(idx, codes, norm, n, levels)
+
+
+def stacked_decode(pkt: StackedPacket, out: Optional[torch.Tensor] = None, weight: float = 1.0,
+                   accumulate: bool = False) -> torch.Tensor:
+    if out is None:
+        out = torch.empty(pkt.n, dtype=torch.float32, device=pkt.idx.device)
+    call("flc_stacked_decode", _p(pkt.idx), _p(pkt.codes), pkt.idx.numel(), pkt.levels, _p(pkt.norm), pkt.n, weight,
+         int(accumulate), _p(out), _stream(out.device))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------- misc
+def copy(x: torch.Tensor) -> torch.Tensor:
+    x = _dev_f32(x)
+    out = torch.empty_like(x)
+    call("flc_copy", _p(x), x.numel(), _p(out), _stream(x.device))
+    return out
+
+
+def scale_div(x: torch.Tensor, p: float) -> torch.Tensor:
+    x = _dev_f32(x)
+    out = torch.empty_like(x)
+    call("flc_scale_div", _p(x), x.numel(), p, _p(out), _stream(x.device))
+    return out
+
+
+def randk_apply(x: torch.Tensor, idx: torch.Tensor, scale: float) -> torch.Tensor:
+    x = _dev_f32(x).reshape(-1)
+    out = torch.empty_like(x)
+    call("flc_randk_apply", _p(x), x.numel(), _p(idx), idx.numel(), scale, _p(out), _stream(x.device))
+    return out
+
+
+def weighted_sum(dst: torch.Tensor, srcs: Sequence[torch.Tensor], weights: Sequence[float], init_mode: int,
+                 beta: float = 0.0) -> torch.Tensor:
+    """dst = {dst*beta | 0 | dst} then dst = fmaf(w_m, src_m, dst) for each message in order."""
+    import ctypes
+
+    if dst.device.type != "cuda" or dst.dtype != torch.float32 or not dst.is_contiguous():
+        raise TypeError("dst must be a contiguous fp32 HIP tensor")
+    n = dst.numel()
+    srcs = [_dev_f32(s, "src") for s in srcs]
+    for s in srcs:
+        if s.numel() != n:
+            raise ValueError("every source must have dst's number of elements")
+    ptrs = (ctypes.c_void_p * max(len(srcs), 1))(*[s.data_ptr() for s in srcs])
+    ws = (ctypes.c_float * max(len(srcs), 1))(*[float(w) for w in weights])
+    call("flc_weighted_sum", ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(ws, ctypes.c_void_p), len(srcs), n,
+         init_mode, float(beta), _p(dst), _stream(dst.device))
+    return dst
+
+
+def fedopt_step(theta: torch.Tensor, delta: torch.Tensor, v: Optional[torch.Tensor], opt: str, lr: float,
+                beta2: float, tau: float) -> None:
+    call("flc_fedopt_step", _p(theta), _p(delta), _p(v), theta.numel(), _lib.FLC_OPT[opt], float(lr), float(beta2),
+         float(tau), _stream(theta.device))

@@ -1,0 +1,419 @@
+"""Drop-in ``Compressor`` with the reference API, running on MI355X kernels.
+
+Mirrors ``fl_sim/compressors/compressors.py`` (class ``Compressor``, lines 35-419; ``CompressorType``,
+lines 20-32): the same constructor, ``make*`` factories, properties (``name``/``fullName`` quirks
+included), ``getW``, ``resetStats``, send-statistics counters and ``compressVector``/``__call__``
+semantics (a new dense decoded vector; the input is never modified).  What changes is where the
+work runs: every branch is a gfx950 kernel of ``libflcodec.so`` (see ``codec.py``).
+
+Inputs:
+  * ``torch.Tensor`` on a HIP device -> device-resident path, returns a tensor on that device;
+  * ``numpy.ndarray`` (or CPU tensor) -> copied to the current HIP device, run there, copied back
+    (the reference's own call signature; end-to-end rate incl. PCIe is reported in DESIGN.md).
+
+RNG (``rng=`` constructor argument):
+  * ``"compat"`` (default): uniforms come from the interpreter's global ``random`` / ``np.random``
+    streams exactly as the reference draws them (one ``random.random()`` per consuming element in
+    index order), so outputs are bit-identical to the reference under the same seed;
+  * ``"philox"``: counter-based Philox4x32-10 on the device, keyed by ``seed``; no host round trip.
+
+Extensions over the reference (documented in DESIGN.md): standard dithering accepts up to 127
+levels (the reference's ``np.arange`` table asserts for > 10), ``encode``/``decode`` expose the
+packed wire, and ``compressBatch`` runs a [clients, d] batch in one launch.
+"""
+
+from __future__ import annotations
+
+import math
+import random
+from enum import Enum, unique
+from typing import Any, Optional
+
+import numpy as np
+import torch
+
+from . import codec
+from . import rng as _rng
+from ._lib import FLC_Q_NATURAL_DITHER, FLC_Q_STANDARD_DITHER
+
+__all__ = ["CompressorType", "Compressor"]
+
+
+@unique
+class CompressorType(Enum):
+    """Same members and values as the reference enum (compressors.py:20-32)."""
+
+    IDENTICAL = 1
+    LAZY_COMPRESSOR = 2
+    RANDK_COMPRESSOR = 3
+    NATURAL_COMPRESSOR_FP64 = 4
+    NATURAL_COMPRESSOR_FP32 = 5
+    STANDARD_DITHERING_FP64 = 6
+    STANDARD_DITHERING_FP32 = 7
+    NATURAL_DITHERING_FP32 = 8
+    NATURAL_DITHERING_FP64 = 9
+    TOPK_COMPRESSOR = 10
+    ADAPTIVE_RANDOM_COMPRESSOR = 11
+
+
+_BIASED = {CompressorType.TOPK_COMPRESSOR, CompressorType.ADAPTIVE_RANDOM_COMPRESSOR}
+_NATURAL = {CompressorType.NATURAL_COMPRESSOR_FP32, CompressorType.NATURAL_COMPRESSOR_FP64}
+_STD = {CompressorType.STANDARD_DITHERING_FP32, CompressorType.STANDARD_DITHERING_FP64}
+_NATD = {CompressorType.NATURAL_DITHERING_FP32, CompressorType.NATURAL_DITHERING_FP64}
+
+
+def standard_levels(levels: int) -> np.ndarray:
+    """lv[i] = i * (1/s), lv[s] = 1 — bit-equal to the reference's np.arange(0, 1.1, 1/s) (s <= 10)."""
+    step = 1.0 / levels
+    lv = np.array([i * step for i in range(levels + 1)], dtype=np.float64)
+    lv[-1] = 1.0
+    return lv
+
+
+def natural_levels(levels: int) -> np.ndarray:
+    """[0, 2^-(s-1), ..., 1/2, 1] (compressors.py:194-197)."""
+    lv = np.zeros(levels + 1)
+    for i in range(levels):
+        lv[i] = (1.0 / 2.0) ** i
+    return np.flip(lv)
+
+
+class Compressor:
+    """MI355X-native drop-in for the reference ``Compressor`` (compressors.py:35-419)."""
+
+    def __init__(self, compressorName: str = "", rng: str = "compat", seed: int = 0):
+        if rng not in ("compat", "philox"):
+            raise ValueError("rng must be 'compat' or 'philox'")
+        self.__compressorName = compressorName
+        self.__compressorType = CompressorType.IDENTICAL
+        self.__w = 0.0
+        self.total_input_components = 0
+        self.really_need_to_send_components = 0
+        self.last_input_advance = 0
+        self.last_need_to_send_advance = 0
+        self.rng_mode = rng
+        self.philox = _rng.PhiloxStream(seed)
+
+    # ------------------------------------------------------------------ properties (compressors.py:58-132)
+    @property
+    def compressorName(self):
+        return self.__compressorName
+
+    @property
+    def compressorType(self):
+        return self.__compressorType
+
+    @property
+    def is_biased(self):
+        return self.__compressorType in _BIASED
+
+    @property
+    def is_unbiased(self):
+        return not self.is_biased
+
+    @property
+    def w(self):
+        return self.__w
+
+    @property
+    def name(self):
+        omega = r"$\omega$"
+        t = self.compressorType
+        if t == CompressorType.IDENTICAL:
+            return "Identical"
+        if t == CompressorType.LAZY_COMPRESSOR:
+            return f"Bernoulli(Lazy) [p={self.P:g},{omega}={self.getW():.1f}]"
+        if t == CompressorType.RANDK_COMPRESSOR:
+            return f"Random-K (K={self.K}) Compressor"
+        if t == CompressorType.TOPK_COMPRESSOR:
+            return f"Top-K (K={self.K}) Compressor"
+        if t == CompressorType.NATURAL_COMPRESSOR_FP64:
+            return f"Natural for fp64 [{omega}={self.getW():.1f}]"
+        if t == CompressorType.NATURAL_COMPRESSOR_FP32:
+            return f"Natural for fp32 [{omega}={self.getW():.1f}]"
+        if t == CompressorType.STANDARD_DITHERING_FP64:
+            return f"Standard Dithering for fp64[s={self.s}]"
+        # the reference tests STANDARD_DITHERING_FP64 twice (compressors.py:93-96), so FP32 falls to "?"
+        if t == CompressorType.NATURAL_DITHERING_FP32:
+            return f"Natural Dithering for fp32[s={self.s},{omega}={self.getW():.1f}]"
+        if t == CompressorType.NATURAL_DITHERING_FP64:
+            return f"Natural Dithering for fp64[s={self.s},{omega}={self.getW():.1f}]"
+        if t == CompressorType.ADAPTIVE_RANDOM_COMPRESSOR:
+            return "Adaptive Random Compressor"
+        return "?"
+
+    @property
+    def fullName(self):
+        omega = r"$\omega$"
+        t = self.compressorType
+        if t == CompressorType.IDENTICAL:
+            return "Identical"
+        if t == CompressorType.LAZY_COMPRESSOR:
+            return f"Bernoulli(Lazy) [p={self.P:g},{omega}={self.getW():.1f}]"
+        if t == CompressorType.RANDK_COMPRESSOR:
+            return f"Rand [K={self.K},D={self.D}]"
+        if t == CompressorType.TOPK_COMPRESSOR:
+            return f"Top [K={self.K},D={self.D}]"
+        if t == CompressorType.NATURAL_COMPRESSOR_FP64:
+            return f"Natural for fp64 [{omega}={self.getW():.1f}]"
+        if t == CompressorType.NATURAL_COMPRESSOR_FP32:
+            return f"Natural for fp32 [{omega}={self.getW():.1f}]"
+        if t == CompressorType.STANDARD_DITHERING_FP64:
+            return f"Standard Dithering for fp64[s={self.s}]"
+        if t == CompressorType.NATURAL_DITHERING_FP32:
+            return f"Natural Dithering for fp32[s={self.s},{omega}={self.getW():.1f}]"
+        if t == CompressorType.NATURAL_DITHERING_FP64:
+            return f"Natural Dithering for fp64[s={self.s},{omega}={self.getW():.1f}]"
+        if t == CompressorType.ADAPTIVE_RANDOM_COMPRESSOR:
+            return f"Adaptive Random [D={self.D}]"
+        return "?"
+
+    def resetStats(self):
+        self.total_input_components = 0
+        self.really_need_to_send_components = 0
+        self.last_input_advance = 0
+        self.last_need_to_send_advance = 0
+
+    # ------------------------------------------------------------------ factories (compressors.py:140-262)
+    def _set(self, name: str, ctype: CompressorType, w: float) -> None:
+        self.__compressorName = name
+        self.__compressorType = ctype
+        self.__w = w
+
+    def makeIdenticalCompressor(self):
+        self._set("IdenticalCompressor", CompressorType.IDENTICAL, 0.0)
+        self.resetStats()
+
+    def makeLazyCompressor(self, P):
+        self._set("LazyCompressor", CompressorType.LAZY_COMPRESSOR, 1.0 / P - 1.0)
+        self.P = P
+        self.resetStats()
+
+    def _make_std(self, name, ctype, levels, vectorNormCompressor, p):
+        if not 1 <= int(levels) <= 127:
+            raise ValueError("standard dithering supports 1..127 levels (8-bit codes)")
+        self._set(name, ctype, 0.0)
+        self.levelsValues = standard_levels(int(levels))
+        self.s = len(self.levelsValues) - 1
+        assert self.s == levels
+        self.p = p
+        self.vectorNormCompressor = vectorNormCompressor
+        self.resetStats()
+
+    def makeStandardDitheringFP64(self, levels, vectorNormCompressor, p=np.inf):
+        self._make_std("StandardDitheringFP64", CompressorType.STANDARD_DITHERING_FP64, levels, vectorNormCompressor, p)
+
+    def makeStandardDitheringFP32(self, levels, vectorNormCompressor, p=np.inf):
+        self._make_std("StandardDitheringFP32", CompressorType.STANDARD_DITHERING_FP32, levels, vectorNormCompressor, p)
+
+    def makeQSGD_FP64(self, levels, dInput):
+        norm_compressor = Compressor("norm_compressor")
+        norm_compressor.makeIdenticalCompressor()
+        self.makeStandardDitheringFP64(levels, norm_compressor, p=2)
+        # Lemma 3.1 of arXiv:1610.02132 (compressors.py:188-189)
+        self.__w = min(dInput / (levels * levels), dInput**0.5 / levels)
+
+    def _make_natd(self, name, ctype, levels, dInput, p):
+        if not 1 <= int(levels) <= 127:
+            raise ValueError("natural dithering supports 1..127 levels (8-bit codes)")
+        self.levelsValues = natural_levels(int(levels))
+        self.s = len(self.levelsValues) - 1
+        assert self.s == levels
+        self.p = p
+        r = min(p, 2)
+        w = 1.0 / 8.0 + (dInput ** (1.0 / r)) / (2 ** (self.s - 1)) * min(1, (dInput ** (1.0 / r)) / (2 ** (self.s - 1)))
+        self._set(name, ctype, w)
+        self.resetStats()
+
+    def makeNaturalDitheringFP64(self, levels, dInput, p=np.inf):
+        self._make_natd("NaturalDitheringFP64", CompressorType.NATURAL_DITHERING_FP64, levels, dInput, p)
+
+    def makeNaturalDitheringFP32(self, levels, dInput, p=np.inf):
+        self._make_natd("NaturalDitheringFP32", CompressorType.NATURAL_DITHERING_FP32, levels, dInput, p)
+
+    def makeRandKCompressor(self, K, D):
+        self._set("RandKCompressor", CompressorType.RANDK_COMPRESSOR, D / K - 1.0)
+        self.D = D
+        self.K = K
+        self.resetStats()
+
+    def makeTopKCompressor(self, K, D):
+        self._set("TopKCompressor", CompressorType.TOPK_COMPRESSOR, 0.0)
+        self.D = D
+        self.K = K
+        self.resetStats()
+
+    def makeNaturalCompressorFP64(self):
+        self._set("NaturalCompressorFP64", CompressorType.NATURAL_COMPRESSOR_FP64, 1.0 / 8.0)
+        self.resetStats()
+
+    def makeNaturalCompressorFP32(self):
+        self._set("NaturalCompressorFP32", CompressorType.NATURAL_COMPRESSOR_FP32, 1.0 / 8.0)
+        self.resetStats()
+
+    def makeAdaptiveRandomCompressor(self, D):
+        self._set("AdaptiveRandomCompressor", CompressorType.ADAPTIVE_RANDOM_COMPRESSOR, 0.0)
+        self.D = D
+        self.K = 1
+        self.resetStats()
+
+    def getW(self):
+        return self.w
+
+    # ------------------------------------------------------------------ codec (compressors.py:267-410)
+    def compressVector(self, x):
+        """Encode + decode ``x`` (1-D); returns the dense decoded vector like the reference."""
+        if isinstance(x, torch.Tensor) and x.device.type == "cuda":
+            return self._compress_device(x)
+        # host input: the reference's own signature (numpy); H2D -> kernels -> D2H
+        is_tensor = isinstance(x, torch.Tensor)
+        arr = x.detach().cpu().numpy() if is_tensor else np.asarray(x)
+        if arr.dtype != np.float32:
+            raise TypeError(f"the MI355X codec path is fp32; got {arr.dtype}")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        out = self._compress_device(torch.from_numpy(np.ascontiguousarray(arr)).to(dev, non_blocking=False))
+        out_host = out.cpu()
+        return out_host if is_tensor else out_host.numpy().reshape(arr.shape)
+
+    def __call__(self, vec):
+        return self.compressVector(vec)
+
+    def __str__(self):
+        return self.name
+
+    def __repr__(self):
+        return self.fullName
+
+    # ----------------------------------------------------------------------------------------------
+    def _uniforms(self, count: int, device) -> torch.Tensor:
+        u = _rng.python_random_doubles(count)
+        return torch.from_numpy(u).to(device)
+
+    def _finish(self, d: int, send) -> None:
+        self.last_input_advance = d
+        self.last_need_to_send_advance = send
+        self.really_need_to_send_components += self.last_need_to_send_advance
+        self.total_input_components += self.last_input_advance
+
+    def _compress_device(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dim() != 1:
+            raise ValueError("compressVector expects a 1-D vector (d = max(x.shape) in the reference)")
+        d = x.numel()
+        t = self.compressorType
+        if t == CompressorType.IDENTICAL:
+            out = codec.copy(x)
+            self._finish(d, d)
+            return out
+        if t == CompressorType.LAZY_COMPRESSOR:
+            testp = random.random() if self.rng_mode == "compat" else self._philox_scalar(x.device)
+            if testp < self.P:
+                out = codec.scale_div(x, float(np.float32(self.P)))
+                self._finish(d, d)
+            else:
+                out = torch.zeros_like(x)
+                self._finish(d, 0)
+            return out
+        if t == CompressorType.RANDK_COMPRESSOR:
+            if self.D != d:
+                raise ValueError(f"RandK compressor built for D={self.D} applied to a vector of length {d}")
+            S = _rng.numpy_shuffle_prefix(self.D, self.K)
+            idx = torch.from_numpy(S).to(x.device)
+            out = codec.randk_apply(x, idx, float(np.float32(self.D / self.K)))
+            self._finish(d, self.K)
+            return out
+        if t == CompressorType.TOPK_COMPRESSOR:
+            K = int(self.K)
+            if K <= 0 or K >= d:
+                # np.argsort(out)[:-K] is empty for K == 0 and K >= d: nothing is zeroed
+                out = codec.copy(x)
+            else:
+                idx, val = codec.topk_encode(x, K)
+                out = codec.sparse_decode(idx, val, d)
+            self._finish(d, self.K)
+            return out
+        if t == CompressorType.ADAPTIVE_RANDOM_COMPRESSOR:
+            raise NotImplementedError("adaptive random compressor: not yet on the device path")
+        if t in _NATURAL:
+            seed, ctr = self.philox.next()
+            compat_u = None
+            if self.rng_mode == "compat":
+                cnt = int(codec.count_consumers(x.reshape(1, -1), None).item())
+                compat_u = self._uniforms(cnt, x.device)
+            codes, _ = codec.natural_encode(x, seed, ctr, compat_u, want_nnz=False)
+            out = codec.natural_decode(codes, d)
+            if t == CompressorType.NATURAL_COMPRESSOR_FP64:
+                self._finish(d, 12.0 / 64.0 * d)
+            else:
+                self._finish(d, 9.0 / 32.0 * d)
+            return out
+        if t in _STD or t in _NATD:
+            kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
+            x2 = x.reshape(1, d)
+            norms = codec.quant_norm(x2, self.p)
+            seed, ctr = self.philox.next()
+            compat_u = None
+            if self.rng_mode == "compat":
+                cnt = int(codec.count_consumers(x2, norms).item())
+                compat_u = self._uniforms(cnt, x.device)
+            pkt = codec.quant_encode(x2, kind, self.s, norms, seed, ctr, compat_u, want_nnz=(t in _STD))
+            out = codec.quant_decode(pkt).reshape(d)
+            if t in _STD:
+                pnorm = np.float32(norms.item())
+                # the norm goes through the norm compressor (compressors.py:334-337)
+                self.vectorNormCompressor.compressVector(np.array([pnorm]))
+                send = self.vectorNormCompressor.last_need_to_send_advance
+                nnz = int(pkt.nnz.item())
+                if nnz:
+                    per = (1.0 + np.ceil(math.log2(self.s))) / (64.0 if t == CompressorType.STANDARD_DITHERING_FP64 else 32.0)
+                    # repeated += of a multiple of 1/64 is exact below 2^46: equals the reference's loop
+                    send = send + nnz * per
+                self._finish(d, send)
+            else:
+                den = 64.0 if t == CompressorType.NATURAL_DITHERING_FP64 else 32.0
+                self._finish(d, d * (1.0 + np.ceil(math.log2(self.s))) / den)
+            return out
+        raise ValueError(f"unknown compressor type {t}")
+
+    def _philox_scalar(self, device) -> float:
+        # one uniform for the Lazy compressor in philox mode (host-side draw from the same key)
+        seed, ctr = self.philox.next()
+        g = np.random.Generator(np.random.Philox(key=seed, counter=ctr))
+        return float(g.random())
+
+    # ------------------------------------------------------------------ extensions
+    def compressBatch(self, X: torch.Tensor) -> torch.Tensor:
+        """[clients, d] batch of deltas in one launch per kernel (dithering types), philox RNG."""
+        t = self.compressorType
+        if t not in _STD and t not in _NATD:
+            raise NotImplementedError("compressBatch: dithering compressors only")
+        kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
+        norms = codec.quant_norm(X, self.p)
+        seed, ctr = self.philox.next()
+        pkt = codec.quant_encode(X, kind, self.s, norms, seed, ctr, None, want_nnz=False)
+        return codec.quant_decode(pkt)
+
+    def encode(self, x: torch.Tensor) -> Any:
+        """Wire packet of ``x`` (device tensors, philox RNG): QuantPacket / (idx, val) / StackedPacket."""
+        t = self.compressorType
+        if t in _STD or t in _NATD:
+            kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
+            x2 = x.reshape(1, -1)
+            seed, ctr = self.philox.next()
+            return codec.quant_encode(x2, kind, self.s, codec.quant_norm(x2, self.p), seed, ctr, None, want_nnz=False)
+        if t == CompressorType.TOPK_COMPRESSOR:
+            return codec.topk_encode(x, int(self.K))
+        if t in _NATURAL:
+            seed, ctr = self.philox.next()
+            return codec.natural_encode(x, seed, ctr, None, want_nnz=False)[0]
+        raise NotImplementedError(f"encode: {t}")
+
+    def decode(self, packet: Any, d: Optional[int] = None) -> torch.Tensor:
+        t = self.compressorType
+        if t in _STD or t in _NATD:
+            return codec.quant_decode(packet).reshape(-1)
+        if t == CompressorType.TOPK_COMPRESSOR:
+            idx, val = packet
+            return codec.sparse_decode(idx, val, int(d if d is not None else self.D))
+        if t in _NATURAL:
+            return codec.natural_decode(packet, int(d if d is not None else packet.numel()))
+        raise NotImplementedError(f"decode: {t}")

@@ -1,0 +1,190 @@
+// flc_device.hpp — device-side building blocks shared by the codec kernels (gfx950 / CDNA4 only).
+//
+// Everything here is written for 64-lane wavefronts: reductions are __shfl_xor butterflies over 64
+// lanes, ballots are 64-bit, and block-level scans go through LDS one value per wave.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace flc {
+
+constexpr int kWave = 64;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// streaming (non-temporal) 16-B load/store: data touched once should not displace L2 lines
+__device__ __forceinline__ float4 ld_stream(const float* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_stream(float* p, float4 v) {
+  f32x4 t = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11).  Counter = (group_lo, group_hi, ctr_lo, ctr_hi), key = seed.
+// One call yields four 32-bit words; element e of a vector uses word (e & 3) of group e >> 2, so the
+// stream is a pure function of (seed, counter, element index) — independent of launch geometry.
+// ------------------------------------------------------------------------------------------------
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+__device__ __forceinline__ U4 philox_group(uint64_t group, uint64_t seed, uint64_t counter) {
+  return philox4x32_10(U4{(uint32_t)group, (uint32_t)(group >> 32), (uint32_t)counter,
+                          (uint32_t)(counter >> 32)},
+                       (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// 32-bit word -> uniform double in [0, 1), exact (r * 2^-32).
+__device__ __forceinline__ double u01(uint32_t r) { return (double)r * 2.3283064365386963e-10; }
+
+__device__ __forceinline__ uint32_t pick(const U4& v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+
+// ------------------------------------------------------------------------------------------------
+// wave / block reductions (64-lane butterflies)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t w = __shfl_xor(v, o, kWave);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+// inclusive prefix sum across the 64 lanes of a wave
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const T w = __shfl_up(v, o, kWave);
+    if (lane >= o) v += w;
+  }
+  return v;
+}
+
+// Block-wide exclusive scan of one value per thread; returns the exclusive prefix, *total gets the
+// block sum.  `lds` must hold NW = blockDim/64 entries.  Contains two __syncthreads().
+template <typename T, int NW>
+__device__ __forceinline__ T block_excl_scan(T v, T* lds, T* total) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+  const T incl = wave_incl_scan(v);
+  if (lane == kWave - 1) lds[wid] = incl;
+  __syncthreads();
+  T base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const T s = lds[w];
+    base += (w < wid) ? s : T(0);
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+template <typename T, int NW>
+__device__ __forceinline__ T block_sum(T v, T* lds) {
+  T tot;
+  (void)block_excl_scan<T, NW>(v, lds, &tot);
+  return tot;
+}
+
+// ------------------------------------------------------------------------------------------------
+// inter-workgroup hand-off (MI355X_MICROARCH.md §Workgroup dispatch / Guideline 16):
+// payload words are stored write-through (sc1) by ONE lane, drained with s_waitcnt vmcnt(0), then an
+// agent-scope release + relaxed ticket add; the last arriver does an agent acquire and reads the
+// payload with sc1 (L1-bypassing) loads or memory-side atomics.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// returns the ticket (0-based arrival order); call from ONE lane after every storing wave drained
+__device__ __forceinline__ unsigned arrive(unsigned* counter) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void acquire_agent() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ------------------------------------------------------------------------------------------------
+// order-preserving key of a float for "largest signed value" selection (np.argsort order,
+// compressors.py:295): -0 == +0, every NaN is the single largest key.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t order_key(uint32_t b) {
+  if ((b & 0x7fffffffu) > 0x7f800000u) return 0xffffffffu;  // NaN
+  if (b == 0x80000000u) b = 0u;                             // -0 -> +0
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+// value of a key (canonical NaN / +0 for the collapsed classes)
+__device__ __forceinline__ float key_value(uint32_t k) {
+  if (k == 0xffffffffu) return __uint_as_float(0x7fc00000u);
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// ------------------------------------------------------------------------------------------------
+// dithering levels (compressors.py:157, 194-197): standard lv(i) = i * (1/s) in fp64 (bit-equal to
+// np.arange(0, 1.1, 1/s)), lv(s) pinned to 1.0; natural lv(0) = 0, lv(i) = 2^(i-s).
+// ------------------------------------------------------------------------------------------------
+template <int KIND>
+__device__ __forceinline__ double level_value(int i, int s, double step) {
+  if (KIND == 0) return (i == s) ? 1.0 : (double)i * step;
+  return (i == 0) ? 0.0 : ldexp(1.0, i - s);
+}
+
+// first index j in [0, s] with lv(j) >= y (y in [0, 1], not NaN)
+template <int KIND>
+__device__ __forceinline__ int level_lower_bound(float yf, int s, double step) {
+  const double y = (double)yf;
+  if (KIND == 0) {
+    int j = (int)ceil(y * (double)s);
+    j = j < 0 ? 0 : (j > s ? s : j);
+    while (j > 0 && level_value<0>(j - 1, s, step) >= y) --j;
+    while (j < s && level_value<0>(j, s, step) < y) ++j;
+    return j;
+  } else {
+    if (yf == 0.0f) return 0;
+    int E;
+    const float m = frexpf(yf, &E);      // yf = m * 2^E, m in [0.5, 1)
+    const int e = (m == 0.5f) ? E - 1 : E;  // ceil(log2 y)
+    int j = s + e;
+    return j < 1 ? 1 : (j > s ? s : j);
+  }
+}
+
+}  // namespace flc

@@ -1,0 +1,54 @@
+// flc_runtime.hpp — host-side plumbing shared by the C-ABI entry points: error reporting, launch
+// checking, and the kernel-duration probe bench.py reads for its live roofline figure.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/flcodec.h"
+
+namespace flc {
+
+int fail(int code, const char* fmt, ...);          // sets flc_last_error, returns code
+int hip_fail(hipError_t e, const char* where);     // FLC_EHIP with the HIP error string
+
+// probe: events recorded around launches of one named kernel (flc_probe_set)
+void probe_before(const char* name, hipStream_t s);
+void probe_after(const char* name, hipStream_t s);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// workspace carving: every region 256-byte aligned
+struct Carver {
+  char* base;
+  size_t off = 0, cap;
+  Carver(void* b, size_t c) : base(static_cast<char*>(b)), cap(c) {}
+  template <typename T>
+  T* take(size_t count) {
+    off = align_up(off, 256);
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += count * sizeof(T);
+    return p;
+  }
+  bool ok() const { return off <= cap; }
+};
+
+}  // namespace flc
+
+#define FLC_LAUNCH(name, kernel, grid, block, shmem, stream, ...)                  \
+  do {                                                                            \
+    flc::probe_before(name, stream);                                              \
+    hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);          \
+    flc::probe_after(name, stream);                                               \
+    hipError_t e_ = hipGetLastError();                                            \
+    if (e_ != hipSuccess) return flc::hip_fail(e_, name);                         \
+  } while (0)
+
+#define FLC_CHECK_HIP(expr)                                                       \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess) return flc::hip_fail(e_, #expr);                        \
+  } while (0)

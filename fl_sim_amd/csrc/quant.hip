@@ -1,0 +1,547 @@
+// quant.hip — dense stochastic quantizer codec for gfx950: standard / natural dithering
+// (reference: fl_sim/compressors/compressors.py:327-365 and 367-404).
+//
+// Data layout in HBM: x is a [rows, d] fp32 batch (one client delta per row).  The wire is
+//   norms[rows] fp32 + a flat packed code stream, BITS (2/4/8) bits per element, element i of the
+//   flattened batch at bit offset i*BITS (little-endian), code = sign << (BITS-1) | level.
+// Kernels (all HBM-streaming, no MFMA):
+//   quant_norm     per-row max|x| (exact) or fp64 sum of squares; partials per block, the last block
+//                  of each row (arrival ticket) folds them in a fixed order -> deterministic.
+//                  algorithmic bytes: 4 per element read.
+//   quant_count    compat mode only: consumers (x != 0) per encode chunk, then one-block scan.
+//   quant_encode   per element: y = fp32(|x| / norm), bracket [lv(s), lv(s+1)] found in fp64,
+//                  p_down = (y - lv(s+1)) / (lv(s) - lv(s+1)) in fp64, level = u < p_down ? s : s+1.
+//                  algorithmic bytes: 4 read + BITS/8 written per element.
+//   quant_decode   v = fp32(fp32(lv) * sign) * norm, optionally fmaf-accumulated with a row weight.
+//                  algorithmic bytes: BITS/8 read + 4 written (+4 read when accumulating).
+// Each thread owns GROUP = 8 consecutive elements (two 16-B loads, one 2..8-B code store): a wave
+// touches 2 KiB of x per step, fully coalesced.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <algorithm>
+
+#include "flc_device.hpp"
+#include "flc_runtime.hpp"
+
+namespace flc {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kNW = kThreads / kWave;
+constexpr int kGroup = 8;                  // elements per thread per step
+constexpr int kGroupsPerBlock = 1024;      // 8192 elements per block (4 steps of 256 groups)
+constexpr int kNormMaxParts = 1024;         // partial blocks per row for the norm
+constexpr int kRowSlots = 16;              // per-block LDS nnz slots
+
+struct QuantWs {
+  unsigned long long* partials;  // [rows * kNormMaxParts]
+  unsigned* tickets;             // [rows]
+  int* chunk_counts;             // [nblocks]  (compat)
+  long long* chunk_offsets;      // [nblocks]  (compat)
+};
+
+QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* need) {
+  Carver c(ws, bytes);
+  QuantWs w;
+  w.partials = c.take<unsigned long long>((size_t)rows * kNormMaxParts);
+  w.tickets = c.take<unsigned>((size_t)rows);
+  w.chunk_counts = c.take<int>((size_t)nblocks);
+  w.chunk_offsets = c.take<long long>((size_t)nblocks);
+  *need = c.off;
+  return w;
+}
+
+// ------------------------------------------------------------------------------------------------
+// norm
+// ------------------------------------------------------------------------------------------------
+template <int NORM>
+__global__ __launch_bounds__(kThreads) void quant_norm_kernel(const float* __restrict__ x, int64_t d,
+                                                              int parts, int64_t chunk, int vec_ok,
+                                                              QuantWs ws, float* __restrict__ norms) {
+  __shared__ unsigned long long s_red[kNW];
+  __shared__ int s_last;
+  const int row = blockIdx.y, part = blockIdx.x;
+  const float* xr = x + (int64_t)row * d;
+  const int64_t lo = (int64_t)part * chunk;
+  const int64_t hi = lo + chunk < d ? lo + chunk : d;
+
+  uint32_t mx = 0;
+  double ss = 0.0;
+  auto take = [&](float v) {
+    if (NORM == FLC_NORM_INF) {
+      const uint32_t a = __float_as_uint(v) & 0x7fffffffu;  // |v| bits; NaN > inf > finite
+      mx = a > mx ? a : mx;
+    } else {
+      const double dv = (double)v;
+      ss = fma(dv, dv, ss);
+    }
+  };
+  if (vec_ok) {
+    // chunk is a multiple of 4 and the row base is 16-B aligned
+    const float4* x4 = reinterpret_cast<const float4*>(xr + lo);
+    const int64_t n4 = (hi - lo) >> 2;
+    for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+      const float4 v = x4[i];
+      take(v.x); take(v.y); take(v.z); take(v.w);
+    }
+    for (int64_t i = lo + (n4 << 2) + threadIdx.x; i < hi; i += kThreads) take(xr[i]);
+  } else {
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) take(xr[i]);
+  }
+
+  unsigned long long part_bits;
+  if (NORM == FLC_NORM_INF) {
+    uint32_t m = wave_max_u32(mx);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t r = 0;
+      for (int w = 0; w < kNW; ++w) r = (uint32_t)s_red[w] > r ? (uint32_t)s_red[w] : r;
+      s_red[0] = r;
+    }
+    __syncthreads();
+    part_bits = s_red[0];
+  } else {
+    double s = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = __double_as_longlong(s);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double r = 0.0;
+      for (int w = 0; w < kNW; ++w) r += __longlong_as_double(s_red[w]);
+      s_red[0] = __double_as_longlong(r);
+    }
+    __syncthreads();
+    part_bits = s_red[0];
+  }
+
+  if (threadIdx.x == 0) {
+    st_sc1(&ws.partials[(int64_t)row * kNormMaxParts + part], part_bits);
+    const unsigned t = arrive(&ws.tickets[row]);
+    s_last = (t == (unsigned)parts - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  acquire_agent();
+  __syncthreads();
+  // last block of this row: fold the partials in a fixed order
+  if (threadIdx.x < kWave) {
+    const int lane = threadIdx.x;
+    if (NORM == FLC_NORM_INF) {
+      uint32_t m = 0;
+      for (int p = lane; p < parts; p += kWave) {
+        const uint32_t v = (uint32_t)ld_sc1(&ws.partials[(int64_t)row * kNormMaxParts + p]);
+        m = v > m ? v : m;
+      }
+      m = wave_max_u32(m);
+      if (lane == 0) norms[row] = __uint_as_float(m);
+    } else {
+      double s = 0.0;
+      for (int p = lane; p < parts; p += kWave)
+        s += __longlong_as_double(ld_sc1(&ws.partials[(int64_t)row * kNormMaxParts + p]));
+      s = wave_sum(s);
+      if (lane == 0) norms[row] = (float)sqrt(s);
+    }
+    if (lane == 0) st_sc1(&ws.tickets[row], 0u);  // self-reset for the next call
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-element quantizer
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool norm_regular(float nrm) { return nrm > 0.0f && nrm <= 3.402823466e38f; }
+
+// consumer = the reference draws random.random() for this element (compressors.py:339-354)
+__device__ __forceinline__ bool consumes(float xv, float nrm) {
+  if (xv == 0.0f) return false;
+  if (norm_regular(nrm)) return true;
+  return !isnan(fabsf(xv) / nrm);
+}
+
+template <int KIND, int BITS>
+__device__ __forceinline__ uint32_t quant_code(float xv, float nrm, int s, double step, double u) {
+  if (xv == 0.0f) return 0u;
+  if (!norm_regular(nrm)) return 1u;
+  const float y = fabsf(xv) / nrm;  // IEEE fp32 division (compressors.py:344)
+  const int j = level_lower_bound<KIND>(y, s, step);
+  const int sl = j > 0 ? j - 1 : 0;
+  const double lo = level_value<KIND>(sl, s, step), hi = level_value<KIND>(sl + 1, s, step);
+  const double p = ((double)y - hi) / (lo - hi);  // fp64 (compressors.py:348)
+  const int lvl = (u < p) ? sl : sl + 1;           // compressors.py:350-353
+  return ((__float_as_uint(xv) >> 31) << (BITS - 1)) | (uint32_t)lvl;
+}
+
+template <int KIND, int BITS>
+__device__ __forceinline__ float dequant(uint32_t code, float nrm, int s, double step) {
+  if (!norm_regular(nrm)) return code == 0u ? 0.0f : __uint_as_float(0x7fc00000u);
+  const uint32_t lvl = code & ((1u << (BITS - 1)) - 1u);
+  const float lv = (float)level_value<KIND>((int)lvl, s, step);
+  const float sv = (code >> (BITS - 1)) ? -lv : lv;  // fp32(lv) * sign, -0 kept
+  return sv * nrm;                                   // compressors.py:357
+}
+
+struct RowCursor {
+  int64_t d;
+  int64_t row, row_end;
+  __device__ __forceinline__ void seek(int64_t e) {
+    row = e / d;
+    row_end = (row + 1) * d;
+  }
+  __device__ __forceinline__ int64_t at(int64_t e) {
+    if (e >= row_end) seek(e);
+    return row;
+  }
+};
+
+__device__ __forceinline__ void load_group(const float* __restrict__ x, int64_t e0, int valid, float v[kGroup]) {
+  if (valid == kGroup) {
+    const float4 a = *reinterpret_cast<const float4*>(x + e0);
+    const float4 b = *reinterpret_cast<const float4*>(x + e0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) v[j] = j < valid ? x[e0 + j] : 0.0f;
+  }
+}
+
+template <int BITS>
+__device__ __forceinline__ void store_codes(uint8_t* __restrict__ codes, int64_t e0, int valid, uint64_t packed) {
+  constexpr int kBytes = kGroup * BITS / 8;
+  uint8_t* dst = codes + (e0 * BITS) / 8;
+  if (valid == kGroup) {
+    if (kBytes == 8) *reinterpret_cast<uint2*>(dst) = make_uint2((uint32_t)packed, (uint32_t)(packed >> 32));
+    else if (kBytes == 4) *reinterpret_cast<uint32_t*>(dst) = (uint32_t)packed;
+    else *reinterpret_cast<uint16_t*>(dst) = (uint16_t)packed;
+  } else {
+    const int nb = (valid * BITS + 7) / 8;
+    for (int b = 0; b < nb; ++b) dst[b] = (uint8_t)(packed >> (8 * b));
+  }
+}
+
+template <int BITS>
+__device__ __forceinline__ uint64_t load_codes(const uint8_t* __restrict__ codes, int64_t e0, int valid) {
+  constexpr int kBytes = kGroup * BITS / 8;
+  const uint8_t* src = codes + (e0 * BITS) / 8;
+  if (valid == kGroup) {
+    if (kBytes == 8) {
+      const uint2 v = *reinterpret_cast<const uint2*>(src);
+      return (uint64_t)v.x | ((uint64_t)v.y << 32);
+    }
+    if (kBytes == 4) return *reinterpret_cast<const uint32_t*>(src);
+    return *reinterpret_cast<const uint16_t*>(src);
+  }
+  uint64_t p = 0;
+  const int nb = (valid * BITS + 7) / 8;
+  for (int b = 0; b < nb; ++b) p |= (uint64_t)src[b] << (8 * b);
+  return p;
+}
+
+// consumers per encode chunk (compat mode)
+__global__ __launch_bounds__(kThreads) void quant_count_kernel(const float* __restrict__ x, int64_t n, int64_t d,
+                                                               const float* __restrict__ norms, QuantWs ws) {
+  __shared__ int s_red[kNW];
+  const int64_t g_begin = (int64_t)blockIdx.x * kGroupsPerBlock;
+  RowCursor rc{d, 0, 0};
+  rc.seek(g_begin * kGroup < n ? g_begin * kGroup : 0);
+  int cnt = 0;
+  for (int it = 0; it < kGroupsPerBlock / kThreads; ++it) {
+    const int64_t g = g_begin + it * kThreads + threadIdx.x;
+    const int64_t e0 = g * kGroup;
+    if (e0 >= n) break;
+    const int valid = n - e0 < kGroup ? (int)(n - e0) : kGroup;
+    float v[kGroup];
+    load_group(x, e0, valid, v);
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j)
+      if (j < valid) cnt += consumes(v[j], norms[rc.at(e0 + j)]) ? 1 : 0;
+  }
+  const int tot = block_sum<int, kNW>(cnt, s_red);
+  if (threadIdx.x == 0) ws.chunk_counts[blockIdx.x] = tot;
+}
+
+// total consumers of a batch (norms == nullptr: x != 0)
+__global__ __launch_bounds__(kThreads) void count_consumers_kernel(const float* __restrict__ x, int64_t n, int64_t d,
+                                                                   const float* __restrict__ norms,
+                                                                   unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s_red[kNW];
+  unsigned long long cnt = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const float v = x[i];
+    cnt += norms ? (consumes(v, norms[i / d]) ? 1 : 0) : (v != 0.0f ? 1 : 0);
+  }
+  const unsigned long long tot = block_sum<unsigned long long, kNW>(cnt, s_red);
+  if (threadIdx.x == 0 && tot) atomicAdd(out, tot);
+}
+
+// exclusive scan of chunk counts (one block)
+__global__ __launch_bounds__(1024) void chunk_scan_kernel(const int* __restrict__ counts, long long* __restrict__ offsets,
+                                                          int64_t nchunks) {
+  __shared__ long long s_red[16];
+  long long running = 0;
+  for (int64_t base = 0; base < nchunks; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const long long v = i < nchunks ? counts[i] : 0;
+    long long tot;
+    const long long ex = block_excl_scan<long long, 16>(v, s_red, &tot);
+    if (i < nchunks) offsets[i] = running + ex;
+    running += tot;
+  }
+}
+
+template <int KIND, int BITS, bool COMPAT>
+__global__ __launch_bounds__(kThreads) void quant_encode_kernel(
+    const float* __restrict__ x, int64_t n, int64_t d, int s, double step, const float* __restrict__ norms,
+    uint64_t seed, uint64_t counter, const double* __restrict__ compat_u, uint8_t* __restrict__ codes,
+    long long* __restrict__ nnz, QuantWs ws) {
+  __shared__ long long s_scan[kNW];
+  __shared__ unsigned long long s_nnz[kRowSlots];
+  const int64_t g_begin = (int64_t)blockIdx.x * kGroupsPerBlock;
+  const int64_t e_first = g_begin * kGroup;
+  RowCursor rc{d, 0, 0};
+  rc.seek(e_first);
+  const int64_t row_base = rc.row;
+  if (threadIdx.x < kRowSlots) s_nnz[threadIdx.x] = 0;
+  __syncthreads();
+  long long running = COMPAT ? ws.chunk_offsets[blockIdx.x] : 0;
+
+  for (int it = 0; it < kGroupsPerBlock / kThreads; ++it) {
+    const int64_t g = g_begin + it * kThreads + threadIdx.x;
+    const int64_t e0 = g * kGroup;
+    const int valid = e0 >= n ? 0 : (n - e0 < kGroup ? (int)(n - e0) : kGroup);
+    float v[kGroup];
+    float nr[kGroup];
+    if (valid > 0) load_group(x, e0, valid, v);
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) nr[j] = (j < valid) ? norms[rc.at(e0 + j)] : 1.0f;
+
+    double u[kGroup];
+    if (COMPAT) {
+      int c[kGroup];
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        c[j] = (j < valid && consumes(v[j], nr[j])) ? 1 : 0;
+        cnt += c[j];
+      }
+      long long tot;
+      const long long ex = block_excl_scan<long long, kNW>((long long)cnt, s_scan, &tot);
+      long long r = running + ex;
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        u[j] = c[j] ? compat_u[r] : 0.0;
+        r += c[j];
+      }
+      running += tot;
+    } else if (valid > 0) {
+      const U4 a = philox_group((uint64_t)e0 >> 2, seed, counter);
+      const U4 b = philox_group(((uint64_t)e0 >> 2) + 1, seed, counter);
+      u[0] = u01(a.x); u[1] = u01(a.y); u[2] = u01(a.z); u[3] = u01(a.w);
+      u[4] = u01(b.x); u[5] = u01(b.y); u[6] = u01(b.z); u[7] = u01(b.w);
+    }
+    if (valid == 0) continue;
+
+    uint64_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      if (j < valid) packed |= (uint64_t)quant_code<KIND, BITS>(v[j], nr[j], s, step, u[j]) << (j * BITS);
+    }
+    store_codes<BITS>(codes, e0, valid, packed);
+
+    if (nnz) {
+      // rows of this group: at most a few; count nonzeros per row into LDS slots
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        if (j < valid && v[j] != 0.0f) {
+          const int64_t r = rc.at(e0 + j) - row_base;
+          if (r < kRowSlots) atomicAdd(&s_nnz[r], 1ull);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r + row_base]), 1ull);
+        }
+      }
+    }
+  }
+  if (nnz) {
+    __syncthreads();
+    if (threadIdx.x < kRowSlots && s_nnz[threadIdx.x] != 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[row_base + threadIdx.x]), s_nnz[threadIdx.x]);
+  }
+}
+
+template <int KIND, int BITS, bool ACC>
+__global__ __launch_bounds__(kThreads) void quant_decode_kernel(const uint8_t* __restrict__ codes, int64_t n, int64_t d,
+                                                                int s, double step, const float* __restrict__ norms,
+                                                                const float* __restrict__ row_w, float* __restrict__ out) {
+  const int64_t ngroups = (n + kGroup - 1) / kGroup;
+  for (int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x; g < ngroups; g += (int64_t)gridDim.x * kThreads) {
+    const int64_t e0 = g * kGroup;
+    const int valid = n - e0 < kGroup ? (int)(n - e0) : kGroup;
+    RowCursor rc{d, 0, 0};
+    rc.seek(e0);
+    const uint64_t packed = load_codes<BITS>(codes, e0, valid);
+    float o[kGroup];
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const int64_t r = rc.at(e0 + j < n ? e0 + j : e0);
+      const float val = dequant<KIND, BITS>((uint32_t)(packed >> (j * BITS)) & ((1u << BITS) - 1u), norms[r], s, step);
+      o[j] = (!ACC && row_w) ? row_w[r] * val : val;
+    }
+    if (ACC) {
+      float prev[kGroup];
+      load_group(out, e0, valid, prev);
+      rc.seek(e0);
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        const int64_t r = rc.at(e0 + j < n ? e0 + j : e0);
+        o[j] = fmaf(row_w ? row_w[r] : 1.0f, o[j], prev[j]);
+      }
+    }
+    if (valid == kGroup) {
+      *reinterpret_cast<float4*>(out + e0) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(out + e0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+      for (int j = 0; j < valid; ++j) out[e0 + j] = o[j];
+    }
+  }
+}
+
+int check_quant_args(int kind, int levels, int bits) {
+  if (kind != FLC_Q_STANDARD_DITHER && kind != FLC_Q_NATURAL_DITHER)
+    return fail(FLC_EINVAL, "quant: unknown kind %d", kind);
+  if (bits != 2 && bits != 4 && bits != 8) return fail(FLC_EINVAL, "quant: bits must be 2, 4 or 8 (got %d)", bits);
+  if (levels < 1 || levels > (1 << (bits - 1)) - 1)
+    return fail(FLC_EINVAL, "quant: levels %d does not fit %d-bit codes", levels, bits);
+  return FLC_OK;
+}
+
+double level_step(int levels) { return 1.0 / (double)levels; }
+
+template <int KIND, int BITS>
+int launch_encode(const float* x, int64_t n, int64_t d, int levels, const float* norms, uint64_t seed, uint64_t counter,
+                  const double* compat_u, uint8_t* codes, int64_t* nnz, const QuantWs& w, int64_t nblocks,
+                  hipStream_t st) {
+  const double step = level_step(levels);
+  long long* nz = reinterpret_cast<long long*>(nnz);
+  if (compat_u) {
+    FLC_LAUNCH("quant_count", quant_count_kernel, dim3((unsigned)nblocks), dim3(kThreads), 0, st, x, n, d, norms, w);
+    FLC_LAUNCH("quant_chunk_scan", chunk_scan_kernel, dim3(1), dim3(1024), 0, st, w.chunk_counts, w.chunk_offsets,
+               nblocks);
+    FLC_LAUNCH("quant_encode", (quant_encode_kernel<KIND, BITS, true>), dim3((unsigned)nblocks), dim3(kThreads), 0, st,
+               x, n, d, levels, step, norms, seed, counter, compat_u, codes, nz, w);
+  } else {
+    FLC_LAUNCH("quant_encode", (quant_encode_kernel<KIND, BITS, false>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+               st, x, n, d, levels, step, norms, seed, counter, compat_u, codes, nz, w);
+  }
+  return FLC_OK;
+}
+
+template <int KIND, int BITS>
+int launch_decode(const uint8_t* codes, int64_t n, int64_t d, int levels, const float* norms, const float* row_w,
+                  int acc, float* out, hipStream_t st) {
+  const double step = level_step(levels);
+  const int64_t ngroups = cdiv(n, kGroup);
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(ngroups, kThreads), 256 * 32);
+  if (acc)
+    FLC_LAUNCH("quant_decode", (quant_decode_kernel<KIND, BITS, true>), dim3(grid), dim3(kThreads), 0, st, codes, n, d,
+               levels, step, norms, row_w, out);
+  else
+    FLC_LAUNCH("quant_decode", (quant_decode_kernel<KIND, BITS, false>), dim3(grid), dim3(kThreads), 0, st, codes, n,
+               d, levels, step, norms, row_w, out);
+  return FLC_OK;
+}
+
+}  // namespace
+}  // namespace flc
+
+using namespace flc;
+
+extern "C" {
+
+size_t flc_quant_workspace_size(int64_t rows, int64_t d) {
+  size_t need = 0;
+  const int64_t nblocks = cdiv(rows * d, (int64_t)kGroup * kGroupsPerBlock);
+  (void)carve(nullptr, 0, rows, nblocks < 1 ? 1 : nblocks, &need);
+  return need;
+}
+
+int flc_quant_norm(const float* x, int64_t rows, int64_t d, int norm_p, float* norms, void* ws, size_t ws_bytes,
+                   void* stream) {
+  if (rows <= 0 || d <= 0 || !x || !norms) return fail(FLC_EINVAL, "flc_quant_norm: bad arguments");
+  if (rows > 65535) return fail(FLC_EINVAL, "flc_quant_norm: at most 65535 rows per call");
+  if (norm_p != FLC_NORM_INF && norm_p != FLC_NORM_L2) return fail(FLC_EINVAL, "flc_quant_norm: p must be inf(0) or 2");
+  size_t need = 0;
+  const int64_t nblocks = cdiv(rows * d, (int64_t)kGroup * kGroupsPerBlock);
+  QuantWs w = carve(ws, ws_bytes, rows, nblocks < 1 ? 1 : nblocks, &need);
+  if (need > ws_bytes || !ws) return fail(FLC_EWORKSPACE, "flc_quant_norm: workspace %zu < %zu", ws_bytes, need);
+  int64_t parts = cdiv(d, 8192);
+  if (parts > kNormMaxParts) parts = kNormMaxParts;
+  int64_t chunk = align_up((size_t)cdiv(d, parts), 4);
+  parts = cdiv(d, chunk);
+  const int vec_ok = (d % 4 == 0) && aligned16(x);
+  hipStream_t st = as_stream(stream);
+  if (norm_p == FLC_NORM_INF)
+    FLC_LAUNCH("quant_norm", quant_norm_kernel<FLC_NORM_INF>, dim3((unsigned)parts, (unsigned)rows), dim3(kThreads), 0,
+               st, x, d, (int)parts, chunk, vec_ok, w, norms);
+  else
+    FLC_LAUNCH("quant_norm", quant_norm_kernel<FLC_NORM_L2>, dim3((unsigned)parts, (unsigned)rows), dim3(kThreads), 0,
+               st, x, d, (int)parts, chunk, vec_ok, w, norms);
+  return FLC_OK;
+}
+
+int flc_quant_encode(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits, const float* norms,
+                     uint64_t seed, uint64_t counter, const double* compat_u, uint8_t* codes, int64_t* nnz, void* ws,
+                     size_t ws_bytes, void* stream) {
+  if (rows <= 0 || d <= 0 || !x || !norms || !codes) return fail(FLC_EINVAL, "flc_quant_encode: bad arguments");
+  if (int rc = check_quant_args(kind, levels, bits)) return rc;
+  if (!aligned16(x) || !aligned16(codes)) return fail(FLC_EINVAL, "flc_quant_encode: x and codes must be 16-B aligned");
+  const int64_t n = rows * d;
+  const int64_t nblocks = cdiv(n, (int64_t)kGroup * kGroupsPerBlock);
+  size_t need = 0;
+  QuantWs w = carve(ws, ws_bytes, rows, nblocks, &need);
+  if (need > ws_bytes || !ws) return fail(FLC_EWORKSPACE, "flc_quant_encode: workspace %zu < %zu", ws_bytes, need);
+  hipStream_t st = as_stream(stream);
+  if (nnz) FLC_CHECK_HIP(hipMemsetAsync(nnz, 0, (size_t)rows * sizeof(int64_t), st));
+#define FLC_ENC(K, B) return launch_encode<K, B>(x, n, d, levels, norms, seed, counter, compat_u, codes, nnz, w, nblocks, st)
+  if (kind == FLC_Q_STANDARD_DITHER) {
+    if (bits == 8) FLC_ENC(0, 8);
+    if (bits == 4) FLC_ENC(0, 4);
+    FLC_ENC(0, 2);
+  } else {
+    if (bits == 8) FLC_ENC(1, 8);
+    if (bits == 4) FLC_ENC(1, 4);
+    FLC_ENC(1, 2);
+  }
+#undef FLC_ENC
+}
+
+int flc_count_consumers(const float* x, int64_t rows, int64_t d, const float* norms, int64_t* count, void* stream) {
+  if (!x || !count || rows <= 0 || d <= 0) return fail(FLC_EINVAL, "flc_count_consumers: bad arguments");
+  hipStream_t st = as_stream(stream);
+  FLC_CHECK_HIP(hipMemsetAsync(count, 0, sizeof(int64_t), st));
+  const int64_t n = rows * d;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(n, kThreads), 256 * 8);
+  FLC_LAUNCH("count_consumers", count_consumers_kernel, dim3(grid), dim3(kThreads), 0, st, x, n, d, norms,
+             reinterpret_cast<unsigned long long*>(count));
+  return FLC_OK;
+}
+
+int flc_quant_decode(const uint8_t* codes, int64_t rows, int64_t d, int kind, int levels, int bits, const float* norms,
+                     const float* row_weights, int accumulate, float* out, void* stream) {
+  if (rows <= 0 || d <= 0 || !codes || !norms || !out) return fail(FLC_EINVAL, "flc_quant_decode: bad arguments");
+  if (int rc = check_quant_args(kind, levels, bits)) return rc;
+  if (!aligned16(out) || !aligned16(codes)) return fail(FLC_EINVAL, "flc_quant_decode: out and codes must be 16-B aligned");
+  const int64_t n = rows * d;
+  hipStream_t st = as_stream(stream);
+#define FLC_DEC(K, B) return launch_decode<K, B>(codes, n, d, levels, norms, row_weights, accumulate, out, st)
+  if (kind == FLC_Q_STANDARD_DITHER) {
+    if (bits == 8) FLC_DEC(0, 8);
+    if (bits == 4) FLC_DEC(0, 4);
+    FLC_DEC(0, 2);
+  } else {
+    if (bits == 8) FLC_DEC(1, 8);
+    if (bits == 4) FLC_DEC(1, 4);
+    FLC_DEC(1, 2);
+  }
+#undef FLC_DEC
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+// runtime.cpp — error state, workspace init and the launch probe of the C ABI (include/flcodec.h).
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "flc_runtime.hpp"
+
+namespace flc {
+
+static thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  return fail(FLC_EHIP, "%s: %s", where, hipGetErrorString(e));
+}
+
+// ---- probe ---------------------------------------------------------------------------------------
+namespace {
+struct ProbeState {
+  std::mutex mu;
+  std::string name;  // empty = disabled
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+  hipEvent_t cur_start = nullptr;
+};
+ProbeState& probe() {
+  static ProbeState p;
+  return p;
+}
+hipEvent_t new_event(ProbeState& p) {
+  (void)p;
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+}  // namespace
+
+void probe_before(const char* name, hipStream_t s) {
+  ProbeState& p = probe();
+  if (p.name.empty() || p.name != name) return;
+  std::lock_guard<std::mutex> lk(p.mu);
+  hipEvent_t a;
+  if (!p.pool.empty()) {
+    a = p.pool.back().first;
+    hipEvent_t b = p.pool.back().second;
+    p.pool.pop_back();
+    p.pending.push_back({a, b});
+  } else {
+    a = new_event(p);
+    p.pending.push_back({a, new_event(p)});
+  }
+  (void)hipEventRecord(p.pending.back().first, s);
+}
+
+void probe_after(const char* name, hipStream_t s) {
+  ProbeState& p = probe();
+  if (p.name.empty() || p.name != name) return;
+  std::lock_guard<std::mutex> lk(p.mu);
+  if (!p.pending.empty()) (void)hipEventRecord(p.pending.back().second, s);
+}
+
+}  // namespace flc
+
+extern "C" {
+
+int flc_abi_version(void) { return FLC_ABI_VERSION; }
+
+const char* flc_last_error(void) { return flc::g_err; }
+
+int flc_workspace_init(void* ws, size_t ws_bytes, void* stream) {
+  if (ws_bytes == 0) return FLC_OK;
+  if (!ws) return flc::fail(FLC_EINVAL, "flc_workspace_init: null workspace");
+  FLC_CHECK_HIP(hipMemsetAsync(ws, 0, ws_bytes, flc::as_stream(stream)));
+  return FLC_OK;
+}
+
+int flc_probe_set(const char* kernel_name) {
+  flc::ProbeState& p = flc::probe();
+  std::lock_guard<std::mutex> lk(p.mu);
+  p.name = kernel_name ? kernel_name : "";
+  return FLC_OK;
+}
+
+int flc_probe_read(double* total_ms, int64_t* launches) {
+  flc::ProbeState& p = flc::probe();
+  std::lock_guard<std::mutex> lk(p.mu);
+  double tot = 0.0;
+  int64_t n = 0;
+  for (auto& ev : p.pending) {
+    FLC_CHECK_HIP(hipEventSynchronize(ev.second));
+    float ms = 0.f;
+    FLC_CHECK_HIP(hipEventElapsedTime(&ms, ev.first, ev.second));
+    tot += ms;
+    ++n;
+    p.pool.push_back(ev);
+  }
+  p.pending.clear();
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = n;
+  return FLC_OK;
+}
+
+}  // extern "C"

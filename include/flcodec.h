@@ -1,0 +1,173 @@
+/*
+ * flcodec.h — C ABI of the MI355X-native gradient codec + aggregation path for fl-sim.
+ *
+ * The reference (wenh06/fl-sim) has no native code and no FFI: its codec is the pure-Python class
+ * `Compressor` (fl_sim/compressors/compressors.py:35-419) and its aggregation is a set of in-place
+ * torch loops on the `Server` (fl_sim/nodes.py:1116-1180, fl_sim/algorithms/fedopt/_fedopt.py:196-265).
+ * Every entry point below replaces one branch of those Python functions; the comment on each cites
+ * the reference lines it stands in for.  INTEGRATION.md shows the ctypes binding a maintainer adds to
+ * the reference (fl_sim_amd/_lib.py is that binding, shipped).
+ *
+ * Conventions (all entry points):
+ *   - plain pointers and sizes, no framework types; every device pointer is HBM memory of the current
+ *     HIP device, every `stream` is a hipStream_t passed as void* (NULL = the default stream);
+ *   - the caller owns every buffer, including the workspace (`*_workspace_size` says how much);
+ *     a workspace must be zero-filled once after allocation (flc_workspace_init) and may then be reused
+ *     by any number of calls on the same stream (counters reset themselves in-kernel);
+ *   - stream-ordered and asynchronous: nothing here synchronises the stream except the host-only RNG
+ *     helpers and flc_probe_read; no allocation happens inside a call, so calls can be graph-captured;
+ *   - the return value is a status code (FLC_OK = 0); flc_last_error() describes the last failure of
+ *     the calling thread;
+ *   - element counts are int64_t but a single vector must have fewer than 2^31 elements (index
+ *     streams are int32, as the reference's argsort indices fit int32 below that size);
+ *   - RNG: every stochastic codec takes (seed, counter) for the counter-based Philox4x32-10 stream
+ *     ("philox" mode), or a device array `compat_u` of fp64 uniforms, one per consuming element in
+ *     index order ("compat" mode: the exact uniforms Python's `random.random()` would have produced —
+ *     see flc_mt_random_doubles).  compat_u == NULL selects philox mode.
+ */
+#ifndef FLCODEC_H_
+#define FLCODEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLC_ABI_VERSION 1
+
+enum flc_status {
+  FLC_OK = 0,
+  FLC_EINVAL = 1,       /* bad argument (sizes, levels, bits, null pointer) */
+  FLC_EHIP = 2,         /* HIP runtime error */
+  FLC_EWORKSPACE = 3,   /* workspace too small */
+  FLC_EUNSUPPORTED = 4  /* valid request this build does not implement */
+};
+
+/* dense quantizer families (compressors.py:327-404) */
+enum flc_quant_kind {
+  FLC_Q_STANDARD_DITHER = 0, /* levels i/s, i = 0..s          (compressors.py:154-182, 327-365) */
+  FLC_Q_NATURAL_DITHER = 1   /* levels 0, 2^-(s-1), .., 1/2, 1 (compressors.py:191-221, 367-404) */
+};
+enum flc_norm_kind { FLC_NORM_INF = 0, FLC_NORM_L2 = 2 };
+
+/* server optimiser of FedOptServer.update (_fedopt.py:196-265) */
+enum flc_fedopt_kind { FLC_OPT_AVG = 0, FLC_OPT_ADAGRAD = 1, FLC_OPT_YOGI = 2, FLC_OPT_ADAM = 3 };
+
+/* ------------------------------------------------------------------ library */
+int flc_abi_version(void);
+const char* flc_last_error(void);
+/* zero a freshly allocated workspace (once); stream-ordered */
+int flc_workspace_init(void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------ host RNG (compat mode)
+ * Python's `random` and numpy's legacy `RandomState` are both MT19937.  These host functions advance
+ * a state exported by `random.getstate()[1]` (624 words + position) or `np.random.get_state()`
+ * (624 words, position) exactly as the interpreter would, so the caller can write the advanced state
+ * back and the global streams stay in lock-step with the reference (misc.py:196-217 seeds them).  */
+
+/* n draws of random.random() (compressors.py:277, 316, 349, 386) == legacy random_sample (res53) */
+int flc_mt_random_doubles(uint32_t* mt_state624, int32_t* mt_pos, double* out, int64_t n);
+/* np.random.shuffle(np.arange(D)) then [:K] (compressors.py:285-287): legacy Fisher-Yates with
+ * masked-rejection random_interval; writes the first K entries of the shuffled permutation */
+int flc_np_shuffle_prefix(uint32_t* mt_state624, int32_t* mt_pos, int64_t D, int64_t K, int32_t* out_idx);
+
+/* ------------------------------------------------------------------ dense quantizer codec
+ * x is a [rows, d] row-major fp32 batch: one client delta per row (rows = 1 for compressVector).
+ * Wire format per row: one fp32 norm + a packed code stream of `bits` (2, 4 or 8) bits per element,
+ *   code = sign << (bits-1) | level, level in 0..s (s < 2^(bits-1)); element i of the flat batch sits
+ *   at bit offset i*bits of `codes` (little-endian within a byte).
+ * A row whose norm is not finite is encoded as code 0 for x == 0 and code 1 otherwise; it decodes to
+ *   +0 / NaN, which is what the reference produces for such rows. */
+size_t flc_quant_workspace_size(int64_t rows, int64_t d);
+/* per-row ||x||_p: p = inf → max |x| (exact, NaN-propagating), p = 2 → sqrt of an fp64 sum of
+ * squares rounded once to fp32 (compressors.py:332, 372; np.linalg.norm) */
+int flc_quant_norm(const float* x, int64_t rows, int64_t d, int norm_p, float* norms, void* ws,
+                   size_t ws_bytes, void* stream);
+/* encode (compressors.py:339-365 / 376-404, the stochastic level choice); `nnz` (device, int64[rows])
+ * receives the count of x != 0 per row, the quantity the reference's send-statistics count. */
+int flc_quant_encode(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits,
+                     const float* norms, uint64_t seed, uint64_t counter, const double* compat_u,
+                     uint8_t* codes, int64_t* nnz, void* ws, size_t ws_bytes, void* stream);
+/* compat mode: how many uniforms the reference draws for this batch — one per element with x != 0
+ * whose y = |x| / norm is not NaN (compressors.py:339-354); norms == NULL counts x != 0 (the natural
+ * compressor, compressors.py:307-316).  *count is a device int64. */
+int flc_count_consumers(const float* x, int64_t rows, int64_t d, const float* norms, int64_t* count,
+                        void* stream);
+/* decode: v = fp32(fp32(level_value) * sign) * norm (compressors.py:357/394);
+ * out = accumulate ? fmaf(row_weight, v, out) : (row_weights ? row_weight * v : v) */
+int flc_quant_decode(const uint8_t* codes, int64_t rows, int64_t d, int kind, int levels, int bits,
+                     const float* norms, const float* row_weights, int accumulate, float* out,
+                     void* stream);
+
+/* ------------------------------------------------------------------ natural compressor
+ * (compressors.py:302-325).  Wire: one uint16 per element, 0 = zero, else sign << 15 | (e + 150)
+ * for the chosen power of two 2^e, e in [-149, 127]. */
+size_t flc_natural_workspace_size(int64_t n);  /* needed in compat mode only */
+int flc_natural_encode(const float* x, int64_t n, uint64_t seed, uint64_t counter,
+                       const double* compat_u, uint16_t* codes, int64_t* nnz, void* ws, size_t ws_bytes,
+                       void* stream);
+int flc_natural_decode(const uint16_t* codes, int64_t n, float weight, int accumulate, float* out,
+                       void* stream);
+
+/* ------------------------------------------------------------------ top-k sparsifier
+ * (compressors.py:293-296): keeps the k largest *signed* values (NaN largest, -0 == +0); among values
+ * equal to the k-th largest the highest indices are kept (the order of a stable ascending argsort).
+ * Output: idx[k] ascending, val[k] the kept values bit-for-bit.  Requires 0 < k < n. */
+size_t flc_topk_workspace_size(int64_t n, int64_t k);
+int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, void* ws,
+                    size_t ws_bytes, void* stream);
+/* dense decode of an ascending sparse stream: out[idx[j]] = scale * val[j], zeros elsewhere
+ * (compressors.py:289-291, 294-295); accumulate: out = fmaf(weight, v, out) over the whole vector */
+int flc_sparse_decode(const int32_t* idx, const float* val, int64_t k, float scale, int64_t n,
+                      float weight, int accumulate, float* out, void* stream);
+
+/* ------------------------------------------------------------------ stacked top-k -> 8-bit dither
+ * Top-k of x (as above), then standard dithering with s = levels (<= 127), p = inf, of the k kept
+ * values: the pipeline TopK(x) followed by StandardDithering on the k-sparse result.
+ * Wire: idx[k] int32 ascending, codes[k] (sign << 7 | level), norm[1] fp32. */
+int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_t seed,
+                       uint64_t counter, const double* compat_u, int32_t* idx, uint8_t* codes,
+                       float* norm, void* ws, size_t ws_bytes, void* stream);
+int flc_stacked_decode(const int32_t* idx, const uint8_t* codes, int64_t k, int levels,
+                       const float* norm, int64_t n, float weight, int accumulate, float* out,
+                       void* stream);
+
+/* ------------------------------------------------------------------ other compressors
+ * identical (compressors.py:273-275): out = +x;  lazy (276-283): out = x / p (fp32 division);
+ * rand-k (284-292): out = 0, out[idx[j]] = scale * x[idx[j]] (idx in any order, unique). */
+int flc_copy(const float* x, int64_t n, float* out, void* stream);
+int flc_scale_div(const float* x, int64_t n, float p, float* out, void* stream);
+int flc_randk_apply(const float* x, int64_t n, const int32_t* idx, int64_t k, float scale, float* out,
+                    void* stream);
+
+/* ------------------------------------------------------------------ aggregation
+ * weighted sum of client tensors into dst, in message order, one fmaf per message per element:
+ *   init_mode 0: dst = dst * beta   (avg_parameters' inertia, nodes.py:1158-1159;
+ *                                   FedOptServer.update's betas[0], _fedopt.py:203)
+ *   init_mode 1: dst = 0            (update_gradients, nodes.py:1173-1174)
+ *   init_mode 2: dst unchanged      (add_parameters, nodes.py:1131-1132)
+ *   then for m in 0..n_src-1: dst = fmaf(weights[m], srcs[m][i], dst)   (nodes.py:1132, 1178; _fedopt.py:204-208)
+ * srcs and weights are HOST arrays of device pointers / fp32 weights (n_src >= 0). */
+int flc_weighted_sum(const float* const* srcs, const float* weights, int n_src, int64_t n, int init_mode,
+                     float beta, float* dst, void* stream);
+/* the rest of FedOptServer.update after the delta average (_fedopt.py:212-265):
+ *   avg:     theta = fmaf(lr, delta, theta)
+ *   adagrad: v = v + delta^2;                               theta += lr * delta / (sqrt(v) + tau)
+ *   yogi:    v = v - (1-beta2) * delta^2 * sign(v - delta^2); theta += ...
+ *   adam:    v = v * beta2 + (1-beta2) * delta^2;            theta += ... */
+int flc_fedopt_step(float* theta, const float* delta, float* v, int64_t n, int opt, double lr, double beta2,
+                    double tau, void* stream);
+
+/* ------------------------------------------------------------------ measurement
+ * Record HIP events around every launch of the kernel named `kernel_name` (NULL disables);
+ * flc_probe_read synchronises those events and returns the summed duration and launch count, then
+ * clears the record. Used by bench.py for the live roofline figure. */
+int flc_probe_set(const char* kernel_name);
+int flc_probe_read(double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLCODEC_H_ */

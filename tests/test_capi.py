@@ -1,0 +1,77 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/flcodec.h declares, and its
+host-side logic (compat RNG, argument validation) is right.  No GPU compute is launched here."""
+
+import ctypes
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+
+from fl_sim_amd import _lib, rng
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "flcodec.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(flc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_abi_version():
+    lib = _lib.load()
+    assert lib.flc_abi_version() == 1
+    assert os.path.isfile(_lib.LIB_PATH)
+
+
+def test_every_header_symbol_is_exported_and_bound():
+    names = header_functions()
+    assert len(names) >= 20
+    lib = _lib.load()
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in flcodec.h but not exported"
+        assert n in _lib.SIGNATURES, f"{n} has no ctypes signature in _lib.py"
+    assert set(_lib.SIGNATURES) == set(names)
+
+
+def test_error_reporting():
+    with pytest.raises(_lib.FlcError, match="levels"):
+        _lib.call("flc_quant_encode", 1, 1, 8, 0, 200, 8, 1, 0, 0, None, 1, None, 1, 1, None)
+    with pytest.raises(_lib.FlcError, match="0 < k < n"):
+        _lib.call("flc_topk_encode", 16, 10, 10, 1, 1, 1, 1, None)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42, 12345])
+@pytest.mark.parametrize("n", [0, 1, 311, 312, 313, 5000])
+def test_python_random_lockstep(seed, n):
+    random.seed(seed)
+    expect = [random.random() for _ in range(n)]
+    after = random.random()
+    random.seed(seed)
+    got = rng.python_random_doubles(n)
+    assert got.tolist() == expect
+    assert random.random() == after
+
+
+@pytest.mark.parametrize("seed", [0, 3, 42])
+@pytest.mark.parametrize("D,K", [(1, 1), (7, 3), (100, 10), (4097, 41), (1000, 1500)])
+def test_numpy_shuffle_lockstep(seed, D, K):
+    np.random.seed(seed)
+    S = np.arange(D)
+    np.random.shuffle(S)
+    expect = S[:K]
+    after = np.random.random_sample()
+    np.random.seed(seed)
+    got = rng.numpy_shuffle_prefix(D, K)
+    assert np.array_equal(got, expect)
+    assert np.random.random_sample() == after
+
+
+def test_workspace_sizes_monotone():
+    a = _lib.size("flc_topk_workspace_size", 1 << 20, 1 << 10)
+    b = _lib.size("flc_topk_workspace_size", 1 << 22, 1 << 12)
+    assert 0 < a < b
+    assert _lib.size("flc_quant_workspace_size", 10, 417482) > 0
+    assert _lib.size("flc_natural_workspace_size", 417482) > 0

@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, smoke, bench. Each GPU step has its own time limit; a crash, abort or
+# timeout (exit status other than 0/1) ends the script before the next GPU step starts.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout-s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+MODE=${1:-all}
+if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
+  step gpu_tests 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+fi
+if [ "$MODE" = all ] || [ "$MODE" = smoke ]; then
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  step bench 600 python bench.py
+fi
