@@ -311,9 +311,14 @@ __global__ __launch_bounds__(kThreads) void quant_encode_kernel(
     const int valid = e0 >= n ? 0 : (n - e0 < kGroup ? (int)(n - e0) : kGroup);
     float v[kGroup];
     float nr[kGroup];
+    int rl[kGroup];  // row of each element relative to the block's first row
     if (valid > 0) load_group(x, e0, valid, v);
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j) nr[j] = (j < valid) ? norms[rc.at(e0 + j)] : 1.0f;
+    for (int j = 0; j < kGroup; ++j) {
+      const int64_t r = (j < valid) ? rc.at(e0 + j) : rc.row;
+      rl[j] = (int)(r - row_base);
+      nr[j] = (j < valid) ? norms[r] : 1.0f;
+    }
 
     double u[kGroup];
     if (COMPAT) {
@@ -353,7 +358,7 @@ __global__ __launch_bounds__(kThreads) void quant_encode_kernel(
 #pragma unroll
       for (int j = 0; j < kGroup; ++j) {
         if (j < valid && v[j] != 0.0f) {
-          const int64_t r = rc.at(e0 + j) - row_base;
+          const int r = rl[j];
           if (r < kRowSlots) atomicAdd(&s_nnz[r], 1ull);
           else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r + row_base]), 1ull);
         }

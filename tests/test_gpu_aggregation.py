@@ -63,11 +63,15 @@ def test_fedopt_update_matches_reference(tag, shapes, opt, lr, betas, tau):
     agg_ref.fedopt_update(p2, d2, v2, msgs, opt, lr, betas, tau)
     exp_v, got_v = _flat(v2), _flat(v_d)
     exp_t = _flat(p2)
-    # torch's scalar tail loop (n % 32 elements per tensor) may be compiled with FMA contraction
+    theta0 = _flat([p.data for p in make_model(shapes, 1).parameters()])
+    # v: bit-exact, or 1 ulp where torch's scalar tail loop may contract to an fma
     ulp_v = np.abs(exp_v.view(np.int32).astype(np.int64) - got_v.view(np.int32).astype(np.int64))
-    ulp_t = np.abs(exp_t.view(np.int32).astype(np.int64) - got.view(np.int32).astype(np.int64))
-    assert ulp_v.max() <= 1 and ulp_t.max() <= 1
-    assert (ulp_v > 0).mean() < 0.01 and (ulp_t > 0).mean() < 0.01
+    assert ulp_v.max() <= 1 and (ulp_v > 0).mean() < 0.01
+    # theta: torch's CPU vectorised sqrt is not correctly rounded (SLEEF u05) while the kernel's is IEEE,
+    # so the update lr*d/(sqrt(v)+tau) may differ in its last bit: tolerance 1e-6 of the update + 1 ulp
+    upd = np.abs(exp_t.astype(np.float64) - theta0)
+    err = np.abs(exp_t.astype(np.float64) - got.astype(np.float64))
+    assert np.all(err <= 1e-6 * upd + np.spacing(np.abs(exp_t)))
 
 
 @pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])

@@ -17,7 +17,7 @@ step() {  # step <name> <timeout-s> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step gpu_tests 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  step gpu_tests 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-}
 fi
 if [ "$MODE" = all ] || [ "$MODE" = smoke ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
