@@ -5,8 +5,8 @@
 //   norms[rows] fp32 + a flat packed code stream, BITS (2/4/8) bits per element, element i of the
 //   flattened batch at bit offset i*BITS (little-endian), code = sign << (BITS-1) | level.
 // Kernels (all HBM-streaming, no MFMA):
-//   quant_norm     per-row max|x| (exact) or fp64 sum of squares; partials per block, the last block
-//                  of each row (arrival ticket) folds them in a fixed order -> deterministic.
+//   quant_norm     per-row max|x| (exact) or fp64 sum of squares; one partial per block, folded per
+//                  row in a fixed order by quant_norm_fold -> deterministic.
 //                  algorithmic bytes: 4 per element read.
 //   quant_count    compat mode only: consumers (x != 0) per encode chunk, then one-block scan.
 //   quant_encode   per element: y = fp32(|x| / norm), bracket [lv(s), lv(s+1)] found in fp64,
@@ -36,7 +36,6 @@ constexpr int kRowSlots = 16;              // per-block LDS nnz slots
 
 struct QuantWs {
   unsigned long long* partials;  // [rows * kNormMaxParts]
-  unsigned* tickets;             // [rows]
   int* chunk_counts;             // [nblocks]  (compat)
   long long* chunk_offsets;      // [nblocks]  (compat)
 };
@@ -45,7 +44,6 @@ QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* nee
   Carver c(ws, bytes);
   QuantWs w;
   w.partials = c.take<unsigned long long>((size_t)rows * kNormMaxParts);
-  w.tickets = c.take<unsigned>((size_t)rows);
   w.chunk_counts = c.take<int>((size_t)nblocks);
   w.chunk_offsets = c.take<long long>((size_t)nblocks);
   *need = c.off;
@@ -58,9 +56,8 @@ QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* nee
 template <int NORM>
 __global__ __launch_bounds__(kThreads) void quant_norm_kernel(const float* __restrict__ x, int64_t d,
                                                               int parts, int64_t chunk, int vec_ok,
-                                                              QuantWs ws, float* __restrict__ norms) {
+                                                              QuantWs ws) {
   __shared__ unsigned long long s_red[kNW];
-  __shared__ int s_last;
   const int row = blockIdx.y, part = blockIdx.x;
   const float* xr = x + (int64_t)row * d;
   const int64_t lo = (int64_t)part * chunk;
@@ -115,34 +112,27 @@ __global__ __launch_bounds__(kThreads) void quant_norm_kernel(const float* __res
     part_bits = s_red[0];
   }
 
-  if (threadIdx.x == 0) {
-    st_sc1(&ws.partials[(int64_t)row * kNormMaxParts + part], part_bits);
-    const unsigned t = arrive(&ws.tickets[row]);
-    s_last = (t == (unsigned)parts - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  acquire_agent();
-  __syncthreads();
-  // last block of this row: fold the partials in a fixed order
-  if (threadIdx.x < kWave) {
-    const int lane = threadIdx.x;
-    if (NORM == FLC_NORM_INF) {
-      uint32_t m = 0;
-      for (int p = lane; p < parts; p += kWave) {
-        const uint32_t v = (uint32_t)ld_sc1(&ws.partials[(int64_t)row * kNormMaxParts + p]);
-        m = v > m ? v : m;
-      }
-      m = wave_max_u32(m);
-      if (lane == 0) norms[row] = __uint_as_float(m);
-    } else {
-      double s = 0.0;
-      for (int p = lane; p < parts; p += kWave)
-        s += __longlong_as_double(ld_sc1(&ws.partials[(int64_t)row * kNormMaxParts + p]));
-      s = wave_sum(s);
-      if (lane == 0) norms[row] = (float)sqrt(s);
+  if (threadIdx.x == 0) ws.partials[(int64_t)row * kNormMaxParts + part] = part_bits;
+}
+
+// fold the per-block partials of each row in a fixed order (deterministic), one wave per row
+template <int NORM>
+__global__ __launch_bounds__(kWave) void quant_norm_fold_kernel(int parts, QuantWs ws, float* __restrict__ norms) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const unsigned long long* pr = ws.partials + (int64_t)row * kNormMaxParts;
+  if (NORM == FLC_NORM_INF) {
+    uint32_t m = 0;
+    for (int p = lane; p < parts; p += kWave) {
+      const uint32_t v = (uint32_t)pr[p];
+      m = v > m ? v : m;
     }
-    if (lane == 0) st_sc1(&ws.tickets[row], 0u);  // self-reset for the next call
+    m = wave_max_u32(m);
+    if (lane == 0) norms[row] = __uint_as_float(m);
+  } else {
+    double acc = 0.0;
+    for (int p = lane; p < parts; p += kWave) acc += __longlong_as_double(pr[p]);
+    acc = wave_sum(acc);
+    if (lane == 0) norms[row] = (float)sqrt(acc);
   }
 }
 
@@ -483,12 +473,17 @@ int flc_quant_norm(const float* x, int64_t rows, int64_t d, int norm_p, float* n
   parts = cdiv(d, chunk);
   const int vec_ok = (d % 4 == 0) && aligned16(x);
   hipStream_t st = as_stream(stream);
-  if (norm_p == FLC_NORM_INF)
+  if (norm_p == FLC_NORM_INF) {
     FLC_LAUNCH("quant_norm", quant_norm_kernel<FLC_NORM_INF>, dim3((unsigned)parts, (unsigned)rows), dim3(kThreads), 0,
-               st, x, d, (int)parts, chunk, vec_ok, w, norms);
-  else
+               st, x, d, (int)parts, chunk, vec_ok, w);
+    FLC_LAUNCH("quant_norm_fold", quant_norm_fold_kernel<FLC_NORM_INF>, dim3((unsigned)rows), dim3(kWave), 0, st,
+               (int)parts, w, norms);
+  } else {
     FLC_LAUNCH("quant_norm", quant_norm_kernel<FLC_NORM_L2>, dim3((unsigned)parts, (unsigned)rows), dim3(kThreads), 0,
-               st, x, d, (int)parts, chunk, vec_ok, w, norms);
+               st, x, d, (int)parts, chunk, vec_ok, w);
+    FLC_LAUNCH("quant_norm_fold", quant_norm_fold_kernel<FLC_NORM_L2>, dim3((unsigned)rows), dim3(kWave), 0, st,
+               (int)parts, w, norms);
+  }
   return FLC_OK;
 }
 

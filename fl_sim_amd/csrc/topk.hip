@@ -1,28 +1,33 @@
-// topk.hip — exact top-k sparsifier, the stacked top-k -> 8-bit dithering codec, and the sparse
-// decoders, for gfx950 (reference: fl_sim/compressors/compressors.py:284-296 and 327-365).
+// topk.hip — exact top-k selection and the stacked top-k -> 8-bit dithering encoder, for gfx950
+// (reference: fl_sim/compressors/compressors.py:293-296 and 327-365).
 //
 // Selection contract (compressors.py:294-295, `out[np.argsort(out)[:-K]] = 0`): keep the k largest
 // *signed* values; -0 == +0; NaN is largest; among elements equal to the k-th largest value the
 // highest indices are kept (stable ascending argsort order; the reference's own argsort is unstable,
 // so any tie choice satisfies it — see DESIGN.md).
 //
-// Pipeline (one HBM read of x; every later pass touches only the ~1.2 k candidates):
-//   topk_sample   1 block: 32 K strided keys -> LDS radix select -> candidate floor t_lo, chosen so
-//                 that count(key >= t_lo) ~ k + 4 sigma with high probability.
-//   topk_filter   one streaming read of x: each wave owns a contiguous run of x and appends its
-//                 candidates (key >= t_lo) in index order to a private staging region (ballot/mbcnt
-//                 compaction, no atomics, no inter-wave sync).  Algorithmic bytes 4/element.
-//   topk_scan     1 block: region offsets, candidate count C, max key; C < k -> fallback mode in which
-//                 every later pass reads x itself instead of the candidate list (always correct).
-//   topk_round x3 radix select (11/11/10-bit digits) over the candidates; LDS histograms, global
-//                 atomics, XCD-sharded last-arriver picks the digit.  Round 1 also gathers the staged
-//                 regions into one ordered candidate array.
-//   topk_count    per-block strict/tie counts, last arriver scans them.
-//   topk_compact  ordered compaction of the kept set into idx[k] / val[k] (or, stacked, into
-//                 idx[k] / codes[k] with the dithering fused in: the norm of the kept set is
-//                 max(|max|, |k-th largest|), known before compaction).
-//   sparse_decode dense output tile by tile: 64-ary wave search of the tile's slice of idx, LDS tile
-//                 zero-fill + scatter, 16-B streaming stores.  Algorithmic bytes 4/element + 5..8/kept.
+// Pipeline: ONE streaming read of x; every later pass touches only the ~1.2 k candidates.
+//   sample_gather  128 blocks: 32 K strided keys of x (order-preserving uint32 keys).
+//   sample_select  1 block, keys in registers: radix select with range-adaptive digits over
+//                  [min, max] of the sample -> candidate floor t_lo with count(key >= t_lo) ~ k + 4 sigma
+//                  (k/n = 1 %: ~1.22 k candidates).
+//   filter         the HBM pass: each wave owns a contiguous run of x and appends its candidates in
+//                  index order to a private staging region (ballot/popcount compaction: no atomics,
+//                  no inter-wave sync).  Algorithmic bytes 4 per element.
+//   round x3       radix select over the candidates, 2048 bins per round over the live key range
+//                  (round 1: [t_lo, max key] -> 3 rounds always resolve the exact threshold).  Round 1
+//                  also scans the region counts in LDS (every block; no separate scan launch) and
+//                  gathers the staged regions into one ordered SoA candidate array.  C < k switches
+//                  every later kernel to "fallback" mode, in which they read x itself (always correct).
+//                  LDS histograms with wave-aggregated atomics (a wave of equal keys = one atomic),
+//                  global atomics, the XCD-sharded last arriving block picks the digit.
+//   count          per-block strict / tie counts of the threshold; the last arriver scans them.
+//   compact        ordered compaction of the kept set into idx[k] / val[k] or, stacked, idx[k] /
+//                  codes[k] with the dithering fused in (the norm of the kept set is
+//                  max(|max key|, |k-th key|), known before compaction).
+// Cross-block hand-offs inside a launch go only through memory-side atomics (histogram adds, arrival
+// tickets, RMW reads by the last arriver) and write-through (sc1) stores, so no L2 write-back fence
+// is needed; everything else crosses a kernel boundary.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -34,59 +39,62 @@
 namespace flc {
 namespace {
 
-constexpr int kSample = 32768;      // sample keys (128 KiB of LDS)
-constexpr int kSampleThreads = 1024;
+constexpr int kSample = 32768;
+constexpr int kSelectThreads = 1024;
+constexpr int kSamplePerThread = kSample / kSelectThreads;  // 32
 constexpr int kThreads = 256;
 constexpr int kNW = kThreads / kWave;
 constexpr int kStep = 1024;         // elements per wave step in the filter (4 x float4 per lane)
-constexpr int kSelBlocks = 256;     // grid of the select / count / compact kernels (multiple of 8)
-constexpr int kHistBins = 2048;
-constexpr int kTile = 8192;         // decode tile (32 KiB of LDS)
+constexpr int kSelBlocks = 1024;    // grid of the round / count / compact kernels (multiple of 8)
+constexpr int kHistBits = 11;
+constexpr int kHistBins = 1 << kHistBits;
 constexpr int kShards = 8;          // XCD shards of the arrival counters
+constexpr int kMaxRegions = 8192;
+constexpr int kRegionsPerThread = kMaxRegions / kThreads;  // 32 (round-1 LDS scan)
 
 struct TopkParams {
-  unsigned t_lo;
-  unsigned fallback;
-  long long C;
+  unsigned t_lo;       // candidate floor (sample)
+  unsigned fallback;   // 1: candidates = all of x
+  long long C;         // candidates
   unsigned maxkey;
-  unsigned prefix;
-  long long rem;
-  unsigned T;
+  unsigned lo;         // select: low end of the live key range
+  int shift;           // select: log2 keys per bin of the next round
+  int done;            // select: threshold resolved
+  unsigned long long width;  // select: keys in the live range [lo, lo + width)
+  long long rem;       // select: rank still to find (from the top) inside the live range
+  unsigned T;          // the k-th largest key
   unsigned err;
-  long long need;
+  long long need;      // elements equal to T that are kept
   long long ties_total;
   long long strict_total;
   long long k;
-  float norm;
 };
 
 struct TopkWs {
   TopkParams* p;
-  unsigned* tickets;          // [4][kShards + 1]
-  unsigned* hist;             // [3][kHistBins]
-  unsigned* region_cnt;       // [R]
-  unsigned* region_max;       // [R]
-  long long* region_off;      // [R + 1]
-  unsigned* blk_strict;       // [kSelBlocks]
-  unsigned* blk_tie;          // [kSelBlocks]
-  long long* blk_strict_off;  // [kSelBlocks]
-  long long* blk_tie_off;     // [kSelBlocks]
-  uint2* cand;                // [cand_cap]  (idx, raw bits), ordered by idx
-  uint2* stage;               // [R * region_cap]
+  unsigned* tickets;            // [4][kShards + 1]: rounds 0..2, count
+  unsigned* hist;               // [3][kHistBins]
+  unsigned* sample;             // [kSample]
+  unsigned* region_cnt;         // [R]
+  unsigned* region_max;         // [R]
+  unsigned long long* blk_cnt;  // [kSelBlocks]  strict << 32 | tie
+  unsigned long long* blk_off;  // [kSelBlocks]
+  unsigned* cand_idx;           // [n]  ordered by index
+  unsigned* cand_raw;           // [n]  raw fp32 bits
+  uint2* stage;                 // [R * region_cap]  (idx, raw) per wave region
   long long region_cap;
-  long long cand_cap;
 };
 
 struct TopkGeom {
   int64_t blocks;      // filter blocks
   int64_t wave_chunk;  // elements per wave region (multiple of kStep)
-  int64_t regions;     // blocks * 4
+  int64_t regions;     // blocks * 4  (<= kMaxRegions)
 };
 
 TopkGeom geometry(int64_t n) {
   TopkGeom g;
   int64_t blocks = cdiv(n, 4 * kStep * 8);  // >= 8 steps per wave
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > kMaxRegions / 4) blocks = kMaxRegions / 4;
   if (blocks < 1) blocks = 1;
   g.wave_chunk = (int64_t)align_up((size_t)cdiv(n, blocks * 4), kStep);
   g.regions = cdiv(n, g.wave_chunk);
@@ -102,16 +110,14 @@ TopkWs carve_topk(void* ws, size_t bytes, int64_t n, size_t* need) {
   w.p = c.take<TopkParams>(1);
   w.tickets = c.take<unsigned>(4 * (kShards + 1));
   w.hist = c.take<unsigned>(3 * kHistBins);
+  w.sample = c.take<unsigned>(kSample);
   w.region_cnt = c.take<unsigned>(g.regions);
   w.region_max = c.take<unsigned>(g.regions);
-  w.region_off = c.take<long long>(g.regions + 1);
-  w.blk_strict = c.take<unsigned>(kSelBlocks);
-  w.blk_tie = c.take<unsigned>(kSelBlocks);
-  w.blk_strict_off = c.take<long long>(kSelBlocks);
-  w.blk_tie_off = c.take<long long>(kSelBlocks);
+  w.blk_cnt = c.take<unsigned long long>(kSelBlocks);
+  w.blk_off = c.take<unsigned long long>(kSelBlocks);
+  w.cand_idx = c.take<unsigned>((size_t)n + 4);
+  w.cand_raw = c.take<unsigned>((size_t)n + 4);
   w.region_cap = g.wave_chunk;
-  w.cand_cap = n;
-  w.cand = c.take<uint2>((size_t)n);
   w.stage = c.take<uint2>((size_t)g.regions * g.wave_chunk);
   *need = c.off;
   return w;
@@ -121,8 +127,8 @@ TopkWs carve_topk(void* ws, size_t bytes, int64_t n, size_t* need) {
 // helpers
 // ------------------------------------------------------------------------------------------------
 
-// One wave: given a histogram h[NB] in LDS and a rank `rem` (1-based, counted from the top),
-// find the bin holding that rank and the rank within it.  Lane 0 writes *digit / *new_rem.
+// One wave: histogram h[NB] (LDS) and a rank `rem` (1-based, from the top) -> the bin holding that
+// rank and the rank inside it.  The lane that finds it writes *digit / *new_rem.
 template <int NB>
 __device__ void wave_select_from_top(const unsigned* h, long long rem, unsigned* digit, long long* new_rem,
                                      unsigned* err) {
@@ -158,8 +164,31 @@ __device__ void wave_select_from_top(const unsigned* h, long long rem, unsigned*
   }
 }
 
-// XCD-sharded last-arriver: returns true in exactly one block, after every block called it.
-// Call from all threads; contains __syncthreads().  Every storing wave must have drained before.
+// LDS histogram add with wave aggregation: when every active lane hits the same bin (ties, narrow
+// key ranges) the wave issues ONE atomic instead of a 64-way conflicting one.
+__device__ __forceinline__ void hist_add(unsigned* h, unsigned bin, bool valid) {
+  const unsigned long long act = __ballot(valid);
+  if (act == 0ull) return;
+  const int first = __ffsll((long long)act) - 1;
+  const unsigned b0 = __shfl(bin, first, kWave);
+  const unsigned long long same = __ballot(valid && bin == b0);
+  if (same == act) {
+    if ((int)(threadIdx.x & (kWave - 1)) == first) atomicAdd(&h[b0], (unsigned)__popcll(act));
+  } else if (valid) {
+    atomicAdd(&h[bin], 1u);
+  }
+}
+
+// shift so that a key range of `width` keys maps onto at most 2^bits bins
+__device__ __forceinline__ int range_shift(unsigned long long width, int bits) {
+  if (width <= 1ull) return 0;
+  const int len = 64 - __clzll((long long)(width - 1ull));
+  return len > bits ? len - bits : 0;
+}
+
+// XCD-sharded last-arriver: true in exactly one block, after every block called it.  Call from all
+// threads (contains __syncthreads()).  Every wave must have drained its atomics / sc1 stores
+// (drain_stores) before; the winner reads the payload with memory-side RMWs (ld_mem).
 __device__ bool last_arriver(unsigned* counters /* kShards + 1 */) {
   __shared__ int s_last;
   __syncthreads();
@@ -168,31 +197,97 @@ __device__ bool last_arriver(unsigned* counters /* kShards + 1 */) {
     const unsigned shard_size = (nb - shard + kShards - 1) / kShards;
     const unsigned active_shards = nb < (unsigned)kShards ? nb : (unsigned)kShards;
     int last = 0;
-    if (arrive(&counters[shard]) == shard_size - 1) {
-      acquire_agent();
-      last = arrive(&counters[kShards]) == active_shards - 1;
-    }
+    if (__hip_atomic_fetch_add(&counters[shard], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == shard_size - 1)
+      last = __hip_atomic_fetch_add(&counters[kShards], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             active_shards - 1;
     s_last = last;
   }
   __syncthreads();
-  if (s_last) {
-    if (threadIdx.x == 0) acquire_agent();
-    __syncthreads();
-  }
   return s_last != 0;
 }
 
+// memory-side reads of words other blocks updated with atomics / sc1 stores in this launch
 __device__ __forceinline__ unsigned ld_mem(unsigned* p) {
   return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ unsigned long long ld_mem(unsigned long long* p) {
+  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// contiguous candidate range of this block (a multiple of 4 long, identical in every select kernel)
+__device__ __forceinline__ void block_range(long long C, long long* v0, long long* v1) {
+  long long per = (C + gridDim.x - 1) / gridDim.x;
+  per = (per + 3) & ~3ll;
+  const long long a = (long long)blockIdx.x * per;
+  *v0 = a < C ? a : C;
+  *v1 = a + per < C ? a + per : C;
+}
+
+// last r in [0, R) with off[r] <= c (off in LDS, nondecreasing, off[R] > c)
+__device__ __forceinline__ int lds_region_search(const unsigned* off, int R, unsigned c) {
+  int lo = 0, hi = R;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (off[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int lds_region_advance(const unsigned* off, int R, int r, unsigned c) {
+  if (off[r + 1] > c) return r;
+  int lo = r + 1, step = 1, hi;
+  for (;;) {
+    hi = lo + step;
+    if (hi >= R) {
+      hi = R;
+      break;
+    }
+    if (off[hi] > c) break;
+    lo = hi;
+    step <<= 1;
+  }
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (off[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// four consecutive candidate keys (raw bits) starting at c0 (a multiple of 4), from x in fallback mode
+__device__ __forceinline__ void load4_raw(const float* __restrict__ x, const TopkWs& w, bool fb, long long c0,
+                                          long long v1, unsigned raw[4]) {
+  if (c0 + 4 <= v1) {
+    if (fb) {
+      const float4 v = *reinterpret_cast<const float4*>(x + c0);
+      raw[0] = __float_as_uint(v.x); raw[1] = __float_as_uint(v.y);
+      raw[2] = __float_as_uint(v.z); raw[3] = __float_as_uint(v.w);
+    } else {
+      const uint4 v = *reinterpret_cast<const uint4*>(w.cand_raw + c0);
+      raw[0] = v.x; raw[1] = v.y; raw[2] = v.z; raw[3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      raw[u] = (c0 + u < v1) ? (fb ? __float_as_uint(x[c0 + u]) : w.cand_raw[c0 + u]) : 0u;
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
-// K0: sample -> candidate floor
+// sample -> candidate floor
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kSampleThreads) void topk_sample_kernel(const float* __restrict__ x, int64_t n, int S,
-                                                                     long long rank_lo, int take_all, TopkWs w) {
-  extern __shared__ __attribute__((aligned(16))) unsigned s_keys[];  // [S]
+__global__ __launch_bounds__(kThreads) void topk_sample_gather_kernel(const float* __restrict__ x, int64_t n, int S,
+                                                                      TopkWs w) {
+  const int j = blockIdx.x * kThreads + threadIdx.x;
+  if (j >= S) return;
+  const int64_t pos = (S == n) ? (int64_t)j : (int64_t)(((double)j + 0.5) * (double)n / (double)S);
+  w.sample[j] = order_key(__float_as_uint(x[pos < n ? pos : n - 1]));
+}
+
+__global__ __launch_bounds__(kSelectThreads) void topk_sample_select_kernel(int S, long long rank_lo, int take_all,
+                                                                            TopkWs w) {
   __shared__ unsigned s_hist[256];
+  __shared__ unsigned s_mm[2][kSelectThreads / kWave];
   __shared__ unsigned s_digit;
   __shared__ long long s_rem;
   __shared__ unsigned s_err;
@@ -200,37 +295,77 @@ __global__ __launch_bounds__(kSampleThreads) void topk_sample_kernel(const float
     if (threadIdx.x == 0) w.p->t_lo = 0u;
     return;
   }
-  for (int j = threadIdx.x; j < S; j += kSampleThreads) {
-    const int64_t pos = (S == n) ? (int64_t)j : (int64_t)(((double)j + 0.5) * (double)n / (double)S);
-    s_keys[j] = order_key(__float_as_uint(x[pos < n ? pos : n - 1]));
+  unsigned keys[kSamplePerThread];
+  unsigned kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+  for (int i = 0; i < kSamplePerThread; ++i) {
+    const int j = threadIdx.x + i * kSelectThreads;
+    keys[i] = j < S ? w.sample[j] : 0u;
+    if (j < S) {
+      kmin = keys[i] < kmin ? keys[i] : kmin;
+      kmax = keys[i] > kmax ? keys[i] : kmax;
+    }
   }
-  unsigned prefix = 0;
-  long long rem = rank_lo;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned a = __shfl_xor(kmin, o, kWave), b = __shfl_xor(kmax, o, kWave);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_mm[0][threadIdx.x >> 6] = kmin;
+    s_mm[1][threadIdx.x >> 6] = kmax;
+  }
   if (threadIdx.x == 0) s_err = 0;
-  for (int pass = 0; pass < 4; ++pass) {
-    const int shift = 24 - 8 * pass;
+  __syncthreads();
+  kmin = 0xffffffffu;
+  kmax = 0u;
+  for (int i = 0; i < kSelectThreads / kWave; ++i) {
+    kmin = s_mm[0][i] < kmin ? s_mm[0][i] : kmin;
+    kmax = s_mm[1][i] > kmax ? s_mm[1][i] : kmax;
+  }
+  unsigned lo = kmin;
+  unsigned long long width = (unsigned long long)kmax - kmin + 1ull;  // live range [lo, lo + width)
+  int shift = range_shift(width, 8);
+  long long rem = rank_lo;
+  for (int pass = 0; pass < 5; ++pass) {
     if (threadIdx.x < 256) s_hist[threadIdx.x] = 0;
     __syncthreads();
-    for (int j = threadIdx.x; j < S; j += kSampleThreads) {
-      const unsigned key = s_keys[j];
-      if (pass == 0 || (key >> (shift + 8)) == prefix) atomicAdd(&s_hist[(key >> shift) & 255u], 1u);
+#pragma unroll
+    for (int i = 0; i < kSamplePerThread; ++i) {
+      const int j = threadIdx.x + i * kSelectThreads;
+      const unsigned key = keys[i];
+      const unsigned long long rel = (unsigned long long)key - lo;
+      const bool valid = j < S && key >= lo && rel < width;
+      hist_add(s_hist, (unsigned)(rel >> shift), valid);
     }
     __syncthreads();
     if (threadIdx.x < kWave) wave_select_from_top<256>(s_hist, rem, &s_digit, &s_rem, &s_err);
     __syncthreads();
-    prefix = (prefix << 8) | s_digit;
+    lo += s_digit << shift;
     rem = s_rem;
     __syncthreads();
+    if (shift == 0) break;
+    width = 1ull << shift;
+    shift = shift > 8 ? shift - 8 : 0;
   }
-  if (threadIdx.x == 0) w.p->t_lo = prefix;
+  if (threadIdx.x == 0) w.p->t_lo = lo;
 }
 
 // ------------------------------------------------------------------------------------------------
-// K1: streaming filter
+// streaming filter (the one HBM pass over x)
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void topk_filter_kernel(const float* __restrict__ x, int64_t n,
                                                                int64_t wave_chunk, TopkWs w) {
   const unsigned t_lo = w.p->t_lo;
+  if (blockIdx.x == 0) {  // reset the select state of this call (read by the next kernels)
+    for (int i = threadIdx.x; i < 3 * kHistBins; i += kThreads) w.hist[i] = 0u;
+    if (threadIdx.x < 4 * (kShards + 1)) w.tickets[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) {
+      w.p->done = 0;
+      w.p->err = 0u;
+    }
+  }
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t r = (int64_t)blockIdx.x * kNW + (threadIdx.x >> 6);
   const int64_t e_begin = r * wave_chunk;
@@ -267,8 +402,7 @@ __global__ __launch_bounds__(kThreads) void topk_filter_kernel(const float* __re
       m = in3 && k3 > m ? k3 : m;
       mx = m > mx ? m : mx;
       const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
-      const unsigned any = (unsigned)((m0 | m1 | m2 | m3) != 0ull);
-      if (any) {
+      if ((m0 | m1 | m2 | m3) != 0ull) {
         unsigned pos = cnt + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
         if (f0) out[pos++] = make_uint2((unsigned)(e + 0), b0);
         if (f1) out[pos++] = make_uint2((unsigned)(e + 1), b1);
@@ -286,363 +420,278 @@ __global__ __launch_bounds__(kThreads) void topk_filter_kernel(const float* __re
 }
 
 // ------------------------------------------------------------------------------------------------
-// K1.5: region scan (1 block)
+// radix-select rounds over the candidates: 2048 bins over the live key range per round
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void topk_scan_kernel(int64_t regions, int64_t n, long long k, TopkWs w) {
-  __shared__ long long s_red[16];
-  __shared__ unsigned s_max[16];
-  long long running = 0;
-  unsigned mx = 0;
-  for (int64_t base = 0; base < regions; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const long long v = i < regions ? (long long)w.region_cnt[i] : 0;
-    if (i < regions) mx = w.region_max[i] > mx ? w.region_max[i] : mx;
-    long long tot;
-    const long long ex = block_excl_scan<long long, 16>(v, s_red, &tot);
-    if (i < regions) w.region_off[i] = running + ex;
-    running += tot;
-  }
-  mx = wave_max_u32(mx);
-  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = mx;
-  // zero the select state (histograms, tickets) for this call
-  for (int i = threadIdx.x; i < 3 * kHistBins; i += 1024) w.hist[i] = 0u;
-  if (threadIdx.x < 4 * (kShards + 1)) w.tickets[threadIdx.x] = 0u;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned m = 0;
-    for (int i = 0; i < 16; ++i) m = s_max[i] > m ? s_max[i] : m;
-    w.region_off[regions] = running;
-    const unsigned fb = running < k ? 1u : 0u;
-    w.p->fallback = fb;
-    w.p->C = fb ? (long long)n : running;
-    w.p->maxkey = m;
-    w.p->prefix = 0u;
-    w.p->rem = k;
-    w.p->k = k;
-    w.p->err = 0u;
-  }
-}
-
-
-// 64-ary search by one wave: last r in [0, R) with off[r] <= v (off nondecreasing, off[R] > v)
-__device__ long long wave_region_search(const long long* __restrict__ off, long long R, long long v) {
-  const int lane = threadIdx.x & (kWave - 1);
-  long long lo = 0, hi = R;
-  while (hi - lo > 1) {
-    const long long stride = (hi - lo + kWave - 1) / kWave;
-    const long long p = lo + (long long)lane * stride;
-    const bool le = p < hi && off[p] <= v;
-    const int cnt = __popcll(__ballot(le));
-    const long long nlo = lo + (long long)(cnt - 1) * stride;
-    hi = nlo + stride < hi ? nlo + stride : hi;
-    lo = nlo;
-  }
-  return lo;
-}
-
-// 64-ary lower bound by one wave: first i in [0, n) with a[i] >= key (n if none), a ascending
-__device__ long long wave_lower_bound(const int* __restrict__ a, long long n, int key) {
-  const int lane = threadIdx.x & (kWave - 1);
-  long long lo = 0, hi = n;  // a[i] < key for i < lo; a[hi] >= key or hi == n
-  while (hi - lo > kWave) {
-    const long long stride = (hi - lo + kWave - 1) / kWave;
-    const long long p = lo + (long long)lane * stride;
-    const bool lt = p < hi && a[p] < key;
-    const int cnt = __popcll(__ballot(lt));  // probes below key form a prefix of the lanes
-    const long long nlo = cnt > 0 ? lo + (long long)(cnt - 1) * stride + 1 : lo;
-    const long long nhi = lo + (long long)cnt * stride < hi ? lo + (long long)cnt * stride : hi;
-    lo = nlo;
-    hi = nhi;
-  }
-  const long long p = lo + lane;
-  const bool lt = p < hi && a[p] < key;
-  return lo + __popcll(__ballot(lt));
-}
-
-// ------------------------------------------------------------------------------------------------
-// K2: radix-select rounds over the candidates (3 x {11, 11, 10} bits)
-// ------------------------------------------------------------------------------------------------
-template <int SHIFT, int BITS, bool FIRST, bool LAST>
-__global__ __launch_bounds__(kThreads) void topk_round_kernel(const float* __restrict__ x, TopkWs w, int round,
-                                                              long long regions) {
+template <bool FIRST>
+__global__ __launch_bounds__(kThreads) void topk_round_kernel(const float* __restrict__ x, TopkWs w, int round, int R,
+                                                              long long k, int64_t n) {
   __shared__ unsigned s_hist[kHistBins];
-  __shared__ long long s_r0;
+  __shared__ unsigned s_off[FIRST ? kMaxRegions + 1 : 1];
+  __shared__ unsigned long long s_red[kNW];
+  __shared__ unsigned s_mx[kNW];
   __shared__ unsigned s_digit;
   __shared__ long long s_rem;
-  constexpr unsigned kMask = (1u << BITS) - 1u;
-  const long long C = w.p->C;
-  const bool fb = w.p->fallback != 0;
-  const unsigned prefix = FIRST ? 0u : w.p->prefix;
-  const long long per = (C + gridDim.x - 1) / gridDim.x;
-  const long long v0 = (long long)blockIdx.x * per;
-  const long long v1 = v0 + per < C ? v0 + per : C;
-  for (int i = threadIdx.x; i < (1 << BITS); i += kThreads) s_hist[i] = 0u;
-  if (FIRST && !fb && threadIdx.x < kWave && v0 < v1) {
-    const long long r0 = wave_region_search(w.region_off, regions, v0);
-    if (threadIdx.x == 0) s_r0 = r0;
+  long long C, rem = 0;
+  bool fb;
+  unsigned lo, maxkey = 0;
+  unsigned long long width;
+  int shift;
+  if (FIRST) {
+    // region scan in LDS, redone by every block (32 KiB of L2-resident counts): offsets, C, max key
+    const int r0 = threadIdx.x * kRegionsPerThread;
+    unsigned loc[kRegionsPerThread];
+    unsigned long long sum = 0;
+    unsigned mx = 0;
+#pragma unroll
+    for (int i = 0; i < kRegionsPerThread; i += 4) {
+      if (r0 + i < R) {  // R is a multiple of 4
+        const uint4 c = *reinterpret_cast<const uint4*>(w.region_cnt + r0 + i);
+        const uint4 m = *reinterpret_cast<const uint4*>(w.region_max + r0 + i);
+        loc[i] = c.x; loc[i + 1] = c.y; loc[i + 2] = c.z; loc[i + 3] = c.w;
+        mx = max(mx, max(max(m.x, m.y), max(m.z, m.w)));
+      } else {
+        loc[i] = loc[i + 1] = loc[i + 2] = loc[i + 3] = 0u;
+      }
+      sum += (unsigned long long)loc[i] + loc[i + 1] + loc[i + 2] + loc[i + 3];
+    }
+    unsigned long long tot;
+    unsigned long long run = block_excl_scan<unsigned long long, kNW>(sum, s_red, &tot);
+#pragma unroll
+    for (int i = 0; i < kRegionsPerThread; ++i) {
+      if (r0 + i < R) s_off[r0 + i] = (unsigned)run;
+      run += loc[i];
+    }
+    mx = wave_max_u32(mx);
+    if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = mx;
+    if (threadIdx.x == 0) s_off[R] = (unsigned)tot;
+    __syncthreads();
+    for (int i = 0; i < kNW; ++i) maxkey = s_mx[i] > maxkey ? s_mx[i] : maxkey;
+    fb = (long long)tot < k;
+    C = fb ? (long long)n : (long long)tot;
+    lo = fb ? 0u : w.p->t_lo;
+    width = (unsigned long long)maxkey - lo + 1ull;
+    shift = range_shift(width, kHistBits);
+    rem = k;
+  } else {
+    if (w.p->done) return;
+    C = w.p->C;
+    fb = w.p->fallback != 0;
+    lo = w.p->lo;
+    width = w.p->width;
+    shift = w.p->shift;
   }
+  long long v0, v1;
+  block_range(C, &v0, &v1);
+  for (int i = threadIdx.x; i < kHistBins; i += kThreads) s_hist[i] = 0u;
   __syncthreads();
 
-  if (fb) {
-    for (long long c = v0 + threadIdx.x; c < v1; c += kThreads) {
-      const unsigned key = order_key(__float_as_uint(x[c]));
-      if (FIRST || ((unsigned long long)key >> (SHIFT + BITS)) == prefix) atomicAdd(&s_hist[(key >> SHIFT) & kMask], 1u);
+  int r = (FIRST && !fb && v0 + 4 * (long long)threadIdx.x < v1)
+              ? lds_region_search(s_off, R, (unsigned)(v0 + 4 * threadIdx.x)) : 0;
+  for (long long c0 = v0 + 4 * threadIdx.x; c0 < v1; c0 += 4 * kThreads) {
+    unsigned raw[4];
+    if (FIRST && !fb) {
+      unsigned id[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long c = c0 + u;
+        if (c < v1) {
+          r = lds_region_advance(s_off, R, r, (unsigned)c);
+          const uint2 e = w.stage[(long long)r * w.region_cap + (c - s_off[r])];
+          id[u] = e.x;
+          raw[u] = e.y;
+        } else {
+          id[u] = 0u;
+          raw[u] = 0u;
+        }
+      }
+      if (c0 + 4 <= v1) {
+        *reinterpret_cast<uint4*>(w.cand_idx + c0) = make_uint4(id[0], id[1], id[2], id[3]);
+        *reinterpret_cast<uint4*>(w.cand_raw + c0) = make_uint4(raw[0], raw[1], raw[2], raw[3]);
+      } else {
+        for (int u = 0; u < 4; ++u)
+          if (c0 + u < v1) {
+            w.cand_idx[c0 + u] = id[u];
+            w.cand_raw[c0 + u] = raw[u];
+          }
+      }
+    } else {
+      load4_raw(x, w, fb, c0, v1, raw);
     }
-  } else if (FIRST) {
-    long long r = s_r0;
-    for (long long c = v0 + threadIdx.x; c < v1; c += kThreads) {
-      while (w.region_off[r + 1] <= c) ++r;
-      const uint2 e = w.stage[r * w.region_cap + (c - w.region_off[r])];
-      w.cand[c] = e;
-      const unsigned key = order_key(e.y);
-      atomicAdd(&s_hist[(key >> SHIFT) & kMask], 1u);
-    }
-  } else {
-    for (long long c = v0 + threadIdx.x; c < v1; c += kThreads) {
-      const unsigned key = order_key(w.cand[c].y);
-      if (((unsigned long long)key >> (SHIFT + BITS)) == prefix) atomicAdd(&s_hist[(key >> SHIFT) & kMask], 1u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned key = order_key(raw[u]);
+      const unsigned long long rel = (unsigned long long)key - lo;
+      const bool valid = c0 + u < v1 && key >= lo && rel < width;
+      hist_add(s_hist, (unsigned)(rel >> shift), valid);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < (1 << BITS); i += kThreads)
+  for (int i = threadIdx.x; i < kHistBins; i += kThreads)
     if (s_hist[i]) atomicAdd(&w.hist[round * kHistBins + i], s_hist[i]);
   drain_stores();
   if (!last_arriver(&w.tickets[round * (kShards + 1)])) return;
-  for (int i = threadIdx.x; i < (1 << BITS); i += kThreads) s_hist[i] = ld_mem(&w.hist[round * kHistBins + i]);
+  for (int i = threadIdx.x; i < kHistBins; i += kThreads) s_hist[i] = ld_mem(&w.hist[round * kHistBins + i]);
+  if (!FIRST && threadIdx.x == 0) s_rem = w.p->rem;
   __syncthreads();
-  if (threadIdx.x < kWave) wave_select_from_top<(1 << BITS)>(s_hist, w.p->rem, &s_digit, &s_rem, &w.p->err);
+  if (!FIRST) rem = s_rem;
+  __syncthreads();
+  if (threadIdx.x < kWave) wave_select_from_top<kHistBins>(s_hist, rem, &s_digit, &s_rem, &w.p->err);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned np = (prefix << BITS) | s_digit;
-    w.p->prefix = np;
-    w.p->rem = s_rem;
-    if (LAST) {
-      w.p->T = np;
+    const unsigned nlo = lo + (s_digit << shift);
+    if (FIRST) {
+      w.p->C = C;
+      w.p->fallback = fb ? 1u : 0u;
+      w.p->maxkey = maxkey;
+      w.p->k = k;
+    }
+    if (shift == 0) {
+      w.p->T = nlo;
       w.p->need = s_rem;
-      w.p->ties_total = s_hist[s_digit];
+      w.p->done = 1;
+    } else {
+      w.p->lo = nlo;
+      w.p->width = 1ull << shift;
+      w.p->shift = shift > kHistBits ? shift - kHistBits : 0;
+      w.p->rem = s_rem;
     }
   }
 }
 
-__device__ __forceinline__ uint2 source_entry(const float* __restrict__ x, const TopkWs& w, bool fb, long long c) {
-  if (fb) return make_uint2((unsigned)c, __float_as_uint(x[c]));
-  return w.cand[c];
-}
-
 // ------------------------------------------------------------------------------------------------
-// K3: per-block strict / tie counts + scan by the last arriver
+// per-block strict / tie counts + scan by the last arriver
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void topk_count_kernel(const float* __restrict__ x, TopkWs w) {
-  __shared__ long long s_red[kNW];
+  __shared__ unsigned long long s_red[kNW];
   const long long C = w.p->C;
   const bool fb = w.p->fallback != 0;
   const unsigned T = w.p->T;
-  const long long per = (C + gridDim.x - 1) / gridDim.x;
-  const long long v0 = (long long)blockIdx.x * per;
-  const long long v1 = v0 + per < C ? v0 + per : C;
-  long long st = 0, ti = 0;
-  for (long long c = v0 + threadIdx.x; c < v1; c += kThreads) {
-    const unsigned key = order_key(source_entry(x, w, fb, c).y);
-    st += key > T;
-    ti += key == T;
+  long long v0, v1;
+  block_range(C, &v0, &v1);
+  unsigned long long cnt = 0;  // strict << 32 | tie
+  for (long long c0 = v0 + 4 * threadIdx.x; c0 < v1; c0 += 4 * kThreads) {
+    unsigned raw[4];
+    load4_raw(x, w, fb, c0, v1, raw);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned key = order_key(raw[u]);
+      if (c0 + u < v1) cnt += (key > T ? (1ull << 32) : 0ull) + (key == T ? 1ull : 0ull);
+    }
   }
-  // pack both counts in one scan value: strict in the high 32 bits (counts < 2^31)
-  const long long both = block_sum<long long, kNW>((st << 32) | ti, s_red);
-  if (threadIdx.x == 0) {
-    st_sc1(&w.blk_strict[blockIdx.x], (unsigned)(both >> 32));
-    st_sc1(&w.blk_tie[blockIdx.x], (unsigned)(both & 0xffffffffll));
-  }
+  const unsigned long long both = block_sum<unsigned long long, kNW>(cnt, s_red);
+  if (threadIdx.x == 0) st_sc1(&w.blk_cnt[blockIdx.x], both);
   drain_stores();
   if (!last_arriver(&w.tickets[3 * (kShards + 1)])) return;
-  // gridDim.x == kSelBlocks == kThreads: one block per thread
-  const long long vs = threadIdx.x < (int)gridDim.x ? (long long)ld_mem(&w.blk_strict[threadIdx.x]) : 0;
-  const long long vt = threadIdx.x < (int)gridDim.x ? (long long)ld_mem(&w.blk_tie[threadIdx.x]) : 0;
-  long long tot_s, tot_t;
-  const long long es = block_excl_scan<long long, kNW>(vs, s_red, &tot_s);
-  const long long et = block_excl_scan<long long, kNW>(vt, s_red, &tot_t);
-  if (threadIdx.x < (int)gridDim.x) {
-    w.blk_strict_off[threadIdx.x] = es;
-    w.blk_tie_off[threadIdx.x] = et;
+  // blocks 4t .. 4t+3 per thread (gridDim.x == kSelBlocks == 4 * kThreads)
+  unsigned long long v[4], s = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int b = 4 * threadIdx.x + u;
+    v[u] = b < (int)gridDim.x ? ld_mem(&w.blk_cnt[b]) : 0ull;
+    s += v[u];
+  }
+  unsigned long long tot;
+  unsigned long long run = block_excl_scan<unsigned long long, kNW>(s, s_red, &tot);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int b = 4 * threadIdx.x + u;
+    if (b < (int)gridDim.x) w.blk_off[b] = run;
+    run += v[u];
   }
   if (threadIdx.x == 0) {
-    w.p->strict_total = tot_s;
-    w.p->ties_total = tot_t;
-    if (tot_s + w.p->need != w.p->k || w.p->need > tot_t) w.p->err |= 2u;
+    const long long st = (long long)(tot >> 32), ti = (long long)(tot & 0xffffffffull);
+    w.p->strict_total = st;
+    w.p->ties_total = ti;
+    if (st + w.p->need != w.p->k || w.p->need > ti) w.p->err |= 2u;
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// K4: ordered compaction of the kept set (plain top-k, or fused 8-bit dithering for the stack)
+// ordered compaction of the kept set (plain top-k, or the stacked codec with fused dithering)
 // ------------------------------------------------------------------------------------------------
 template <bool STACKED>
 __global__ __launch_bounds__(kThreads) void topk_compact_kernel(const float* __restrict__ x, TopkWs w,
                                                                 int* __restrict__ idx_out, float* __restrict__ val_out,
                                                                 uint8_t* __restrict__ code_out, float* __restrict__ norm_out,
                                                                 int levels, double step, uint64_t seed, uint64_t counter) {
-  __shared__ unsigned s_ws[2][kNW], s_wt[2][kNW];
+  __shared__ unsigned long long s_red[kNW];
   const long long C = w.p->C;
   const bool fb = w.p->fallback != 0;
   const unsigned T = w.p->T;
   const long long skip = w.p->ties_total - w.p->need;  // ties with rank < skip are dropped
   const long long kk = w.p->k;
-  const long long per = (C + gridDim.x - 1) / gridDim.x;
-  const long long v0 = (long long)blockIdx.x * per;
-  const long long v1 = v0 + per < C ? v0 + per : C;
-  long long run_s = w.blk_strict_off[blockIdx.x];
-  long long run_t = w.blk_tie_off[blockIdx.x];
+  long long v0, v1;
+  block_range(C, &v0, &v1);
+  const unsigned long long off = w.blk_off[blockIdx.x];
+  long long run_s = (long long)(off >> 32), run_t = (long long)(off & 0xffffffffull);
   float nrm = 0.0f;
   if (STACKED) {
     const float a = fabsf(key_value(w.p->maxkey)), b = fabsf(key_value(T));
     nrm = (isnan(a) || isnan(b)) ? __uint_as_float(0x7fc00000u) : (a > b ? a : b);
     if (blockIdx.x == 0 && threadIdx.x == 0) *norm_out = nrm;
   }
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  int par = 0;
-  for (long long base = v0; base < v1; base += kThreads, par ^= 1) {
-    const long long c = base + threadIdx.x;
-    const bool in = c < v1;
-    const uint2 e = in ? source_entry(x, w, fb, c) : make_uint2(0u, 0u);
-    const unsigned key = order_key(e.y);
-    const bool is_s = in && key > T, is_t = in && key == T;
-    const unsigned long long ms = __ballot(is_s), mt = __ballot(is_t);
-    if (lane == 0) {
-      s_ws[par][wid] = (unsigned)__popcll(ms);
-      s_wt[par][wid] = (unsigned)__popcll(mt);
-    }
-    __syncthreads();
-    long long ws_before = 0, wt_before = 0, tot_s = 0, tot_t = 0;
+  for (long long base = v0; base < v1; base += 4 * kThreads) {
+    const long long c0 = base + 4 * threadIdx.x;
+    unsigned raw[4], id[4];
+    load4_raw(x, w, fb, c0, v1, raw);
+    if (fb) {
 #pragma unroll
-    for (int q = 0; q < kNW; ++q) {
-      ws_before += q < wid ? s_ws[par][q] : 0u;
-      wt_before += q < wid ? s_wt[par][q] : 0u;
-      tot_s += s_ws[par][q];
-      tot_t += s_wt[par][q];
-    }
-    const long long s_before = run_s + ws_before + __popcll(ms & lt);
-    const long long t_before = run_t + wt_before + __popcll(mt & lt);
-    const bool keep = is_s || (is_t && t_before >= skip);
-    const long long pos = s_before + (t_before > skip ? t_before - skip : 0);
-    if (keep && pos >= 0 && pos < kk) {
-      idx_out[pos] = (int)e.x;
-      if (STACKED) {
-        const float v = __uint_as_float(e.y);
-        uint32_t code = 0u;
-        if (v != 0.0f) {
-          if (!(nrm > 0.0f && nrm <= 3.402823466e38f)) {
-            code = 1u;
-          } else {
-            const float y = fabsf(v) / nrm;
-            const int j = level_lower_bound<0>(y, levels, step);
-            const int sl = j > 0 ? j - 1 : 0;
-            const double lo = level_value<0>(sl, levels, step), hi = level_value<0>(sl + 1, levels, step);
-            const double p = ((double)y - hi) / (lo - hi);
-            const U4 r4 = philox_group((uint64_t)e.x >> 2, seed, counter);
-            const double u = u01(pick(r4, (int)(e.x & 3u)));
-            const int lvl = (u < p) ? sl : sl + 1;
-            code = ((e.y >> 31) << 7) | (uint32_t)lvl;
-          }
-        }
-        code_out[pos] = (uint8_t)code;
-      } else {
-        val_out[pos] = __uint_as_float(e.y);
-      }
-    }
-    run_s += tot_s;
-    run_t += tot_t;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// K5: sparse -> dense decode (tile = 8192 outputs, LDS scatter, 16-B stores)
-//   MODE 0: v = scale * val[j];  MODE 1: v = dithering decode of codes[j] (s = levels, norm)
-// ------------------------------------------------------------------------------------------------
-template <int MODE, bool ACC>
-__global__ __launch_bounds__(kThreads) void sparse_decode_kernel(const int* __restrict__ idx, const float* __restrict__ val,
-                                                                 const uint8_t* __restrict__ codes, long long k, float scale,
-                                                                 int levels, double step, const float* __restrict__ norm_ptr,
-                                                                 int64_t n, float weight, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float s_tile[kTile];
-  __shared__ long long s_lo, s_hi;
-  const int64_t t0 = (int64_t)blockIdx.x * kTile;
-  const int64_t t1 = t0 + kTile < n ? t0 + kTile : n;
-  const int wid = threadIdx.x >> 6;
-  if (wid == 0) {
-    const long long lo = wave_lower_bound(idx, k, (int)t0);
-    if (threadIdx.x == 0) s_lo = lo;
-  } else if (wid == 1) {
-    const long long hi = t1 >= n ? k : wave_lower_bound(idx, k, (int)t1);
-    if (threadIdx.x == kWave) s_hi = hi;
-  }
-  float4* tile4 = reinterpret_cast<float4*>(s_tile);
-  for (int i = threadIdx.x; i < kTile / 4; i += kThreads) tile4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-  const long long lo = s_lo, hi = s_hi;
-  float nrm = 0.f;
-  if (MODE == 1) nrm = *norm_ptr;
-  for (long long j = lo + threadIdx.x; j < hi; j += kThreads) {
-    float v;
-    if (MODE == 0) {
-      v = scale * val[j];
+      for (int u = 0; u < 4; ++u) id[u] = (unsigned)(c0 + u);
+    } else if (c0 + 4 <= v1) {
+      const uint4 t = *reinterpret_cast<const uint4*>(w.cand_idx + c0);
+      id[0] = t.x; id[1] = t.y; id[2] = t.z; id[3] = t.w;
     } else {
-      const uint32_t code = codes[j];
-      if (!(nrm > 0.0f && nrm <= 3.402823466e38f)) {
-        v = code == 0u ? 0.0f : __uint_as_float(0x7fc00000u);
-      } else {
-        const float lv = (float)level_value<0>((int)(code & 127u), levels, step);
-        v = ((code >> 7) ? -lv : lv) * nrm;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) id[u] = c0 + u < v1 ? w.cand_idx[c0 + u] : 0u;
+    }
+    bool is_s[4], is_t[4];
+    unsigned long long cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned key = order_key(raw[u]);
+      const bool in = c0 + u < v1;
+      is_s[u] = in && key > T;
+      is_t[u] = in && key == T;
+      cnt += (is_s[u] ? (1ull << 32) : 0ull) + (is_t[u] ? 1ull : 0ull);
+    }
+    unsigned long long tot;
+    const unsigned long long ex = block_excl_scan<unsigned long long, kNW>(cnt, s_red, &tot);
+    long long s_before = run_s + (long long)(ex >> 32), t_before = run_t + (long long)(ex & 0xffffffffull);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool keep = is_s[u] || (is_t[u] && t_before >= skip);
+      const long long pos = s_before + (t_before > skip ? t_before - skip : 0);
+      if (keep && pos >= 0 && pos < kk) {
+        idx_out[pos] = (int)id[u];
+        if (STACKED) {
+          const float v = __uint_as_float(raw[u]);
+          uint32_t code = 0u;
+          if (v != 0.0f) {
+            if (!(nrm > 0.0f && nrm <= 3.402823466e38f)) {
+              code = 1u;
+            } else {
+              const float y = fabsf(v) / nrm;  // compressors.py:344
+              const int j = level_lower_bound<0>(y, levels, step);
+              const int sl = j > 0 ? j - 1 : 0;
+              const double lo = level_value<0>(sl, levels, step), hi = level_value<0>(sl + 1, levels, step);
+              const double p = ((double)y - hi) / (lo - hi);  // compressors.py:348
+              const U4 r4 = philox_group((uint64_t)id[u] >> 2, seed, counter);
+              const double uu = u01(pick(r4, (int)(id[u] & 3u)));
+              const int lvl = (uu < p) ? sl : sl + 1;
+              code = ((raw[u] >> 31) << 7) | (uint32_t)lvl;
+            }
+          }
+          code_out[pos] = (uint8_t)code;
+        } else {
+          val_out[pos] = __uint_as_float(raw[u]);
+        }
       }
+      s_before += is_s[u] ? 1 : 0;
+      t_before += is_t[u] ? 1 : 0;
     }
-    const unsigned long long off = (unsigned long long)((long long)idx[j] - (long long)t0);
-    if (off < (unsigned long long)kTile) s_tile[off] = v;
+    run_s += (long long)(tot >> 32);
+    run_t += (long long)(tot & 0xffffffffull);
   }
-  __syncthreads();
-  const int64_t len = t1 - t0;
-  if (len == kTile && ((reinterpret_cast<uintptr_t>(out) & 15u) == 0)) {
-    float4* o4 = reinterpret_cast<float4*>(out + t0);
-    for (int i = threadIdx.x; i < kTile / 4; i += kThreads) {
-      float4 v = tile4[i];
-      if (ACC) {
-        const float4 p = o4[i];
-        v = make_float4(fmaf(weight, v.x, p.x), fmaf(weight, v.y, p.y), fmaf(weight, v.z, p.z), fmaf(weight, v.w, p.w));
-      } else if (weight != 1.0f) {
-        v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
-      }
-      st_stream(out + t0 + 4 * (int64_t)i, v);
-    }
-  } else {
-    for (int64_t i = threadIdx.x; i < len; i += kThreads) {
-      float v = s_tile[i];
-      if (ACC) v = fmaf(weight, v, out[t0 + i]);
-      else if (weight != 1.0f) v = weight * v;
-      out[t0 + i] = v;
-    }
-  }
-}
-
-// rand-k scatter: out[idx[j]] = scale * x[idx[j]] (out pre-zeroed)
-__global__ __launch_bounds__(kThreads) void randk_scatter_kernel(const float* __restrict__ x, const int* __restrict__ idx,
-                                                                 long long k, float scale, float* __restrict__ out) {
-  for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j < k; j += (long long)gridDim.x * kThreads) {
-    const int i = idx[j];
-    out[i] = scale * x[i];
-  }
-}
-
-// out = x / p (lazy) or out = x (identical, p == 1 handled as a copy)
-template <bool DIV>
-__global__ __launch_bounds__(kThreads) void elementwise_kernel(const float* __restrict__ x, int64_t n, float p,
-                                                               float* __restrict__ out) {
-  const int64_t n4 = n >> 2;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  float4* o4 = reinterpret_cast<float4*>(out);
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads) {
-    float4 v = x4[i];
-    if (DIV) v = make_float4(v.x / p, v.y / p, v.z / p, v.w / p);
-    o4[i] = v;
-  }
-  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads)
-    out[i] = DIV ? x[i] / p : x[i];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -665,27 +714,19 @@ SampleSetup sample_setup(int64_t n, int64_t k) {
   return s;
 }
 
-bool g_sample_attr_set = false;
-
 int launch_select(const float* x, int64_t n, int64_t k, const TopkWs& w, hipStream_t st) {
   const TopkGeom g = geometry(n);
   const SampleSetup ss = sample_setup(n, k);
-  const size_t lds = (size_t)ss.S * sizeof(unsigned);
-  if (!g_sample_attr_set) {
-    FLC_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(topk_sample_kernel),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kSample * sizeof(unsigned))));
-    g_sample_attr_set = true;
-  }
-  FLC_LAUNCH("topk_sample", topk_sample_kernel, dim3(1), dim3(kSampleThreads), lds, st, x, n, ss.S, ss.rank_lo,
+  const int R = (int)g.regions;
+  if (!ss.take_all)
+    FLC_LAUNCH("topk_sample_gather", topk_sample_gather_kernel, dim3((unsigned)cdiv(ss.S, kThreads)), dim3(kThreads), 0,
+               st, x, n, ss.S, w);
+  FLC_LAUNCH("topk_sample_select", topk_sample_select_kernel, dim3(1), dim3(kSelectThreads), 0, st, ss.S, ss.rank_lo,
              ss.take_all, w);
   FLC_LAUNCH("topk_filter", topk_filter_kernel, dim3((unsigned)g.blocks), dim3(kThreads), 0, st, x, n, g.wave_chunk, w);
-  FLC_LAUNCH("topk_scan", topk_scan_kernel, dim3(1), dim3(1024), 0, st, g.regions, n, (long long)k, w);
-  FLC_LAUNCH("topk_round", (topk_round_kernel<21, 11, true, false>), dim3(kSelBlocks), dim3(kThreads), 0, st, x, w, 0,
-             (long long)g.regions);
-  FLC_LAUNCH("topk_round", (topk_round_kernel<10, 11, false, false>), dim3(kSelBlocks), dim3(kThreads), 0, st, x, w, 1,
-             (long long)g.regions);
-  FLC_LAUNCH("topk_round", (topk_round_kernel<0, 10, false, true>), dim3(kSelBlocks), dim3(kThreads), 0, st, x, w, 2,
-             (long long)g.regions);
+  FLC_LAUNCH("topk_round", topk_round_kernel<true>, dim3(kSelBlocks), dim3(kThreads), 0, st, x, w, 0, R, (long long)k, n);
+  FLC_LAUNCH("topk_round", topk_round_kernel<false>, dim3(kSelBlocks), dim3(kThreads), 0, st, x, w, 1, R, (long long)k, n);
+  FLC_LAUNCH("topk_round", topk_round_kernel<false>, dim3(kSelBlocks), dim3(kThreads), 0, st, x, w, 2, R, (long long)k, n);
   FLC_LAUNCH("topk_count", topk_count_kernel, dim3(kSelBlocks), dim3(kThreads), 0, st, x, w);
   return FLC_OK;
 }
@@ -726,21 +767,6 @@ int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* v
   return FLC_OK;
 }
 
-int flc_sparse_decode(const int32_t* idx, const float* val, int64_t k, float scale, int64_t n, float weight,
-                      int accumulate, float* out, void* stream) {
-  if (!out || n <= 0 || k < 0 || (k > 0 && (!idx || !val))) return fail(FLC_EINVAL, "flc_sparse_decode: bad arguments");
-  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_sparse_decode: n must be < 2^31");
-  hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)cdiv(n, kTile);
-  if (accumulate)
-    FLC_LAUNCH("sparse_decode", (sparse_decode_kernel<0, true>), dim3(grid), dim3(kThreads), 0, st, idx, val,
-               (const uint8_t*)nullptr, (long long)k, scale, 0, 0.0, (const float*)nullptr, n, weight, out);
-  else
-    FLC_LAUNCH("sparse_decode", (sparse_decode_kernel<0, false>), dim3(grid), dim3(kThreads), 0, st, idx, val,
-               (const uint8_t*)nullptr, (long long)k, scale, 0, 0.0, (const float*)nullptr, n, weight, out);
-  return FLC_OK;
-}
-
 int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_t seed, uint64_t counter,
                        const double* compat_u, int32_t* idx, uint8_t* codes, float* norm, void* ws, size_t ws_bytes,
                        void* stream) {
@@ -757,53 +783,6 @@ int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_
   if (int rc = launch_select(x, n, k, w, st)) return rc;
   FLC_LAUNCH("stacked_compact", topk_compact_kernel<true>, dim3(kSelBlocks), dim3(kThreads), 0, st, x, w, idx,
              (float*)nullptr, codes, norm, levels, 1.0 / (double)levels, seed, counter);
-  return FLC_OK;
-}
-
-int flc_stacked_decode(const int32_t* idx, const uint8_t* codes, int64_t k, int levels, const float* norm, int64_t n,
-                       float weight, int accumulate, float* out, void* stream) {
-  if (!out || !norm || n <= 0 || k < 0 || (k > 0 && (!idx || !codes)))
-    return fail(FLC_EINVAL, "flc_stacked_decode: bad arguments");
-  if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_stacked_decode: levels must be in [1, 127]");
-  hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)cdiv(n, kTile);
-  const double step = 1.0 / (double)levels;
-  if (accumulate)
-    FLC_LAUNCH("stacked_decode", (sparse_decode_kernel<1, true>), dim3(grid), dim3(kThreads), 0, st, idx,
-               (const float*)nullptr, codes, (long long)k, 1.0f, levels, step, norm, n, weight, out);
-  else
-    FLC_LAUNCH("stacked_decode", (sparse_decode_kernel<1, false>), dim3(grid), dim3(kThreads), 0, st, idx,
-               (const float*)nullptr, codes, (long long)k, 1.0f, levels, step, norm, n, weight, out);
-  return FLC_OK;
-}
-
-int flc_copy(const float* x, int64_t n, float* out, void* stream) {
-  if (!x || !out || n < 0) return fail(FLC_EINVAL, "flc_copy: bad arguments");
-  if (n == 0) return FLC_OK;
-  if (!aligned16(x) || !aligned16(out)) return fail(FLC_EINVAL, "flc_copy: 16-B aligned buffers required");
-  hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 4), kThreads), 256 * 16);
-  FLC_LAUNCH("copy", elementwise_kernel<false>, dim3(grid), dim3(kThreads), 0, st, x, n, 1.0f, out);
-  return FLC_OK;
-}
-
-int flc_scale_div(const float* x, int64_t n, float p, float* out, void* stream) {
-  if (!x || !out || n < 0) return fail(FLC_EINVAL, "flc_scale_div: bad arguments");
-  if (n == 0) return FLC_OK;
-  if (!aligned16(x) || !aligned16(out)) return fail(FLC_EINVAL, "flc_scale_div: 16-B aligned buffers required");
-  hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 4), kThreads), 256 * 16);
-  FLC_LAUNCH("scale_div", elementwise_kernel<true>, dim3(grid), dim3(kThreads), 0, st, x, n, p, out);
-  return FLC_OK;
-}
-
-int flc_randk_apply(const float* x, int64_t n, const int32_t* idx, int64_t k, float scale, float* out, void* stream) {
-  if (!x || !out || n <= 0 || k < 0 || (k > 0 && !idx)) return fail(FLC_EINVAL, "flc_randk_apply: bad arguments");
-  hipStream_t st = as_stream(stream);
-  FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)n * sizeof(float), st));
-  if (k == 0) return FLC_OK;
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(k, kThreads), 256 * 16);
-  FLC_LAUNCH("randk_scatter", randk_scatter_kernel, dim3(grid), dim3(kThreads), 0, st, x, idx, (long long)k, scale, out);
   return FLC_OK;
 }
 
