@@ -47,14 +47,18 @@ SIGNATURES = {
     "flc_natural_decode": (c_int, [c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p]),
     "flc_topk_workspace_size": (c_size_t, [c_int64, c_int64]),
     "flc_topk_encode": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
-    "flc_sparse_decode": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_int64, c_float, c_int, c_void_p, c_void_p]),
+    "flc_sparse_decode_workspace_size": (c_size_t, [c_int64]),
+    "flc_sparse_decode": (
+        c_int, [c_void_p, c_void_p, c_int64, c_float, c_int64, c_float, c_int, c_void_p, c_void_p, c_size_t, c_void_p]
+    ),
     "flc_stacked_encode": (
         c_int,
         [c_void_p, c_int64, c_int64, c_int, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_size_t, c_void_p],
     ),
     "flc_stacked_decode": (
-        c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p]
+        c_int,
+        [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p, c_size_t, c_void_p],
     ),
     "flc_copy": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_scale_div": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),

@@ -166,8 +166,9 @@ def sparse_decode(idx: torch.Tensor, val: torch.Tensor, n: int, scale: float = 1
                   weight: float = 1.0, accumulate: bool = False) -> torch.Tensor:
     if out is None:
         out = torch.empty(n, dtype=torch.float32, device=val.device)
-    call("flc_sparse_decode", _p(idx), _p(val), idx.numel(), scale, n, weight, int(accumulate), _p(out),
-         _stream(out.device))
+    ws = workspace(out.device, _lib.size("flc_sparse_decode_workspace_size", n), "decode")
+    call("flc_sparse_decode", _p(idx), _p(val), idx.numel(), scale, n, weight, int(accumulate), _p(out), _p(ws),
+         ws.numel(), _stream(out.device))
     return out
 
 
@@ -202,8 +203,9 @@ def stacked_decode(pkt: StackedPacket, out: Optional[torch.Tensor] = None, weigh
                    accumulate: bool = False) -> torch.Tensor:
     if out is None:
         out = torch.empty(pkt.n, dtype=torch.float32, device=pkt.idx.device)
+    ws = workspace(out.device, _lib.size("flc_sparse_decode_workspace_size", pkt.n), "decode")
     call("flc_stacked_decode", _p(pkt.idx), _p(pkt.codes), pkt.idx.numel(), pkt.levels, _p(pkt.norm), pkt.n, weight,
-         int(accumulate), _p(out), _stream(out.device))
+         int(accumulate), _p(out), _p(ws), ws.numel(), _stream(out.device))
     return out
 
 

@@ -1,15 +1,19 @@
 // sparse.hip — dense decoders of the sparse wires and the elementwise compressors, for gfx950
 // (reference: fl_sim/compressors/compressors.py:273-296).
 //
-//   sparse_decode   dense output tile by tile (8192 outputs = 32 KiB of LDS per block): a 64-ary wave
-//                   search finds the tile's slice of the ascending index stream, the tile is zero-filled
-//                   in LDS, the slice scattered into it, and the tile streamed out with 16-B stores.
+//   tile_index      tile_start[t] = first kept entry of output tile t (one thread per kept entry).
+//   sparse_decode   dense output, one block per 1024-output tile: the tile is zero-filled in LDS, its
+//                   slice of the ascending index stream scattered into it, and it is streamed out with
+//                   one 16-B store per thread (the store shape that reaches ~7 TB/s on MI355X, see
+//                   tools/bwprobe.hip).
 //                   Algorithmic bytes: 4 per output element + 8 (top-k: idx+val) or 5 (stacked:
 //                   idx+code) per kept entry.  Optionally fused with the aggregation: out = fmaf(w, v, out).
 //   randk_scatter   out[idx[j]] = fp32(D/K) * x[idx[j]] after a zero fill (compressors.py:289-291).
 //   elementwise     identical (+x) and lazy (x / p) (compressors.py:273-283).
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -20,55 +24,49 @@ namespace flc {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kTile = 8192;
+constexpr int kDecodeVariant = 40;  // V * 10 + EARLY (see launch_decode)
 
-// 64-ary lower bound by one wave: first i in [0, n) with a[i] >= key (n if none), a ascending
-__device__ long long wave_lower_bound(const int* __restrict__ a, long long n, int key) {
-  const int lane = threadIdx.x & (kWave - 1);
-  long long lo = 0, hi = n;  // a[i] < key for i < lo; a[hi] >= key or hi == n
-  while (hi - lo > kWave) {
-    const long long stride = (hi - lo + kWave - 1) / kWave;
-    const long long p = lo + (long long)lane * stride;
-    const bool lt = p < hi && a[p] < key;
-    const int cnt = __popcll(__ballot(lt));  // probes below key form a prefix of the lanes
-    const long long nlo = cnt > 0 ? lo + (long long)(cnt - 1) * stride + 1 : lo;
-    const long long nhi = lo + (long long)cnt * stride < hi ? lo + (long long)cnt * stride : hi;
-    lo = nlo;
-    hi = nhi;
+// tile_start[t] = first j with idx[j] >= t * TILE (t = 0 .. ntiles); idx ascending.  One thread per
+// kept entry: entry j fills the tiles between its predecessor's tile and its own.
+template <int TILE_LOG>
+__global__ __launch_bounds__(kThreads) void tile_index_kernel(const int* __restrict__ idx, long long k, long long ntiles,
+                                                              unsigned* __restrict__ tile_start) {
+  for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j <= k; j += (long long)gridDim.x * kThreads) {
+    long long tj = j < k ? ((long long)(unsigned)idx[j] >> TILE_LOG) : ntiles;
+    tj = tj < ntiles ? tj : ntiles;
+    const long long tp = j > 0 ? ((long long)(unsigned)idx[j - 1] >> TILE_LOG) : -1;
+    for (long long t = tp + 1; t <= tj; ++t) tile_start[t] = (unsigned)j;
   }
-  const long long p = lo + lane;
-  const bool lt = p < hi && a[p] < key;
-  return lo + __popcll(__ballot(lt));
 }
 
-// ------------------------------------------------------------------------------------------------
-// K5: sparse -> dense decode (tile = 8192 outputs, LDS scatter, 16-B stores)
+// one block per output tile of TILE = 256 * V floats: zero the tile in LDS, scatter the tile's kept
+// entries (tile_start[t] .. tile_start[t+1]), stream it out with V 16-B stores per thread.
 //   MODE 0: v = scale * val[j];  MODE 1: v = dithering decode of codes[j] (s = levels, norm)
-// ------------------------------------------------------------------------------------------------
-template <int MODE, bool ACC>
+template <int MODE, bool ACC, int V, bool EARLY>
 __global__ __launch_bounds__(kThreads) void sparse_decode_kernel(const int* __restrict__ idx, const float* __restrict__ val,
-                                                                 const uint8_t* __restrict__ codes, long long k, float scale,
+                                                                 const uint8_t* __restrict__ codes, float scale,
                                                                  int levels, double step, const float* __restrict__ norm_ptr,
-                                                                 int64_t n, float weight, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float s_tile[kTile];
-  __shared__ long long s_lo, s_hi;
-  const int64_t t0 = (int64_t)blockIdx.x * kTile;
-  const int64_t t1 = t0 + kTile < n ? t0 + kTile : n;
-  const int wid = threadIdx.x >> 6;
-  if (wid == 0) {
-    const long long lo = wave_lower_bound(idx, k, (int)t0);
-    if (threadIdx.x == 0) s_lo = lo;
-  } else if (wid == 1) {
-    const long long hi = t1 >= n ? k : wave_lower_bound(idx, k, (int)t1);
-    if (threadIdx.x == kWave) s_hi = hi;
+                                                                 int64_t n, float weight, float* __restrict__ out,
+                                                                 const unsigned* __restrict__ tile_start) {
+  constexpr int TILE = kThreads * 4 * V;
+  __shared__ __attribute__((aligned(16))) float s_tile[TILE];
+  const int64_t t0 = (int64_t)blockIdx.x * TILE;
+  const bool full = t0 + TILE <= n;
+  // EARLY: the zero stores of a full, non-accumulating tile leave before any load returns; the few
+  // float4s that hold kept entries are stored again below (same thread, program order)
+  if (EARLY && !ACC && full) {
+#pragma unroll
+    for (int u = 0; u < V; ++u)
+      *reinterpret_cast<float4*>(out + t0 + 4 * (int64_t)(threadIdx.x + u * kThreads)) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  const unsigned lo = tile_start[blockIdx.x], hi = tile_start[blockIdx.x + 1];
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
-  for (int i = threadIdx.x; i < kTile / 4; i += kThreads) tile4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int u = 0; u < V; ++u) tile4[threadIdx.x + u * kThreads] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  const long long lo = s_lo, hi = s_hi;
   float nrm = 0.f;
   if (MODE == 1) nrm = *norm_ptr;
-  for (long long j = lo + threadIdx.x; j < hi; j += kThreads) {
+  for (unsigned j = lo + threadIdx.x; j < hi; j += kThreads) {
     float v;
     if (MODE == 0) {
       v = scale * val[j];
@@ -78,32 +76,35 @@ __global__ __launch_bounds__(kThreads) void sparse_decode_kernel(const int* __re
         v = code == 0u ? 0.0f : __uint_as_float(0x7fc00000u);
       } else {
         const float lv = (float)level_value<0>((int)(code & 127u), levels, step);
-        v = ((code >> 7) ? -lv : lv) * nrm;
+        v = ((code >> 7) ? -lv : lv) * nrm;  // compressors.py:357
       }
     }
-    const unsigned long long off = (unsigned long long)((long long)idx[j] - (long long)t0);
-    if (off < (unsigned long long)kTile) s_tile[off] = v;
+    const unsigned long long off = (unsigned long long)((long long)(unsigned)idx[j] - (long long)t0);
+    if (off < (unsigned long long)TILE) s_tile[off] = v;
   }
   __syncthreads();
-  const int64_t len = t1 - t0;
-  if (len == kTile && ((reinterpret_cast<uintptr_t>(out) & 15u) == 0)) {
-    float4* o4 = reinterpret_cast<float4*>(out + t0);
-    for (int i = threadIdx.x; i < kTile / 4; i += kThreads) {
-      float4 v = tile4[i];
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const int q = threadIdx.x + u * kThreads;
+    const int64_t e = t0 + 4 * (int64_t)q;
+    float4 v = tile4[q];
+    if (e + 4 <= n) {
       if (ACC) {
-        const float4 p = o4[i];
+        const float4 p = *reinterpret_cast<const float4*>(out + e);
         v = make_float4(fmaf(weight, v.x, p.x), fmaf(weight, v.y, p.y), fmaf(weight, v.z, p.z), fmaf(weight, v.w, p.w));
       } else if (weight != 1.0f) {
         v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
       }
-      st_stream(out + t0 + 4 * (int64_t)i, v);
-    }
-  } else {
-    for (int64_t i = threadIdx.x; i < len; i += kThreads) {
-      float v = s_tile[i];
-      if (ACC) v = fmaf(weight, v, out[t0 + i]);
-      else if (weight != 1.0f) v = weight * v;
-      out[t0 + i] = v;
+      const bool nz = __float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z) | __float_as_uint(v.w);
+      if (!(EARLY && !ACC && full) || nz) *reinterpret_cast<float4*>(out + e) = v;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int c = 0; c < 4 && e + c < n; ++c) {
+        float o = vv[c];
+        if (ACC) o = fmaf(weight, o, out[e + c]);
+        else if (weight != 1.0f) o = weight * o;
+        out[e + c] = o;
+      }
     }
   }
 }
@@ -133,6 +134,57 @@ __global__ __launch_bounds__(kThreads) void elementwise_kernel(const float* __re
     out[i] = DIV ? x[i] / p : x[i];
 }
 
+size_t decode_ws_bytes(int64_t n) {  // tile index for the smallest tile (1024 outputs)
+  return (size_t)(cdiv(n < 1 ? 1 : n, (int64_t)kThreads * 4) + 1) * sizeof(unsigned);
+}
+
+template <int MODE, int V, bool EARLY>
+int launch_decode_v(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
+                    const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws, size_t ws_bytes,
+                    hipStream_t st, const char* name) {
+  constexpr int TILE = kThreads * 4 * V;
+  constexpr int TILE_LOG = V == 1 ? 10 : (V == 2 ? 11 : (V == 4 ? 12 : 13));
+  const int64_t ntiles = cdiv(n, TILE);
+  const size_t need = (size_t)(ntiles + 1) * sizeof(unsigned);
+  if (!ws || ws_bytes < need) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", name, ws_bytes, need);
+  if (!aligned16(out)) return fail(FLC_EINVAL, "%s: out must be 16-B aligned", name);
+  unsigned* tile_start = static_cast<unsigned*>(ws);
+  const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(k + 1, kThreads), 2048));
+  FLC_LAUNCH("tile_index", tile_index_kernel<TILE_LOG>, dim3(gi), dim3(kThreads), 0, st, idx, (long long)k,
+             (long long)ntiles, tile_start);
+  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
+  if (accumulate)
+    FLC_LAUNCH(name, (sparse_decode_kernel<MODE, true, V, EARLY>), dim3((unsigned)ntiles), dim3(kThreads), 0, st, idx,
+               val, codes, scale, levels, step, norm, n, weight, out, tile_start);
+  else
+    FLC_LAUNCH(name, (sparse_decode_kernel<MODE, false, V, EARLY>), dim3((unsigned)ntiles), dim3(kThreads), 0, st, idx,
+               val, codes, scale, levels, step, norm, n, weight, out, tile_start);
+  return FLC_OK;
+}
+
+int decode_variant() {
+  const char* e = getenv("FLC_DECODE_VARIANT");
+  return e ? atoi(e) : kDecodeVariant;
+}
+
+template <int MODE>
+int launch_decode(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
+                  const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws, size_t ws_bytes,
+                  hipStream_t st, const char* name) {
+#define FLC_DV(V, E) return launch_decode_v<MODE, V, E>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name)
+  switch (decode_variant()) {
+    case 10: FLC_DV(1, false);
+    case 11: FLC_DV(1, true);
+    case 20: FLC_DV(2, false);
+    case 21: FLC_DV(2, true);
+    case 40: FLC_DV(4, false);
+    case 41: FLC_DV(4, true);
+    case 80: FLC_DV(8, false);
+    default: FLC_DV(8, true);
+  }
+#undef FLC_DV
+}
+
 }  // namespace
 }  // namespace flc
 
@@ -140,36 +192,24 @@ using namespace flc;
 
 extern "C" {
 
+size_t flc_sparse_decode_workspace_size(int64_t n) { return decode_ws_bytes(n); }
+
 int flc_sparse_decode(const int32_t* idx, const float* val, int64_t k, float scale, int64_t n, float weight,
-                      int accumulate, float* out, void* stream) {
+                      int accumulate, float* out, void* ws, size_t ws_bytes, void* stream) {
   if (!out || n <= 0 || k < 0 || (k > 0 && (!idx || !val))) return fail(FLC_EINVAL, "flc_sparse_decode: bad arguments");
   if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_sparse_decode: n must be < 2^31");
-  hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)cdiv(n, kTile);
-  if (accumulate)
-    FLC_LAUNCH("sparse_decode", (sparse_decode_kernel<0, true>), dim3(grid), dim3(kThreads), 0, st, idx, val,
-               (const uint8_t*)nullptr, (long long)k, scale, 0, 0.0, (const float*)nullptr, n, weight, out);
-  else
-    FLC_LAUNCH("sparse_decode", (sparse_decode_kernel<0, false>), dim3(grid), dim3(kThreads), 0, st, idx, val,
-               (const uint8_t*)nullptr, (long long)k, scale, 0, 0.0, (const float*)nullptr, n, weight, out);
-  return FLC_OK;
+  return launch_decode<0>(idx, val, nullptr, k, scale, 0, nullptr, n, weight, accumulate, out, ws, ws_bytes,
+                          as_stream(stream), "sparse_decode");
 }
 
 int flc_stacked_decode(const int32_t* idx, const uint8_t* codes, int64_t k, int levels, const float* norm, int64_t n,
-                       float weight, int accumulate, float* out, void* stream) {
+                       float weight, int accumulate, float* out, void* ws, size_t ws_bytes, void* stream) {
   if (!out || !norm || n <= 0 || k < 0 || (k > 0 && (!idx || !codes)))
     return fail(FLC_EINVAL, "flc_stacked_decode: bad arguments");
+  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_stacked_decode: n must be < 2^31");
   if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_stacked_decode: levels must be in [1, 127]");
-  hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)cdiv(n, kTile);
-  const double step = 1.0 / (double)levels;
-  if (accumulate)
-    FLC_LAUNCH("stacked_decode", (sparse_decode_kernel<1, true>), dim3(grid), dim3(kThreads), 0, st, idx,
-               (const float*)nullptr, codes, (long long)k, 1.0f, levels, step, norm, n, weight, out);
-  else
-    FLC_LAUNCH("stacked_decode", (sparse_decode_kernel<1, false>), dim3(grid), dim3(kThreads), 0, st, idx,
-               (const float*)nullptr, codes, (long long)k, 1.0f, levels, step, norm, n, weight, out);
-  return FLC_OK;
+  return launch_decode<1>(idx, nullptr, codes, k, 1.0f, levels, norm, n, weight, accumulate, out, ws, ws_bytes,
+                          as_stream(stream), "stacked_decode");
 }
 
 int flc_copy(const float* x, int64_t n, float* out, void* stream) {

@@ -119,9 +119,11 @@ size_t flc_topk_workspace_size(int64_t n, int64_t k);
 int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, void* ws,
                     size_t ws_bytes, void* stream);
 /* dense decode of an ascending sparse stream: out[idx[j]] = scale * val[j], zeros elsewhere
- * (compressors.py:289-291, 294-295); accumulate: out = fmaf(weight, v, out) over the whole vector */
+ * (compressors.py:289-291, 294-295); out = weight * v, or with accumulate out = fmaf(weight, v, out)
+ * over the whole vector (the fused aggregation).  Workspace: a per-tile index of the stream. */
+size_t flc_sparse_decode_workspace_size(int64_t n);
 int flc_sparse_decode(const int32_t* idx, const float* val, int64_t k, float scale, int64_t n,
-                      float weight, int accumulate, float* out, void* stream);
+                      float weight, int accumulate, float* out, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------ stacked top-k -> 8-bit dither
  * Top-k of x (as above), then standard dithering with s = levels (<= 127), p = inf, of the k kept
@@ -132,7 +134,7 @@ int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_
                        float* norm, void* ws, size_t ws_bytes, void* stream);
 int flc_stacked_decode(const int32_t* idx, const uint8_t* codes, int64_t k, int levels,
                        const float* norm, int64_t n, float weight, int accumulate, float* out,
-                       void* stream);
+                       void* ws, size_t ws_bytes, void* stream);  /* ws: flc_sparse_decode_workspace_size */
 
 /* ------------------------------------------------------------------ other compressors
  * identical (compressors.py:273-275): out = +x;  lazy (276-283): out = x / p (fp32 division);
