@@ -36,8 +36,10 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
   constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-    const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    // 64-bit products: one v_mad_u64_u32 each instead of a mul_hi + mul_lo pair
+    const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += W0;
     k1 += W1;
@@ -165,6 +167,39 @@ template <int KIND>
 __device__ __forceinline__ double level_value(int i, int s, double step) {
   if (KIND == 0) return (i == s) ? 1.0 : (double)i * step;
   return (i == 0) ? 0.0 : ldexp(1.0, i - s);
+}
+
+template <int KIND>
+__device__ __forceinline__ int level_lower_bound(float yf, int s, double step);
+
+// Level index chosen for y = fp32(|x| / norm) in [0, 1] and uniform u — the rule of
+// compressors.py:346-353: bracket [lv(sl), lv(sl+1)] = the first with lv(sl) <= y <= lv(sl+1) (fp64),
+// p = (y - lv(sl+1)) / (lv(sl) - lv(sl+1)) in fp64, lower level iff u < p.  Bit-exact with that rule:
+//  * standard: an fp32 fast path decides whenever t = y*s is >= 1e-4 from an integer and |u - p| > 3e-5
+//    (its error is < 1e-5), otherwise the fp64 rule runs (probability ~1e-4 per element);
+//  * natural: levels are powers of two, so the division is an exact power-of-two scaling.
+template <int KIND>
+__device__ __forceinline__ int dither_level(float y, int s, double step, double u) {
+  if (KIND == 0) {
+    const float t = y * (float)s;
+    const float jf = ceilf(t);
+    if (jf - t > 1e-4f && t - (jf - 1.0f) > 1e-4f) {
+      const float pf = jf - t;
+      const float uf = (float)u;
+      if (fabsf(uf - pf) > 3e-5f) return (uf < pf) ? (int)jf - 1 : (int)jf;
+    }
+  }
+  const int j = level_lower_bound<KIND>(y, s, step);
+  const int sl = j > 0 ? j - 1 : 0;
+  const double lo = level_value<KIND>(sl, s, step), hi = level_value<KIND>(sl + 1, s, step);
+  double p;
+  if (KIND == 0) {
+    p = ((double)y - hi) / (lo - hi);
+  } else {
+    // lo - hi = -2^(sl+1-s) (sl >= 1) or -hi (sl == 0): multiply by the exact power-of-two inverse
+    p = ((double)y - hi) * -ldexp(1.0, (sl == 0 ? s - 1 : s - sl));
+  }
+  return (u < p) ? sl : sl + 1;
 }
 
 // first index j in [0, s] with lv(j) >= y (y in [0, 1], not NaN)

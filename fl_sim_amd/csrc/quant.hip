@@ -153,11 +153,7 @@ __device__ __forceinline__ uint32_t quant_code(float xv, float nrm, int s, doubl
   if (xv == 0.0f) return 0u;
   if (!norm_regular(nrm)) return 1u;
   const float y = fabsf(xv) / nrm;  // IEEE fp32 division (compressors.py:344)
-  const int j = level_lower_bound<KIND>(y, s, step);
-  const int sl = j > 0 ? j - 1 : 0;
-  const double lo = level_value<KIND>(sl, s, step), hi = level_value<KIND>(sl + 1, s, step);
-  const double p = ((double)y - hi) / (lo - hi);  // fp64 (compressors.py:348)
-  const int lvl = (u < p) ? sl : sl + 1;           // compressors.py:350-353
+  const int lvl = dither_level<KIND>(y, s, step, u);  // compressors.py:346-353 (fp64 rule, exact)
   return ((__float_as_uint(xv) >> 31) << (BITS - 1)) | (uint32_t)lvl;
 }
 

@@ -8,26 +8,31 @@
 //
 // Pipeline: ONE streaming read of x; every later pass touches only the ~1.2 k candidates.
 //   sample_gather  128 blocks: 32 K strided keys of x (order-preserving uint32 keys).
-//   sample_select  1 block, keys in registers: radix select (2048-bin digits over the live range of
-//                  the sample) -> candidate floor t_lo with count(key >= t_lo) ~ k + 4 sigma
-//                  (k/n = 1 %: ~1.22 k candidates).
-//   filter         the HBM pass: each wave owns a contiguous run of x and appends its candidates in
-//                  index order to a private staging region (ballot/mbcnt compaction: no atomics, no
-//                  inter-wave sync).  Algorithmic bytes 4 per element.
-//   select         ONE persistent launch, one 1024-thread block per CU, five phases separated by
-//                  XCD-sharded grid barriers whose last arriver ("leader") does the serial step:
+//   sample_select  1 block, keys in registers: two fixed 11-bit digit passes locate the sample
+//                  quantiles at ranks m + 4 sqrt(m) + 16 and m - 4 sqrt(m) - 16 (m = k S / n): the
+//                  candidate floor t_lo (count(key >= t_lo) ~ k + 4 sigma, so ~1.22 k candidates at
+//                  k/n = 1 %) and a ceiling t_hi that very likely lies above the k-th largest key.
+//   filter         the HBM pass: one-shot 64 KB blocks (4 waves x 16 float4 per lane, all loads in
+//                  flight at once); each block appends its candidates in index order to a private
+//                  staging region (ballot/mbcnt compaction, one LDS exchange of wave counts, no
+//                  atomics).  Algorithmic bytes: 4 per element.
+//   select         ONE persistent launch, one 1024-thread block per CU:
 //                    P0  region offsets in LDS (every block), candidate count C, max key;
-//                    P1  gather the staged candidates into an ordered SoA array + radix round 1;
-//                    P2  radix rounds 2-3 (2048 bins over the live key range; 3 rounds always resolve
-//                        the exact k-th largest key T);
-//                    P3  per-block strict / tie counts, scanned by the leader;
-//                    P4  ordered compaction into idx[k] / val[k], or, stacked, idx[k] / codes[k] with
-//                        the dithering fused in (norm of the kept set = max(|max key|, |T|)).
+//                    rounds  gather the staged candidates (round 0) into an index-ordered array and an
+//                        LDS key cache, then 2048-bin radix rounds over the live key range (round 0:
+//                        [t_lo, t_hi), keys above it counted apart) until the exact k-th largest key
+//                        T is resolved (usually 2 rounds);
+//                    counts  strict / tie counts per block come from the resolving round's local
+//                        histogram (no extra pass), scanned by the barrier leader;
+//                    compaction  ordered write of idx[k] / val[k], or, stacked, idx[k] / codes[k]
+//                        with the dithering fused in (norm of the kept set = max(|max key|, |T|)).
+//                  Rounds are separated by grid barriers: every block raises its own arrival flag,
+//                  block 0 polls them, runs the serial "leader" step and publishes a generation word.
 //                  C < k switches every phase to "fallback" mode, reading x itself (always correct).
-// Cross-block hand-offs inside a launch go through memory-side atomics only (histogram adds, arrival
-// counters, RMW reads, atomic exchanges of the published state); candidates are re-read only by the
-// thread that wrote them.  Spins are bounded (error flag), and the host serialises the persistent
-// launches of different streams so two of them never compete for residency.
+// Cross-block hand-offs inside a launch go through memory-side atomics only (histogram adds, flag
+// and state exchanges, RMW reads); candidates are re-read only by the thread that wrote them.  Spins
+// are bounded (error flag), and the host serialises the persistent launches of different streams so
+// two of them never compete for residency.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -46,24 +51,29 @@ constexpr int kSample = 32768;
 constexpr int kSelectThreads = 1024;
 constexpr int kSamplePerThread = kSample / kSelectThreads;  // 32
 constexpr int kThreads = 256;
-constexpr int kNW = kThreads / kWave;
-constexpr int kStep = 1024;         // elements per wave step in the filter (4 x float4 per lane)
-constexpr int kSelThreads = 1024;   // persistent select: one block of 16 waves per CU
+constexpr int kFNW = kThreads / kWave;       // filter: 4 waves per block
+constexpr int kWaveSpan = 4096;              // elements per wave per block step (16 float4 per lane)
+constexpr int kBlockSpan = kFNW * kWaveSpan; // 16384 elements = 64 KB per block step
+constexpr int kSelThreads = 1024;            // persistent select: one block of 16 waves per CU
 constexpr int kSelNW = kSelThreads / kWave;
 constexpr int kMaxSelBlocks = 1024;
 constexpr int kHistBits = 11;
 constexpr int kHistBins = 1 << kHistBits;
-constexpr int kShards = 8;          // XCD shards of the arrival counters
-constexpr int kMaxRegions = 8192;
-constexpr int kRegionsPerThread = kMaxRegions / kSelThreads;  // 8 (P0 LDS scan)
+constexpr int kHistStride = kHistBins + 64;  // a round's bins + its "above the range" counter
+constexpr int kMaxRounds = 6;
+constexpr int kMaxRegions = 16384;           // filter blocks = staging regions
+constexpr int kRegionsPerThread = kMaxRegions / kSelThreads;  // 16 (P0 LDS scan)
+constexpr int kKeyCache = 16384;             // candidates per select block kept in LDS
+constexpr int kFlagStride = 16;              // one 64-B line per barrier arrival flag
 
 struct TopkParams {
-  unsigned t_lo;       // candidate floor (sample_select -> filter, select)
+  unsigned t_lo;             // candidate floor (sample_select -> filter, select)
   unsigned pad;
+  unsigned long long t_hi;   // likely ceiling of the k-th largest key (<= 2^32)
 };
 
-// state published by the grid-barrier leaders of the select launch (64-bit words, memory-side
-// atomics only); zeroed per call by the filter
+// state published by the barrier leader of the select launch (64-bit words, memory-side atomics
+// only); zeroed per call by the filter
 struct SelState {
   unsigned long long gen;     // barrier generation
   unsigned long long lo;      // live key range [lo, lo + width), log2 keys per bin, rank left
@@ -79,39 +89,39 @@ struct SelState {
   unsigned long long C;       // diagnostics
   unsigned long long fallback;
   unsigned long long maxkey;
+  unsigned long long rounds;
 };
 
 struct TopkWs {
   TopkParams* p;
   SelState* st;
-  unsigned* bar;                // [kShards + 1] grid-barrier arrival counters (monotonic per call)
-  unsigned* hist;               // [3][kHistBins]
+  unsigned* flags;              // [kMaxSelBlocks * kFlagStride] barrier arrival flags
+  unsigned* hist;               // [kMaxRounds][kHistStride]
   unsigned* sample;             // [kSample]
   unsigned* region_cnt;         // [R]
   unsigned* region_max;         // [R]
   unsigned long long* blk_cnt;  // [kMaxSelBlocks]  strict << 32 | tie
   unsigned long long* blk_off;  // [kMaxSelBlocks]
   unsigned* cand_idx;           // [n]  ordered by index
-  unsigned* cand_raw;           // [n]  raw fp32 bits
-  uint2* stage;                 // [R * region_cap]  (idx, raw) per wave region
+  unsigned* cand_raw;           // [n]  raw fp32 bits (only when the LDS key cache is too small)
+  uint2* stage;                 // [R * region_cap]  (idx, raw) per filter block
   long long region_cap;
+  unsigned long long* stamps;   // [16] diagnostic build only (FLC_SELECT_STAMPS)
+  unsigned long long* trace;    // [kMaxRounds * 8] leader's per-round record (diagnostics)
 };
 
 struct TopkGeom {
-  int64_t blocks;      // filter blocks
-  int64_t wave_chunk;  // elements per wave region (multiple of kStep)
-  int64_t regions;     // blocks * 4  (<= kMaxRegions)
+  int64_t chunk;    // elements per filter block (multiple of kBlockSpan)
+  int64_t regions;  // filter blocks launched, a multiple of 4 (trailing blocks may be empty)
 };
 
 TopkGeom geometry(int64_t n) {
   TopkGeom g;
-  int64_t blocks = cdiv(n, 4 * kStep * 8);  // >= 8 steps per wave
-  if (blocks > kMaxRegions / 4) blocks = kMaxRegions / 4;
+  int64_t blocks = cdiv(n, kBlockSpan);
+  if (blocks > kMaxRegions) blocks = kMaxRegions;
   if (blocks < 1) blocks = 1;
-  g.wave_chunk = (int64_t)align_up((size_t)cdiv(n, blocks * 4), kStep);
-  g.regions = cdiv(n, g.wave_chunk);
-  g.blocks = cdiv(g.regions, 4);
-  g.regions = g.blocks * 4;
+  g.chunk = (int64_t)align_up((size_t)cdiv(n, blocks), kBlockSpan);
+  g.regions = (int64_t)align_up((size_t)cdiv(n, g.chunk), 4);
   return g;
 }
 
@@ -120,9 +130,11 @@ TopkWs carve_topk(void* ws, size_t bytes, int64_t n, size_t* need) {
   Carver c(ws, bytes);
   TopkWs w;
   w.p = c.take<TopkParams>(1);
+  w.stamps = c.take<unsigned long long>(16);
   w.st = c.take<SelState>(1);
-  w.bar = c.take<unsigned>(kShards + 1);
-  w.hist = c.take<unsigned>(3 * kHistBins);
+  w.trace = c.take<unsigned long long>(kMaxRounds * 8);
+  w.flags = c.take<unsigned>((size_t)kMaxSelBlocks * kFlagStride);
+  w.hist = c.take<unsigned>((size_t)kMaxRounds * kHistStride);
   w.sample = c.take<unsigned>(kSample);
   w.region_cnt = c.take<unsigned>(g.regions);
   w.region_max = c.take<unsigned>(g.regions);
@@ -130,8 +142,8 @@ TopkWs carve_topk(void* ws, size_t bytes, int64_t n, size_t* need) {
   w.blk_off = c.take<unsigned long long>(kMaxSelBlocks);
   w.cand_idx = c.take<unsigned>((size_t)n + 4);
   w.cand_raw = c.take<unsigned>((size_t)n + 4);
-  w.region_cap = g.wave_chunk;
-  w.stage = c.take<uint2>((size_t)g.regions * g.wave_chunk);
+  w.region_cap = g.chunk;
+  w.stage = c.take<uint2>((size_t)g.regions * g.chunk);
   *need = c.off;
   return w;
 }
@@ -199,12 +211,15 @@ __device__ __forceinline__ int range_shift(unsigned long long width, int bits) {
   return len > bits ? len - bits : 0;
 }
 
-// memory-side reads of words other blocks updated with atomics / sc1 stores in this launch
+// memory-side reads / writes of words other blocks update with atomics in this launch
 __device__ __forceinline__ unsigned ld_mem(unsigned* p) {
   return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ unsigned long long ld_mem(unsigned long long* p) {
+__device__ __forceinline__ unsigned long long ld_mem64(unsigned long long* p) {
   return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_mem64(unsigned long long* p, unsigned long long v) {
+  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // last r in [0, R) with off[r] <= c (off in LDS, nondecreasing, off[R] > c)
@@ -239,7 +254,7 @@ __device__ __forceinline__ int lds_region_advance(const unsigned* off, int R, in
 }
 
 // ------------------------------------------------------------------------------------------------
-// sample -> candidate floor
+// sample -> candidate floor and ceiling
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void topk_sample_gather_kernel(const float* __restrict__ x, int64_t n, int S,
                                                                       TopkWs w) {
@@ -249,72 +264,65 @@ __global__ __launch_bounds__(kThreads) void topk_sample_gather_kernel(const floa
   w.sample[j] = order_key(__float_as_uint(x[pos < n ? pos : n - 1]));
 }
 
-__global__ __launch_bounds__(kSelectThreads) void topk_sample_select_kernel(int S, long long rank_lo, int take_all,
+// Two fixed digit passes (key bits 31..21, then 20..10) per target rank.  Only the count guarantees
+// matter: every sample key in or above the floor's bin is >= t_lo (so >= rank_lo of them), and fewer
+// than rank_hi sample keys are >= t_hi (the end of the ceiling's bin).
+__global__ __launch_bounds__(kSelectThreads) void topk_sample_select_kernel(int S, long long rank_lo,
+                                                                            long long rank_hi, int take_all,
                                                                             TopkWs w) {
-  __shared__ unsigned s_hist[kHistBins];
-  __shared__ unsigned s_mm[2][kSelectThreads / kWave];
-  __shared__ unsigned s_digit;
-  __shared__ long long s_rem;
+  __shared__ unsigned s_hist[2][kHistBins];
+  __shared__ unsigned s_digit[2];
+  __shared__ long long s_rem[2];
   __shared__ unsigned s_err;
+  const int tid = threadIdx.x, wid = tid >> 6;
   if (take_all) {
-    if (threadIdx.x == 0) w.p->t_lo = 0u;
+    if (tid == 0) {
+      w.p->t_lo = 0u;
+      w.p->t_hi = 1ull << 32;
+    }
     return;
   }
+  const bool two = rank_hi > 0;
   unsigned keys[kSamplePerThread];
-  unsigned kmin = 0xffffffffu, kmax = 0u;
 #pragma unroll
   for (int i = 0; i < kSamplePerThread; ++i) {
-    const int j = threadIdx.x + i * kSelectThreads;
+    const int j = tid + i * kSelectThreads;
     keys[i] = j < S ? w.sample[j] : 0u;
-    if (j < S) {
-      kmin = keys[i] < kmin ? keys[i] : kmin;
-      kmax = keys[i] > kmax ? keys[i] : kmax;
-    }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned a = __shfl_xor(kmin, o, kWave), b = __shfl_xor(kmax, o, kWave);
-    kmin = a < kmin ? a : kmin;
-    kmax = b > kmax ? b : kmax;
-  }
-  if ((threadIdx.x & 63) == 0) {
-    s_mm[0][threadIdx.x >> 6] = kmin;
-    s_mm[1][threadIdx.x >> 6] = kmax;
-  }
-  if (threadIdx.x == 0) s_err = 0;
+  for (int i = tid; i < 2 * kHistBins; i += kSelectThreads) (&s_hist[0][0])[i] = 0u;
+  if (tid == 0) s_err = 0;
   __syncthreads();
-  kmin = 0xffffffffu;
-  kmax = 0u;
-  for (int i = 0; i < kSelectThreads / kWave; ++i) {
-    kmin = s_mm[0][i] < kmin ? s_mm[0][i] : kmin;
-    kmax = s_mm[1][i] > kmax ? s_mm[1][i] : kmax;
-  }
-  unsigned lo = kmin;
-  unsigned long long width = (unsigned long long)kmax - kmin + 1ull;  // live range [lo, lo + width)
-  int shift = range_shift(width, kHistBits);
-  long long rem = rank_lo;
-  for (int pass = 0; pass < 4; ++pass) {
-    for (int i = threadIdx.x; i < kHistBins; i += kSelectThreads) s_hist[i] = 0;
-    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kSamplePerThread; ++i) {
-      const int j = threadIdx.x + i * kSelectThreads;
-      const unsigned key = keys[i];
-      const unsigned long long rel = (unsigned long long)key - lo;
-      const bool valid = j < S && key >= lo && rel < width;
-      hist_add(s_hist, (unsigned)(rel >> shift), valid);
-    }
-    __syncthreads();
-    if (threadIdx.x < kWave) wave_select_from_top<kHistBins>(s_hist, rem, &s_digit, &s_rem, &s_err);
-    __syncthreads();
-    lo += s_digit << shift;
-    rem = s_rem;
-    __syncthreads();
-    if (shift == 0) break;
-    width = 1ull << shift;
-    shift = shift > kHistBits ? shift - kHistBits : 0;
+  for (int i = 0; i < kSamplePerThread; ++i) hist_add(s_hist[0], keys[i] >> 21, tid + i * kSelectThreads < S);
+  __syncthreads();
+  if (wid == 0) wave_select_from_top<kHistBins>(s_hist[0], rank_lo, &s_digit[0], &s_rem[0], &s_err);
+  else if (wid == 1 && two) wave_select_from_top<kHistBins>(s_hist[0], rank_hi, &s_digit[1], &s_rem[1], &s_err);
+  __syncthreads();
+  const unsigned d0 = s_digit[0], d1 = two ? s_digit[1] : 0u;
+  const long long r0 = s_rem[0], r1 = two ? s_rem[1] : 0;
+  for (int i = tid; i < 2 * kHistBins; i += kSelectThreads) (&s_hist[0][0])[i] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSamplePerThread; ++i) {
+    const bool in = tid + i * kSelectThreads < S;
+    const unsigned hi = keys[i] >> 21, bin = (keys[i] >> 10) & (kHistBins - 1);
+    hist_add(s_hist[0], bin, in && hi == d0);
+    if (two) hist_add(s_hist[1], bin, in && hi == d1);
   }
-  if (threadIdx.x == 0) w.p->t_lo = lo;
+  __syncthreads();
+  if (wid == 0) wave_select_from_top<kHistBins>(s_hist[0], r0, &s_digit[0], &s_rem[0], &s_err);
+  else if (wid == 1 && two) wave_select_from_top<kHistBins>(s_hist[1], r1, &s_digit[1], &s_rem[1], &s_err);
+  __syncthreads();
+  if (tid == 0) {
+    unsigned t_lo = (d0 << 21) | (s_digit[0] << 10);
+    unsigned long long t_hi = two ? (unsigned long long)((d1 << 21) | (s_digit[1] << 10)) + 1024ull : 1ull << 32;
+    if (s_err) {  // cannot happen for 0 < rank <= S; stay correct anyway: everything is a candidate
+      t_lo = 0u;
+      t_hi = 1ull << 32;
+    }
+    w.p->t_lo = t_lo;
+    w.p->t_hi = t_hi;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -326,90 +334,139 @@ __device__ __forceinline__ float floor_value(unsigned t_lo) {
   return t_lo <= 0x007fffffu ? -__builtin_inff() : key_value(t_lo);  // keys below -inf: negative NaNs
 }
 
-// one 1024-element step of a wave: 4 x float4 per lane (q-major: lane l, q -> elements 256q + 4l + c)
-template <bool TAIL>
-__device__ __forceinline__ void filter_step(const float* __restrict__ x, int64_t base, int64_t e_end, float tf,
-                                            uint2* __restrict__ out, unsigned& cnt, float& vmax, bool& saw_nan,
-                                            int lane) {
-  float4 v[4];
+__device__ __forceinline__ bool is_cand(float a, float tf) { return a >= tf || a != a; }
+
+// one wave's 4096-element span of a block step: 16 float4 per lane (q-major: lane l, step q ->
+// elements 256q + 4l + c).  A partial span (the last block only) clamps each float4 to the last one
+// holding valid data (16-B aligned, so it never crosses a page); `lim` masks everything past b_end.
+template <bool FULL>
+__device__ __forceinline__ void filter_load(const float* __restrict__ x, int64_t wb, int64_t b_end, int lane,
+                                            float4 (&v)[16]) {
+  if (FULL) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t e = base + 256 * q + 4 * lane;
-    if (!TAIL) {
-      v[q] = ld_stream(x + e);
-    } else {
-      v[q].x = e + 0 < e_end ? x[e + 0] : -__builtin_inff();
-      v[q].y = e + 1 < e_end ? x[e + 1] : -__builtin_inff();
-      v[q].z = e + 2 < e_end ? x[e + 2] : -__builtin_inff();
-      v[q].w = e + 3 < e_end ? x[e + 3] : -__builtin_inff();
-    }
-  }
+    for (int q = 0; q < 16; ++q) v[q] = ld_stream(x + wb + 256 * q + 4 * lane);
+  } else {
+    const int64_t last4 = (b_end - 1) & ~(int64_t)3;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float a0 = v[q].x, a1 = v[q].y, a2 = v[q].z, a3 = v[q].w;
-    vmax = fmaxf(vmax, fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));  // fmaxf ignores NaN; NaN tracked apart
-    const bool n0 = a0 != a0, n1 = a1 != a1, n2 = a2 != a2, n3 = a3 != a3;
-    saw_nan |= n0 | n1 | n2 | n3;
-    // tail padding is -inf, which passes only when tf == -inf: exclude it explicitly there
-    const int64_t e = base + 256 * q + 4 * lane;
-    const bool f0 = (a0 >= tf || n0) && (!TAIL || e + 0 < e_end);
-    const bool f1 = (a1 >= tf || n1) && (!TAIL || e + 1 < e_end);
-    const bool f2 = (a2 >= tf || n2) && (!TAIL || e + 2 < e_end);
-    const bool f3 = (a3 >= tf || n3) && (!TAIL || e + 3 < e_end);
-    const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
-    if ((m0 | m1 | m2 | m3) == 0ull) continue;
-    unsigned pos = cnt;
-    pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m0, pos));
-    pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m1, pos));
-    pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, pos));
-    pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m3, pos));
-    if (f0 | f1 | f2 | f3) {
-      if (f0) out[pos++] = make_uint2((unsigned)(e + 0), __float_as_uint(a0));
-      if (f1) out[pos++] = make_uint2((unsigned)(e + 1), __float_as_uint(a1));
-      if (f2) out[pos++] = make_uint2((unsigned)(e + 2), __float_as_uint(a2));
-      if (f3) out[pos++] = make_uint2((unsigned)(e + 3), __float_as_uint(a3));
+    for (int q = 0; q < 16; ++q) {
+      const int64_t e = wb + 256 * q + 4 * lane;
+      v[q] = *reinterpret_cast<const float4*>(x + (e < last4 ? e : last4));
     }
-    cnt += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
   }
 }
 
-__global__ __launch_bounds__(kThreads) void topk_filter_kernel(const float* __restrict__ x, int64_t n,
-                                                               int64_t wave_chunk, TopkWs w) {
+template <bool FULL>
+__device__ __forceinline__ bool in_span(int o, int lim) { return FULL || o < lim; }
+
+// this lane's candidate flags (bit 4q + c, kept in VGPRs so the write pass does not re-derive 64
+// wave masks); running max and NaN flag for the region's max key
+template <bool FULL>
+__device__ __forceinline__ void filter_flags(const float4 (&v)[16], float tf, int lim, int lane, float& vmax,
+                                             bool& saw_nan, unsigned (&fl)[2]) {
+  fl[0] = fl[1] = 0u;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int o = 256 * q + 4 * lane;
+    const float ninf = -__builtin_inff();  // past b_end (partial spans): neutral for max and NaN
+    const bool i0 = in_span<FULL>(o + 0, lim), i1 = in_span<FULL>(o + 1, lim);
+    const bool i2 = in_span<FULL>(o + 2, lim), i3 = in_span<FULL>(o + 3, lim);
+    const float a0 = i0 ? v[q].x : ninf, a1 = i1 ? v[q].y : ninf, a2 = i2 ? v[q].z : ninf, a3 = i3 ? v[q].w : ninf;
+    vmax = fmaxf(vmax, fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));  // fmaxf ignores NaN; NaN tracked apart
+    saw_nan |= (a0 != a0) | (a1 != a1) | (a2 != a2) | (a3 != a3);
+    const unsigned nib = (unsigned)(is_cand(a0, tf) && i0) | ((unsigned)(is_cand(a1, tf) && i1) << 1) |
+                         ((unsigned)(is_cand(a2, tf) && i2) << 2) | ((unsigned)(is_cand(a3, tf) && i3) << 3);
+    fl[q >> 3] |= nib << (4 * (q & 7));
+  }
+}
+
+// ordered append from position `pos` (element order within a step q: lane-major, then the 4 components)
+__device__ __forceinline__ void filter_write(const float4 (&v)[16], const unsigned (&fl)[2], int lane, unsigned wbu,
+                                             unsigned pos, uint2* __restrict__ out) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const unsigned nib = (fl[q >> 3] >> (4 * (q & 7))) & 15u;
+    const bool f0 = nib & 1u, f1 = nib & 2u, f2 = nib & 4u, f3 = nib & 8u;
+    const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
+    if ((m0 | m1 | m2 | m3) != 0ull) {
+      unsigned p = pos;
+      p = __builtin_amdgcn_mbcnt_hi((unsigned)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m0, p));
+      p = __builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m1, p));
+      p = __builtin_amdgcn_mbcnt_hi((unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, p));
+      p = __builtin_amdgcn_mbcnt_hi((unsigned)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m3, p));
+      const unsigned e = wbu + (unsigned)(256 * q + 4 * lane);
+      if (f0) out[p++] = make_uint2(e + 0u, __float_as_uint(v[q].x));
+      if (f1) out[p++] = make_uint2(e + 1u, __float_as_uint(v[q].y));
+      if (f2) out[p++] = make_uint2(e + 2u, __float_as_uint(v[q].z));
+      if (f3) out[p++] = make_uint2(e + 3u, __float_as_uint(v[q].w));
+      pos += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+    }
+  }
+}
+
+// one block step (4 waves x 4096 elements): load, flag, exchange the wave counts, append in order
+template <bool FULL>
+__device__ __forceinline__ void filter_step(const float* __restrict__ x, int64_t s, int64_t b_end, float tf,
+                                            uint2* __restrict__ out, unsigned* s_cnt, unsigned& run, float& vmax,
+                                            bool& saw_nan) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+  const int64_t wb = s + (int64_t)wid * kWaveSpan;
+  const int lim = FULL ? kWaveSpan : (int)(b_end > wb ? (b_end - wb < kWaveSpan ? b_end - wb : kWaveSpan) : 0);
+  float4 v[16];
+  unsigned fl[2];
+  filter_load<FULL>(x, wb, b_end, lane, v);
+  filter_flags<FULL>(v, tf, lim, lane, vmax, saw_nan, fl);
+  const unsigned wcnt = wave_sum((unsigned)(__popc(fl[0]) + __popc(fl[1])));
+  if (lane == 0) s_cnt[wid] = wcnt;
+  __syncthreads();
+  unsigned pos = run, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kFNW; ++i) {
+    const unsigned c = s_cnt[i];
+    pos += i < wid ? c : 0u;
+    tot += c;
+  }
+  run += tot;
+  if (wcnt != 0u) filter_write(v, fl, lane, (unsigned)wb, pos, out);
+}
+
+__global__ __launch_bounds__(kThreads) void topk_filter_kernel(const float* __restrict__ x, int64_t n, int64_t chunk,
+                                                               int sel_grid, TopkWs w) {
+  __shared__ unsigned s_cnt[2][kFNW];
+  __shared__ unsigned s_mx[kFNW];
   const float tf = floor_value(w.p->t_lo);
   if (blockIdx.x == 0) {  // reset the select state of this call (read by the next launch)
-    for (int i = threadIdx.x; i < 3 * kHistBins; i += kThreads) w.hist[i] = 0u;
-    if (threadIdx.x < kShards + 1) w.bar[threadIdx.x] = 0u;
+    for (int i = threadIdx.x; i < kMaxRounds * kHistStride; i += kThreads) w.hist[i] = 0u;
+    for (int i = threadIdx.x; i < sel_grid; i += kThreads) w.flags[i * kFlagStride] = 0u;
     if (threadIdx.x < (int)(sizeof(SelState) / 8)) reinterpret_cast<unsigned long long*>(w.st)[threadIdx.x] = 0ull;
   }
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t r = (int64_t)blockIdx.x * kNW + (threadIdx.x >> 6);
-  const int64_t e_begin = r * wave_chunk;
-  const int64_t e_end = e_begin + wave_chunk < n ? e_begin + wave_chunk : n;
-  uint2* __restrict__ out = w.stage + r * w.region_cap;
-  unsigned cnt = 0;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+  const int64_t b_begin = (int64_t)blockIdx.x * chunk;
+  const int64_t b_end = b_begin + chunk < n ? b_begin + chunk : n;
+  uint2* __restrict__ out = w.stage + (int64_t)blockIdx.x * w.region_cap;
+  unsigned run = 0;
   float vmax = -__builtin_inff();
   bool saw_nan = false;
-  int64_t base = e_begin;
-  for (; base + kStep <= e_end; base += kStep) filter_step<false>(x, base, e_end, tf, out, cnt, vmax, saw_nan, lane);
-  if (base < e_end) filter_step<true>(x, base, e_end, tf, out, cnt, vmax, saw_nan, lane);
+  int par = 0;  // the wave-count slots alternate, so one barrier per step suffices
+  int64_t s = b_begin;
+  for (; s + kBlockSpan <= b_end; s += kBlockSpan, par ^= 1)
+    filter_step<true>(x, s, b_end, tf, out, s_cnt[par], run, vmax, saw_nan);
+  if (s < b_end) filter_step<false>(x, s, b_end, tf, out, s_cnt[par], run, vmax, saw_nan);
   unsigned mx = order_key(__float_as_uint(vmax));
   mx = __ballot(saw_nan) ? 0xffffffffu : mx;
   mx = wave_max_u32(mx);
-  if (lane == 0) {
-    w.region_cnt[r] = e_begin < n ? cnt : 0u;
-    w.region_max[r] = e_begin < n ? mx : 0u;
+  if (lane == 0) s_mx[wid] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned m = 0;
+    for (int i = 0; i < kFNW; ++i) m = s_mx[i] > m ? s_mx[i] : m;
+    w.region_cnt[blockIdx.x] = run;
+    w.region_max[blockIdx.x] = b_begin < n ? m : 0u;
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// persistent select: P0 scan | P1 gather + round 1 | rounds 2-3 | counts | compaction
+// persistent select: P0 scan | radix rounds | counts | compaction
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ unsigned long long ld_mem64(unsigned long long* p) {
-  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_mem64(unsigned long long* p, unsigned long long v) {
-  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // the per-block copy of the leader-published state
 struct SelView {
@@ -419,40 +476,42 @@ struct SelView {
   long long rem;
   int done;
   unsigned T;
-  long long need, ties;
+  long long need;
 };
 
-// Grid barrier: every block arrives on its XCD shard counter, the last of each shard on the top
-// counter; the last arriver overall runs `lead` (all of its threads) and then bumps the generation
-// word the others poll (relaxed agent-scope loads + s_sleep, bounded).  Counters are monotonic within
-// a call, so barrier number `nbar` waits for (nbar + 1) full sets of arrivals.
+// Grid barrier: every block but 0 raises its arrival flag (one 64-B line each, no contended
+// counter); block 0 polls all flags in parallel, runs `lead` (all of its threads) and bumps the
+// generation word the others poll (relaxed agent-scope loads + s_sleep, bounded).
 template <typename F>
 __device__ void grid_barrier(const TopkWs& w, unsigned nbar, F&& lead) {
-  __shared__ int s_lead;
+  const unsigned target = nbar + 1;
   drain_stores();
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned nb = gridDim.x, shard = blockIdx.x % kShards;
-    const unsigned shard_size = (nb - shard + kShards - 1) / kShards;
-    const unsigned active = nb < (unsigned)kShards ? nb : (unsigned)kShards;
-    int l = 0;
-    if (__hip_atomic_fetch_add(&w.bar[shard], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        shard_size * (nbar + 1) - 1)
-      l = __hip_atomic_fetch_add(&w.bar[kShards], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-          active * (nbar + 1) - 1;
-    s_lead = l;
-  }
-  __syncthreads();
-  if (s_lead) {
+  if (blockIdx.x == 0) {
+    const int tid = threadIdx.x;
+    if (tid > 0 && tid < (int)gridDim.x) {
+      unsigned* f = w.flags + (size_t)tid * kFlagStride;
+      unsigned spins = 0;
+      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 24)) {  // ~1 s: a block never arrived; flag it and let the launch drain
+          __hip_atomic_fetch_or(&w.st->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
     lead();
     drain_stores();
     __syncthreads();
-    if (threadIdx.x == 0) st_mem64(&w.st->gen, nbar + 1);
+    if (tid == 0) st_mem64(&w.st->gen, target);
   } else if (threadIdx.x == 0) {
+    (void)__hip_atomic_exchange(w.flags + (size_t)blockIdx.x * kFlagStride, target, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
-    while (__hip_atomic_load(&w.st->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nbar + 1ull) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {  // ~1 s: a block never arrived; flag it and let the launch drain
+    while (__hip_atomic_load(&w.st->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {
         __hip_atomic_fetch_or(&w.st->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -470,37 +529,70 @@ __device__ void read_view(const TopkWs& w, SelView* v) {
     v->done = (int)ld_mem64(&w.st->done);
     v->T = (unsigned)ld_mem64(&w.st->T);
     v->need = (long long)ld_mem64(&w.st->need);
-    v->ties = (long long)ld_mem64(&w.st->ties);
   }
   __syncthreads();
 }
 
-// leader step of a radix round: digit of the rank `rem` in the global histogram of round r
-__device__ void lead_pick(const TopkWs& w, int r, const SelView& cur, unsigned* s_hist) {
+// leader step of a radix round.  `rem` is the rank (from the top) of the k-th largest key among all
+// keys >= lo, so it stays k; the round's `A` keys above the live range come first: if A >= rem the
+// key lies above the range (re-range to [lo + width, top)), otherwise pick the bin of rank rem - A in
+// the global histogram of round r and narrow the range to it.
+__device__ void lead_pick(const TopkWs& w, int r, const SelView& cur, unsigned long long top, unsigned* s_ghist) {
   __shared__ unsigned s_digit;
   __shared__ long long s_rem;
   __shared__ unsigned s_err;
-  for (int i = threadIdx.x; i < kHistBins; i += kSelThreads) s_hist[i] = ld_mem(&w.hist[r * kHistBins + i]);
-  if (threadIdx.x == 0) s_err = 0;
+  __shared__ long long s_above;
+  unsigned* h = w.hist + (size_t)r * kHistStride;
+  for (int i = threadIdx.x; i < kHistBins; i += kSelThreads) s_ghist[i] = ld_mem(&h[i]);
+  if (threadIdx.x == 0) {
+    s_err = 0;
+    s_above = (long long)ld_mem(&h[kHistBins]);
+    st_mem64(&w.st->rounds, (unsigned long long)r + 1ull);
+  }
   __syncthreads();
-  if (threadIdx.x < kWave) wave_select_from_top<kHistBins>(s_hist, cur.rem, &s_digit, &s_rem, &s_err);
+  const long long A = s_above;
+  if (A >= cur.rem) {  // the k-th largest key is above the range (block-uniform branch)
+    if (threadIdx.x == 0) {
+      const unsigned long long nlo = (unsigned long long)cur.lo + cur.width;
+      const unsigned long long nw = top > nlo ? top - nlo : 0ull;
+      if (nw == 0ull) __hip_atomic_fetch_or(&w.st->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st_mem64(&w.st->lo, nlo);
+      st_mem64(&w.st->width, nw);
+      st_mem64(&w.st->shift, (unsigned long long)range_shift(nw, kHistBits));
+      st_mem64(&w.st->rem, (unsigned long long)cur.rem);
+    }
+    return;
+  }
+  if (threadIdx.x < kWave) wave_select_from_top<kHistBins>(s_ghist, cur.rem - A, &s_digit, &s_rem, &s_err);
   __syncthreads();
   if (threadIdx.x == 0) {
+    unsigned long long* tr = w.trace + r * 8;
+    tr[0] = cur.lo; tr[1] = cur.width; tr[2] = (unsigned long long)cur.shift; tr[3] = (unsigned long long)cur.rem;
+    tr[4] = (unsigned long long)A; tr[5] = s_digit; tr[6] = (unsigned long long)s_rem; tr[7] = s_ghist[s_digit];
     const unsigned nlo = cur.lo + (s_digit << cur.shift);
     if (s_err) __hip_atomic_fetch_or(&w.st->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur.shift == 0) {
       st_mem64(&w.st->T, nlo);
       st_mem64(&w.st->need, (unsigned long long)s_rem);
-      st_mem64(&w.st->ties, s_hist[s_digit]);
       st_mem64(&w.st->done, 1ull);
     } else {
+      const unsigned long long nw = 1ull << cur.shift;
       st_mem64(&w.st->lo, nlo);
-      st_mem64(&w.st->width, 1ull << cur.shift);
-      st_mem64(&w.st->shift, (unsigned long long)(cur.shift > kHistBits ? cur.shift - kHistBits : 0));
-      st_mem64(&w.st->rem, (unsigned long long)s_rem);
+      st_mem64(&w.st->width, nw);
+      st_mem64(&w.st->shift, (unsigned long long)range_shift(nw, kHistBits));
+      st_mem64(&w.st->rem, (unsigned long long)cur.rem);  // rank from the top among keys >= lo: unchanged
     }
   }
 }
+
+#ifdef FLC_SELECT_STAMPS
+#define STAMP(i)                                                                                 \
+  do {                                                                                           \
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.stamps[i] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
 
 template <bool STACKED>
 __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* __restrict__ x, TopkWs w, int R,
@@ -510,11 +602,14 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
                                                                   float* __restrict__ norm_out, int levels, double step,
                                                                   uint64_t seed, uint64_t counter) {
   __shared__ unsigned s_off[kMaxRegions + 1];
+  __shared__ __attribute__((aligned(16))) unsigned s_keys[kKeyCache];
   __shared__ unsigned s_hist[kHistBins];
+  __shared__ unsigned s_ghist[kHistBins];
   __shared__ unsigned long long s_red[kSelNW];
   __shared__ unsigned s_mx[kSelNW];
   __shared__ SelView s_view;
   const int tid = threadIdx.x;
+  STAMP(0);
 
   // ---- P0: region offsets in LDS, candidate count, max key (identical in every block)
   {
@@ -552,62 +647,82 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
   const unsigned long long c_cand = s_red[0];
   unsigned maxkey = 0;
   for (int i = 0; i < kSelNW; ++i) maxkey = s_mx[i] > maxkey ? s_mx[i] : maxkey;
+  __syncthreads();  // s_red is reused below
   const bool fb = (long long)c_cand < k;
   const long long C = fb ? (long long)n : (long long)c_cand;
   long long per = (C + gridDim.x - 1) / gridDim.x;
   per = (per + 3) & ~3ll;
   const long long v0 = min((long long)blockIdx.x * per, C), v1 = min(v0 + per, C);
+  const bool cached = per <= kKeyCache;  // grid-uniform
 
+  const unsigned long long top = (unsigned long long)maxkey + 1ull;
   SelView cur;
   cur.lo = fb ? 0u : w.p->t_lo;
-  cur.width = (unsigned long long)maxkey - cur.lo + 1ull;
+  unsigned long long hi_end = fb ? top : min(w.p->t_hi, top);
+  if (hi_end <= (unsigned long long)cur.lo) hi_end = top;
+  cur.width = hi_end - cur.lo;
   cur.shift = range_shift(cur.width, kHistBits);
   cur.rem = k;
   cur.done = 0;
+  cur.T = 0;
+  cur.need = 0;
+  SelView prev = cur;
+  unsigned long long a_blk = 0;  // keys above the live range in this block (last round)
   unsigned nbar = 0;
+  STAMP(1);
 
-  // ---- P1 + rounds: histogram of the live range, leader picks the digit
-  for (int round = 0; round < 3; ++round) {
+  // ---- radix rounds: histogram of the live range (+ count above it), leader picks the digit
+  for (int round = 0; round < kMaxRounds; ++round) {
     for (int i = tid; i < kHistBins; i += kSelThreads) s_hist[i] = 0u;
     __syncthreads();
+    unsigned above = 0;
     int r = 0;
     if (round == 0 && !fb && v0 + 4 * (long long)tid < v1) r = lds_region_search(s_off, R, (unsigned)(v0 + 4 * tid));
     for (long long c0 = v0 + 4 * tid; c0 < v1; c0 += 4 * kSelThreads) {
       unsigned raw[4];
-      if (fb) {
-        if (c0 + 4 <= v1) {
-          const float4 v = *reinterpret_cast<const float4*>(x + c0);
-          raw[0] = __float_as_uint(v.x); raw[1] = __float_as_uint(v.y);
-          raw[2] = __float_as_uint(v.z); raw[3] = __float_as_uint(v.w);
-        } else {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) raw[u] = c0 + u < v1 ? __float_as_uint(x[c0 + u]) : 0u;
-        }
-      } else if (round == 0) {
-        unsigned id[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const long long c = c0 + u;
-          if (c < v1) {
-            r = lds_region_advance(s_off, R, r, (unsigned)c);
-            const uint2 e = w.stage[(long long)r * w.region_cap + (c - s_off[r])];
-            id[u] = e.x;
-            raw[u] = e.y;
+      if (round == 0) {
+        if (fb) {
+          if (c0 + 4 <= v1) {
+            const float4 v = *reinterpret_cast<const float4*>(x + c0);
+            raw[0] = __float_as_uint(v.x); raw[1] = __float_as_uint(v.y);
+            raw[2] = __float_as_uint(v.z); raw[3] = __float_as_uint(v.w);
           } else {
-            id[u] = 0u;
-            raw[u] = 0u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) raw[u] = c0 + u < v1 ? __float_as_uint(x[c0 + u]) : 0u;
+          }
+        } else {
+          unsigned id[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const long long c = c0 + u;
+            if (c < v1) {
+              r = lds_region_advance(s_off, R, r, (unsigned)c);
+              const uint2 e = w.stage[(long long)r * w.region_cap + (c - s_off[r])];
+              id[u] = e.x;
+              raw[u] = e.y;
+            } else {
+              id[u] = 0u;
+              raw[u] = 0u;
+            }
+          }
+          if (c0 + 4 <= v1) {
+            *reinterpret_cast<uint4*>(w.cand_idx + c0) = make_uint4(id[0], id[1], id[2], id[3]);
+            if (!cached) *reinterpret_cast<uint4*>(w.cand_raw + c0) = make_uint4(raw[0], raw[1], raw[2], raw[3]);
+          } else {
+            for (int u = 0; u < 4; ++u)
+              if (c0 + u < v1) {
+                w.cand_idx[c0 + u] = id[u];
+                if (!cached) w.cand_raw[c0 + u] = raw[u];
+              }
           }
         }
-        if (c0 + 4 <= v1) {
-          *reinterpret_cast<uint4*>(w.cand_idx + c0) = make_uint4(id[0], id[1], id[2], id[3]);
-          *reinterpret_cast<uint4*>(w.cand_raw + c0) = make_uint4(raw[0], raw[1], raw[2], raw[3]);
-        } else {
-          for (int u = 0; u < 4; ++u)
-            if (c0 + u < v1) {
-              w.cand_idx[c0 + u] = id[u];
-              w.cand_raw[c0 + u] = raw[u];
-            }
-        }
+        if (cached) *reinterpret_cast<uint4*>(s_keys + (c0 - v0)) = make_uint4(raw[0], raw[1], raw[2], raw[3]);
+      } else if (cached) {  // re-read what this thread cached in round 0
+        const uint4 t = *reinterpret_cast<const uint4*>(s_keys + (c0 - v0));
+        raw[0] = t.x; raw[1] = t.y; raw[2] = t.z; raw[3] = t.w;
+      } else if (fb) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) raw[u] = c0 + u < v1 ? __float_as_uint(x[c0 + u]) : 0u;
       } else if (c0 + 4 <= v1) {  // re-read what this thread wrote in round 0
         const uint4 t = *reinterpret_cast<const uint4*>(w.cand_raw + c0);
         raw[0] = t.x; raw[1] = t.y; raw[2] = t.z; raw[3] = t.w;
@@ -619,37 +734,42 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
       for (int u = 0; u < 4; ++u) {
         const unsigned key = order_key(raw[u]);
         const unsigned long long rel = (unsigned long long)key - cur.lo;
-        const bool valid = c0 + u < v1 && key >= cur.lo && rel < cur.width;
-        hist_add(s_hist, (unsigned)(rel >> cur.shift), valid);
+        const bool in = c0 + u < v1 && key >= cur.lo;
+        above += (in && rel >= cur.width) ? 1u : 0u;
+        hist_add(s_hist, (unsigned)(rel >> cur.shift), in && rel < cur.width);
       }
     }
     __syncthreads();
+    unsigned* h = w.hist + (size_t)round * kHistStride;
     for (int i = tid; i < kHistBins; i += kSelThreads)
-      if (s_hist[i]) atomicAdd(&w.hist[round * kHistBins + i], s_hist[i]);
-    grid_barrier(w, nbar++, [&] { lead_pick(w, round, cur, s_hist); });
+      if (s_hist[i]) atomicAdd(&h[i], s_hist[i]);
+    a_blk = block_sum<unsigned long long, kSelNW>((unsigned long long)above, s_red);
+    if (tid == 0 && a_blk) atomicAdd(&h[kHistBins], (unsigned)a_blk);
+    STAMP(2 + 2 * round);
+    prev = cur;
+    grid_barrier(w, nbar++, [&] { lead_pick(w, round, cur, top, s_ghist); });
+    STAMP(3 + 2 * round);
     read_view(w, &s_view);
     cur = s_view;
     __syncthreads();
     if (cur.done) break;
   }
+  if (!cur.done && blockIdx.x == 0 && tid == 0)
+    __hip_atomic_fetch_or(&w.st->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-  // ---- counts: strict / ties of T per block, scanned by the leader
+  // ---- counts from the resolving round's local histogram: strict = above + bins past T's bin
   const unsigned T = cur.T;
   {
-    unsigned long long cnt = 0;  // strict << 32 | tie
-    for (long long c0 = v0 + 4 * tid; c0 < v1; c0 += 4 * kSelThreads) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const long long c = c0 + u;
-        if (c < v1) {
-          const unsigned key = order_key(fb ? __float_as_uint(x[c]) : w.cand_raw[c]);
-          cnt += (key > T ? (1ull << 32) : 0ull) + (key == T ? 1ull : 0ull);
-        }
-      }
+    const unsigned d = T - prev.lo;  // the resolving round has shift 0: bin = key - lo
+    unsigned long long cnt = 0;      // strict << 32 | tie
+    for (int i = tid; i < kHistBins; i += kSelThreads) {
+      const unsigned hv = s_hist[i];
+      cnt += ((unsigned)i > d ? ((unsigned long long)hv << 32) : 0ull) + ((unsigned)i == d ? hv : 0ull);
     }
-    const unsigned long long both = block_sum<unsigned long long, kSelNW>(cnt, s_red);
+    const unsigned long long both = block_sum<unsigned long long, kSelNW>(cnt, s_red) + (a_blk << 32);
     if (tid == 0) st_mem64(&w.blk_cnt[blockIdx.x], both);
   }
+  STAMP(14);
   grid_barrier(w, nbar++, [&] {
     const unsigned long long v = tid < (int)gridDim.x ? ld_mem64(&w.blk_cnt[tid]) : 0ull;
     unsigned long long tot;
@@ -666,6 +786,7 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
         __hip_atomic_fetch_or(&w.st->err, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   });
+  STAMP(15);
   __shared__ unsigned long long s_off_blk, s_ties;
   if (tid == 0) {
     s_off_blk = ld_mem64(&w.blk_off[blockIdx.x]);
@@ -686,11 +807,16 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
   for (long long base = v0; base < v1; base += 4 * kSelThreads) {
     const long long c0 = base + 4 * tid;
     unsigned raw[4], id[4];
+    if (cached) {
+      const uint4 t = *reinterpret_cast<const uint4*>(s_keys + (c0 < v1 ? c0 - v0 : 0));
+      raw[0] = t.x; raw[1] = t.y; raw[2] = t.z; raw[3] = t.w;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const long long c = c0 + u;
       const bool in = c < v1;
-      raw[u] = in ? (fb ? __float_as_uint(x[c]) : w.cand_raw[c]) : 0u;
+      if (!cached) raw[u] = in ? (fb ? __float_as_uint(x[c]) : w.cand_raw[c]) : 0u;
+      raw[u] = in ? raw[u] : 0u;
       id[u] = in ? (fb ? (unsigned)c : w.cand_idx[c]) : 0u;
     }
     bool is_s[4], is_t[4];
@@ -713,13 +839,9 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
       for (int u = 0; u < 4; ++u) {
         const float v = __uint_as_float(raw[u]);
         const float y = nrm_ok ? fabsf(v) / nrm : 0.0f;  // compressors.py:344
-        const int j = level_lower_bound<0>(y, levels, step);
-        const int sl = j > 0 ? j - 1 : 0;
-        const double lo = level_value<0>(sl, levels, step), hi = level_value<0>(sl + 1, levels, step);
-        const double p = ((double)y - hi) / (lo - hi);  // compressors.py:348
         const U4 r4 = philox_group((uint64_t)id[u] >> 2, seed, counter);
         const double uu = u01(pick(r4, (int)(id[u] & 3u)));
-        const uint32_t lvl = (uint32_t)((uu < p) ? sl : sl + 1);
+        const uint32_t lvl = (uint32_t)dither_level<0>(y, levels, step, uu);  // compressors.py:346-353
         const uint32_t c = nrm_ok ? (((raw[u] >> 31) << 7) | lvl) : 1u;
         code[u] = (v != 0.0f) ? c : 0u;
       }
@@ -739,6 +861,7 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
     run_s += (long long)(tot >> 32);
     run_t += (long long)(tot & 0xffffffffull);
   }
+  STAMP(13);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -746,7 +869,7 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
 // ------------------------------------------------------------------------------------------------
 struct SampleSetup {
   int S;
-  long long rank_lo;
+  long long rank_lo, rank_hi;
   int take_all;
 };
 
@@ -754,8 +877,9 @@ SampleSetup sample_setup(int64_t n, int64_t k) {
   SampleSetup s;
   s.S = (int)(n < kSample ? n : kSample);
   const double m = (double)s.S * (double)k / (double)n;
-  const double r = ceil(m + 4.0 * sqrt(m) + 16.0);
-  s.rank_lo = (long long)r;
+  s.rank_lo = (long long)ceil(m + 4.0 * sqrt(m) + 16.0);
+  const double rh = floor(m - 4.0 * sqrt(m) - 16.0);
+  s.rank_hi = rh >= 1.0 ? (long long)rh : 0;
   s.take_all = (s.rank_lo >= s.S) ? 1 : 0;
   if (s.take_all) s.rank_lo = s.S;
   return s;
@@ -775,6 +899,7 @@ SelectGate& gate() {
 
 int select_grid(int dev) {
   SelectGate& g = gate();
+  std::lock_guard<std::mutex> lk(g.mu);
   if (g.grid[dev] == 0) {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0) cu = 256;
@@ -789,16 +914,16 @@ int launch_topk(const float* x, int64_t n, int64_t k, const TopkWs& w, hipStream
   const TopkGeom g = geometry(n);
   const SampleSetup ss = sample_setup(n, k);
   const int R = (int)g.regions;
-  if (!ss.take_all)
-    FLC_LAUNCH("topk_sample_gather", topk_sample_gather_kernel, dim3((unsigned)cdiv(ss.S, kThreads)), dim3(kThreads), 0,
-               st, x, n, ss.S, w);
-  FLC_LAUNCH("topk_sample_select", topk_sample_select_kernel, dim3(1), dim3(kSelectThreads), 0, st, ss.S, ss.rank_lo,
-             ss.take_all, w);
-  FLC_LAUNCH("topk_filter", topk_filter_kernel, dim3((unsigned)g.blocks), dim3(kThreads), 0, st, x, n, g.wave_chunk, w);
   int dev = 0;
   FLC_CHECK_HIP(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64) return fail(FLC_EUNSUPPORTED, "device index %d", dev);
   const int grid = select_grid(dev);
+  if (!ss.take_all)
+    FLC_LAUNCH("topk_sample_gather", topk_sample_gather_kernel, dim3((unsigned)cdiv(ss.S, kThreads)), dim3(kThreads), 0,
+               st, x, n, ss.S, w);
+  FLC_LAUNCH("topk_sample_select", topk_sample_select_kernel, dim3(1), dim3(kSelectThreads), 0, st, ss.S, ss.rank_lo,
+             ss.rank_hi, ss.take_all, w);
+  FLC_LAUNCH("topk_filter", topk_filter_kernel, dim3((unsigned)R), dim3(kThreads), 0, st, x, n, g.chunk, grid, w);
   SelectGate& gt = gate();
   std::lock_guard<std::mutex> lk(gt.mu);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
