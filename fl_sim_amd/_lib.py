@@ -13,7 +13,8 @@ import os
 import threading
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libflcodec.so")
+# FLC_LIB overrides the path (calibration builds under tools/ only)
+LIB_PATH = os.environ.get("FLC_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libflcodec.so")
 
 FLC_OK = 0
 FLC_Q_STANDARD_DITHER = 0

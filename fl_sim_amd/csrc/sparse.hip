@@ -109,6 +109,130 @@ __global__ __launch_bounds__(kThreads) void sparse_decode_kernel(const int* __re
   }
 }
 
+// raw wire word of kept entry j (MODE 0: fp32 bits of val; MODE 1: the code byte) and its decoded value
+template <int MODE>
+__device__ __forceinline__ uint32_t entry_raw(const float* __restrict__ val, const uint8_t* __restrict__ codes,
+                                              unsigned j) {
+  return MODE == 0 ? __float_as_uint(val[j]) : (uint32_t)codes[j];
+}
+template <int MODE>
+__device__ __forceinline__ float entry_value(uint32_t raw, float scale, int levels, double step, float nrm) {
+  if (MODE == 0) return scale * __uint_as_float(raw);
+  if (!(nrm > 0.0f && nrm <= 3.402823466e38f)) return raw == 0u ? 0.0f : __uint_as_float(0x7fc00000u);
+  const float lv = (float)level_value<0>((int)(raw & 127u), levels, step);
+  return ((raw >> 7) ? -lv : lv) * nrm;  // compressors.py:357
+}
+
+// Streaming decode: persistent blocks, block b owns the contiguous tiles [b * tpb, (b + 1) * tpb) of
+// kStreamTile outputs.  While tile t is assembled in LDS and stored, the first kept entry per thread of
+// tile t + 1 (and, accumulating, its slice of `out`) is already in flight, so no store waits on a
+// dependent load chain.  Tiles with more than 256 kept entries take the rest straight from memory.
+constexpr int kStreamTile = kThreads * 16;  // 4096 outputs, 4 float4 per thread
+constexpr int kMaxTilesPerBlock = 512;
+
+template <int MODE, bool ACC>
+__global__ __launch_bounds__(kThreads) void sparse_decode_stream_kernel(
+    const int* __restrict__ idx, const float* __restrict__ val, const uint8_t* __restrict__ codes, float scale,
+    int levels, double step, const float* __restrict__ norm_ptr, int64_t n, float weight, float* __restrict__ out,
+    const unsigned* __restrict__ tile_start, int64_t ntiles, int tpb) {
+  __shared__ __attribute__((aligned(16))) float s_tile[kStreamTile];
+  __shared__ unsigned s_ts[kMaxTilesPerBlock + 1];
+  const int tid = threadIdx.x;
+  const int64_t tb = (int64_t)blockIdx.x * tpb;
+  const int64_t te = tb + tpb < ntiles ? tb + tpb : ntiles;
+  if (tb >= te) return;
+  const int nt = (int)(te - tb);
+  for (int i = tid; i <= nt; i += kThreads) s_ts[i] = tile_start[tb + i];
+  float4* tile4 = reinterpret_cast<float4*>(s_tile);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) tile4[tid + u * kThreads] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float nrm = MODE == 1 ? *norm_ptr : 0.0f;
+  __syncthreads();
+  // prefetch of tile tb: raw words only, consumed one tile later (no use before the next barrier)
+  unsigned p_idx = 0xffffffffu;
+  uint32_t p_raw = 0u;
+  {
+    const unsigned j = s_ts[0] + tid;
+    if (j < s_ts[1]) {
+      p_idx = (unsigned)idx[j];
+      p_raw = entry_raw<MODE>(val, codes, j);
+    }
+  }
+  float4 p_acc[4];
+  if (ACC) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = tb * kStreamTile + 4 * (int64_t)(tid + u * kThreads);
+      p_acc[u] = e + 4 <= n ? *reinterpret_cast<const float4*>(out + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  for (int i = 0; i < nt; ++i) {
+    const int64_t t0 = (tb + i) * kStreamTile;
+    const unsigned lo = s_ts[i], hi = s_ts[i + 1];
+    // issue the next tile's loads first
+    unsigned n_idx = 0xffffffffu;
+    uint32_t n_raw = 0u;
+    float4 n_acc[4];
+    if (i + 1 < nt) {
+      const unsigned j = hi + tid;
+      if (j < s_ts[i + 2]) {
+        n_idx = (unsigned)idx[j];
+        n_raw = entry_raw<MODE>(val, codes, j);
+      }
+      if (ACC) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t e = t0 + kStreamTile + 4 * (int64_t)(tid + u * kThreads);
+          n_acc[u] = e + 4 <= n ? *reinterpret_cast<const float4*>(out + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+    // scatter this tile's entries
+    if (p_idx != 0xffffffffu) {
+      const int64_t off = (int64_t)p_idx - t0;
+      if (off >= 0 && off < kStreamTile) s_tile[off] = entry_value<MODE>(p_raw, scale, levels, step, nrm);
+    }
+    for (unsigned j = lo + kThreads + tid; j < hi; j += kThreads) {
+      const int64_t off = (int64_t)(unsigned)idx[j] - t0;
+      if (off >= 0 && off < kStreamTile)
+        s_tile[off] = entry_value<MODE>(entry_raw<MODE>(val, codes, j), scale, levels, step, nrm);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + u * kThreads;
+      const int64_t e = t0 + 4 * (int64_t)q;
+      float4 v = tile4[q];
+      tile4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e + 4 <= n) {
+        if (ACC) {
+          const float4 pa = p_acc[u];
+          v = make_float4(fmaf(weight, v.x, pa.x), fmaf(weight, v.y, pa.y), fmaf(weight, v.z, pa.z),
+                          fmaf(weight, v.w, pa.w));
+        } else if (weight != 1.0f) {
+          v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
+        }
+        *reinterpret_cast<float4*>(out + e) = v;
+      } else {
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        for (int c = 0; c < 4 && e + c < n; ++c) {
+          float o = vv[c];
+          if (ACC) o = fmaf(weight, o, out[e + c]);
+          else if (weight != 1.0f) o = weight * o;
+          out[e + c] = o;
+        }
+      }
+    }
+    __syncthreads();
+    p_idx = n_idx;
+    p_raw = n_raw;
+    if (ACC) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p_acc[u] = n_acc[u];
+    }
+  }
+}
+
 // rand-k scatter: out[idx[j]] = scale * x[idx[j]] (out pre-zeroed)
 __global__ __launch_bounds__(kThreads) void randk_scatter_kernel(const float* __restrict__ x, const int* __restrict__ idx,
                                                                  long long k, float scale, float* __restrict__ out) {
@@ -162,6 +286,44 @@ int launch_decode_v(const int32_t* idx, const float* val, const uint8_t* codes, 
   return FLC_OK;
 }
 
+int64_t decode_stream_blocks() {  // persistent grid: FLC_DECODE_BLOCKS or 8 blocks per CU
+  const char* e = getenv("FLC_DECODE_BLOCKS");
+  if (e && atoi(e) > 0) return atoi(e);
+  int dev = 0, cu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || cu <= 0)
+    cu = 256;
+  return (int64_t)cu * 8;
+}
+
+template <int MODE>
+int launch_decode_stream(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale,
+                         int levels, const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws,
+                         size_t ws_bytes, hipStream_t st, const char* name) {
+  constexpr int TILE_LOG = 12;
+  static_assert((1 << TILE_LOG) == kStreamTile, "tile index granularity");
+  const int64_t ntiles = cdiv(n, kStreamTile);
+  const size_t need = (size_t)(ntiles + 1) * sizeof(unsigned);
+  if (!ws || ws_bytes < need) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", name, ws_bytes, need);
+  if (!aligned16(out)) return fail(FLC_EINVAL, "%s: out must be 16-B aligned", name);
+  unsigned* tile_start = static_cast<unsigned*>(ws);
+  const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(k + 1, kThreads), 2048));
+  FLC_LAUNCH("tile_index", tile_index_kernel<TILE_LOG>, dim3(gi), dim3(kThreads), 0, st, idx, (long long)k,
+             (long long)ntiles, tile_start);
+  int64_t grid = std::min<int64_t>(ntiles, decode_stream_blocks());
+  int64_t tpb = cdiv(ntiles, grid);
+  if (tpb > kMaxTilesPerBlock) tpb = kMaxTilesPerBlock;
+  grid = cdiv(ntiles, tpb);
+  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
+  if (accumulate)
+    FLC_LAUNCH(name, (sparse_decode_stream_kernel<MODE, true>), dim3((unsigned)grid), dim3(kThreads), 0, st, idx, val,
+               codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, (int)tpb);
+  else
+    FLC_LAUNCH(name, (sparse_decode_stream_kernel<MODE, false>), dim3((unsigned)grid), dim3(kThreads), 0, st, idx,
+               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, (int)tpb);
+  return FLC_OK;
+}
+
 int decode_variant() {
   const char* e = getenv("FLC_DECODE_VARIANT");
   return e ? atoi(e) : kDecodeVariant;
@@ -172,7 +334,10 @@ int launch_decode(const int32_t* idx, const float* val, const uint8_t* codes, in
                   const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws, size_t ws_bytes,
                   hipStream_t st, const char* name) {
 #define FLC_DV(V, E) return launch_decode_v<MODE, V, E>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name)
-  switch (decode_variant()) {
+  const int dv = decode_variant();
+  if (dv == 90) return launch_decode_stream<MODE>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out,
+                                                  ws, ws_bytes, st, name);
+  switch (dv) {
     case 10: FLC_DV(1, false);
     case 11: FLC_DV(1, true);
     case 20: FLC_DV(2, false);

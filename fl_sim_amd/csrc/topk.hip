@@ -17,11 +17,11 @@
 //                  staging region (ballot/mbcnt compaction, one LDS exchange of wave counts, no
 //                  atomics).  Algorithmic bytes: 4 per element.
 //   select         ONE persistent launch, one 1024-thread block per CU:
-//                    P0  region offsets in LDS (every block), candidate count C, max key;
+//                    P0  region offsets in LDS (every block) and the candidate count C;
 //                    rounds  gather the staged candidates (round 0) into an index-ordered array and an
-//                        LDS key cache, then 2048-bin radix rounds over the live key range (round 0:
-//                        [t_lo, t_hi), keys above it counted apart) until the exact k-th largest key
-//                        T is resolved (usually 2 rounds);
+//                        LDS key cache (and reduce the max key), then 2048-bin radix rounds over the
+//                        live key range (round 0: [t_lo, t_hi), keys above it counted apart) until
+//                        the exact k-th largest key T is resolved (usually 2 rounds);
 //                    counts  strict / tie counts per block come from the resolving round's local
 //                        histogram (no extra pass), scanned by the barrier leader;
 //                    compaction  ordered write of idx[k] / val[k], or, stacked, idx[k] / codes[k]
@@ -46,6 +46,10 @@
 
 namespace flc {
 namespace {
+
+#ifndef FLC_FILTER_VARIANT
+#define FLC_FILTER_VARIANT 0  // != 0 only in calibration builds (tools/calib_variants.sh): results invalid
+#endif
 
 constexpr int kSample = 32768;
 constexpr int kSelectThreads = 1024;
@@ -99,7 +103,6 @@ struct TopkWs {
   unsigned* hist;               // [kMaxRounds][kHistStride]
   unsigned* sample;             // [kSample]
   unsigned* region_cnt;         // [R]
-  unsigned* region_max;         // [R]
   unsigned long long* blk_cnt;  // [kMaxSelBlocks]  strict << 32 | tie
   unsigned long long* blk_off;  // [kMaxSelBlocks]
   unsigned* cand_idx;           // [n]  ordered by index
@@ -137,7 +140,6 @@ TopkWs carve_topk(void* ws, size_t bytes, int64_t n, size_t* need) {
   w.hist = c.take<unsigned>((size_t)kMaxRounds * kHistStride);
   w.sample = c.take<unsigned>(kSample);
   w.region_cnt = c.take<unsigned>(g.regions);
-  w.region_max = c.take<unsigned>(g.regions);
   w.blk_cnt = c.take<unsigned long long>(kMaxSelBlocks);
   w.blk_off = c.take<unsigned long long>(kMaxSelBlocks);
   w.cand_idx = c.take<unsigned>((size_t)n + 4);
@@ -334,7 +336,8 @@ __device__ __forceinline__ float floor_value(unsigned t_lo) {
   return t_lo <= 0x007fffffu ? -__builtin_inff() : key_value(t_lo);  // keys below -inf: negative NaNs
 }
 
-__device__ __forceinline__ bool is_cand(float a, float tf) { return a >= tf || a != a; }
+// key(v) >= t_lo as one unordered compare: true for v >= tf and for NaN
+__device__ __forceinline__ bool is_cand(float a, float tf) { return !(a < tf); }
 
 // one wave's 4096-element span of a block step: 16 float4 per lane (q-major: lane l, step q ->
 // elements 256q + 4l + c).  A partial span (the last block only) clamps each float4 to the last one
@@ -358,34 +361,36 @@ __device__ __forceinline__ void filter_load(const float* __restrict__ x, int64_t
 template <bool FULL>
 __device__ __forceinline__ bool in_span(int o, int lim) { return FULL || o < lim; }
 
-// this lane's candidate flags (bit 4q + c, kept in VGPRs so the write pass does not re-derive 64
-// wave masks); running max and NaN flag for the region's max key
 template <bool FULL>
-__device__ __forceinline__ void filter_flags(const float4 (&v)[16], float tf, int lim, int lane, float& vmax,
-                                             bool& saw_nan, unsigned (&fl)[2]) {
-  fl[0] = fl[1] = 0u;
+__device__ __forceinline__ void cand4(const float4& v, float tf, int o, int lim, bool& f0, bool& f1, bool& f2,
+                                      bool& f3) {
+  f0 = is_cand(v.x, tf) && in_span<FULL>(o + 0, lim);
+  f1 = is_cand(v.y, tf) && in_span<FULL>(o + 1, lim);
+  f2 = is_cand(v.z, tf) && in_span<FULL>(o + 2, lim);
+  f3 = is_cand(v.w, tf) && in_span<FULL>(o + 3, lim);
+}
+
+// the wave's candidate count: one compare per element into a wave mask, scalar popcounts
+template <bool FULL>
+__device__ __forceinline__ unsigned filter_count(const float4 (&v)[16], float tf, int lim, int lane) {
+  unsigned cnt = 0;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const int o = 256 * q + 4 * lane;
-    const float ninf = -__builtin_inff();  // past b_end (partial spans): neutral for max and NaN
-    const bool i0 = in_span<FULL>(o + 0, lim), i1 = in_span<FULL>(o + 1, lim);
-    const bool i2 = in_span<FULL>(o + 2, lim), i3 = in_span<FULL>(o + 3, lim);
-    const float a0 = i0 ? v[q].x : ninf, a1 = i1 ? v[q].y : ninf, a2 = i2 ? v[q].z : ninf, a3 = i3 ? v[q].w : ninf;
-    vmax = fmaxf(vmax, fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));  // fmaxf ignores NaN; NaN tracked apart
-    saw_nan |= (a0 != a0) | (a1 != a1) | (a2 != a2) | (a3 != a3);
-    const unsigned nib = (unsigned)(is_cand(a0, tf) && i0) | ((unsigned)(is_cand(a1, tf) && i1) << 1) |
-                         ((unsigned)(is_cand(a2, tf) && i2) << 2) | ((unsigned)(is_cand(a3, tf) && i3) << 3);
-    fl[q >> 3] |= nib << (4 * (q & 7));
+    bool f0, f1, f2, f3;
+    cand4<FULL>(v[q], tf, 256 * q + 4 * lane, lim, f0, f1, f2, f3);
+    cnt += __popcll(__ballot(f0)) + __popcll(__ballot(f1)) + __popcll(__ballot(f2)) + __popcll(__ballot(f3));
   }
+  return cnt;
 }
 
 // ordered append from position `pos` (element order within a step q: lane-major, then the 4 components)
-__device__ __forceinline__ void filter_write(const float4 (&v)[16], const unsigned (&fl)[2], int lane, unsigned wbu,
+template <bool FULL>
+__device__ __forceinline__ void filter_write(const float4 (&v)[16], float tf, int lim, int lane, unsigned wbu,
                                              unsigned pos, uint2* __restrict__ out) {
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const unsigned nib = (fl[q >> 3] >> (4 * (q & 7))) & 15u;
-    const bool f0 = nib & 1u, f1 = nib & 2u, f2 = nib & 4u, f3 = nib & 8u;
+    bool f0, f1, f2, f3;
+    cand4<FULL>(v[q], tf, 256 * q + 4 * lane, lim, f0, f1, f2, f3);
     const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
     if ((m0 | m1 | m2 | m3) != 0ull) {
       unsigned p = pos;
@@ -393,29 +398,33 @@ __device__ __forceinline__ void filter_write(const float4 (&v)[16], const unsign
       p = __builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m1, p));
       p = __builtin_amdgcn_mbcnt_hi((unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, p));
       p = __builtin_amdgcn_mbcnt_hi((unsigned)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m3, p));
-      const unsigned e = wbu + (unsigned)(256 * q + 4 * lane);
-      if (f0) out[p++] = make_uint2(e + 0u, __float_as_uint(v[q].x));
-      if (f1) out[p++] = make_uint2(e + 1u, __float_as_uint(v[q].y));
-      if (f2) out[p++] = make_uint2(e + 2u, __float_as_uint(v[q].z));
-      if (f3) out[p++] = make_uint2(e + 3u, __float_as_uint(v[q].w));
+      if (f0 | f1 | f2 | f3) {
+        uint2* dst = out + p;
+        const unsigned e = wbu + (unsigned)(256 * q + 4 * lane);
+        if (f0) *dst++ = make_uint2(e + 0u, __float_as_uint(v[q].x));
+        if (f1) *dst++ = make_uint2(e + 1u, __float_as_uint(v[q].y));
+        if (f2) *dst++ = make_uint2(e + 2u, __float_as_uint(v[q].z));
+        if (f3) *dst = make_uint2(e + 3u, __float_as_uint(v[q].w));
+      }
       pos += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
     }
   }
 }
 
-// one block step (4 waves x 4096 elements): load, flag, exchange the wave counts, append in order
+// one block step (4 waves x 4096 elements): load, count, exchange the wave counts, append in order
 template <bool FULL>
 __device__ __forceinline__ void filter_step(const float* __restrict__ x, int64_t s, int64_t b_end, float tf,
-                                            uint2* __restrict__ out, unsigned* s_cnt, unsigned& run, float& vmax,
-                                            bool& saw_nan) {
+                                            uint2* __restrict__ out, unsigned* s_cnt, unsigned& run) {
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
   const int64_t wb = s + (int64_t)wid * kWaveSpan;
   const int lim = FULL ? kWaveSpan : (int)(b_end > wb ? (b_end - wb < kWaveSpan ? b_end - wb : kWaveSpan) : 0);
   float4 v[16];
-  unsigned fl[2];
   filter_load<FULL>(x, wb, b_end, lane, v);
-  filter_flags<FULL>(v, tf, lim, lane, vmax, saw_nan, fl);
-  const unsigned wcnt = wave_sum((unsigned)(__popc(fl[0]) + __popc(fl[1])));
+  const unsigned wcnt = filter_count<FULL>(v, tf, lim, lane);
+#if FLC_FILTER_VARIANT == 2  // calibration only: loads + count, no exchange, no append
+  run += wcnt;
+  return;
+#endif
   if (lane == 0) s_cnt[wid] = wcnt;
   __syncthreads();
   unsigned pos = run, tot = 0;
@@ -426,42 +435,34 @@ __device__ __forceinline__ void filter_step(const float* __restrict__ x, int64_t
     tot += c;
   }
   run += tot;
-  if (wcnt != 0u) filter_write(v, fl, lane, (unsigned)wb, pos, out);
+  // re-derive the masks rather than keep 64 of them live across the barrier (an opaque copy of the
+  // floor stops the compiler from reusing the count pass's compares)
+  float tf2 = tf;
+  asm volatile("" : "+v"(tf2));
+#if FLC_FILTER_VARIANT == 1  // calibration only: no append
+  return;
+#endif
+  if (wcnt != 0u) filter_write<FULL>(v, tf2, lim, lane, (unsigned)wb, pos, out);
 }
 
 __global__ __launch_bounds__(kThreads) void topk_filter_kernel(const float* __restrict__ x, int64_t n, int64_t chunk,
                                                                int sel_grid, TopkWs w) {
   __shared__ unsigned s_cnt[2][kFNW];
-  __shared__ unsigned s_mx[kFNW];
   const float tf = floor_value(w.p->t_lo);
   if (blockIdx.x == 0) {  // reset the select state of this call (read by the next launch)
     for (int i = threadIdx.x; i < kMaxRounds * kHistStride; i += kThreads) w.hist[i] = 0u;
     for (int i = threadIdx.x; i < sel_grid; i += kThreads) w.flags[i * kFlagStride] = 0u;
     if (threadIdx.x < (int)(sizeof(SelState) / 8)) reinterpret_cast<unsigned long long*>(w.st)[threadIdx.x] = 0ull;
   }
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
   const int64_t b_begin = (int64_t)blockIdx.x * chunk;
   const int64_t b_end = b_begin + chunk < n ? b_begin + chunk : n;
   uint2* __restrict__ out = w.stage + (int64_t)blockIdx.x * w.region_cap;
   unsigned run = 0;
-  float vmax = -__builtin_inff();
-  bool saw_nan = false;
   int par = 0;  // the wave-count slots alternate, so one barrier per step suffices
   int64_t s = b_begin;
-  for (; s + kBlockSpan <= b_end; s += kBlockSpan, par ^= 1)
-    filter_step<true>(x, s, b_end, tf, out, s_cnt[par], run, vmax, saw_nan);
-  if (s < b_end) filter_step<false>(x, s, b_end, tf, out, s_cnt[par], run, vmax, saw_nan);
-  unsigned mx = order_key(__float_as_uint(vmax));
-  mx = __ballot(saw_nan) ? 0xffffffffu : mx;
-  mx = wave_max_u32(mx);
-  if (lane == 0) s_mx[wid] = mx;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned m = 0;
-    for (int i = 0; i < kFNW; ++i) m = s_mx[i] > m ? s_mx[i] : m;
-    w.region_cnt[blockIdx.x] = run;
-    w.region_max[blockIdx.x] = b_begin < n ? m : 0u;
-  }
+  for (; s + kBlockSpan <= b_end; s += kBlockSpan, par ^= 1) filter_step<true>(x, s, b_end, tf, out, s_cnt[par], run);
+  if (s < b_end) filter_step<false>(x, s, b_end, tf, out, s_cnt[par], run);
+  if (threadIdx.x == 0) w.region_cnt[blockIdx.x] = run;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -477,6 +478,7 @@ struct SelView {
   int done;
   unsigned T;
   long long need;
+  unsigned maxkey;
 };
 
 // Grid barrier: every block but 0 raises its arrival flag (one 64-B line each, no contended
@@ -529,6 +531,7 @@ __device__ void read_view(const TopkWs& w, SelView* v) {
     v->done = (int)ld_mem64(&w.st->done);
     v->T = (unsigned)ld_mem64(&w.st->T);
     v->need = (long long)ld_mem64(&w.st->need);
+    v->maxkey = (unsigned)ld_mem64(&w.st->maxkey);
   }
   __syncthreads();
 }
@@ -537,16 +540,19 @@ __device__ void read_view(const TopkWs& w, SelView* v) {
 // keys >= lo, so it stays k; the round's `A` keys above the live range come first: if A >= rem the
 // key lies above the range (re-range to [lo + width, top)), otherwise pick the bin of rank rem - A in
 // the global histogram of round r and narrow the range to it.
-__device__ void lead_pick(const TopkWs& w, int r, const SelView& cur, unsigned long long top, unsigned* s_ghist) {
+__device__ void lead_pick(const TopkWs& w, int r, const SelView& cur, unsigned* s_ghist) {
   __shared__ unsigned s_digit;
   __shared__ long long s_rem;
   __shared__ unsigned s_err;
   __shared__ long long s_above;
   unsigned* h = w.hist + (size_t)r * kHistStride;
   for (int i = threadIdx.x; i < kHistBins; i += kSelThreads) s_ghist[i] = ld_mem(&h[i]);
+  __shared__ unsigned s_maxkey;
   if (threadIdx.x == 0) {
     s_err = 0;
     s_above = (long long)ld_mem(&h[kHistBins]);
+    s_maxkey = r == 0 ? ld_mem(&w.hist[kHistBins + 1]) : cur.maxkey;
+    if (r == 0) st_mem64(&w.st->maxkey, s_maxkey);
     st_mem64(&w.st->rounds, (unsigned long long)r + 1ull);
   }
   __syncthreads();
@@ -554,6 +560,7 @@ __device__ void lead_pick(const TopkWs& w, int r, const SelView& cur, unsigned l
   if (A >= cur.rem) {  // the k-th largest key is above the range (block-uniform branch)
     if (threadIdx.x == 0) {
       const unsigned long long nlo = (unsigned long long)cur.lo + cur.width;
+      const unsigned long long top = (unsigned long long)s_maxkey + 1ull;
       const unsigned long long nw = top > nlo ? top - nlo : 0ull;
       if (nw == 0ull) __hip_atomic_fetch_or(&w.st->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       st_mem64(&w.st->lo, nlo);
@@ -611,19 +618,16 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
   const int tid = threadIdx.x;
   STAMP(0);
 
-  // ---- P0: region offsets in LDS, candidate count, max key (identical in every block)
+  // ---- P0: region offsets in LDS and the candidate count (identical in every block)
   {
     const int r0 = tid * kRegionsPerThread;
     unsigned loc[kRegionsPerThread];
     unsigned long long sum = 0;
-    unsigned mx = 0;
 #pragma unroll
     for (int i = 0; i < kRegionsPerThread; i += 4) {
       if (r0 + i < R) {  // R is a multiple of 4
         const uint4 c = *reinterpret_cast<const uint4*>(w.region_cnt + r0 + i);
-        const uint4 m = *reinterpret_cast<const uint4*>(w.region_max + r0 + i);
         loc[i] = c.x; loc[i + 1] = c.y; loc[i + 2] = c.z; loc[i + 3] = c.w;
-        mx = max(mx, max(max(m.x, m.y), max(m.z, m.w)));
       } else {
         loc[i] = loc[i + 1] = loc[i + 2] = loc[i + 3] = 0u;
       }
@@ -636,8 +640,6 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
       if (r0 + i < R) s_off[r0 + i] = (unsigned)run;
       run += loc[i];
     }
-    mx = wave_max_u32(mx);
-    if ((tid & 63) == 0) s_mx[tid >> 6] = mx;
     if (tid == 0) {
       s_off[R] = (unsigned)tot;
       s_red[0] = tot;
@@ -645,8 +647,6 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
     __syncthreads();
   }
   const unsigned long long c_cand = s_red[0];
-  unsigned maxkey = 0;
-  for (int i = 0; i < kSelNW; ++i) maxkey = s_mx[i] > maxkey ? s_mx[i] : maxkey;
   __syncthreads();  // s_red is reused below
   const bool fb = (long long)c_cand < k;
   const long long C = fb ? (long long)n : (long long)c_cand;
@@ -655,17 +655,18 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
   const long long v0 = min((long long)blockIdx.x * per, C), v1 = min(v0 + per, C);
   const bool cached = per <= kKeyCache;  // grid-uniform
 
-  const unsigned long long top = (unsigned long long)maxkey + 1ull;
+  // round 0 covers [t_lo, t_hi) (fallback: every key); keys above it are counted apart
   SelView cur;
   cur.lo = fb ? 0u : w.p->t_lo;
-  unsigned long long hi_end = fb ? top : min(w.p->t_hi, top);
-  if (hi_end <= (unsigned long long)cur.lo) hi_end = top;
+  unsigned long long hi_end = fb ? (1ull << 32) : w.p->t_hi;
+  if (hi_end <= (unsigned long long)cur.lo || hi_end > (1ull << 32)) hi_end = 1ull << 32;
   cur.width = hi_end - cur.lo;
   cur.shift = range_shift(cur.width, kHistBits);
   cur.rem = k;
   cur.done = 0;
   cur.T = 0;
   cur.need = 0;
+  cur.maxkey = 0;
   SelView prev = cur;
   unsigned long long a_blk = 0;  // keys above the live range in this block (last round)
   unsigned nbar = 0;
@@ -675,7 +676,7 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
   for (int round = 0; round < kMaxRounds; ++round) {
     for (int i = tid; i < kHistBins; i += kSelThreads) s_hist[i] = 0u;
     __syncthreads();
-    unsigned above = 0;
+    unsigned above = 0, mk = 0;
     int r = 0;
     if (round == 0 && !fb && v0 + 4 * (long long)tid < v1) r = lds_region_search(s_off, R, (unsigned)(v0 + 4 * tid));
     for (long long c0 = v0 + 4 * tid; c0 < v1; c0 += 4 * kSelThreads) {
@@ -735,6 +736,7 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
         const unsigned key = order_key(raw[u]);
         const unsigned long long rel = (unsigned long long)key - cur.lo;
         const bool in = c0 + u < v1 && key >= cur.lo;
+        if (round == 0) mk = (c0 + u < v1 && key > mk) ? key : mk;
         above += (in && rel >= cur.width) ? 1u : 0u;
         hist_add(s_hist, (unsigned)(rel >> cur.shift), in && rel < cur.width);
       }
@@ -745,9 +747,19 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
       if (s_hist[i]) atomicAdd(&h[i], s_hist[i]);
     a_blk = block_sum<unsigned long long, kSelNW>((unsigned long long)above, s_red);
     if (tid == 0 && a_blk) atomicAdd(&h[kHistBins], (unsigned)a_blk);
+    if (round == 0) {  // the max key (norm of the stacked codec, top of a re-range)
+      mk = wave_max_u32(mk);
+      if ((tid & 63) == 0) s_mx[tid >> 6] = mk;
+      __syncthreads();
+      if (tid == 0) {
+        unsigned m = 0;
+        for (int i = 0; i < kSelNW; ++i) m = s_mx[i] > m ? s_mx[i] : m;
+        if (v0 < v1) atomicMax(&h[kHistBins + 1], m);
+      }
+    }
     STAMP(2 + 2 * round);
     prev = cur;
-    grid_barrier(w, nbar++, [&] { lead_pick(w, round, cur, top, s_ghist); });
+    grid_barrier(w, nbar++, [&] { lead_pick(w, round, cur, s_ghist); });
     STAMP(3 + 2 * round);
     read_view(w, &s_view);
     cur = s_view;
@@ -781,7 +793,6 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
       st_mem64(&w.st->ties, (unsigned long long)ti);
       st_mem64(&w.st->C, (unsigned long long)C);
       st_mem64(&w.st->fallback, fb ? 1ull : 0ull);
-      st_mem64(&w.st->maxkey, maxkey);
       if (st + cur.need != k || cur.need > ti)
         __hip_atomic_fetch_or(&w.st->err, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -799,7 +810,7 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
   long long run_s = (long long)(s_off_blk >> 32), run_t = (long long)(s_off_blk & 0xffffffffull);
   float nrm = 0.0f;
   if (STACKED) {
-    const float a = fabsf(key_value(maxkey)), b = fabsf(key_value(T));
+    const float a = fabsf(key_value(cur.maxkey)), b = fabsf(key_value(T));
     nrm = (isnan(a) || isnan(b)) ? __uint_as_float(0x7fc00000u) : (a > b ? a : b);
     if (blockIdx.x == 0 && tid == 0) *norm_out = nrm;
   }

@@ -114,3 +114,21 @@ def test_weighted_sum_chain_is_sequential_fmaf(n_src, n):
     dst = dst0.cuda()
     codec.weighted_sum(dst, [s.cuda() for s in srcs], w, init_mode=0, beta=0.3)
     assert gc.same_bits(dst.cpu().numpy(), exp.numpy())
+
+
+@pytest.mark.gpu
+def test_dist_fold_with_device_codec_single_rank():
+    """fl_sim_amd/dist.py with the HIP codec step: the in-rank fold equals decode-then-fmaf per client."""
+    from fl_sim_amd import codec
+    from fl_sim_amd import dist as fdist
+
+    n, k, ts = 1_000_003, 10_000, [100, 200, 300]
+    g = torch.Generator(device="cuda").manual_seed(5)
+    deltas = [torch.randn(n, generator=g, device="cuda") * 1e-3 for _ in ts]
+    w = fdist.sample_weights(ts)
+    got = fdist.aggregate_round(deltas, w, [0, 1, 2], fdist.stacked_decode_accumulate(k, seed=11, counter=3))
+    exp = torch.zeros(n, dtype=torch.float32)
+    for c, (d, wi) in enumerate(zip(deltas, w)):
+        v = codec.stacked_decode(codec.stacked_encode(d, k, 127, seed=11 + c, counter=3)).cpu()
+        exp.add_(v, alpha=float(np.float32(wi)))  # torch CPU add_(alpha): one fp32 fma per element
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), exp.numpy().view(np.uint32))
