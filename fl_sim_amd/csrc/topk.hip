@@ -56,8 +56,9 @@ constexpr int kSelectThreads = 1024;
 constexpr int kSamplePerThread = kSample / kSelectThreads;  // 32
 constexpr int kThreads = 256;
 constexpr int kFNW = kThreads / kWave;       // filter: 4 waves per block
-constexpr int kWaveSpan = 4096;              // elements per wave per block step (16 float4 per lane)
-constexpr int kBlockSpan = kFNW * kWaveSpan; // 16384 elements = 64 KB per block step
+constexpr int kStepF4 = 8;                   // float4 per lane per wave step
+constexpr int kWaveSpan = kStepF4 * 256;     // 2048 elements per wave step (8 KB)
+constexpr int kBlockSpan = kFNW * kWaveSpan; // 8192 elements: filter chunks are multiples of this
 constexpr int kSelThreads = 1024;            // persistent select: one block of 16 waves per CU
 constexpr int kSelNW = kSelThreads / kWave;
 constexpr int kMaxSelBlocks = 1024;
@@ -65,9 +66,13 @@ constexpr int kHistBits = 11;
 constexpr int kHistBins = 1 << kHistBits;
 constexpr int kHistStride = kHistBins + 64;  // a round's bins + its "above the range" counter
 constexpr int kMaxRounds = 6;
-constexpr int kMaxRegions = 16384;           // filter blocks = staging regions
+#ifndef FLC_MAX_REGIONS
+#define FLC_MAX_REGIONS 16384
+#endif
+constexpr int kMaxRegions = FLC_MAX_REGIONS; // filter blocks = staging regions
 constexpr int kRegionsPerThread = kMaxRegions / kSelThreads;  // 16 (P0 LDS scan)
-constexpr int kKeyCache = 16384;             // candidates per select block kept in LDS
+constexpr int kKeyCache = 14336;             // candidates per select block kept in LDS
+constexpr int kWcCap = 512;                  // block regions whose wave counts a select block keeps in LDS
 constexpr int kFlagStride = 16;              // one 64-B line per barrier arrival flag
 
 struct TopkParams {
@@ -102,13 +107,16 @@ struct TopkWs {
   unsigned* flags;              // [kMaxSelBlocks * kFlagStride] barrier arrival flags
   unsigned* hist;               // [kMaxRounds][kHistStride]
   unsigned* sample;             // [kSample]
-  unsigned* region_cnt;         // [R]
+  unsigned* region_cnt;         // [R]      candidates per filter block
+  unsigned* wave_cnt;           // [4 R]    candidates per wave quarter of a block
   unsigned long long* blk_cnt;  // [kMaxSelBlocks]  strict << 32 | tie
   unsigned long long* blk_off;  // [kMaxSelBlocks]
   unsigned* cand_idx;           // [n]  ordered by index
   unsigned* cand_raw;           // [n]  raw fp32 bits (only when the LDS key cache is too small)
-  uint2* stage;                 // [R * region_cap]  (idx, raw) per filter block
-  long long region_cap;
+  uint2* stage;                 // [4 R * dcap]  (idx, raw): the first dcap candidates of each wave, dense
+  uint2* spill;                 // [4 R * qc]    the rest (worst case, rarely touched)
+  long long dcap;               // dense staging entries per wave (~2x the expected candidates)
+  long long qc;                 // elements per wave quarter of a filter block (chunk / 4)
   unsigned long long* stamps;   // [16] diagnostic build only (FLC_SELECT_STAMPS)
   unsigned long long* trace;    // [kMaxRounds * 8] leader's per-round record (diagnostics)
 };
@@ -128,7 +136,39 @@ TopkGeom geometry(int64_t n) {
   return g;
 }
 
-TopkWs carve_topk(void* ws, size_t bytes, int64_t n, size_t* need) {
+struct SampleSetup {
+  int S;
+  long long rank_lo, rank_hi;
+  int take_all;
+};
+
+SampleSetup sample_setup(int64_t n, int64_t k) {
+  SampleSetup s;
+  s.S = (int)(n < kSample ? n : kSample);
+  const double m = (double)s.S * (double)k / (double)n;
+  s.rank_lo = (long long)ceil(m + 4.0 * sqrt(m) + 16.0);
+  const double rh = floor(m - 4.0 * sqrt(m) - 16.0);
+  s.rank_hi = rh >= 1.0 ? (long long)rh : 0;
+  s.take_all = (s.rank_lo >= s.S) ? 1 : 0;
+  if (s.take_all) s.rank_lo = s.S;
+  return s;
+}
+
+// dense staging per wave: twice the expected candidate count (the sample's floor admits ~rank_lo / S of
+// the elements) plus slack; waves with more candidates continue in their worst-case spill region.
+// Keeping the common case dense keeps the appends of all active waves inside a few MB (TLB / DRAM
+// page locality); a worst-case-sized region per wave made the staging writes 3-4x slower.
+int64_t dense_cap(int64_t n, int64_t k) {
+  const TopkGeom g = geometry(n);
+  const int64_t qc = g.chunk / kFNW;
+  const SampleSetup ss = sample_setup(n, k < 1 ? 1 : k);
+  if (ss.take_all) return qc;
+  const double frac = std::min(1.0, (double)ss.rank_lo / (double)ss.S);
+  const int64_t cap = (int64_t)align_up((size_t)(2.0 * frac * (double)qc) + 64, 32);
+  return cap < qc ? cap : qc;
+}
+
+TopkWs carve_topk(void* ws, size_t bytes, int64_t n, int64_t k, size_t* need) {
   const TopkGeom g = geometry(n);
   Carver c(ws, bytes);
   TopkWs w;
@@ -140,12 +180,17 @@ TopkWs carve_topk(void* ws, size_t bytes, int64_t n, size_t* need) {
   w.hist = c.take<unsigned>((size_t)kMaxRounds * kHistStride);
   w.sample = c.take<unsigned>(kSample);
   w.region_cnt = c.take<unsigned>(g.regions);
+  w.wave_cnt = c.take<unsigned>(4 * g.regions);
   w.blk_cnt = c.take<unsigned long long>(kMaxSelBlocks);
   w.blk_off = c.take<unsigned long long>(kMaxSelBlocks);
   w.cand_idx = c.take<unsigned>((size_t)n + 4);
   w.cand_raw = c.take<unsigned>((size_t)n + 4);
-  w.region_cap = g.chunk;
-  w.stage = c.take<uint2>((size_t)g.regions * g.chunk);
+  // region stride = chunk + a 2304-B skew: with a power-of-two stride every block's appends would land
+  // on the same HBM channel (measured: 34 us instead of 8 us of staging writes on 1 GiB)
+  w.qc = g.chunk / kFNW;
+  w.dcap = dense_cap(n, k);
+  w.stage = c.take<uint2>((size_t)g.regions * kFNW * w.dcap);
+  w.spill = c.take<uint2>((size_t)g.regions * kFNW * w.qc);
   *need = c.off;
   return w;
 }
@@ -344,14 +389,14 @@ __device__ __forceinline__ bool is_cand(float a, float tf) { return !(a < tf); }
 // holding valid data (16-B aligned, so it never crosses a page); `lim` masks everything past b_end.
 template <bool FULL>
 __device__ __forceinline__ void filter_load(const float* __restrict__ x, int64_t wb, int64_t b_end, int lane,
-                                            float4 (&v)[16]) {
+                                            float4 (&v)[kStepF4]) {
   if (FULL) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = ld_stream(x + wb + 256 * q + 4 * lane);
+    for (int q = 0; q < kStepF4; ++q) v[q] = ld_stream(x + wb + 256 * q + 4 * lane);
   } else {
     const int64_t last4 = (b_end - 1) & ~(int64_t)3;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < kStepF4; ++q) {
       const int64_t e = wb + 256 * q + 4 * lane;
       v[q] = *reinterpret_cast<const float4*>(x + (e < last4 ? e : last4));
     }
@@ -372,10 +417,10 @@ __device__ __forceinline__ void cand4(const float4& v, float tf, int o, int lim,
 
 // the wave's candidate count: one compare per element into a wave mask, scalar popcounts
 template <bool FULL>
-__device__ __forceinline__ unsigned filter_count(const float4 (&v)[16], float tf, int lim, int lane) {
+__device__ __forceinline__ unsigned filter_count(const float4 (&v)[kStepF4], float tf, int lim, int lane) {
   unsigned cnt = 0;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
+  for (int q = 0; q < kStepF4; ++q) {
     bool f0, f1, f2, f3;
     cand4<FULL>(v[q], tf, 256 * q + 4 * lane, lim, f0, f1, f2, f3);
     cnt += __popcll(__ballot(f0)) + __popcll(__ballot(f1)) + __popcll(__ballot(f2)) + __popcll(__ballot(f3));
@@ -383,12 +428,26 @@ __device__ __forceinline__ unsigned filter_count(const float4 (&v)[16], float tf
   return cnt;
 }
 
+#ifndef FLC_STAGE_NT
+#define FLC_STAGE_NT 0
+#endif
+__device__ __forceinline__ void st_stage(uint2* dst, unsigned idx, float v) {
+  if (FLC_STAGE_NT) {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 t = {idx, __float_as_uint(v)};
+    __builtin_nontemporal_store(t, reinterpret_cast<u32x2*>(dst));
+  } else {
+    *dst = make_uint2(idx, __float_as_uint(v));
+  }
+}
+
 // ordered append from position `pos` (element order within a step q: lane-major, then the 4 components)
 template <bool FULL>
-__device__ __forceinline__ void filter_write(const float4 (&v)[16], float tf, int lim, int lane, unsigned wbu,
-                                             unsigned pos, uint2* __restrict__ out) {
+__device__ __forceinline__ void filter_write(const float4 (&v)[kStepF4], float tf, int lim, int lane, unsigned wbu,
+                                             unsigned pos, uint2* __restrict__ out, uint2* __restrict__ spill,
+                                             unsigned dcap) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
+  for (int q = 0; q < kStepF4; ++q) {
     bool f0, f1, f2, f3;
     cand4<FULL>(v[q], tf, 256 * q + 4 * lane, lim, f0, f1, f2, f3);
     const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
@@ -399,70 +458,87 @@ __device__ __forceinline__ void filter_write(const float4 (&v)[16], float tf, in
       p = __builtin_amdgcn_mbcnt_hi((unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, p));
       p = __builtin_amdgcn_mbcnt_hi((unsigned)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m3, p));
       if (f0 | f1 | f2 | f3) {
-        uint2* dst = out + p;
         const unsigned e = wbu + (unsigned)(256 * q + 4 * lane);
-        if (f0) *dst++ = make_uint2(e + 0u, __float_as_uint(v[q].x));
-        if (f1) *dst++ = make_uint2(e + 1u, __float_as_uint(v[q].y));
-        if (f2) *dst++ = make_uint2(e + 2u, __float_as_uint(v[q].z));
-        if (f3) *dst = make_uint2(e + 3u, __float_as_uint(v[q].w));
+        if (f0) { st_stage(p < dcap ? out + p : spill + (p - dcap), e + 0u, v[q].x); ++p; }
+        if (f1) { st_stage(p < dcap ? out + p : spill + (p - dcap), e + 1u, v[q].y); ++p; }
+        if (f2) { st_stage(p < dcap ? out + p : spill + (p - dcap), e + 2u, v[q].z); ++p; }
+        if (f3) st_stage(p < dcap ? out + p : spill + (p - dcap), e + 3u, v[q].w);
       }
       pos += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
     }
   }
 }
 
-// one block step (4 waves x 4096 elements): load, count, exchange the wave counts, append in order
+// one wave step (2048 elements, already loaded into v): count, append in order after the wave's
+// earlier candidates
 template <bool FULL>
-__device__ __forceinline__ void filter_step(const float* __restrict__ x, int64_t s, int64_t b_end, float tf,
-                                            uint2* __restrict__ out, unsigned* s_cnt, unsigned& run) {
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
-  const int64_t wb = s + (int64_t)wid * kWaveSpan;
-  const int lim = FULL ? kWaveSpan : (int)(b_end > wb ? (b_end - wb < kWaveSpan ? b_end - wb : kWaveSpan) : 0);
-  float4 v[16];
-  filter_load<FULL>(x, wb, b_end, lane, v);
+__device__ __forceinline__ void filter_process(const float4 (&v)[kStepF4], int64_t wb, int64_t q_end, float tf,
+                                               uint2* __restrict__ out, uint2* __restrict__ spill, unsigned dcap,
+                                               unsigned& run) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int lim = FULL ? kWaveSpan : (int)(q_end > wb ? (q_end - wb < kWaveSpan ? q_end - wb : kWaveSpan) : 0);
   const unsigned wcnt = filter_count<FULL>(v, tf, lim, lane);
-#if FLC_FILTER_VARIANT == 2  // calibration only: loads + count, no exchange, no append
+#if FLC_FILTER_VARIANT == 2  // calibration only: loads + count, no append
   run += wcnt;
   return;
 #endif
-  if (lane == 0) s_cnt[wid] = wcnt;
-  __syncthreads();
-  unsigned pos = run, tot = 0;
-#pragma unroll
-  for (int i = 0; i < kFNW; ++i) {
-    const unsigned c = s_cnt[i];
-    pos += i < wid ? c : 0u;
-    tot += c;
-  }
-  run += tot;
-  // re-derive the masks rather than keep 64 of them live across the barrier (an opaque copy of the
-  // floor stops the compiler from reusing the count pass's compares)
+  // re-derive the masks rather than keep them live across the count (an opaque copy of the floor
+  // stops the compiler from reusing the count pass's compares)
   float tf2 = tf;
   asm volatile("" : "+v"(tf2));
-#if FLC_FILTER_VARIANT == 1  // calibration only: no append
-  return;
-#endif
-  if (wcnt != 0u) filter_write<FULL>(v, tf2, lim, lane, (unsigned)wb, pos, out);
+  if (wcnt != 0u) filter_write<FULL>(v, tf2, lim, lane, (unsigned)wb, run, out, spill, dcap);
+  run += wcnt;
 }
 
+// Each wave owns a contiguous quarter of its block's chunk and appends to its own quarter of the
+// block's staging region: no barrier between the waves.  The block total (for the select's region
+// scan) is formed by the last wave to finish, via one 64-bit LDS ticket (waves done << 32 | count).
 __global__ __launch_bounds__(kThreads) void topk_filter_kernel(const float* __restrict__ x, int64_t n, int64_t chunk,
                                                                int sel_grid, TopkWs w) {
-  __shared__ unsigned s_cnt[2][kFNW];
+  __shared__ unsigned long long s_tick;
   const float tf = floor_value(w.p->t_lo);
+  if (threadIdx.x == 0) s_tick = 0ull;
   if (blockIdx.x == 0) {  // reset the select state of this call (read by the next launch)
     for (int i = threadIdx.x; i < kMaxRounds * kHistStride; i += kThreads) w.hist[i] = 0u;
     for (int i = threadIdx.x; i < sel_grid; i += kThreads) w.flags[i * kFlagStride] = 0u;
     if (threadIdx.x < (int)(sizeof(SelState) / 8)) reinterpret_cast<unsigned long long*>(w.st)[threadIdx.x] = 0ull;
   }
-  const int64_t b_begin = (int64_t)blockIdx.x * chunk;
-  const int64_t b_end = b_begin + chunk < n ? b_begin + chunk : n;
-  uint2* __restrict__ out = w.stage + (int64_t)blockIdx.x * w.region_cap;
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+  const int64_t qc = chunk / kFNW;
+  const int64_t q_begin = (int64_t)blockIdx.x * chunk + wid * qc;
+  const int64_t q_end = q_begin + qc < n ? q_begin + qc : n;
+  const int64_t wave_id = (int64_t)blockIdx.x * kFNW + wid;
+  uint2* __restrict__ out = w.stage + wave_id * w.dcap;
+  uint2* __restrict__ spill = w.spill + wave_id * qc;
+  const unsigned dcap = (unsigned)w.dcap;
   unsigned run = 0;
-  int par = 0;  // the wave-count slots alternate, so one barrier per step suffices
-  int64_t s = b_begin;
-  for (; s + kBlockSpan <= b_end; s += kBlockSpan, par ^= 1) filter_step<true>(x, s, b_end, tf, out, s_cnt[par], run);
-  if (s < b_end) filter_step<false>(x, s, b_end, tf, out, s_cnt[par], run);
-  if (threadIdx.x == 0) w.region_cnt[blockIdx.x] = run;
+  // software pipeline over the wave's full steps: step i + 1 is in flight while step i is processed
+  const int64_t nfull = q_end > q_begin ? (q_end - q_begin) / kWaveSpan : 0;
+  int64_t s = q_begin, i = 0;
+  float4 va[kStepF4], vb[kStepF4];
+  if (nfull > 0) filter_load<true>(x, s, q_end, lane, va);
+  for (; i + 2 <= nfull; i += 2) {
+    filter_load<true>(x, s + kWaveSpan, q_end, lane, vb);
+    filter_process<true>(va, s, q_end, tf, out, spill, dcap, run);
+    s += kWaveSpan;
+    if (i + 2 < nfull) filter_load<true>(x, s + kWaveSpan, q_end, lane, va);
+    filter_process<true>(vb, s, q_end, tf, out, spill, dcap, run);
+    s += kWaveSpan;
+  }
+  if (i < nfull) {
+    filter_process<true>(va, s, q_end, tf, out, spill, dcap, run);
+    s += kWaveSpan;
+  }
+  if (s < q_end) {
+    filter_load<false>(x, s, q_end, lane, va);
+    filter_process<false>(va, s, q_end, tf, out, spill, dcap, run);
+  }
+  if (lane == 0) {
+    w.wave_cnt[blockIdx.x * kFNW + wid] = run;
+    const unsigned long long old = atomicAdd(&s_tick, (1ull << 32) | run);
+    if ((old >> 32) == (unsigned long long)(kFNW - 1)) w.region_cnt[blockIdx.x] = (unsigned)old + run;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -612,6 +688,7 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
   __shared__ __attribute__((aligned(16))) unsigned s_keys[kKeyCache];
   __shared__ unsigned s_hist[kHistBins];
   __shared__ unsigned s_ghist[kHistBins];
+  __shared__ uint4 s_wc[kWcCap];
   __shared__ unsigned long long s_red[kSelNW];
   __shared__ unsigned s_mx[kSelNW];
   __shared__ SelView s_view;
@@ -677,8 +754,22 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
     for (int i = tid; i < kHistBins; i += kSelThreads) s_hist[i] = 0u;
     __syncthreads();
     unsigned above = 0, mk = 0;
-    int r = 0;
-    if (round == 0 && !fb && v0 + 4 * (long long)tid < v1) r = lds_region_search(s_off, R, (unsigned)(v0 + 4 * tid));
+    int r = 0, r_cur = -1, r_first = 0;
+    bool wc_lds = false;
+    uint4 wc = make_uint4(0u, 0u, 0u, 0u);
+    if (round == 0 && !fb) {
+      // wave counts of the block regions this select block gathers from, staged in LDS when they fit
+      if (v0 < v1) {
+        r_first = lds_region_search(s_off, R, (unsigned)v0);
+        const int r_last = lds_region_search(s_off, R, (unsigned)(v1 - 1));
+        wc_lds = r_last - r_first + 1 <= kWcCap;
+        if (wc_lds)
+          for (int i = tid; i <= r_last - r_first; i += kSelThreads)
+            s_wc[i] = *reinterpret_cast<const uint4*>(w.wave_cnt + (size_t)(r_first + i) * kFNW);
+      }
+      __syncthreads();
+      if (v0 + 4 * (long long)tid < v1) r = lds_region_search(s_off, R, (unsigned)(v0 + 4 * tid));
+    }
     for (long long c0 = v0 + 4 * tid; c0 < v1; c0 += 4 * kSelThreads) {
       unsigned raw[4];
       if (round == 0) {
@@ -698,7 +789,18 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
             const long long c = c0 + u;
             if (c < v1) {
               r = lds_region_advance(s_off, R, r, (unsigned)c);
-              const uint2 e = w.stage[(long long)r * w.region_cap + (c - s_off[r])];
+              if (r != r_cur) {
+                r_cur = r;
+                wc = wc_lds ? s_wc[r - r_first] : *reinterpret_cast<const uint4*>(w.wave_cnt + (size_t)r * kFNW);
+              }
+              // candidate -> (block region, wave quarter, offset): the quarters are in index order
+              unsigned loc = (unsigned)(c - s_off[r]);
+              long long q = 0;
+              if (loc >= wc.x) { loc -= wc.x; q = 1;
+                if (loc >= wc.y) { loc -= wc.y; q = 2;
+                  if (loc >= wc.z) { loc -= wc.z; q = 3; } } }
+              const long long wv = (long long)r * kFNW + q;
+              const uint2 e = loc < (unsigned)w.dcap ? w.stage[wv * w.dcap + loc] : w.spill[wv * w.qc + (loc - w.dcap)];
               id[u] = e.x;
               raw[u] = e.y;
             } else {
@@ -878,24 +980,6 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* _
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-struct SampleSetup {
-  int S;
-  long long rank_lo, rank_hi;
-  int take_all;
-};
-
-SampleSetup sample_setup(int64_t n, int64_t k) {
-  SampleSetup s;
-  s.S = (int)(n < kSample ? n : kSample);
-  const double m = (double)s.S * (double)k / (double)n;
-  s.rank_lo = (long long)ceil(m + 4.0 * sqrt(m) + 16.0);
-  const double rh = floor(m - 4.0 * sqrt(m) - 16.0);
-  s.rank_hi = rh >= 1.0 ? (long long)rh : 0;
-  s.take_all = (s.rank_lo >= s.S) ? 1 : 0;
-  if (s.take_all) s.rank_lo = s.S;
-  return s;
-}
-
 // one persistent select launch per device at a time: launches on different streams are ordered with an
 // event chain (stream-ordered, no host blocking), so two never compete for co-residency
 struct SelectGate {
@@ -969,7 +1053,7 @@ extern "C" {
 size_t flc_topk_workspace_size(int64_t n, int64_t k) {
   (void)k;
   size_t need = 0;
-  (void)carve_topk(nullptr, 0, n < 1 ? 1 : n, &need);
+  (void)carve_topk(nullptr, 0, n < 1 ? 1 : n, k, &need);
   return need;
 }
 
@@ -978,7 +1062,7 @@ int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* v
   if (int rc = check_topk(x, n, k, "flc_topk_encode")) return rc;
   if (!idx || !val) return fail(FLC_EINVAL, "flc_topk_encode: null output");
   size_t need = 0;
-  TopkWs w = carve_topk(ws, ws_bytes, n, &need);
+  TopkWs w = carve_topk(ws, ws_bytes, n, k, &need);
   if (!ws || need > ws_bytes) return fail(FLC_EWORKSPACE, "flc_topk_encode: workspace %zu < %zu", ws_bytes, need);
   return launch_topk<false>(x, n, k, w, as_stream(stream), idx, val, nullptr, nullptr, 0, 0, 0);
 }
@@ -993,7 +1077,7 @@ int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_
     return fail(FLC_EUNSUPPORTED,
                 "flc_stacked_encode: compat RNG is composed by the caller (flc_topk_encode + flc_quant_encode)");
   size_t need = 0;
-  TopkWs w = carve_topk(ws, ws_bytes, n, &need);
+  TopkWs w = carve_topk(ws, ws_bytes, n, k, &need);
   if (!ws || need > ws_bytes) return fail(FLC_EWORKSPACE, "flc_stacked_encode: workspace %zu < %zu", ws_bytes, need);
   return launch_topk<true>(x, n, k, w, as_stream(stream), idx, nullptr, codes, norm, levels, seed, counter);
 }

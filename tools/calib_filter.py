@@ -38,8 +38,8 @@ dec = lambda: codec.stacked_decode(pkt, out=out)  # noqa: E731
 res = {}
 for nm in ("topk_sample_gather", "topk_sample_select", "topk_filter", "stacked_select"):
     res[nm] = round(probe(nm, enc), 1)
-for nm in ("tile_index", "sparse_decode"):
+for nm in ("tile_index", "stacked_decode"):
     res[nm] = round(probe(nm, dec), 1)
 res["filter_GBps"] = round(4 * n / res["topk_filter"] / 1e3, 0)
-res["decode_GBps"] = round(4 * n / res["sparse_decode"] / 1e3, 0)
+res["decode_GBps"] = round(4 * n / res["stacked_decode"] / 1e3, 0)
 print(sys.argv[1] if len(sys.argv) > 1 else "", res, flush=True)
