@@ -182,10 +182,45 @@ def main():
             "avg_ms": round(probe_ms, 5),
             "algorithmic_bytes": kernel_bytes.get(args.probe),
         }
+    extra = {}
+    if not args.skip_extra:
+        # host-resident path (north_star: client state lives on the CPU simulator): pinned host delta ->
+        # H2D -> encode + decode -> D2H of the dense decoded vector; PCIe-bound, never `value`
+        hx = torch.empty(D, dtype=torch.float32, pin_memory=True)
+        hx.copy_(x, non_blocking=False)
+        hout = torch.empty(D, dtype=torch.float32, pin_memory=True)
+        ce = [0]
+
+        def step_host():
+            ce[0] += 1
+            x.copy_(hx, non_blocking=True)
+            pkt = codec.stacked_encode(x, K, LEVELS, seed=rank, counter=ce[0])
+            codec.stacked_decode(pkt, out=out)
+            hout.copy_(out, non_blocking=True)
+
+        ms_h, _ = timed(step_host, 3, 1, world)
+        ms_h = max_over_ranks(ms_h, world)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            x.copy_(hx, non_blocking=True)
+        torch.cuda.synchronize()
+        h2d = 3 * 4 * D / (time.perf_counter() - t0) / 1e9
+        t0 = time.perf_counter()
+        for _ in range(3):
+            hout.copy_(out, non_blocking=True)
+        torch.cuda.synchronize()
+        d2h = 3 * 4 * D / (time.perf_counter() - t0) / 1e9
+        extra["e2e_host"] = {
+            "ms_per_step": round(ms_h, 4),
+            "GB_s": round(world * stacked_bytes(D, K) / (ms_h * 1e-3) / 1e9, 1),
+            "h2d_GB_s": round(h2d, 1),
+            "d2h_GB_s": round(d2h, 1),
+            "note": "pinned host x -> H2D -> stacked encode+decode -> D2H of the dense output; same bytes formula",
+        }
+        del hx, hout
     del x, out
     torch.cuda.empty_cache()
 
-    extra = {}
     if not args.skip_extra:
         # configs[1]: 8-bit dithering, 10 clients x cnn_femmist_tiny (417,482 params), one batched launch
         d2, b2 = 417_482, 10
