@@ -99,8 +99,8 @@ __device__ __forceinline__ T block_excl_scan(T v, T* lds, T* total) {
   if (lane == kWave - 1) lds[wid] = incl;
   __syncthreads();
   T base = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) {
+#pragma unroll 4
+  for (int w = 0; w < NW; ++w) {  // (partially unrolled: NW 64-bit LDS loads in flight cost 2 NW VGPRs)
     const T s = lds[w];
     base += (w < wid) ? s : T(0);
     tot += s;
@@ -143,6 +143,12 @@ __device__ __forceinline__ void acquire_agent() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope fence + s_barrier, and
+// on gfx950 that fence waits for vmcnt(0): every global load and store the wave has in flight.  Kernels
+// that keep prefetched loads (or fire-and-forget stores) in flight across a barrier use this instead:
+// LDS operations drained, no wait on the vector-memory counter.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ------------------------------------------------------------------------------------------------
 // order-preserving key of a float for "largest signed value" selection (np.argsort order,

@@ -42,7 +42,15 @@ __global__ __launch_bounds__(kThreads) void tile_index_kernel(const int* __restr
 // one block per output tile of TILE = 256 * V floats: zero the tile in LDS, scatter the tile's kept
 // entries (tile_start[t] .. tile_start[t+1]), stream it out with V 16-B stores per thread.
 //   MODE 0: v = scale * val[j];  MODE 1: v = dithering decode of codes[j] (s = levels, norm)
-template <int MODE, bool ACC, int V, bool EARLY>
+// XCD-aware tile order: the dispatcher deals consecutive blocks round-robin to the 8 XCDs; remapping
+// block b to tile (b % 8) * (T / 8) + b / 8 makes each XCD write one contiguous eighth of the output
+// (1 GiB of zero-dominated stores: 162 vs 175 us at 4096-output tiles, tools/bwprobe4.hip)
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
+  const int64_t per = nb >> 3;
+  return b < (per << 3) ? (b & 7) * per + (b >> 3) : b;
+}
+
+template <int MODE, bool ACC, int V, bool EARLY, bool XCD>
 __global__ __launch_bounds__(kThreads) void sparse_decode_kernel(const int* __restrict__ idx, const float* __restrict__ val,
                                                                  const uint8_t* __restrict__ codes, float scale,
                                                                  int levels, double step, const float* __restrict__ norm_ptr,
@@ -50,7 +58,8 @@ __global__ __launch_bounds__(kThreads) void sparse_decode_kernel(const int* __re
                                                                  const unsigned* __restrict__ tile_start) {
   constexpr int TILE = kThreads * 4 * V;
   __shared__ __attribute__((aligned(16))) float s_tile[TILE];
-  const int64_t t0 = (int64_t)blockIdx.x * TILE;
+  const int64_t tile = XCD ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t t0 = tile * TILE;
   const bool full = t0 + TILE <= n;
   // EARLY: the zero stores of a full, non-accumulating tile leave before any load returns; the few
   // float4s that hold kept entries are stored again below (same thread, program order)
@@ -59,7 +68,7 @@ __global__ __launch_bounds__(kThreads) void sparse_decode_kernel(const int* __re
     for (int u = 0; u < V; ++u)
       *reinterpret_cast<float4*>(out + t0 + 4 * (int64_t)(threadIdx.x + u * kThreads)) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  const unsigned lo = tile_start[blockIdx.x], hi = tile_start[blockIdx.x + 1];
+  const unsigned lo = tile_start[tile], hi = tile_start[tile + 1];
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
 #pragma unroll
   for (int u = 0; u < V; ++u) tile4[threadIdx.x + u * kThreads] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -233,6 +242,196 @@ __global__ __launch_bounds__(kThreads) void sparse_decode_stream_kernel(
   }
 }
 
+// One-wave decode: one 64-lane workgroup per 1024-output tile (4 KB of output).  Measured on MI355X
+// (tools/bwprobe4.hip), 1 GiB of 16-B stores reaches 6.8-6.9 TB/s when every workgroup writes one
+// contiguous 4 KB piece, but only 5.6-6.1 TB/s with 8-16 KB per workgroup; a single wave also needs no
+// s_barrier between its LDS scatter and its LDS read.  Per tile: the kept-entry range from tile_start
+// (scalar loads), the tile's entries (one per lane, more in a loop), a scatter into the wave's 4 KB LDS
+// tile, four 1-KB coalesced stores.
+template <int MODE, bool ACC>
+__global__ __launch_bounds__(kWave) void sparse_decode_wave_kernel(const int* __restrict__ idx,
+                                                                   const float* __restrict__ val,
+                                                                   const uint8_t* __restrict__ codes, float scale,
+                                                                   int levels, double step,
+                                                                   const float* __restrict__ norm_ptr, int64_t n,
+                                                                   float weight, float* __restrict__ out,
+                                                                   const unsigned* __restrict__ tile_start, int dbg) {
+  constexpr int TILE = 1024;
+  __shared__ __attribute__((aligned(16))) float s_tile[TILE];
+  const int lane = threadIdx.x;
+  const int64_t t0 = (int64_t)blockIdx.x * TILE;
+  float4 acc[4];
+  if (ACC) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
+      acc[u] = e + 4 <= n ? *reinterpret_cast<const float4*>(out + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  unsigned lo = 0, hi = 0;
+  if (dbg != 1) { lo = tile_start[blockIdx.x]; hi = tile_start[blockIdx.x + 1]; }
+  if (dbg == 2) hi = lo;
+  float4* tile4 = reinterpret_cast<float4*>(s_tile);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) tile4[lane + u * kWave] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float nrm = MODE == 1 ? *norm_ptr : 0.0f;
+  for (unsigned j = lo + lane; j < hi; j += kWave) {
+    const int64_t off = (int64_t)(unsigned)idx[j] - t0;
+    if (off >= 0 && off < TILE) s_tile[off] = entry_value<MODE>(entry_raw<MODE>(val, codes, j), scale, levels, step, nrm);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = lane + u * kWave;
+    const int64_t e = t0 + 4 * (int64_t)q;
+    float4 v = tile4[q];
+    if (e + 4 <= n) {
+      if (ACC) {
+        v = make_float4(fmaf(weight, v.x, acc[u].x), fmaf(weight, v.y, acc[u].y), fmaf(weight, v.z, acc[u].z),
+                        fmaf(weight, v.w, acc[u].w));
+      } else if (weight != 1.0f) {
+        v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
+      }
+      *reinterpret_cast<float4*>(out + e) = v;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int c = 0; c < 4 && e + c < n; ++c) {
+        float o = vv[c];
+        if (ACC) o = fmaf(weight, o, out[e + c]);
+        else if (weight != 1.0f) o = weight * o;
+        out[e + c] = o;
+      }
+    }
+  }
+}
+
+// Grid-stride pipelined decode: G resident blocks, block b assembles tiles b, b + G, b + 2G, ... of
+// TILE = 1024 V outputs.  The whole grid's stores of one iteration cover ONE contiguous window (the write
+// order HBM3E takes at full rate, tools/bwprobe4.hip), and each block's dependent load chain
+// (tile_start -> kept entries) runs ahead of its stores: tile i + 2's range and tile i + 1's entries
+// (and, accumulating, its slice of `out`) are in flight while tile i is scattered and stored.  Two LDS
+// tiles alternate, so one barrier per tile suffices; the barrier is LDS-only (lds_barrier), so the
+// prefetches stay in flight across it.  Tiles with more than 256 kept entries take the rest straight
+// from memory.  The loop is unrolled by two with explicit A/B register sets: no loop-carried copies
+// of loaded registers, which would make the compiler wait for the prefetch it just issued.
+template <int V>
+struct GsRegs {
+  unsigned e_idx;
+  uint32_t e_raw;
+  float4 acc[V];
+};
+
+template <int MODE, bool ACC, int V>
+__device__ __forceinline__ void gs_tile(const int* __restrict__ idx, const float* __restrict__ val,
+                                        const uint8_t* __restrict__ codes, float scale, int levels, double step,
+                                        float nrm, int64_t n, float weight, float* __restrict__ out,
+                                        const unsigned* __restrict__ tile_start, int64_t ntiles, int64_t t, int64_t G,
+                                        float* tl, unsigned& lo0, unsigned& hi0, unsigned& lo1, unsigned& hi1,
+                                        const GsRegs<V>& cur, GsRegs<V>& nxt) {
+  constexpr int TILE = kThreads * 4 * V;
+  const int tid = threadIdx.x;
+  const int64_t t0 = t * TILE;
+  nxt.e_idx = 0xffffffffu;
+  nxt.e_raw = 0u;
+  if (lo1 + tid < hi1) {
+    nxt.e_idx = (unsigned)idx[lo1 + tid];
+    nxt.e_raw = entry_raw<MODE>(val, codes, lo1 + tid);
+  }
+  unsigned lo2 = 0, hi2 = 0;
+  if (t + 2 * G < ntiles) {
+    lo2 = tile_start[t + 2 * G];
+    hi2 = tile_start[t + 2 * G + 1];
+  }
+  if (ACC) {
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int64_t e = (t + G) * TILE + 4 * (int64_t)(tid + u * kThreads);
+      nxt.acc[u] = (t + G < ntiles && e + 4 <= n) ? *reinterpret_cast<const float4*>(out + e)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if (cur.e_idx != 0xffffffffu) {
+    const int64_t off = (int64_t)cur.e_idx - t0;
+    if (off >= 0 && off < TILE) tl[off] = entry_value<MODE>(cur.e_raw, scale, levels, step, nrm);
+  }
+  for (unsigned j = lo0 + kThreads + tid; j < hi0; j += kThreads) {
+    const int64_t off = (int64_t)(unsigned)idx[j] - t0;
+    if (off >= 0 && off < TILE) tl[off] = entry_value<MODE>(entry_raw<MODE>(val, codes, j), scale, levels, step, nrm);
+  }
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const int q = tid + u * kThreads;
+    const int64_t e = t0 + 4 * (int64_t)q;
+    float4 v = reinterpret_cast<float4*>(tl)[q];
+    reinterpret_cast<float4*>(tl)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e + 4 <= n) {
+      if (ACC) {
+        v = make_float4(fmaf(weight, v.x, cur.acc[u].x), fmaf(weight, v.y, cur.acc[u].y),
+                        fmaf(weight, v.z, cur.acc[u].z), fmaf(weight, v.w, cur.acc[u].w));
+      } else if (weight != 1.0f) {
+        v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
+      }
+      *reinterpret_cast<float4*>(out + e) = v;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int c = 0; c < 4 && e + c < n; ++c) {
+        float o = vv[c];
+        if (ACC) o = fmaf(weight, o, out[e + c]);
+        else if (weight != 1.0f) o = weight * o;
+        out[e + c] = o;
+      }
+    }
+  }
+  lo0 = lo1;
+  hi0 = hi1;
+  lo1 = lo2;
+  hi1 = hi2;
+}
+
+template <int MODE, bool ACC, int V>
+__global__ __launch_bounds__(kThreads) void sparse_decode_gs_kernel(
+    const int* __restrict__ idx, const float* __restrict__ val, const uint8_t* __restrict__ codes, float scale,
+    int levels, double step, const float* __restrict__ norm_ptr, int64_t n, float weight, float* __restrict__ out,
+    const unsigned* __restrict__ tile_start, int64_t ntiles) {
+  constexpr int TILE = kThreads * 4 * V;
+  __shared__ __attribute__((aligned(16))) float s_tile[2][TILE];
+  const int tid = threadIdx.x;
+  const int64_t G = gridDim.x;
+  const float nrm = MODE == 1 ? *norm_ptr : 0.0f;
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    reinterpret_cast<float4*>(s_tile[0])[tid + u * kThreads] = make_float4(0.f, 0.f, 0.f, 0.f);
+    reinterpret_cast<float4*>(s_tile[1])[tid + u * kThreads] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  int64_t t = blockIdx.x;
+  unsigned lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
+  if (t < ntiles) { lo0 = tile_start[t]; hi0 = tile_start[t + 1]; }
+  if (t + G < ntiles) { lo1 = tile_start[t + G]; hi1 = tile_start[t + G + 1]; }
+  GsRegs<V> A, B;
+  A.e_idx = 0xffffffffu;
+  A.e_raw = 0u;
+  if (lo0 + tid < hi0) { A.e_idx = (unsigned)idx[lo0 + tid]; A.e_raw = entry_raw<MODE>(val, codes, lo0 + tid); }
+  if (ACC) {
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      const int64_t e = t * TILE + 4 * (int64_t)(tid + u * kThreads);
+      A.acc[u] = (t < ntiles && e + 4 <= n) ? *reinterpret_cast<const float4*>(out + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __syncthreads();
+  while (t < ntiles) {
+    gs_tile<MODE, ACC, V>(idx, val, codes, scale, levels, step, nrm, n, weight, out, tile_start, ntiles, t, G, s_tile[0],
+                          lo0, hi0, lo1, hi1, A, B);
+    t += G;
+    if (t >= ntiles) break;
+    gs_tile<MODE, ACC, V>(idx, val, codes, scale, levels, step, nrm, n, weight, out, tile_start, ntiles, t, G, s_tile[1],
+                          lo0, hi0, lo1, hi1, B, A);
+    t += G;
+  }
+}
+
 // rand-k scatter: out[idx[j]] = scale * x[idx[j]] (out pre-zeroed)
 __global__ __launch_bounds__(kThreads) void randk_scatter_kernel(const float* __restrict__ x, const int* __restrict__ idx,
                                                                  long long k, float scale, float* __restrict__ out) {
@@ -262,7 +461,7 @@ size_t decode_ws_bytes(int64_t n) {  // tile index for the smallest tile (1024 o
   return (size_t)(cdiv(n < 1 ? 1 : n, (int64_t)kThreads * 4) + 1) * sizeof(unsigned);
 }
 
-template <int MODE, int V, bool EARLY>
+template <int MODE, int V, bool EARLY, bool XCD>
 int launch_decode_v(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
                     const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws, size_t ws_bytes,
                     hipStream_t st, const char* name) {
@@ -278,10 +477,10 @@ int launch_decode_v(const int32_t* idx, const float* val, const uint8_t* codes, 
              (long long)ntiles, tile_start);
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   if (accumulate)
-    FLC_LAUNCH(name, (sparse_decode_kernel<MODE, true, V, EARLY>), dim3((unsigned)ntiles), dim3(kThreads), 0, st, idx,
+    FLC_LAUNCH(name, (sparse_decode_kernel<MODE, true, V, EARLY, XCD>), dim3((unsigned)ntiles), dim3(kThreads), 0, st, idx,
                val, codes, scale, levels, step, norm, n, weight, out, tile_start);
   else
-    FLC_LAUNCH(name, (sparse_decode_kernel<MODE, false, V, EARLY>), dim3((unsigned)ntiles), dim3(kThreads), 0, st, idx,
+    FLC_LAUNCH(name, (sparse_decode_kernel<MODE, false, V, EARLY, XCD>), dim3((unsigned)ntiles), dim3(kThreads), 0, st, idx,
                val, codes, scale, levels, step, norm, n, weight, out, tile_start);
   return FLC_OK;
 }
@@ -324,6 +523,65 @@ int launch_decode_stream(const int32_t* idx, const float* val, const uint8_t* co
   return FLC_OK;
 }
 
+template <int MODE>
+int launch_decode_wave(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
+                       const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws,
+                       size_t ws_bytes, hipStream_t st, const char* name) {
+  const int64_t ntiles = cdiv(n, (int64_t)1024);
+  const size_t need = (size_t)(ntiles + 1) * sizeof(unsigned);
+  if (!ws || ws_bytes < need) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", name, ws_bytes, need);
+  if (!aligned16(out)) return fail(FLC_EINVAL, "%s: out must be 16-B aligned", name);
+  unsigned* tile_start = static_cast<unsigned*>(ws);
+  const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(k + 1, kThreads), 2048));
+  FLC_LAUNCH("tile_index", tile_index_kernel<10>, dim3(gi), dim3(kThreads), 0, st, idx, (long long)k,
+             (long long)ntiles, tile_start);
+  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
+  const int dbg = getenv("FLC_DECODE_DBG") ? atoi(getenv("FLC_DECODE_DBG")) : 0;
+  if (accumulate)
+    FLC_LAUNCH(name, (sparse_decode_wave_kernel<MODE, true>), dim3((unsigned)ntiles), dim3(kWave), 0, st, idx, val,
+               codes, scale, levels, step, norm, n, weight, out, tile_start, dbg);
+  else
+    FLC_LAUNCH(name, (sparse_decode_wave_kernel<MODE, false>), dim3((unsigned)ntiles), dim3(kWave), 0, st, idx, val,
+               codes, scale, levels, step, norm, n, weight, out, tile_start, dbg);
+  return FLC_OK;
+}
+
+int64_t decode_gs_blocks() {  // resident grid: FLC_DECODE_BLOCKS or 8 blocks of 256 threads per CU
+  const char* e = getenv("FLC_DECODE_BLOCKS");
+  if (e && atoi(e) > 0) return atoi(e);
+  int dev = 0, cu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || cu <= 0)
+    cu = 256;
+  return (int64_t)cu * 8;
+}
+
+template <int MODE, int V>
+int launch_decode_gs(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
+                     const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws, size_t ws_bytes,
+                     hipStream_t st, const char* name) {
+  constexpr int TILE = kThreads * 4 * V;
+  constexpr int TILE_LOG = V == 1 ? 10 : (V == 2 ? 11 : 12);
+  static_assert((1 << TILE_LOG) == TILE, "tile index granularity");
+  const int64_t ntiles = cdiv(n, TILE);
+  const size_t need = (size_t)(ntiles + 1) * sizeof(unsigned);
+  if (!ws || ws_bytes < need) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", name, ws_bytes, need);
+  if (!aligned16(out)) return fail(FLC_EINVAL, "%s: out must be 16-B aligned", name);
+  unsigned* tile_start = static_cast<unsigned*>(ws);
+  const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(k + 1, kThreads), 2048));
+  FLC_LAUNCH("tile_index", tile_index_kernel<TILE_LOG>, dim3(gi), dim3(kThreads), 0, st, idx, (long long)k,
+             (long long)ntiles, tile_start);
+  const int64_t grid = std::min<int64_t>(ntiles, decode_gs_blocks());
+  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
+  if (accumulate)
+    FLC_LAUNCH(name, (sparse_decode_gs_kernel<MODE, true, V>), dim3((unsigned)grid), dim3(kThreads), 0, st, idx, val,
+               codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles);
+  else
+    FLC_LAUNCH(name, (sparse_decode_gs_kernel<MODE, false, V>), dim3((unsigned)grid), dim3(kThreads), 0, st, idx, val,
+               codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles);
+  return FLC_OK;
+}
+
 int decode_variant() {
   const char* e = getenv("FLC_DECODE_VARIANT");
   return e ? atoi(e) : kDecodeVariant;
@@ -333,19 +591,27 @@ template <int MODE>
 int launch_decode(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
                   const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws, size_t ws_bytes,
                   hipStream_t st, const char* name) {
-#define FLC_DV(V, E) return launch_decode_v<MODE, V, E>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name)
+#define FLC_DV(V, E, X) return launch_decode_v<MODE, V, E, X>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name)
   const int dv = decode_variant();
   if (dv == 90) return launch_decode_stream<MODE>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out,
                                                   ws, ws_bytes, st, name);
   switch (dv) {
-    case 10: FLC_DV(1, false);
-    case 11: FLC_DV(1, true);
-    case 20: FLC_DV(2, false);
-    case 21: FLC_DV(2, true);
-    case 40: FLC_DV(4, false);
-    case 41: FLC_DV(4, true);
-    case 80: FLC_DV(8, false);
-    default: FLC_DV(8, true);
+    case 300: return launch_decode_wave<MODE>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
+    case 201: return launch_decode_gs<MODE, 1>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
+    case 202: return launch_decode_gs<MODE, 2>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
+    case 204: return launch_decode_gs<MODE, 4>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
+    case 10: FLC_DV(1, false, false);
+    case 11: FLC_DV(1, true, false);
+    case 20: FLC_DV(2, false, false);
+    case 40: FLC_DV(4, false, false);
+    case 41: FLC_DV(4, true, false);
+    case 80: FLC_DV(8, false, false);
+    case 110: FLC_DV(1, false, true);
+    case 111: FLC_DV(1, true, true);
+    case 120: FLC_DV(2, false, true);
+    case 140: FLC_DV(4, false, true);
+    case 141: FLC_DV(4, true, true);
+    default: FLC_DV(8, true, false);
   }
 #undef FLC_DV
 }

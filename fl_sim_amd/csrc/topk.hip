@@ -1,4 +1,4 @@
-// topk.hip — exact top-k selection and the stacked top-k -> 8-bit dithering encoder, for gfx950
+// topk.hip — exact top-k selection and the stacked top-k -> 8-bit dithering encoder for gfx950
 // (reference: fl_sim/compressors/compressors.py:293-296 and 327-365).
 //
 // Selection contract (compressors.py:294-295, `out[np.argsort(out)[:-K]] = 0`): keep the k largest
@@ -6,33 +6,31 @@
 // highest indices are kept (stable ascending argsort order; the reference's own argsort is unstable,
 // so any tie choice satisfies it — see DESIGN.md).
 //
-// Pipeline: ONE streaming read of x; every later pass touches only the ~1.2 k candidates.
-//   sample_gather  128 blocks: 32 K strided keys of x (order-preserving uint32 keys).
-//   sample_select  1 block, keys in registers: two fixed 11-bit digit passes locate the sample
-//                  quantiles at ranks m + 4 sqrt(m) + 16 and m - 4 sqrt(m) - 16 (m = k S / n): the
-//                  candidate floor t_lo (count(key >= t_lo) ~ k + 4 sigma, so ~1.22 k candidates at
-//                  k/n = 1 %) and a ceiling t_hi that very likely lies above the k-th largest key.
-//   filter         the HBM pass: one-shot 64 KB blocks (4 waves x 16 float4 per lane, all loads in
-//                  flight at once); each block appends its candidates in index order to a private
-//                  staging region (ballot/mbcnt compaction, one LDS exchange of wave counts, no
-//                  atomics).  Algorithmic bytes: 4 per element.
-//   select         ONE persistent launch, one 1024-thread block per CU:
-//                    P0  region offsets in LDS (every block) and the candidate count C;
-//                    rounds  gather the staged candidates (round 0) into an index-ordered array and an
-//                        LDS key cache (and reduce the max key), then 2048-bin radix rounds over the
-//                        live key range (round 0: [t_lo, t_hi), keys above it counted apart) until
-//                        the exact k-th largest key T is resolved (usually 2 rounds);
-//                    counts  strict / tie counts per block come from the resolving round's local
-//                        histogram (no extra pass), scanned by the barrier leader;
-//                    compaction  ordered write of idx[k] / val[k], or, stacked, idx[k] / codes[k]
-//                        with the dithering fused in (norm of the kept set = max(|max key|, |T|)).
-//                  Rounds are separated by grid barriers: every block raises its own arrival flag,
-//                  block 0 polls them, runs the serial "leader" step and publishes a generation word.
-//                  C < k switches every phase to "fallback" mode, reading x itself (always correct).
-// Cross-block hand-offs inside a launch go through memory-side atomics only (histogram adds, flag
-// and state exchanges, RMW reads); candidates are re-read only by the thread that wrote them.  Spins
-// are bounded (error flag), and the host serialises the persistent launches of different streams so
-// two of them never compete for residency.
+// Three launches; block b of the filter and of the select owns the element range [b M, (b + 1) M):
+//   sample   32 K strided keys of x (order-preserving uint32 keys).
+//   filter   one block of 1024 threads per CU.  Every block derives, identically, from the sample a
+//            candidate floor t_lo (count(key >= t_lo) ~ k + 4 sigma: ~1.27 k candidates at k/n = 1 %)
+//            and a likely ceiling t_hi of the k-th largest key; then the one HBM pass over its range
+//            (4 B/element): 16 waves stream 16 K-element block steps (4 float4 per lane, the next step
+//            in flight), one float compare per element, ballot/mbcnt compaction, the step's 16 wave
+//            counts exchanged through LDS so that the block's candidates land in index order in LDS;
+//            candidates in [t_lo, t_hi) are binned into a 2048-bin LDS histogram on the fly.  At the
+//            end the candidates go to the block's staging slot (<= 16 K; beyond, only counted) and the
+//            histogram, above-the-band count, max key and candidate count are added to global
+//            memory (memory-side atomics).  The kernel boundary is the grid-wide hand-off.
+//   select   one block of 1024 threads per CU, its own register budget: the summed histogram picks
+//            the bin holding the k-th largest key; every block publishes its candidates inside that
+//            bin (~3 each at the headline) and its count above it; after ONE exchange every block
+//            resolves the exact k-th largest key T among those keys and its own output offset
+//            locally, then writes its slice of the kept entries in index order: idx[k] + val[k] or
+//            idx[k] + codes[k] with the dithering fused.  Rare paths (a list overflow, a re-range,
+//            a floor that admitted fewer than k elements — then every block reads its x range
+//            directly) fall back to histogram rounds, each one exchange.
+// An exchange: the block drains its stores/atomics, raises its own flag to the exchange's epoch
+// (call * 32 + phase, from a call counter in the workspace), one wave polls all flags.  The histograms
+// are zeroed by the select at the end of each call; the workspace is zero-initialised once by its
+// owner.  Select launches on different streams of one device are serialised by an event chain, so two
+// never compete for co-residency; spins are bounded (error flag).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -47,92 +45,84 @@
 namespace flc {
 namespace {
 
-#ifndef FLC_FILTER_VARIANT
-#define FLC_FILTER_VARIANT 0  // != 0 only in calibration builds (tools/calib_variants.sh): results invalid
-#endif
-
+constexpr int kET = 1024;                     // threads per block of the filter / select kernels (one per CU)
+constexpr int kENW = kET / kWave;             // 16 waves
+constexpr int kStepF4 = 4;                    // float4 per lane per wave step
+constexpr int kWaveSpan = kStepF4 * 256;      // 1024 elements per wave step
+constexpr int kBlockStep = kENW * kWaveSpan;  // 16384 elements per block step
+constexpr int kCap = 16384;                   // candidates per block kept in LDS
 constexpr int kSample = 32768;
-constexpr int kSelectThreads = 1024;
-constexpr int kSamplePerThread = kSample / kSelectThreads;  // 32
-constexpr int kThreads = 256;
-constexpr int kFNW = kThreads / kWave;       // filter: 4 waves per block
-constexpr int kStepF4 = 8;                   // float4 per lane per wave step
-constexpr int kWaveSpan = kStepF4 * 256;     // 2048 elements per wave step (8 KB)
-constexpr int kBlockSpan = kFNW * kWaveSpan; // 8192 elements: filter chunks are multiples of this
-constexpr int kSelThreads = 1024;            // persistent select: one block of 16 waves per CU
-constexpr int kSelNW = kSelThreads / kWave;
-constexpr int kMaxSelBlocks = 1024;
+constexpr int kSPT = kSample / kET;           // 32 sample keys per thread
 constexpr int kHistBits = 11;
 constexpr int kHistBins = 1 << kHistBits;
-constexpr int kHistStride = kHistBins + 64;  // a round's bins + its "above the range" counter
-constexpr int kMaxRounds = 6;
-#ifndef FLC_MAX_REGIONS
-#define FLC_MAX_REGIONS 16384
-#endif
-constexpr int kMaxRegions = FLC_MAX_REGIONS; // filter blocks = staging regions
-constexpr int kRegionsPerThread = kMaxRegions / kSelThreads;  // 16 (P0 LDS scan)
-constexpr int kKeyCache = 14336;             // candidates per select block kept in LDS
-constexpr int kWcCap = 512;                  // block regions whose wave counts a select block keeps in LDS
-constexpr int kFlagStride = 16;              // one 64-B line per barrier arrival flag
+constexpr int kHistStride = kHistBins + 64;   // bins, [kHistBins] above-the-range count, [+1] max key
+constexpr int kMaxSlots = 12;                 // histogram rounds per call (normal + fallback pass)
+constexpr int kEpochStride = 32;              // exchanges per call < 32
+constexpr int kMaxBlocks = 1024;              // <= kET (per-block words are read one per thread)
+constexpr int kInbin = 32;                    // in-bin keys a block may publish (more: histogram rounds)
+constexpr int kInbinAll = 1024;               // in-bin keys of all blocks resolved locally
+constexpr int kFlagStride = 16;               // workspace words reserved per block for flags
 
-struct TopkParams {
-  unsigned t_lo;             // candidate floor (sample_select -> filter, select)
-  unsigned pad;
-  unsigned long long t_hi;   // likely ceiling of the k-th largest key (<= 2^32)
-};
-
-// state published by the barrier leader of the select launch (64-bit words, memory-side atomics
-// only); zeroed per call by the filter
-struct SelState {
-  unsigned long long gen;     // barrier generation
-  unsigned long long lo;      // live key range [lo, lo + width), log2 keys per bin, rank left
-  unsigned long long width;
-  unsigned long long shift;
-  unsigned long long rem;
-  unsigned long long done;    // threshold resolved
-  unsigned long long T;       // the k-th largest key
-  unsigned long long need;    // elements equal to T that are kept
-  unsigned long long ties;
-  unsigned long long strict;
-  unsigned long long err;     // 1: digit not found, 2: count mismatch, 4: barrier spin timeout
-  unsigned long long C;       // diagnostics
+// diagnostics and the call counter (64-bit words, memory-side atomics only)
+struct EncState {
+  unsigned long long call;   // calls completed on this workspace (epoch base)
+  unsigned long long err;    // 1: digit not found, 2: count mismatch, 4: exchange spin timeout
+  unsigned long long C;      // candidates (floor admitted)
   unsigned long long fallback;
+  unsigned long long T;      // the k-th largest key
   unsigned long long maxkey;
   unsigned long long rounds;
+  unsigned long long t_lo, t_hi;
+  unsigned long long need, ties, strict;
+  unsigned long long sample_path;  // 0 fast, 1 general radix, 2 take-all
+  unsigned long long pad[3];
 };
 
-struct TopkWs {
-  TopkParams* p;
-  SelState* st;
-  unsigned* flags;              // [kMaxSelBlocks * kFlagStride] barrier arrival flags
-  unsigned* hist;               // [kMaxRounds][kHistStride]
-  unsigned* sample;             // [kSample]
-  unsigned* region_cnt;         // [R]      candidates per filter block
-  unsigned* wave_cnt;           // [4 R]    candidates per wave quarter of a block
-  unsigned long long* blk_cnt;  // [kMaxSelBlocks]  strict << 32 | tie
-  unsigned long long* blk_off;  // [kMaxSelBlocks]
-  unsigned* cand_idx;           // [n]  ordered by index
-  unsigned* cand_raw;           // [n]  raw fp32 bits (only when the LDS key cache is too small)
-  uint2* stage;                 // [4 R * dcap]  (idx, raw): the first dcap candidates of each wave, dense
-  uint2* spill;                 // [4 R * qc]    the rest (worst case, rarely touched)
-  long long dcap;               // dense staging entries per wave (~2x the expected candidates)
-  long long qc;                 // elements per wave quarter of a filter block (chunk / 4)
-  unsigned long long* stamps;   // [16] diagnostic build only (FLC_SELECT_STAMPS)
-  unsigned long long* trace;    // [kMaxRounds * 8] leader's per-round record (diagnostics)
+// workspace layout: fixed offsets from one base pointer (every region 256-B aligned; only the staging
+// area at the end depends on n), so a kernel carries one pointer instead of a struct of them
+constexpr size_t al256(size_t v) { return (v + 255) / 256 * 256; }
+constexpr size_t kOffSt = 0;
+constexpr size_t kOffFlags = al256(kOffSt + 128);
+constexpr size_t kOffHist = al256(kOffFlags + (size_t)kMaxBlocks * kFlagStride * 4);
+constexpr size_t kOffAcc = kOffHist + (size_t)kMaxSlots * kHistStride * 4;  // contiguous with hist (zeroed together)
+constexpr size_t kOffBlk = al256(kOffAcc + 64);
+constexpr size_t kOffStamps = al256(kOffBlk + (size_t)kMaxBlocks * 8);
+constexpr size_t kOffSample = al256(kOffStamps + 128);
+constexpr size_t kOffInbin = al256(kOffSample + (size_t)kSample * 4);
+constexpr size_t kOffBlkC = al256(kOffInbin + (size_t)kMaxBlocks * kInbin * 4);
+constexpr size_t kOffStage = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // + G * kCap * 8 (keys, then indices)
+static_assert(kOffAcc % 8 == 0, "acc words are 64-bit");
+static_assert(sizeof(EncState) <= 128, "state block");
+
+struct EncWs {
+  char* base;
+  int64_t M;  // elements per block range (multiple of kBlockStep)
+  __device__ EncState* st() const { return reinterpret_cast<EncState*>(base + kOffSt); }
+  __device__ unsigned* flags() const { return reinterpret_cast<unsigned*>(base + kOffFlags); }
+  __device__ unsigned* hist() const { return reinterpret_cast<unsigned*>(base + kOffHist); }
+  __device__ unsigned long long* acc() const { return reinterpret_cast<unsigned long long*>(base + kOffAcc); }
+  __device__ unsigned long long* blk_cnt() const { return reinterpret_cast<unsigned long long*>(base + kOffBlk); }
+  __device__ unsigned long long* stamps() const { return reinterpret_cast<unsigned long long*>(base + kOffStamps); }
+  __device__ unsigned* sample() const { return reinterpret_cast<unsigned*>(base + kOffSample); }
+  __device__ unsigned* inbin() const { return reinterpret_cast<unsigned*>(base + kOffInbin); }
+  __device__ unsigned* blk_c() const { return reinterpret_cast<unsigned*>(base + kOffBlkC); }  // candidates / block
+  __device__ unsigned* stage_key(int b) const {
+    return reinterpret_cast<unsigned*>(base + kOffStage) + (size_t)b * 2 * kCap;
+  }
+  __device__ unsigned* stage_idx(int b) const { return stage_key(b) + kCap; }
 };
 
-struct TopkGeom {
-  int64_t chunk;    // elements per filter block (multiple of kBlockSpan)
-  int64_t regions;  // filter blocks launched, a multiple of 4 (trailing blocks may be empty)
+struct EncGeom {
+  int G;
+  int64_t M;
 };
 
-TopkGeom geometry(int64_t n) {
-  TopkGeom g;
-  int64_t blocks = cdiv(n, kBlockSpan);
-  if (blocks > kMaxRegions) blocks = kMaxRegions;
-  if (blocks < 1) blocks = 1;
-  g.chunk = (int64_t)align_up((size_t)cdiv(n, blocks), kBlockSpan);
-  g.regions = (int64_t)align_up((size_t)cdiv(n, g.chunk), 4);
+EncGeom enc_geometry(int64_t n, int cus) {
+  EncGeom g;
+  int64_t G0 = std::min<int64_t>(std::min<int64_t>(cus, kMaxBlocks), cdiv(n, kBlockStep));
+  if (G0 < 1) G0 = 1;
+  g.M = (int64_t)align_up((size_t)cdiv(n, G0), kBlockStep);
+  g.G = (int)cdiv(n, g.M);
   return g;
 }
 
@@ -154,86 +144,62 @@ SampleSetup sample_setup(int64_t n, int64_t k) {
   return s;
 }
 
-// dense staging per wave: twice the expected candidate count (the sample's floor admits ~rank_lo / S of
-// the elements) plus slack; waves with more candidates continue in their worst-case spill region.
-// Keeping the common case dense keeps the appends of all active waves inside a few MB (TLB / DRAM
-// page locality); a worst-case-sized region per wave made the staging writes 3-4x slower.
-int64_t dense_cap(int64_t n, int64_t k) {
-  const TopkGeom g = geometry(n);
-  const int64_t qc = g.chunk / kFNW;
-  const SampleSetup ss = sample_setup(n, k < 1 ? 1 : k);
-  if (ss.take_all) return qc;
-  const double frac = std::min(1.0, (double)ss.rank_lo / (double)ss.S);
-  const int64_t cap = (int64_t)align_up((size_t)(2.0 * frac * (double)qc) + 64, 32);
-  return cap < qc ? cap : qc;
-}
-
-TopkWs carve_topk(void* ws, size_t bytes, int64_t n, int64_t k, size_t* need) {
-  const TopkGeom g = geometry(n);
-  Carver c(ws, bytes);
-  TopkWs w;
-  w.p = c.take<TopkParams>(1);
-  w.stamps = c.take<unsigned long long>(16);
-  w.st = c.take<SelState>(1);
-  w.trace = c.take<unsigned long long>(kMaxRounds * 8);
-  w.flags = c.take<unsigned>((size_t)kMaxSelBlocks * kFlagStride);
-  w.hist = c.take<unsigned>((size_t)kMaxRounds * kHistStride);
-  w.sample = c.take<unsigned>(kSample);
-  w.region_cnt = c.take<unsigned>(g.regions);
-  w.wave_cnt = c.take<unsigned>(4 * g.regions);
-  w.blk_cnt = c.take<unsigned long long>(kMaxSelBlocks);
-  w.blk_off = c.take<unsigned long long>(kMaxSelBlocks);
-  w.cand_idx = c.take<unsigned>((size_t)n + 4);
-  w.cand_raw = c.take<unsigned>((size_t)n + 4);
-  // region stride = chunk + a 2304-B skew: with a power-of-two stride every block's appends would land
-  // on the same HBM channel (measured: 34 us instead of 8 us of staging writes on 1 GiB)
-  w.qc = g.chunk / kFNW;
-  w.dcap = dense_cap(n, k);
-  w.stage = c.take<uint2>((size_t)g.regions * kFNW * w.dcap);
-  w.spill = c.take<uint2>((size_t)g.regions * kFNW * w.qc);
-  *need = c.off;
+EncWs carve_enc(void* ws, int64_t n, int cus, size_t* need) {
+  EncWs w;
+  w.base = static_cast<char*>(ws);
+  const EncGeom g = enc_geometry(n, cus);
+  w.M = g.M;
+  *need = kOffStage + (size_t)g.G * kCap * 8;
   return w;
 }
+constexpr int kZeroWords = kMaxSlots * kHistStride + 16;  // hist + acc, as 32-bit words
 
 // ------------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------------
 
-// One wave: histogram h[NB] (LDS) and a rank `rem` (1-based, from the top) -> the bin holding that
-// rank and the rank inside it.  The lane that finds it writes *digit / *new_rem.
-template <int NB>
-__device__ void wave_select_from_top(const unsigned* h, long long rem, unsigned* digit, long long* new_rem,
-                                     unsigned* err) {
-  constexpr int B = NB / kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  long long ls = 0;
+// Histogram select: a histogram h[2048] (LDS) and a rank r (1-based, from the top) -> the bin holding
+// that rank and the rank inside it.
+// Block-wide (all kET threads call it; contains barriers): thread t holds the adjacent bins below
+// 2047 - BPT t (no LDS bank conflicts), one block scan from the top gives each thread the count above
+// its bins, and the thread holding rank r[j] writes digit[j] / new_rem[j].  (A wave-wide select reading
+// 32 bins per lane at a 128-B lane stride hits one bank 64 ways.)
+template <int NR>
+__device__ void block_select_from_top(const unsigned* h, const long long (&r)[NR], unsigned* digit,
+                                      long long* new_rem, unsigned* err, unsigned long long* s_red) {
+  constexpr int BPT = kHistBins / kET;  // bins per thread, highest first
+  static_assert(BPT * kET == kHistBins, "bins per thread");
+  const int t = threadIdx.x;
+  const int top = kHistBins - 1 - BPT * t;
+  unsigned c[BPT];
+  unsigned long long sum = 0;
 #pragma unroll
-  for (int i = 0; i < B; ++i) ls += h[lane * B + i];
-  const long long incl = wave_incl_scan(ls);
-  const long long total = __shfl(incl, kWave - 1, kWave);
-  const long long above = total - incl;  // bins of higher lanes
-  const bool hit = above < rem && rem <= above + ls;
-  const unsigned long long m = __ballot(hit);
-  if (m == 0) {
-    if (lane == 0) {
-      *digit = 0;
-      *new_rem = 1;
+  for (int i = 0; i < BPT; ++i) {
+    c[i] = h[top - i];
+    sum += c[i];
+  }
+  unsigned long long tot;
+  const long long ex = (long long)block_excl_scan<unsigned long long, kENW>(sum, s_red, &tot);
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const long long rj = r[j];
+    if (rj <= 0) continue;
+    long long above = ex;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      if (above < rj && rj <= above + (long long)c[i]) {
+        digit[j] = (unsigned)(top - i);
+        new_rem[j] = rj - above;
+      }
+      above += c[i];
+    }
+    if (t == 0 && (long long)tot < rj) {
+      digit[j] = 0u;
+      new_rem[j] = 1;
       *err |= 1u;
     }
-    return;
   }
-  if (lane == __ffsll((long long)m) - 1) {
-    long long cum = above;
-    for (int i = B - 1; i >= 0; --i) {
-      const long long c = h[lane * B + i];
-      if (cum + c >= rem) {
-        *digit = (unsigned)(lane * B + i);
-        *new_rem = rem - cum;
-        break;
-      }
-      cum += c;
-    }
-  }
+  __syncthreads();
 }
 
 // LDS histogram add with wave aggregation: when every active lane hits the same bin (ties, narrow
@@ -258,147 +224,170 @@ __device__ __forceinline__ int range_shift(unsigned long long width, int bits) {
   return len > bits ? len - bits : 0;
 }
 
-// memory-side reads / writes of words other blocks update with atomics in this launch
+__device__ __forceinline__ int64_t cdiv_dev(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// coherent (agent-scope) reads / writes of words other blocks update in this launch: relaxed atomic
+// loads, not read-modify-writes, so that all G blocks reading one word do not serialise on it
 __device__ __forceinline__ unsigned ld_mem(unsigned* p) {
-  return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned long long ld_mem64(unsigned long long* p) {
-  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_mem64(unsigned long long* p, unsigned long long v) {
   (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// last r in [0, R) with off[r] <= c (off in LDS, nondecreasing, off[R] > c)
-__device__ __forceinline__ int lds_region_search(const unsigned* off, int R, unsigned c) {
-  int lo = 0, hi = R;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (off[mid] <= c) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-__device__ __forceinline__ int lds_region_advance(const unsigned* off, int R, int r, unsigned c) {
-  if (off[r + 1] > c) return r;
-  int lo = r + 1, step = 1, hi;
-  for (;;) {
-    hi = lo + step;
-    if (hi >= R) {
-      hi = R;
-      break;
-    }
-    if (off[hi] > c) break;
-    lo = hi;
-    step <<= 1;
-  }
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (off[mid] <= c) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// ------------------------------------------------------------------------------------------------
-// sample -> candidate floor and ceiling
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void topk_sample_gather_kernel(const float* __restrict__ x, int64_t n, int S,
-                                                                      TopkWs w) {
-  const int j = blockIdx.x * kThreads + threadIdx.x;
-  if (j >= S) return;
-  const int64_t pos = (S == n) ? (int64_t)j : (int64_t)(((double)j + 0.5) * (double)n / (double)S);
-  w.sample[j] = order_key(__float_as_uint(x[pos < n ? pos : n - 1]));
-}
-
-// Two fixed digit passes (key bits 31..21, then 20..10) per target rank.  Only the count guarantees
-// matter: every sample key in or above the floor's bin is >= t_lo (so >= rank_lo of them), and fewer
-// than rank_hi sample keys are >= t_hi (the end of the ceiling's bin).
-__global__ __launch_bounds__(kSelectThreads) void topk_sample_select_kernel(int S, long long rank_lo,
-                                                                            long long rank_hi, int take_all,
-                                                                            TopkWs w) {
-  __shared__ unsigned s_hist[2][kHistBins];
-  __shared__ unsigned s_digit[2];
-  __shared__ long long s_rem[2];
-  __shared__ unsigned s_err;
-  const int tid = threadIdx.x, wid = tid >> 6;
-  if (take_all) {
-    if (tid == 0) {
-      w.p->t_lo = 0u;
-      w.p->t_hi = 1ull << 32;
-    }
-    return;
-  }
-  const bool two = rank_hi > 0;
-  unsigned keys[kSamplePerThread];
-#pragma unroll
-  for (int i = 0; i < kSamplePerThread; ++i) {
-    const int j = tid + i * kSelectThreads;
-    keys[i] = j < S ? w.sample[j] : 0u;
-  }
-  for (int i = tid; i < 2 * kHistBins; i += kSelectThreads) (&s_hist[0][0])[i] = 0u;
-  if (tid == 0) s_err = 0;
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kSamplePerThread; ++i) hist_add(s_hist[0], keys[i] >> 21, tid + i * kSelectThreads < S);
-  __syncthreads();
-  if (wid == 0) wave_select_from_top<kHistBins>(s_hist[0], rank_lo, &s_digit[0], &s_rem[0], &s_err);
-  else if (wid == 1 && two) wave_select_from_top<kHistBins>(s_hist[0], rank_hi, &s_digit[1], &s_rem[1], &s_err);
-  __syncthreads();
-  const unsigned d0 = s_digit[0], d1 = two ? s_digit[1] : 0u;
-  const long long r0 = s_rem[0], r1 = two ? s_rem[1] : 0;
-  for (int i = tid; i < 2 * kHistBins; i += kSelectThreads) (&s_hist[0][0])[i] = 0u;
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kSamplePerThread; ++i) {
-    const bool in = tid + i * kSelectThreads < S;
-    const unsigned hi = keys[i] >> 21, bin = (keys[i] >> 10) & (kHistBins - 1);
-    hist_add(s_hist[0], bin, in && hi == d0);
-    if (two) hist_add(s_hist[1], bin, in && hi == d1);
-  }
-  __syncthreads();
-  if (wid == 0) wave_select_from_top<kHistBins>(s_hist[0], r0, &s_digit[0], &s_rem[0], &s_err);
-  else if (wid == 1 && two) wave_select_from_top<kHistBins>(s_hist[1], r1, &s_digit[1], &s_rem[1], &s_err);
-  __syncthreads();
-  if (tid == 0) {
-    unsigned t_lo = (d0 << 21) | (s_digit[0] << 10);
-    unsigned long long t_hi = two ? (unsigned long long)((d1 << 21) | (s_digit[1] << 10)) + 1024ull : 1ull << 32;
-    if (s_err) {  // cannot happen for 0 < rank <= S; stay correct anyway: everything is a candidate
-      t_lo = 0u;
-      t_hi = 1ull << 32;
-    }
-    w.p->t_lo = t_lo;
-    w.p->t_hi = t_hi;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// streaming filter (the one HBM pass over x)
-// ------------------------------------------------------------------------------------------------
-// candidate test on values: key(v) >= t_lo  <=>  v >= t_lo_value  or  v is NaN (NaN is the largest
-// key; -0 == +0 holds for the float compare as for the keys)
+// candidate test on values: key(v) >= t_lo  <=>  v >= t_lo_value  or  v is NaN.  Exact for
+// t_lo <= key(+inf) (the host-side clamp below): below key(-inf) every value qualifies.
 __device__ __forceinline__ float floor_value(unsigned t_lo) {
-  return t_lo <= 0x007fffffu ? -__builtin_inff() : key_value(t_lo);  // keys below -inf: negative NaNs
+  return t_lo <= 0x007fffffu ? -__builtin_inff() : key_value(t_lo);
 }
-
-// key(v) >= t_lo as one unordered compare: true for v >= tf and for NaN
 __device__ __forceinline__ bool is_cand(float a, float tf) { return !(a < tf); }
 
-// one wave's 4096-element span of a block step: 16 float4 per lane (q-major: lane l, step q ->
-// elements 256q + 4l + c).  A partial span (the last block only) clamps each float4 to the last one
-// holding valid data (16-B aligned, so it never crosses a page); `lim` masks everything past b_end.
+// ------------------------------------------------------------------------------------------------
+// sample -> candidate floor and ceiling, computed identically by every block
+// ------------------------------------------------------------------------------------------------
+struct SampleLds {
+  unsigned hist2[kHistBins];
+  unsigned wmin[kENW];
+  unsigned wmax[kENW];
+  unsigned digit[2];
+  long long rem[2];
+  unsigned err;
+};
+
+// sample index of a thread's key slot i: 16-B runs, so the coherent read is 8 x 16 B per thread
+__device__ __forceinline__ int sample_j(int i) { return 4 * (int)threadIdx.x + 4 * kET * (i >> 2) + (i & 3); }
+
+// ascending bitonic sort of one value per lane across the wave
+__device__ __forceinline__ unsigned wave_sort_u32(unsigned v) {
+  const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int k = 2; k <= kWave; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const unsigned o = __shfl_xor(v, j, kWave);
+      const bool up = (lane & k) == 0;
+      const bool lower = (lane & j) == 0;
+      const unsigned mn = o < v ? o : v, mx = o < v ? v : o;
+      v = (lower == up) ? mn : mx;
+    }
+  }
+  return v;
+}
+
+// Fast path (rank_lo <= 1024): B = min over waves of the wave's ceil(rank_lo / 16)-th largest lane
+// maximum, so at least rank_lo sample keys are >= B (each wave holds that many), typically ~1.4 rank_lo.
+// ONE range-adaptive 11-bit histogram of the keys in [B, max] (straight from registers) then locates
+// the bins of ranks rank_lo and rank_hi: a bin holds ~0.3 sample keys here, so the bin floor of the
+// rank_lo-th key is a floor admitting rank_lo + O(1) sample keys and the end of the rank_hi-th key's
+// bin a ceiling with fewer than rank_hi sample keys at or above it.
+__device__ __forceinline__ bool sample_fast(const unsigned (&keys)[kSPT], int S, long long rank_lo, long long rank_hi,
+                                            SampleLds& L, unsigned* s_hist, unsigned long long* s_red,
+                                            unsigned* t_lo_out, unsigned long long* t_hi_out) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
+  unsigned m = 0;
+#pragma unroll
+  for (int i = 0; i < kSPT; ++i) m = keys[i] > m ? keys[i] : m;  // invalid slots hold key 0
+  const int q = (int)((rank_lo + kENW - 1) / kENW);              // 1 <= q <= 64
+  const unsigned srt = wave_sort_u32(m);
+  const unsigned bw = __shfl(srt, kWave - q, kWave);
+  const unsigned wmx = __shfl(srt, kWave - 1, kWave);
+  if (lane == 0) {
+    L.wmin[wid] = bw;
+    L.wmax[wid] = wmx;
+  }
+  if (tid == 0) L.err = 0;
+  for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
+  __syncthreads();
+  unsigned B = 0xffffffffu, mx = 0;
+#pragma unroll
+  for (int w = 0; w < kENW; ++w) {
+    B = L.wmin[w] < B ? L.wmin[w] : B;
+    mx = L.wmax[w] > mx ? L.wmax[w] : mx;
+  }
+  const int sh = range_shift((unsigned long long)mx - B + 1ull, kHistBits);
+#pragma unroll
+  for (int i = 0; i < kSPT; ++i) {
+    const bool f = sample_j(i) < S && keys[i] >= B;
+    if (__ballot(f)) hist_add(s_hist, (keys[i] - B) >> sh, f);
+  }
+  __syncthreads();
+  const bool two = rank_hi > 0;
+  const long long rk[2] = {rank_lo, two ? rank_hi : 0};
+  block_select_from_top<2>(s_hist, rk, L.digit, L.rem, &L.err, s_red);
+  if (L.err) return false;  // block-uniform
+  *t_lo_out = B + (L.digit[0] << sh);
+  *t_hi_out = two ? (unsigned long long)B + ((unsigned long long)(L.digit[1] + 1u) << sh) : (1ull << 32);
+  return true;
+}
+
+// General path (any rank): two fixed 11-bit digit passes (key bits 31..21, then 20..10) per target.
+__device__ __forceinline__ void sample_general(const unsigned (&keys)[kSPT], int S, long long rank_lo, long long rank_hi,
+                                               SampleLds& L, unsigned* s_hist, unsigned long long* s_red,
+                                               unsigned* t_lo_out, unsigned long long* t_hi_out) {
+  const int tid = threadIdx.x;
+  const bool two = rank_hi > 0;
+  __syncthreads();
+  for (int i = tid; i < kHistBins; i += kET) {
+    s_hist[i] = 0u;
+    L.hist2[i] = 0u;
+  }
+  if (tid == 0) L.err = 0;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSPT; ++i) hist_add(s_hist, keys[i] >> 21, sample_j(i) < S);
+  __syncthreads();
+  {
+    const long long rk[2] = {rank_lo, two ? rank_hi : 0};
+    block_select_from_top<2>(s_hist, rk, L.digit, L.rem, &L.err, s_red);
+  }
+  const unsigned d0 = L.digit[0], d1 = two ? L.digit[1] : 0u;
+  const long long r0 = L.rem[0], r1 = two ? L.rem[1] : 0;
+  for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSPT; ++i) {
+    const bool in = sample_j(i) < S;
+    const unsigned hi = keys[i] >> 21, bin = (keys[i] >> 10) & (kHistBins - 1);
+    hist_add(s_hist, bin, in && hi == d0);
+    if (two) hist_add(L.hist2, bin, in && hi == d1);
+  }
+  __syncthreads();
+  {
+    const long long ra[1] = {r0}, rb[1] = {two ? r1 : 0};
+    block_select_from_top<1>(s_hist, ra, &L.digit[0], &L.rem[0], &L.err, s_red);
+    block_select_from_top<1>(L.hist2, rb, &L.digit[1], &L.rem[1], &L.err, s_red);
+  }
+  unsigned t_lo = (d0 << 21) | (L.digit[0] << 10);
+  unsigned long long t_hi = two ? (unsigned long long)((d1 << 21) | (L.digit[1] << 10)) + 1024ull : 1ull << 32;
+  if (L.err) {  // cannot happen for 0 < rank <= S; stay correct anyway: everything is a candidate
+    t_lo = 0u;
+    t_hi = 1ull << 32;
+  }
+  *t_lo_out = t_lo;
+  *t_hi_out = t_hi;
+}
+
+// ------------------------------------------------------------------------------------------------
+// filter
+// ------------------------------------------------------------------------------------------------
+// one wave's 2048-element step: 8 float4 per lane (q-major: lane l, step q -> elements 256q + 4l + c).
+// A partial step (the last block only) clamps each float4 to the last one holding valid data
+// (16-B aligned, so it never crosses a page); `lim` masks everything past the range end.
 template <bool FULL>
-__device__ __forceinline__ void filter_load(const float* __restrict__ x, int64_t wb, int64_t b_end, int lane,
-                                            float4 (&v)[kStepF4]) {
+__device__ __forceinline__ void step_load(const float* __restrict__ x, int64_t wb, int64_t end, int lane,
+                                          float4 (&v)[kStepF4]) {
   if (FULL) {
 #pragma unroll
     for (int q = 0; q < kStepF4; ++q) v[q] = ld_stream(x + wb + 256 * q + 4 * lane);
   } else {
-    const int64_t last4 = (b_end - 1) & ~(int64_t)3;
+    const int64_t last4 = (end - 1) & ~(int64_t)3;
 #pragma unroll
     for (int q = 0; q < kStepF4; ++q) {
       const int64_t e = wb + 256 * q + 4 * lane;
-      v[q] = *reinterpret_cast<const float4*>(x + (e < last4 ? e : last4));
+      v[q] = *reinterpret_cast<const float4*>(x + (e < last4 ? e : (last4 >= 0 ? last4 : 0)));
     }
   }
 }
@@ -415,9 +404,8 @@ __device__ __forceinline__ void cand4(const float4& v, float tf, int o, int lim,
   f3 = is_cand(v.w, tf) && in_span<FULL>(o + 3, lim);
 }
 
-// the wave's candidate count: one compare per element into a wave mask, scalar popcounts
 template <bool FULL>
-__device__ __forceinline__ unsigned filter_count(const float4 (&v)[kStepF4], float tf, int lim, int lane) {
+__device__ __forceinline__ unsigned step_count(const float4 (&v)[kStepF4], float tf, int lim, int lane) {
   unsigned cnt = 0;
 #pragma unroll
   for (int q = 0; q < kStepF4; ++q) {
@@ -428,24 +416,34 @@ __device__ __forceinline__ unsigned filter_count(const float4 (&v)[kStepF4], flo
   return cnt;
 }
 
-#ifndef FLC_STAGE_NT
-#define FLC_STAGE_NT 0
-#endif
-__device__ __forceinline__ void st_stage(uint2* dst, unsigned idx, float v) {
-  if (FLC_STAGE_NT) {
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-    u32x2 t = {idx, __float_as_uint(v)};
-    __builtin_nontemporal_store(t, reinterpret_cast<u32x2*>(dst));
-  } else {
-    *dst = make_uint2(idx, __float_as_uint(v));
+struct FilterCtx {
+  unsigned* s_key;
+  unsigned* s_idx;
+  unsigned* s_hist;
+  unsigned t_lo;
+  unsigned long long width0;  // t_hi - t_lo
+  int sh0;
+  unsigned above;         // per thread: candidates >= t_hi
+  unsigned mk;            // per thread: max candidate key
+};
+
+__device__ __forceinline__ void emit(FilterCtx& c, unsigned p, unsigned e, float v) {
+  const unsigned raw = __float_as_uint(v);
+  if (p < (unsigned)kCap) {  // beyond: the block counts on, and later phases re-read its x range
+    c.s_key[p] = raw;
+    c.s_idx[p] = e;
   }
+  const unsigned key = order_key(raw);
+  const unsigned long long rel = (unsigned long long)(key - c.t_lo);
+  if (rel >= c.width0) ++c.above;
+  else atomicAdd(&c.s_hist[(unsigned)(rel >> c.sh0)], 1u);
+  c.mk = key > c.mk ? key : c.mk;
 }
 
-// ordered append from position `pos` (element order within a step q: lane-major, then the 4 components)
+// ordered append from position `pos` (within a q: lane-major, then the 4 components)
 template <bool FULL>
-__device__ __forceinline__ void filter_write(const float4 (&v)[kStepF4], float tf, int lim, int lane, unsigned wbu,
-                                             unsigned pos, uint2* __restrict__ out, uint2* __restrict__ spill,
-                                             unsigned dcap) {
+__device__ __forceinline__ void step_write(const float4 (&v)[kStepF4], float tf, int lim, int lane, unsigned wbu,
+                                           unsigned pos, FilterCtx& c) {
 #pragma unroll
   for (int q = 0; q < kStepF4; ++q) {
     bool f0, f1, f2, f3;
@@ -459,138 +457,62 @@ __device__ __forceinline__ void filter_write(const float4 (&v)[kStepF4], float t
       p = __builtin_amdgcn_mbcnt_hi((unsigned)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m3, p));
       if (f0 | f1 | f2 | f3) {
         const unsigned e = wbu + (unsigned)(256 * q + 4 * lane);
-        if (f0) { st_stage(p < dcap ? out + p : spill + (p - dcap), e + 0u, v[q].x); ++p; }
-        if (f1) { st_stage(p < dcap ? out + p : spill + (p - dcap), e + 1u, v[q].y); ++p; }
-        if (f2) { st_stage(p < dcap ? out + p : spill + (p - dcap), e + 2u, v[q].z); ++p; }
-        if (f3) st_stage(p < dcap ? out + p : spill + (p - dcap), e + 3u, v[q].w);
+        if (f0) { emit(c, p, e + 0u, v[q].x); ++p; }
+        if (f1) { emit(c, p, e + 1u, v[q].y); ++p; }
+        if (f2) { emit(c, p, e + 2u, v[q].z); ++p; }
+        if (f3) emit(c, p, e + 3u, v[q].w);
       }
       pos += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
     }
   }
 }
 
-// one wave step (2048 elements, already loaded into v): count, append in order after the wave's
-// earlier candidates
+// one block step: count, exchange the 16 wave counts through LDS, append in index order
 template <bool FULL>
-__device__ __forceinline__ void filter_process(const float4 (&v)[kStepF4], int64_t wb, int64_t q_end, float tf,
-                                               uint2* __restrict__ out, uint2* __restrict__ spill, unsigned dcap,
-                                               unsigned& run) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int lim = FULL ? kWaveSpan : (int)(q_end > wb ? (q_end - wb < kWaveSpan ? q_end - wb : kWaveSpan) : 0);
-  const unsigned wcnt = filter_count<FULL>(v, tf, lim, lane);
-#if FLC_FILTER_VARIANT == 2  // calibration only: loads + count, no append
-  run += wcnt;
-  return;
-#endif
+__device__ __forceinline__ void step_process(const float4 (&v)[kStepF4], int64_t wb, int64_t end, float tf,
+                                             unsigned (&s_wc)[2][kENW], int par, unsigned& base, FilterCtx& c) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+  const int lim = FULL ? kWaveSpan : (int)(end > wb ? (end - wb < kWaveSpan ? end - wb : kWaveSpan) : 0);
+  const unsigned cnt = step_count<FULL>(v, tf, lim, lane);
+  if (lane == 0) s_wc[par][wid] = cnt;
+  lds_barrier();
+  unsigned pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kENW; ++w) {
+    const unsigned cw = s_wc[par][w];
+    pre += w < wid ? cw : 0u;
+    tot += cw;
+  }
   // re-derive the masks rather than keep them live across the count (an opaque copy of the floor
   // stops the compiler from reusing the count pass's compares)
   float tf2 = tf;
   asm volatile("" : "+v"(tf2));
-  if (wcnt != 0u) filter_write<FULL>(v, tf2, lim, lane, (unsigned)wb, run, out, spill, dcap);
-  run += wcnt;
-}
-
-// Each wave owns a contiguous quarter of its block's chunk and appends to its own quarter of the
-// block's staging region: no barrier between the waves.  The block total (for the select's region
-// scan) is formed by the last wave to finish, via one 64-bit LDS ticket (waves done << 32 | count).
-__global__ __launch_bounds__(kThreads) void topk_filter_kernel(const float* __restrict__ x, int64_t n, int64_t chunk,
-                                                               int sel_grid, TopkWs w) {
-  __shared__ unsigned long long s_tick;
-  const float tf = floor_value(w.p->t_lo);
-  if (threadIdx.x == 0) s_tick = 0ull;
-  if (blockIdx.x == 0) {  // reset the select state of this call (read by the next launch)
-    for (int i = threadIdx.x; i < kMaxRounds * kHistStride; i += kThreads) w.hist[i] = 0u;
-    for (int i = threadIdx.x; i < sel_grid; i += kThreads) w.flags[i * kFlagStride] = 0u;
-    if (threadIdx.x < (int)(sizeof(SelState) / 8)) reinterpret_cast<unsigned long long*>(w.st)[threadIdx.x] = 0ull;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
-  const int64_t qc = chunk / kFNW;
-  const int64_t q_begin = (int64_t)blockIdx.x * chunk + wid * qc;
-  const int64_t q_end = q_begin + qc < n ? q_begin + qc : n;
-  const int64_t wave_id = (int64_t)blockIdx.x * kFNW + wid;
-  uint2* __restrict__ out = w.stage + wave_id * w.dcap;
-  uint2* __restrict__ spill = w.spill + wave_id * qc;
-  const unsigned dcap = (unsigned)w.dcap;
-  unsigned run = 0;
-  // software pipeline over the wave's full steps: step i + 1 is in flight while step i is processed
-  const int64_t nfull = q_end > q_begin ? (q_end - q_begin) / kWaveSpan : 0;
-  int64_t s = q_begin, i = 0;
-  float4 va[kStepF4], vb[kStepF4];
-  if (nfull > 0) filter_load<true>(x, s, q_end, lane, va);
-  for (; i + 2 <= nfull; i += 2) {
-    filter_load<true>(x, s + kWaveSpan, q_end, lane, vb);
-    filter_process<true>(va, s, q_end, tf, out, spill, dcap, run);
-    s += kWaveSpan;
-    if (i + 2 < nfull) filter_load<true>(x, s + kWaveSpan, q_end, lane, va);
-    filter_process<true>(vb, s, q_end, tf, out, spill, dcap, run);
-    s += kWaveSpan;
-  }
-  if (i < nfull) {
-    filter_process<true>(va, s, q_end, tf, out, spill, dcap, run);
-    s += kWaveSpan;
-  }
-  if (s < q_end) {
-    filter_load<false>(x, s, q_end, lane, va);
-    filter_process<false>(va, s, q_end, tf, out, spill, dcap, run);
-  }
-  if (lane == 0) {
-    w.wave_cnt[blockIdx.x * kFNW + wid] = run;
-    const unsigned long long old = atomicAdd(&s_tick, (1ull << 32) | run);
-    if ((old >> 32) == (unsigned long long)(kFNW - 1)) w.region_cnt[blockIdx.x] = (unsigned)old + run;
-  }
+  if (cnt != 0u) step_write<FULL>(v, tf2, lim, lane, (unsigned)wb, base + pre, c);
+  base += tot;
 }
 
 // ------------------------------------------------------------------------------------------------
-// persistent select: P0 scan | radix rounds | counts | compaction
+// exchanges and the per-block view of the selection state
 // ------------------------------------------------------------------------------------------------
-
-// the per-block copy of the leader-published state
-struct SelView {
-  unsigned lo;
-  unsigned long long width;
-  int shift;
-  long long rem;
-  int done;
-  unsigned T;
-  long long need;
-  unsigned maxkey;
-};
-
-// Grid barrier: every block but 0 raises its arrival flag (one 64-B line each, no contended
-// counter); block 0 polls all flags in parallel, runs `lead` (all of its threads) and bumps the
-// generation word the others poll (relaxed agent-scope loads + s_sleep, bounded).
-template <typename F>
-__device__ void grid_barrier(const TopkWs& w, unsigned nbar, F&& lead) {
-  const unsigned target = nbar + 1;
+// Exchange (grid barrier with data): the block's prior atomics / stores drained, its own flag raised to
+// `ep` (packed flags, one word per block), then one wave polls all G flags (each lane a few words per
+// round, relaxed agent-scope loads, a wave-wide vote, sleep between rounds).  No leader and no
+// contended counter: 256 arrivals on ONE word serialise at the memory-side atomic unit (measured ~5 us).
+__device__ void exchange(const EncWs& w, unsigned ep) {
   drain_stores();
   __syncthreads();
-  if (blockIdx.x == 0) {
-    const int tid = threadIdx.x;
-    if (tid > 0 && tid < (int)gridDim.x) {
-      unsigned* f = w.flags + (size_t)tid * kFlagStride;
-      unsigned spins = 0;
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 24)) {  // ~1 s: a block never arrived; flag it and let the launch drain
-          __hip_atomic_fetch_or(&w.st->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    lead();
-    drain_stores();
-    __syncthreads();
-    if (tid == 0) st_mem64(&w.st->gen, target);
-  } else if (threadIdx.x == 0) {
-    (void)__hip_atomic_exchange(w.flags + (size_t)blockIdx.x * kFlagStride, target, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
+  const int tid = threadIdx.x;
+  if (tid == 0) __hip_atomic_store(w.flags() + blockIdx.x, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < kWave) {
     unsigned spins = 0;
-    while (__hip_atomic_load(&w.st->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)target) {
+    for (;;) {
+      bool ok = true;
+      for (int b = tid; b < (int)gridDim.x; b += kWave)
+        ok = ok && (int)(__hip_atomic_load(w.flags() + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ep) >= 0;
+      if (__ballot(!ok) == 0ull) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {
-        __hip_atomic_fetch_or(&w.st->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > (1u << 22)) {  // ~1 s: a block never arrived; flag it and let the launch drain
+        if (tid == 0) __hip_atomic_fetch_or(&w.st()->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -598,427 +520,747 @@ __device__ void grid_barrier(const TopkWs& w, unsigned nbar, F&& lead) {
   __syncthreads();
 }
 
-__device__ void read_view(const TopkWs& w, SelView* v) {
-  if (threadIdx.x == 0) {
-    v->lo = (unsigned)ld_mem64(&w.st->lo);
-    v->width = ld_mem64(&w.st->width);
-    v->shift = (int)ld_mem64(&w.st->shift);
-    v->rem = (long long)ld_mem64(&w.st->rem);
-    v->done = (int)ld_mem64(&w.st->done);
-    v->T = (unsigned)ld_mem64(&w.st->T);
-    v->need = (long long)ld_mem64(&w.st->need);
-    v->maxkey = (unsigned)ld_mem64(&w.st->maxkey);
-  }
+struct SelState {
+  unsigned lo;
+  unsigned long long width;
+  int shift;
+  long long rem;
+  int done;
+  int narrowed;    // the last pick narrowed the range to one bin (need = rank inside it, from the top)
+  unsigned T;
+  long long need;
+};
+
+// after the exchange of round slot r: the summed histogram, its above-the-range count and max key (and,
+// for round 0, the candidate total) read into LDS in one batch of coherent loads (one round trip)
+__device__ __forceinline__ void load_hist(const EncWs& w, int r, unsigned* s_ghist, unsigned long long* s_ex,
+                                          bool with_total) {
+  constexpr int BPT = kHistBins / kET;
+  unsigned* h = w.hist() + (size_t)r * kHistStride;
+  const int tid = threadIdx.x;
+  unsigned v[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) v[i] = ld_mem(&h[tid + i * kET]);
+  unsigned long long e = 0;
+  if (tid < 2) e = ld_mem(&h[kHistBins + tid]);  // above count, max key
+  else if (tid == 2 && with_total) e = ld_mem64(&w.acc()[0]);
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) s_ghist[tid + i * kET] = v[i];
+  if (tid < 3) s_ex[tid] = e;
   __syncthreads();
 }
 
-// leader step of a radix round.  `rem` is the rank (from the top) of the k-th largest key among all
-// keys >= lo, so it stays k; the round's `A` keys above the live range come first: if A >= rem the
-// key lies above the range (re-range to [lo + width, top)), otherwise pick the bin of rank rem - A in
-// the global histogram of round r and narrow the range to it.
-__device__ void lead_pick(const TopkWs& w, int r, const SelView& cur, unsigned* s_ghist) {
+// pick (identically in every block) from the loaded histogram; `cur` lives in LDS (block-uniform state
+// kept out of registers: at 1024 threads a wave has 128 VGPRs, and the filter's live set left none).  `rem` is the rank (from the top) of
+// the k-th largest key among keys >= lo, so it stays k; the round's `A` keys above the live range
+// come first: if A >= rem the key lies above the range (re-range to [lo + width, max + 1)), otherwise
+// pick the bin of rank rem - A and narrow to it.
+__device__ void pick_digit(const EncWs& w, SelState& cur, long long A, unsigned maxkey, const unsigned* s_ghist,
+                           unsigned* s_err, unsigned long long* s_red) {
   __shared__ unsigned s_digit;
   __shared__ long long s_rem;
-  __shared__ unsigned s_err;
-  __shared__ long long s_above;
-  unsigned* h = w.hist + (size_t)r * kHistStride;
-  for (int i = threadIdx.x; i < kHistBins; i += kSelThreads) s_ghist[i] = ld_mem(&h[i]);
-  __shared__ unsigned s_maxkey;
-  if (threadIdx.x == 0) {
-    s_err = 0;
-    s_above = (long long)ld_mem(&h[kHistBins]);
-    s_maxkey = r == 0 ? ld_mem(&w.hist[kHistBins + 1]) : cur.maxkey;
-    if (r == 0) st_mem64(&w.st->maxkey, s_maxkey);
-    st_mem64(&w.st->rounds, (unsigned long long)r + 1ull);
-  }
+  if (threadIdx.x == 0) *s_err = 0;
   __syncthreads();
-  const long long A = s_above;
+  SelState nx = cur;
+  nx.narrowed = 0;
   if (A >= cur.rem) {  // the k-th largest key is above the range (block-uniform branch)
-    if (threadIdx.x == 0) {
-      const unsigned long long nlo = (unsigned long long)cur.lo + cur.width;
-      const unsigned long long top = (unsigned long long)s_maxkey + 1ull;
-      const unsigned long long nw = top > nlo ? top - nlo : 0ull;
-      if (nw == 0ull) __hip_atomic_fetch_or(&w.st->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      st_mem64(&w.st->lo, nlo);
-      st_mem64(&w.st->width, nw);
-      st_mem64(&w.st->shift, (unsigned long long)range_shift(nw, kHistBits));
-      st_mem64(&w.st->rem, (unsigned long long)cur.rem);
-    }
+    const unsigned long long nlo = (unsigned long long)cur.lo + cur.width;
+    const unsigned long long top = (unsigned long long)maxkey + 1ull;
+    const unsigned long long nw = top > nlo ? top - nlo : 0ull;
+    if (nw == 0ull && threadIdx.x == 0)
+      __hip_atomic_fetch_or(&w.st()->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nx.lo = (unsigned)nlo;
+    nx.width = nw ? nw : 1ull;
+    nx.shift = range_shift(nx.width, kHistBits);
+    __syncthreads();
+    if (threadIdx.x == 0) cur = nx;
+    __syncthreads();
     return;
   }
-  if (threadIdx.x < kWave) wave_select_from_top<kHistBins>(s_ghist, cur.rem - A, &s_digit, &s_rem, &s_err);
+  {
+    const long long rk[1] = {cur.rem - A};
+    block_select_from_top<1>(s_ghist, rk, &s_digit, &s_rem, s_err, s_red);
+  }
+  const unsigned d = s_digit;
+  const long long rr = s_rem;
+  if (*s_err && threadIdx.x == 0) __hip_atomic_fetch_or(&w.st()->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned nlo = cur.lo + (d << cur.shift);
+  if (cur.shift == 0) {
+    nx.T = nlo;
+    nx.need = rr;
+    nx.done = 1;
+  } else {
+    nx.lo = nlo;
+    nx.width = 1ull << cur.shift;
+    nx.shift = range_shift(nx.width, kHistBits);
+    nx.narrowed = 1;
+    nx.need = rr;
+  }
+  __syncthreads();  // every thread has read cur, s_digit, s_rem
+  if (threadIdx.x == 0) cur = nx;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long* tr = w.trace + r * 8;
-    tr[0] = cur.lo; tr[1] = cur.width; tr[2] = (unsigned long long)cur.shift; tr[3] = (unsigned long long)cur.rem;
-    tr[4] = (unsigned long long)A; tr[5] = s_digit; tr[6] = (unsigned long long)s_rem; tr[7] = s_ghist[s_digit];
-    const unsigned nlo = cur.lo + (s_digit << cur.shift);
-    if (s_err) __hip_atomic_fetch_or(&w.st->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur.shift == 0) {
-      st_mem64(&w.st->T, nlo);
-      st_mem64(&w.st->need, (unsigned long long)s_rem);
-      st_mem64(&w.st->done, 1ull);
-    } else {
-      const unsigned long long nw = 1ull << cur.shift;
-      st_mem64(&w.st->lo, nlo);
-      st_mem64(&w.st->width, nw);
-      st_mem64(&w.st->shift, (unsigned long long)range_shift(nw, kHistBits));
-      st_mem64(&w.st->rem, (unsigned long long)cur.rem);  // rank from the top among keys >= lo: unchanged
-    }
+}
+
+// candidate p of this block: its LDS array, or (fallback, or more candidates than kCap) the block's x
+// range itself — every element, since no later phase keeps an element below the floor anyway
+struct CandSrc {
+  const unsigned* s_key;
+  const unsigned* s_idx;
+  const float* x;
+  int64_t b0;
+  bool xmode;
+};
+__device__ __forceinline__ void cand_get(const CandSrc& c, unsigned p, unsigned& raw, unsigned& id) {
+  if (c.xmode) {
+    raw = __float_as_uint(c.x[c.b0 + p]);
+    id = (unsigned)(c.b0 + p);
+  } else {
+    raw = c.s_key[p];
+    id = c.s_idx[p];
   }
 }
 
 #ifdef FLC_SELECT_STAMPS
+// phase stamps of block 0, kept in LDS and written out at the end (slots: filter kernel 0-3, select
+// kernel 4-15; s_memrealtime, 100 MHz)
 #define STAMP(i)                                                                                 \
   do {                                                                                           \
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.stamps[i] = __builtin_amdgcn_s_memrealtime();     \
+    if (blockIdx.x == 0 && threadIdx.x == 0) s_stamp[i] = __builtin_amdgcn_s_memrealtime();      \
   } while (0)
+#define STAMP_INIT()                                                                             \
+  __shared__ unsigned long long s_stamp[16];                                                     \
+  if (threadIdx.x < 16) s_stamp[threadIdx.x] = 0ull;                                             \
+  __syncthreads()
+#define STAMP_OUT(lo, hi)                                                                        \
+  if (blockIdx.x == 0 && (int)threadIdx.x >= (lo) && (int)threadIdx.x < (hi))                    \
+  w.stamps()[threadIdx.x] = s_stamp[threadIdx.x]
 #else
 #define STAMP(i) do { } while (0)
+#define STAMP_INIT() do { } while (0)
+#define STAMP_OUT(lo, hi) do { } while (0)
 #endif
 
-template <bool STACKED>
-__global__ __launch_bounds__(kSelThreads) void topk_select_kernel(const float* __restrict__ x, TopkWs w, int R,
-                                                                  long long k, int64_t n, int* __restrict__ idx_out,
-                                                                  float* __restrict__ val_out,
-                                                                  uint8_t* __restrict__ code_out,
-                                                                  float* __restrict__ norm_out, int levels, double step,
-                                                                  uint64_t seed, uint64_t counter) {
-  __shared__ unsigned s_off[kMaxRegions + 1];
-  __shared__ __attribute__((aligned(16))) unsigned s_keys[kKeyCache];
+// ------------------------------------------------------------------------------------------------
+// sample kernel
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void topk_sample_kernel(const float* __restrict__ x, int64_t n, int S, EncWs w) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= S) return;
+  const int64_t pos = (S == n) ? (int64_t)j : (int64_t)(((double)j + 0.5) * (double)n / (double)S);
+  w.sample()[j] = order_key(__float_as_uint(x[pos < n ? pos : n - 1]));
+}
+
+// ------------------------------------------------------------------------------------------------
+// filter kernel: floor / ceiling from the sample, the HBM pass, staging + round-0 histogram
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restrict__ x, int64_t n, EncWs w, int S,
+                                                          long long rank_lo, long long rank_hi, int take_all) {
+  __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
+  __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
   __shared__ unsigned s_hist[kHistBins];
-  __shared__ unsigned s_ghist[kHistBins];
-  __shared__ uint4 s_wc[kWcCap];
-  __shared__ unsigned long long s_red[kSelNW];
-  __shared__ unsigned s_mx[kSelNW];
-  __shared__ SelView s_view;
-  const int tid = threadIdx.x;
+  __shared__ unsigned s_wc[2][kENW];
+  __shared__ unsigned long long s_red[kENW];
+  __shared__ unsigned s_mx[kENW];
+  SampleLds& SL = *reinterpret_cast<SampleLds*>(s_key);  // the sample phase precedes every candidate write
+  static_assert(sizeof(SampleLds) <= sizeof(unsigned) * kCap, "sample scratch must fit the key array");
+  STAMP_INIT();
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
+  const int64_t b0 = (int64_t)blockIdx.x * w.M;
+  const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
+  const int nsteps = (int)cdiv_dev(b1 - b0, (int64_t)kBlockStep);
   STAMP(0);
 
-  // ---- P0: region offsets in LDS and the candidate count (identical in every block)
-  {
-    const int r0 = tid * kRegionsPerThread;
-    unsigned loc[kRegionsPerThread];
-    unsigned long long sum = 0;
+  // ---- floor / ceiling (identical in every block)
+  unsigned t_lo;
+  unsigned long long t_hi;
+  if (take_all) {
+    t_lo = 0u;
+    t_hi = 1ull << 32;
+    if (blockIdx.x == 0 && tid == 0) w.st()->sample_path = 2ull;
+  } else {
+    unsigned keys[kSPT];
 #pragma unroll
-    for (int i = 0; i < kRegionsPerThread; i += 4) {
-      if (r0 + i < R) {  // R is a multiple of 4
-        const uint4 c = *reinterpret_cast<const uint4*>(w.region_cnt + r0 + i);
-        loc[i] = c.x; loc[i + 1] = c.y; loc[i + 2] = c.z; loc[i + 3] = c.w;
+    for (int i = 0; i < kSPT; i += 4) {
+      const int j = sample_j(i);
+      if (j + 4 <= S) {
+        const uint4 t = *reinterpret_cast<const uint4*>(w.sample() + j);
+        keys[i] = t.x; keys[i + 1] = t.y; keys[i + 2] = t.z; keys[i + 3] = t.w;
       } else {
-        loc[i] = loc[i + 1] = loc[i + 2] = loc[i + 3] = 0u;
-      }
-      sum += (unsigned long long)loc[i] + loc[i + 1] + loc[i + 2] + loc[i + 3];
-    }
-    unsigned long long tot;
-    unsigned long long run = block_excl_scan<unsigned long long, kSelNW>(sum, s_red, &tot);
 #pragma unroll
-    for (int i = 0; i < kRegionsPerThread; ++i) {
-      if (r0 + i < R) s_off[r0 + i] = (unsigned)run;
-      run += loc[i];
+        for (int c = 0; c < 4; ++c) keys[i + c] = j + c < S ? w.sample()[j + c] : 0u;  // 0: below every key
+      }
     }
-    if (tid == 0) {
-      s_off[R] = (unsigned)tot;
-      s_red[0] = tot;
-    }
-    __syncthreads();
+    bool ok = false;
+    if (rank_lo <= kWave * kENW) ok = sample_fast(keys, S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
+    if (!ok) sample_general(keys, S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
+    if (blockIdx.x == 0 && tid == 0) w.st()->sample_path = ok ? 0ull : 1ull;
   }
-  const unsigned long long c_cand = s_red[0];
-  __syncthreads();  // s_red is reused below
-  const bool fb = (long long)c_cand < k;
-  const long long C = fb ? (long long)n : (long long)c_cand;
-  long long per = (C + gridDim.x - 1) / gridDim.x;
-  per = (per + 3) & ~3ll;
-  const long long v0 = min((long long)blockIdx.x * per, C), v1 = min(v0 + per, C);
-  const bool cached = per <= kKeyCache;  // grid-uniform
-
-  // round 0 covers [t_lo, t_hi) (fallback: every key); keys above it are counted apart
-  SelView cur;
-  cur.lo = fb ? 0u : w.p->t_lo;
-  unsigned long long hi_end = fb ? (1ull << 32) : w.p->t_hi;
-  if (hi_end <= (unsigned long long)cur.lo || hi_end > (1ull << 32)) hi_end = 1ull << 32;
-  cur.width = hi_end - cur.lo;
-  cur.shift = range_shift(cur.width, kHistBits);
-  cur.rem = k;
-  cur.done = 0;
-  cur.T = 0;
-  cur.need = 0;
-  cur.maxkey = 0;
-  SelView prev = cur;
-  unsigned long long a_blk = 0;  // keys above the live range in this block (last round)
-  unsigned nbar = 0;
+  // the float predicate !(v < key_value(t_lo)) equals key >= t_lo for t_lo <= key(+inf)
+  if (t_lo > 0xff800000u) t_lo = 0xff800000u;
+  if (t_hi <= (unsigned long long)t_lo || t_hi > (1ull << 32)) t_hi = 1ull << 32;
+  if (blockIdx.x == 0 && tid == 0) {
+    w.st()->t_lo = t_lo;
+    w.st()->t_hi = t_hi;
+  }
+  __syncthreads();  // sample scratch (aliases s_key) dead from here
+  for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
+  __syncthreads();
   STAMP(1);
 
-  // ---- radix rounds: histogram of the live range (+ count above it), leader picks the digit
-  for (int round = 0; round < kMaxRounds; ++round) {
-    for (int i = tid; i < kHistBins; i += kSelThreads) s_hist[i] = 0u;
-    __syncthreads();
-    unsigned above = 0, mk = 0;
-    int r = 0, r_cur = -1, r_first = 0;
-    bool wc_lds = false;
-    uint4 wc = make_uint4(0u, 0u, 0u, 0u);
-    if (round == 0 && !fb) {
-      // wave counts of the block regions this select block gathers from, staged in LDS when they fit
-      if (v0 < v1) {
-        r_first = lds_region_search(s_off, R, (unsigned)v0);
-        const int r_last = lds_region_search(s_off, R, (unsigned)(v1 - 1));
-        wc_lds = r_last - r_first + 1 <= kWcCap;
-        if (wc_lds)
-          for (int i = tid; i <= r_last - r_first; i += kSelThreads)
-            s_wc[i] = *reinterpret_cast<const uint4*>(w.wave_cnt + (size_t)(r_first + i) * kFNW);
-      }
-      __syncthreads();
-      if (v0 + 4 * (long long)tid < v1) r = lds_region_search(s_off, R, (unsigned)(v0 + 4 * tid));
+  // ---- the HBM pass
+  const float tf = floor_value(t_lo);
+  FilterCtx fc;
+  fc.s_key = s_key;
+  fc.s_idx = s_idx;
+  fc.s_hist = s_hist;
+  fc.t_lo = t_lo;
+  fc.width0 = t_hi - t_lo;
+  fc.sh0 = range_shift(fc.width0, kHistBits);
+  fc.above = 0;
+  fc.mk = 0;
+  unsigned base = 0;
+  float4 va[kStepF4], vb[kStepF4];
+  const int64_t wb0 = b0 + (int64_t)wid * kWaveSpan;
+  {
+    // full block steps in a two-deep software pipeline; every load in the loop body is unconditional
+    // (a conditional prefetch makes the compiler copy the loaded registers on a side path, and the copy
+    // waits for the load), and the partial tail step is peeled off
+    const int nfull = (int)((b1 - b0) / kBlockStep);
+    int s = 0;
+    if (nfull > 0) step_load<true>(x, wb0, b1, lane, va);
+    for (; s + 3 <= nfull; s += 2) {
+      const int64_t wa = wb0 + (int64_t)s * kBlockStep, wbn = wa + kBlockStep;
+      step_load<true>(x, wbn, b1, lane, vb);
+      step_process<true>(va, wa, b1, tf, s_wc, 0, base, fc);
+      step_load<true>(x, wbn + kBlockStep, b1, lane, va);
+      step_process<true>(vb, wbn, b1, tf, s_wc, 1, base, fc);
     }
-    for (long long c0 = v0 + 4 * tid; c0 < v1; c0 += 4 * kSelThreads) {
-      unsigned raw[4];
-      if (round == 0) {
-        if (fb) {
-          if (c0 + 4 <= v1) {
-            const float4 v = *reinterpret_cast<const float4*>(x + c0);
-            raw[0] = __float_as_uint(v.x); raw[1] = __float_as_uint(v.y);
-            raw[2] = __float_as_uint(v.z); raw[3] = __float_as_uint(v.w);
-          } else {
+    if (s + 2 == nfull) {
+      const int64_t wa = wb0 + (int64_t)s * kBlockStep, wbn = wa + kBlockStep;
+      step_load<true>(x, wbn, b1, lane, vb);
+      step_process<true>(va, wa, b1, tf, s_wc, 0, base, fc);
+      step_process<true>(vb, wbn, b1, tf, s_wc, 1, base, fc);
+      s += 2;
+    } else if (s + 1 == nfull) {
+      step_process<true>(va, wb0 + (int64_t)s * kBlockStep, b1, tf, s_wc, 0, base, fc);
+      ++s;
+    }
+    if (s < nsteps) {  // the partial last step of the last block
+      const int64_t wa = wb0 + (int64_t)s * kBlockStep;
+      step_load<false>(x, wa, b1, lane, va);
+      step_process<false>(va, wa, b1, tf, s_wc, s & 1, base, fc);
+    }
+  }
+  const unsigned C_b = base;
+  __syncthreads();
+  STAMP(2);
+
+  // ---- staging (16-B stores) and the round-0 histogram / counts
+  {
+    const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
+    uint4* dk = reinterpret_cast<uint4*>(w.stage_key(blockIdx.x));
+    uint4* di = reinterpret_cast<uint4*>(w.stage_idx(blockIdx.x));
+    const uint4* sk = reinterpret_cast<const uint4*>(s_key);
+    const uint4* si = reinterpret_cast<const uint4*>(s_idx);
+    for (unsigned q = tid; q < (nst + 3u) / 4u; q += kET) {
+      dk[q] = sk[q];
+      di[q] = si[q];
+    }
+  }
+  unsigned* h = w.hist();
+  for (int i = tid; i < kHistBins; i += kET)
+    if (s_hist[i]) atomicAdd(&h[i], s_hist[i]);
+  const unsigned long long ab = block_sum<unsigned long long, kENW>((unsigned long long)fc.above, s_red);
+  const unsigned mkw = wave_max_u32(fc.mk);
+  if (lane == 0) s_mx[wid] = mkw;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned m = 0;
+    for (int i = 0; i < kENW; ++i) m = s_mx[i] > m ? s_mx[i] : m;
+    if (ab) atomicAdd(&h[kHistBins], (unsigned)ab);
+    atomicMax(&h[kHistBins + 1], m);
+    atomicAdd(&w.acc()[0], (unsigned long long)C_b);
+    w.blk_c()[blockIdx.x] = C_b;
+  }
+  STAMP(3);
+  STAMP_OUT(0, 4);
+}
+
+// ------------------------------------------------------------------------------------------------
+// select kernel: the k-th largest key, the block offsets, the ordered compaction
+// ------------------------------------------------------------------------------------------------
+template <bool STACKED>
+__global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restrict__ x, int64_t n, long long k, EncWs w,
+                                                          int* __restrict__ idx_out, float* __restrict__ val_out,
+                                                          uint8_t* __restrict__ code_out, float* __restrict__ norm_out,
+                                                          int levels, double step, uint64_t seed, uint64_t counter) {
+  __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
+  __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
+  __shared__ unsigned s_hist[kHistBins];
+  __shared__ unsigned s_ghist[kHistBins];
+  __shared__ unsigned long long s_red[kENW];
+  __shared__ unsigned s_mx[kENW];
+  __shared__ unsigned s_err;
+  __shared__ unsigned long long s_glob[4];
+  __shared__ unsigned long long s_ex[3];
+  __shared__ SelState s_cur, s_prev;
+  STAMP_INIT();
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
+  const int64_t b0 = (int64_t)blockIdx.x * w.M;
+  const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
+  STAMP(4);
+
+  // ---- one batch of loads: this block's candidates (staging), the round-0 histogram and counts
+  unsigned* hist = w.hist();
+  const unsigned C_b = w.blk_c()[blockIdx.x];
+  const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
+  {
+    const uint4* sk = reinterpret_cast<const uint4*>(w.stage_key(blockIdx.x));
+    const uint4* si = reinterpret_cast<const uint4*>(w.stage_idx(blockIdx.x));
+    uint4* dk = reinterpret_cast<uint4*>(s_key);
+    uint4* di = reinterpret_cast<uint4*>(s_idx);
+    for (unsigned q = tid; q < (nst + 3u) / 4u; q += kET) {
+      dk[q] = sk[q];
+      di[q] = si[q];
+    }
+  }
+  if (tid == 0) {
+    s_glob[0] = w.st()->t_lo;
+    s_glob[1] = w.st()->t_hi;
+    s_glob[2] = ld_mem64(&w.st()->call);
+  }
+  load_hist(w, 0, s_ghist, s_ex, true);  // (ends in a barrier)
+  const unsigned t_lo = (unsigned)s_glob[0];
+  const unsigned long long t_hi = s_glob[1];
+  const unsigned call = (unsigned)s_glob[2];
+  unsigned ep = call * kEpochStride;
+  const unsigned long long C_tot = s_ex[2];
+  const bool fb = (long long)C_tot < k;  // grid-uniform
+  unsigned maxkey = (unsigned)s_ex[1];
+  long long A_cur = (long long)s_ex[0];
+  int slot = 0;
+  unsigned long long a_blk = 0;
+  STAMP(5);
+
+  SelState& cur = s_cur;
+  SelState& prev = s_prev;
+  if (tid == 0) {
+    cur.lo = t_lo;
+    cur.width = t_hi - t_lo;
+    cur.shift = range_shift(cur.width, kHistBits);
+    cur.rem = k;
+    cur.done = 0;
+    cur.narrowed = 0;
+    cur.T = 0;
+    cur.need = 0;
+    prev = cur;
+  }
+  CandSrc src;
+  src.s_key = s_key;
+  src.s_idx = s_idx;
+  src.x = x;
+  src.b0 = b0;
+  src.xmode = fb || C_b > (unsigned)kCap;  // block-uniform
+  const unsigned ncand = src.xmode ? (unsigned)(b1 - b0) : C_b;
+
+  auto flush = [&](int sl, unsigned above_t, unsigned mk_t) {
+    unsigned* h = hist + (size_t)sl * kHistStride;
+    for (int i = tid; i < kHistBins; i += kET)
+      if (s_hist[i]) atomicAdd(&h[i], s_hist[i]);
+    const unsigned long long ab = block_sum<unsigned long long, kENW>((unsigned long long)above_t, s_red);
+    const unsigned mkw = wave_max_u32(mk_t);
+    if (lane == 0) s_mx[wid] = mkw;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned m = 0;
+      for (int i = 0; i < kENW; ++i) m = s_mx[i] > m ? s_mx[i] : m;
+      if (ab) atomicAdd(&h[kHistBins], (unsigned)ab);
+      atomicMax(&h[kHistBins + 1], m);
+    }
+    return ab;
+  };
+
+  if (fb) {
+    // fallback pass: every element is a candidate; a round over the full key range from x
+    if (tid == 0) {
+      cur.lo = 0u;
+      cur.width = 1ull << 32;
+      cur.shift = range_shift(cur.width, kHistBits);
+    }
+    slot = 1;
+    for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
+    __syncthreads();
+    unsigned mk = 0;
+    const int sh = cur.shift;
+    for (unsigned p0 = 0; p0 < ncand; p0 += kET) {
+      const unsigned p = p0 + tid;
+      unsigned raw = 0, id = 0;
+      if (p < ncand) cand_get(src, p, raw, id);
+      const unsigned key = order_key(raw);
+      mk = (p < ncand && key > mk) ? key : mk;
+      hist_add(s_hist, key >> sh, p < ncand);
+    }
+    __syncthreads();
+    a_blk = flush(slot, 0u, mk);
+    exchange(w, ++ep);
+    load_hist(w, slot, s_ghist, s_ex, false);
+    maxkey = (unsigned)s_ex[1];
+    A_cur = (long long)s_ex[0];
+  }
+  // pick on the histogram just summed
+  __syncthreads();
+  if (tid == 0) prev = cur;
+  pick_digit(w, cur, A_cur, maxkey, s_ghist, &s_err, s_red);
+  STAMP(6);
+  unsigned long long pre = 0, tot = 0;
+  bool counted = false;
+  if (!fb && cur.narrowed && slot == 0) {
+    // ---- in-bin exchange: every block publishes its candidates inside the chosen bin (~3 per block at
+    // the headline) and its count of candidates above the bin; one exchange later every block resolves T
+    // among those keys and forms its own prefix locally: no second histogram round and no separate
+    // count exchange.  Falls through to the histogram rounds if any list overflows.
+    __shared__ unsigned s_nl;
+    if (tid == 0) s_nl = 0u;
+    __syncthreads();
+    const unsigned lo0 = cur.lo;
+    const unsigned long long wd0 = cur.width;
+    unsigned* my_list = w.inbin() + (size_t)blockIdx.x * kInbin;
+    unsigned gtc = 0;
+    const unsigned pend = (ncand + kET - 1) / kET * kET;
+    for (unsigned p0 = 0; p0 < pend; p0 += kET) {
+      const unsigned p = p0 + tid;
+      unsigned raw = 0, id = 0;
+      if (p < ncand) cand_get(src, p, raw, id);
+      const unsigned key = order_key(raw);
+      const unsigned long long rel = (unsigned long long)key - lo0;
+      const bool valid = p < ncand && key >= lo0 && key >= t_lo;  // (x-mode: below the floor never counts)
+      gtc += (valid && rel >= wd0) ? 1u : 0u;
+      const bool f = valid && rel < wd0;
+      const unsigned long long bm = __ballot(f);
+      if (bm) {
+        unsigned base_l = 0;
+        if (lane == 0) base_l = atomicAdd(&s_nl, (unsigned)__popcll(bm));
+        base_l = __shfl(base_l, 0, kWave);
+        const unsigned q = base_l + __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+        if (f && q < (unsigned)kInbin)  // write-through: read by other XCDs after the exchange
+          __hip_atomic_store(my_list + q, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const unsigned long long gt = block_sum<unsigned long long, kENW>((unsigned long long)gtc, s_red);
+    if (tid == 0) st_mem64(&w.blk_cnt()[blockIdx.x], ((unsigned long long)s_nl << 32) | (gt & 0xffffffffull));
+    STAMP(7);
+    exchange(w, ++ep);
+    STAMP(8);
+    // all-gather: per-block list sizes and counts above the bin, then the lists themselves
+    unsigned* s_lkey = s_ghist;               // <= kInbinAll keys
+    unsigned* s_lblk = s_ghist + kInbinAll;   // their blocks
+    static_assert(2 * kInbinAll <= kHistBins, "in-bin list fits the histogram buffer");
+    __shared__ unsigned s_nb[kMaxBlocks];
+    __shared__ unsigned s_ovf, s_nall;
+    if (tid == 0) { s_ovf = 0u; s_nall = 0u; }
+    __syncthreads();
+    unsigned long long my_gt = 0, pre_gt = 0;
+    if (tid < (int)gridDim.x) {
+      const unsigned long long m = ld_mem64(&w.blk_cnt()[tid]);
+      const unsigned nb = (unsigned)(m >> 32);
+      s_nb[tid] = nb;
+      my_gt = m & 0xffffffffull;
+      pre_gt = tid < (int)blockIdx.x ? my_gt : 0ull;
+      if (nb > (unsigned)kInbin) atomicOr(&s_ovf, 1u);
+    }
+    const unsigned long long gt_all = block_sum<unsigned long long, kENW>(my_gt, s_red);
+    const unsigned long long gt_pre = block_sum<unsigned long long, kENW>(pre_gt, s_red);
+    if (s_ovf == 0u) {
+      // list words in batches of 8 per thread in flight together (G <= 256 blocks: one batch)
+      constexpr int kLW = 8;
+      const int words = (int)gridDim.x * kInbin;
+      for (int c0 = 0; c0 < words; c0 += kLW * kET) {
+        unsigned lw[kLW];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) raw[u] = c0 + u < v1 ? __float_as_uint(x[c0 + u]) : 0u;
-          }
-        } else {
-          unsigned id[4];
+        for (int i = 0; i < kLW; ++i) {
+          const int j = c0 + i * kET + tid;
+          const int bb = j / kInbin;
+          lw[i] = (j < words && (unsigned)(j % kInbin) < s_nb[bb < (int)gridDim.x ? bb : 0]) ? ld_mem(w.inbin() + j) : 0u;
+        }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const long long c = c0 + u;
-            if (c < v1) {
-              r = lds_region_advance(s_off, R, r, (unsigned)c);
-              if (r != r_cur) {
-                r_cur = r;
-                wc = wc_lds ? s_wc[r - r_first] : *reinterpret_cast<const uint4*>(w.wave_cnt + (size_t)r * kFNW);
-              }
-              // candidate -> (block region, wave quarter, offset): the quarters are in index order
-              unsigned loc = (unsigned)(c - s_off[r]);
-              long long q = 0;
-              if (loc >= wc.x) { loc -= wc.x; q = 1;
-                if (loc >= wc.y) { loc -= wc.y; q = 2;
-                  if (loc >= wc.z) { loc -= wc.z; q = 3; } } }
-              const long long wv = (long long)r * kFNW + q;
-              const uint2 e = loc < (unsigned)w.dcap ? w.stage[wv * w.dcap + loc] : w.spill[wv * w.qc + (loc - w.dcap)];
-              id[u] = e.x;
-              raw[u] = e.y;
-            } else {
-              id[u] = 0u;
-              raw[u] = 0u;
+        for (int i = 0; i < kLW; ++i) {
+          const int j = c0 + i * kET + tid;
+          const int bb = j / kInbin;
+          const bool v = j < words && (unsigned)(j % kInbin) < s_nb[bb < (int)gridDim.x ? bb : 0];
+          const unsigned long long bm = __ballot(v);
+          if (bm) {
+            unsigned base_l = 0;
+            if (lane == 0) base_l = atomicAdd(&s_nall, (unsigned)__popcll(bm));
+            base_l = __shfl(base_l, 0, kWave);
+            const unsigned q = base_l + __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
+            if (v && q < (unsigned)kInbinAll) {
+              s_lkey[q] = lw[i];
+              s_lblk[q] = (unsigned)bb;
             }
           }
-          if (c0 + 4 <= v1) {
-            *reinterpret_cast<uint4*>(w.cand_idx + c0) = make_uint4(id[0], id[1], id[2], id[3]);
-            if (!cached) *reinterpret_cast<uint4*>(w.cand_raw + c0) = make_uint4(raw[0], raw[1], raw[2], raw[3]);
-          } else {
-            for (int u = 0; u < 4; ++u)
-              if (c0 + u < v1) {
-                w.cand_idx[c0 + u] = id[u];
-                if (!cached) w.cand_raw[c0 + u] = raw[u];
-              }
-          }
         }
-        if (cached) *reinterpret_cast<uint4*>(s_keys + (c0 - v0)) = make_uint4(raw[0], raw[1], raw[2], raw[3]);
-      } else if (cached) {  // re-read what this thread cached in round 0
-        const uint4 t = *reinterpret_cast<const uint4*>(s_keys + (c0 - v0));
-        raw[0] = t.x; raw[1] = t.y; raw[2] = t.z; raw[3] = t.w;
-      } else if (fb) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) raw[u] = c0 + u < v1 ? __float_as_uint(x[c0 + u]) : 0u;
-      } else if (c0 + 4 <= v1) {  // re-read what this thread wrote in round 0
-        const uint4 t = *reinterpret_cast<const uint4*>(w.cand_raw + c0);
-        raw[0] = t.x; raw[1] = t.y; raw[2] = t.z; raw[3] = t.w;
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) raw[u] = c0 + u < v1 ? w.cand_raw[c0 + u] : 0u;
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const unsigned key = order_key(raw[u]);
-        const unsigned long long rel = (unsigned long long)key - cur.lo;
-        const bool in = c0 + u < v1 && key >= cur.lo;
-        if (round == 0) mk = (c0 + u < v1 && key > mk) ? key : mk;
-        above += (in && rel >= cur.width) ? 1u : 0u;
-        hist_add(s_hist, (unsigned)(rel >> cur.shift), in && rel < cur.width);
-      }
-    }
-    __syncthreads();
-    unsigned* h = w.hist + (size_t)round * kHistStride;
-    for (int i = tid; i < kHistBins; i += kSelThreads)
-      if (s_hist[i]) atomicAdd(&h[i], s_hist[i]);
-    a_blk = block_sum<unsigned long long, kSelNW>((unsigned long long)above, s_red);
-    if (tid == 0 && a_blk) atomicAdd(&h[kHistBins], (unsigned)a_blk);
-    if (round == 0) {  // the max key (norm of the stacked codec, top of a re-range)
-      mk = wave_max_u32(mk);
-      if ((tid & 63) == 0) s_mx[tid >> 6] = mk;
       __syncthreads();
-      if (tid == 0) {
-        unsigned m = 0;
-        for (int i = 0; i < kSelNW; ++i) m = s_mx[i] > m ? s_mx[i] : m;
-        if (v0 < v1) atomicMax(&h[kHistBins + 1], m);
+      if (s_nall <= (unsigned)kInbinAll) {  // block-uniform
+        const unsigned nall = s_nall;
+        // exact k-th largest among the in-bin keys: rank cur.need from the top, local radix passes
+        unsigned lo = lo0;
+        unsigned long long width = wd0;
+        long long r = cur.need;
+        __shared__ unsigned s_d;
+        __shared__ long long s_r;
+        for (int pass = 0; pass < 4; ++pass) {
+          const int sh = range_shift(width, kHistBits);
+          for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
+          __syncthreads();
+          for (unsigned p0 = 0; p0 < ((nall + 63u) & ~63u); p0 += kET) {
+            const unsigned p = p0 + tid;
+            const unsigned key = p < nall ? s_lkey[p] : lo;
+            const unsigned long long rel = (unsigned long long)key - lo;
+            hist_add(s_hist, (unsigned)(rel >> sh), p < nall && key >= lo && rel < width);
+          }
+          __syncthreads();
+          {
+            const long long rk[1] = {r};
+            block_select_from_top<1>(s_hist, rk, &s_d, &s_r, &s_err, s_red);
+          }
+          lo += s_d << sh;
+          r = s_r;
+          width = 1ull << sh;
+          __syncthreads();
+          if (sh == 0) break;
+        }
+        if (tid == 0) {
+          cur.T = lo;
+          cur.need = r;
+          cur.done = 1;
+        }
+        // strict / tie counts: above-the-bin counts + in-bin keys > T / == T, by block
+        const unsigned T0 = lo;
+        unsigned long long ps = 0, pt = 0, as = 0, at = 0;
+        for (unsigned p = tid; p < nall; p += kET) {
+          const unsigned key = s_lkey[p], bb = s_lblk[p];
+          const unsigned long long s1 = key > T0 ? 1ull : 0ull, t1 = key == T0 ? 1ull : 0ull;
+          as += s1;
+          at += t1;
+          if (bb < blockIdx.x) { ps += s1; pt += t1; }
+        }
+        const unsigned long long A_s = block_sum<unsigned long long, kENW>(as, s_red);
+        const unsigned long long A_t = block_sum<unsigned long long, kENW>(at, s_red);
+        const unsigned long long P_s = block_sum<unsigned long long, kENW>(ps, s_red);
+        const unsigned long long P_t = block_sum<unsigned long long, kENW>(pt, s_red);
+        pre = ((gt_pre + P_s) << 32) | P_t;
+        tot = ((gt_all + A_s) << 32) | A_t;
+        counted = true;
       }
     }
-    STAMP(2 + 2 * round);
-    prev = cur;
-    grid_barrier(w, nbar++, [&] { lead_pick(w, round, cur, s_ghist); });
-    STAMP(3 + 2 * round);
-    read_view(w, &s_view);
-    cur = s_view;
     __syncthreads();
-    if (cur.done) break;
+    STAMP(9);
   }
-  if (!cur.done && blockIdx.x == 0 && tid == 0)
-    __hip_atomic_fetch_or(&w.st->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-  // ---- counts from the resolving round's local histogram: strict = above + bins past T's bin
-  const unsigned T = cur.T;
-  {
-    const unsigned d = T - prev.lo;  // the resolving round has shift 0: bin = key - lo
-    unsigned long long cnt = 0;      // strict << 32 | tie
-    for (int i = tid; i < kHistBins; i += kSelThreads) {
-      const unsigned hv = s_hist[i];
-      cnt += ((unsigned)i > d ? ((unsigned long long)hv << 32) : 0ull) + ((unsigned)i == d ? hv : 0ull);
-    }
-    const unsigned long long both = block_sum<unsigned long long, kSelNW>(cnt, s_red) + (a_blk << 32);
-    if (tid == 0) st_mem64(&w.blk_cnt[blockIdx.x], both);
+  // histogram rounds over the block's candidates until T is resolved (rare paths)
+  if (!counted && cur.narrowed && !fb && slot == 0) {
+    // the round-0 local histogram is not kept by this kernel: nothing to reuse, start a round
   }
-  STAMP(14);
-  grid_barrier(w, nbar++, [&] {
-    const unsigned long long v = tid < (int)gridDim.x ? ld_mem64(&w.blk_cnt[tid]) : 0ull;
-    unsigned long long tot;
-    const unsigned long long ex = block_excl_scan<unsigned long long, kSelNW>(v, s_red, &tot);
-    if (tid < (int)gridDim.x) st_mem64(&w.blk_off[tid], ex);
-    if (tid == 0) {
-      const long long st = (long long)(tot >> 32), ti = (long long)(tot & 0xffffffffull);
-      st_mem64(&w.st->strict, (unsigned long long)st);
-      st_mem64(&w.st->ties, (unsigned long long)ti);
-      st_mem64(&w.st->C, (unsigned long long)C);
-      st_mem64(&w.st->fallback, fb ? 1ull : 0ull);
-      if (st + cur.need != k || cur.need > ti)
-        __hip_atomic_fetch_or(&w.st->err, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int guard = 0; !cur.done && guard < kMaxSlots && slot + 1 < kMaxSlots; ++guard) {
+    ++slot;
+    for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
+    __syncthreads();
+    const unsigned lo = cur.lo;
+    const unsigned long long wd = cur.width;
+    const int sh = cur.shift;
+    unsigned above = 0;
+    const unsigned pend = (ncand + kET - 1) / kET * kET;
+    for (unsigned p0 = 0; p0 < pend; p0 += kET) {
+      const unsigned p = p0 + tid;
+      unsigned raw = 0, id = 0;
+      if (p < ncand) cand_get(src, p, raw, id);
+      const unsigned key = order_key(raw);
+      const unsigned long long rel = (unsigned long long)key - lo;
+      const bool in = p < ncand && key >= lo;
+      above += (in && rel >= wd) ? 1u : 0u;
+      hist_add(s_hist, (unsigned)(rel >> sh), in && rel < wd);
     }
-  });
-  STAMP(15);
-  __shared__ unsigned long long s_off_blk, s_ties;
-  if (tid == 0) {
-    s_off_blk = ld_mem64(&w.blk_off[blockIdx.x]);
-    s_ties = ld_mem64(&w.st->ties);
+    __syncthreads();
+    a_blk = flush(slot, above, 0u);
+    exchange(w, ++ep);
+    load_hist(w, slot, s_ghist, s_ex, false);
+    if (tid == 0) prev = cur;
+    pick_digit(w, cur, (long long)s_ex[0], maxkey, s_ghist, &s_err, s_red);
   }
   __syncthreads();
+  if (!cur.done && blockIdx.x == 0 && tid == 0)
+    __hip_atomic_fetch_or(&w.st()->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned T = cur.T;
+  const long long need = cur.need;
+  if (!counted) {
+    // ---- counts from the resolving round's local histogram: strict = above + bins past T's bin
+    // (the round-0 band resolving directly has no local histogram here: count from the candidates)
+    unsigned long long cnt = 0;  // strict << 32 | tie
+    if (slot == 0) {
+      const unsigned pend = (ncand + kET - 1) / kET * kET;
+      for (unsigned p0 = 0; p0 < pend; p0 += kET) {
+        const unsigned p = p0 + tid;
+        unsigned raw = 0, id = 0;
+        if (p < ncand) cand_get(src, p, raw, id);
+        const unsigned key = order_key(raw);
+        cnt += (p < ncand && key > T) ? (1ull << 32) : 0ull;
+        cnt += (p < ncand && key == T) ? 1ull : 0ull;
+      }
+    } else {
+      const unsigned d = T - prev.lo;  // the resolving round has shift 0: bin = key - lo
+      for (int i = tid; i < kHistBins; i += kET) {
+        const unsigned hv = s_hist[i];
+        cnt += ((unsigned)i > d ? ((unsigned long long)hv << 32) : 0ull) + ((unsigned)i == d ? hv : 0ull);
+      }
+    }
+    const unsigned long long both = block_sum<unsigned long long, kENW>(cnt, s_red) + (slot == 0 ? 0ull : (a_blk << 32));
+    if (tid == 0) st_mem64(&w.blk_cnt()[blockIdx.x], both);
+    exchange(w, ++ep);
+    const unsigned long long v = tid < (int)gridDim.x ? ld_mem64(&w.blk_cnt()[tid]) : 0ull;
+    unsigned long long t_all;
+    const unsigned long long ex = block_excl_scan<unsigned long long, kENW>(v, s_red, &t_all);
+    if (tid == (int)blockIdx.x) s_glob[3] = ex;
+    __syncthreads();
+    pre = s_glob[3];
+    tot = t_all;
+  }
+  STAMP(10);
+  const long long strict_tot = (long long)(tot >> 32), ties_tot = (long long)(tot & 0xffffffffull);
+  // every hist / acc read of this call happened before the last exchange: zero them for the next call
+  // (my slice), and the call counter advances
+  {
+    unsigned* z = hist;
+    const int per = (kZeroWords + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int z0 = (int)blockIdx.x * per, z1 = z0 + per < kZeroWords ? z0 + per : kZeroWords;
+    for (int i = z0 + tid; i < z1; i += kET) z[i] = 0u;
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    (void)__hip_atomic_fetch_add(&w.st()->call, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    EncState* st = w.st();
+    st->C = C_tot;
+    st->fallback = fb ? 1ull : 0ull;
+    st->T = T;
+    st->maxkey = maxkey;
+    st->rounds = (unsigned long long)slot + 1ull;
+    st->need = (unsigned long long)need;
+    st->ties = (unsigned long long)ties_tot;
+    st->strict = (unsigned long long)strict_tot;
+    if (strict_tot + need != k || need > ties_tot)
+      __hip_atomic_fetch_or(&st->err, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
-  // ---- ordered compaction of the kept set
-  const long long skip = (long long)s_ties - cur.need;  // ties with rank < skip are dropped
-  long long run_s = (long long)(s_off_blk >> 32), run_t = (long long)(s_off_blk & 0xffffffffull);
+  // ---- ordered compaction: wave `wid` owns candidates [wid * Q, (wid + 1) * Q) of this block
+  const long long skip = ties_tot - need;  // ties with global tie rank < skip are dropped
   float nrm = 0.0f;
   if (STACKED) {
-    const float a = fabsf(key_value(cur.maxkey)), b = fabsf(key_value(T));
+    const float a = fabsf(key_value(maxkey)), b = fabsf(key_value(T));
     nrm = (isnan(a) || isnan(b)) ? __uint_as_float(0x7fc00000u) : (a > b ? a : b);
     if (blockIdx.x == 0 && tid == 0) *norm_out = nrm;
   }
   const bool nrm_ok = nrm > 0.0f && nrm <= 3.402823466e38f;
-  for (long long base = v0; base < v1; base += 4 * kSelThreads) {
-    const long long c0 = base + 4 * tid;
-    unsigned raw[4], id[4];
-    if (cached) {
-      const uint4 t = *reinterpret_cast<const uint4*>(s_keys + (c0 < v1 ? c0 - v0 : 0));
-      raw[0] = t.x; raw[1] = t.y; raw[2] = t.z; raw[3] = t.w;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long long c = c0 + u;
-      const bool in = c < v1;
-      if (!cached) raw[u] = in ? (fb ? __float_as_uint(x[c]) : w.cand_raw[c]) : 0u;
-      raw[u] = in ? raw[u] : 0u;
-      id[u] = in ? (fb ? (unsigned)c : w.cand_idx[c]) : 0u;
-    }
-    bool is_s[4], is_t[4];
-    unsigned long long cnt = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const unsigned key = order_key(raw[u]);
-      const bool in = c0 + u < v1;
-      is_s[u] = in && key > T;
-      is_t[u] = in && key == T;
-      cnt += (is_s[u] ? (1ull << 32) : 0ull) + (is_t[u] ? 1ull : 0ull);
-    }
-    unsigned long long tot;
-    const unsigned long long ex = block_excl_scan<unsigned long long, kSelNW>(cnt, s_red, &tot);
-    long long s_before = run_s + (long long)(ex >> 32), t_before = run_t + (long long)(ex & 0xffffffffull);
-    // dithering of the 4 values first, branch-free, so the 4 chains overlap
-    uint32_t code[4];
-    if (STACKED) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float v = __uint_as_float(raw[u]);
-        const float y = nrm_ok ? fabsf(v) / nrm : 0.0f;  // compressors.py:344
-        const U4 r4 = philox_group((uint64_t)id[u] >> 2, seed, counter);
-        const double uu = u01(pick(r4, (int)(id[u] & 3u)));
-        const uint32_t lvl = (uint32_t)dither_level<0>(y, levels, step, uu);  // compressors.py:346-353
-        const uint32_t c = nrm_ok ? (((raw[u] >> 31) << 7) | lvl) : 1u;
-        code[u] = (v != 0.0f) ? c : 0u;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const bool keep = is_s[u] || (is_t[u] && t_before >= skip);
-      const long long pos = s_before + (t_before > skip ? t_before - skip : 0);
-      if (keep && pos >= 0 && pos < k) {
-        idx_out[pos] = (int)id[u];
-        if (STACKED) code_out[pos] = (uint8_t)code[u];
-        else val_out[pos] = __uint_as_float(raw[u]);
-      }
-      s_before += is_s[u] ? 1 : 0;
-      t_before += is_t[u] ? 1 : 0;
-    }
-    run_s += (long long)(tot >> 32);
-    run_t += (long long)(tot & 0xffffffffull);
+  const unsigned Q = ((ncand + kENW - 1) / kENW + kWave - 1) / kWave * kWave;
+  const unsigned q0 = (unsigned)wid * Q < ncand ? (unsigned)wid * Q : ncand;
+  const unsigned q1 = q0 + Q < ncand ? q0 + Q : ncand;
+  // pass 1: this wave's strict / tie counts
+  unsigned ws = 0, wt = 0;
+  for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
+    const unsigned p = p0 + lane;
+    unsigned raw = 0, id = 0;
+    if (p < q1) cand_get(src, p, raw, id);
+    const unsigned key = order_key(raw);
+    ws += __popcll(__ballot(p < q1 && key > T));
+    wt += __popcll(__ballot(p < q1 && key == T));
   }
-  STAMP(13);
+  __syncthreads();
+  if (lane == 0) s_red[wid] = ((unsigned long long)ws << 32) | wt;
+  __syncthreads();
+  long long s_before = (long long)(pre >> 32), t_before = (long long)(pre & 0xffffffffull);
+  for (int v2 = 0; v2 < wid; ++v2) {
+    s_before += (long long)(s_red[v2] >> 32);
+    t_before += (long long)(s_red[v2] & 0xffffffffull);
+  }
+  // pass 2: keep decisions and the writes
+  for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
+    const unsigned p = p0 + lane;
+    const bool in = p < q1;
+    unsigned raw = 0, id = 0;
+    if (in) cand_get(src, p, raw, id);
+    const unsigned key = order_key(raw);
+    const bool is_s = in && key > T, is_t = in && key == T;
+    const unsigned long long ms = __ballot(is_s), mt = __ballot(is_t);
+    const long long sb = s_before + __builtin_amdgcn_mbcnt_hi((unsigned)(ms >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ms, 0u));
+    const long long tb = t_before + __builtin_amdgcn_mbcnt_hi((unsigned)(mt >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mt, 0u));
+    const bool keep = is_s || (is_t && tb >= skip);
+    const long long pos = sb + (tb > skip ? tb - skip : 0);
+    if (keep && pos >= 0 && pos < k) {
+      idx_out[pos] = (int)id;
+      if (STACKED) {
+        const float v = __uint_as_float(raw);
+        const float y = nrm_ok ? fabsf(v) / nrm : 0.0f;  // compressors.py:344
+        const U4 r4 = philox_group((uint64_t)id >> 2, seed, counter);
+        const double uu = u01(pick(r4, (int)(id & 3u)));
+        const uint32_t lvl = (uint32_t)dither_level<0>(y, levels, step, uu);  // compressors.py:346-353
+        const uint32_t c = nrm_ok ? (((raw >> 31) << 7) | lvl) : 1u;
+        code_out[pos] = (uint8_t)((v != 0.0f) ? c : 0u);
+      } else {
+        val_out[pos] = __uint_as_float(raw);
+      }
+    }
+    s_before += __popcll(ms);
+    t_before += __popcll(mt);
+  }
+  STAMP(11);
+  STAMP_OUT(4, 16);
 }
 
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-// one persistent select launch per device at a time: launches on different streams are ordered with an
-// event chain (stream-ordered, no host blocking), so two never compete for co-residency
+// one select launch per device at a time: launches on different streams are ordered with an event
+// chain (stream-ordered, no host blocking), so two never compete for co-residency
 struct SelectGate {
   std::mutex mu;
   hipEvent_t last[64] = {};
-  int grid[64] = {};
+  int cus[64] = {};
 };
 SelectGate& gate() {
   static SelectGate g;
   return g;
 }
 
-int select_grid(int dev) {
+int device_cus(int dev) {
   SelectGate& g = gate();
   std::lock_guard<std::mutex> lk(g.mu);
-  if (g.grid[dev] == 0) {
+  if (g.cus[dev] == 0) {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0) cu = 256;
-    g.grid[dev] = cu < kMaxSelBlocks ? cu : kMaxSelBlocks;
+    g.cus[dev] = cu;
   }
-  return g.grid[dev];
+  return g.cus[dev];
+}
+
+int current_cus(int* dev_out) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (dev_out) *dev_out = dev;
+  return device_cus(dev);
 }
 
 template <bool STACKED>
-int launch_topk(const float* x, int64_t n, int64_t k, const TopkWs& w, hipStream_t st, int* idx, float* val,
-                uint8_t* codes, float* norm, int levels, uint64_t seed, uint64_t counter) {
-  const TopkGeom g = geometry(n);
-  const SampleSetup ss = sample_setup(n, k);
-  const int R = (int)g.regions;
+int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes, hipStream_t st, int* idx, float* val,
+                uint8_t* codes, float* norm, int levels, uint64_t seed, uint64_t counter, const char* who) {
   int dev = 0;
-  FLC_CHECK_HIP(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) return fail(FLC_EUNSUPPORTED, "device index %d", dev);
-  const int grid = select_grid(dev);
+  const int cus = current_cus(&dev);
+  size_t need = 0;
+  EncWs w = carve_enc(ws, n, cus, &need);
+  if (!ws || need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
+  const EncGeom g = enc_geometry(n, cus);
+  const SampleSetup ss = sample_setup(n, k);
   if (!ss.take_all)
-    FLC_LAUNCH("topk_sample_gather", topk_sample_gather_kernel, dim3((unsigned)cdiv(ss.S, kThreads)), dim3(kThreads), 0,
-               st, x, n, ss.S, w);
-  FLC_LAUNCH("topk_sample_select", topk_sample_select_kernel, dim3(1), dim3(kSelectThreads), 0, st, ss.S, ss.rank_lo,
-             ss.rank_hi, ss.take_all, w);
-  FLC_LAUNCH("topk_filter", topk_filter_kernel, dim3((unsigned)R), dim3(kThreads), 0, st, x, n, g.chunk, grid, w);
+    FLC_LAUNCH("topk_sample", topk_sample_kernel, dim3((unsigned)cdiv(ss.S, 256)), dim3(256), 0, st, x, n, ss.S, w);
+  FLC_LAUNCH("topk_filter", topk_filter_kernel, dim3((unsigned)g.G), dim3(kET), 0, st, x, n, w, ss.S, ss.rank_lo,
+             ss.rank_hi, ss.take_all);
   SelectGate& gt = gate();
   std::lock_guard<std::mutex> lk(gt.mu);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1029,8 +1271,8 @@ int launch_topk(const float* x, int64_t n, int64_t k, const TopkWs& w, hipStream
     else FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
   }
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
-  FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", topk_select_kernel<STACKED>, dim3((unsigned)grid),
-             dim3(kSelThreads), 0, st, x, w, R, (long long)k, n, idx, val, codes, norm, levels, step, seed, counter);
+  FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", topk_select_kernel<STACKED>, dim3((unsigned)g.G), dim3(kET),
+             0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter);
   if (gated) FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
   return FLC_OK;
 }
@@ -1053,7 +1295,7 @@ extern "C" {
 size_t flc_topk_workspace_size(int64_t n, int64_t k) {
   (void)k;
   size_t need = 0;
-  (void)carve_topk(nullptr, 0, n < 1 ? 1 : n, k, &need);
+  (void)carve_enc(nullptr, n < 1 ? 1 : n, current_cus(nullptr), &need);
   return need;
 }
 
@@ -1061,10 +1303,8 @@ int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* v
                     void* stream) {
   if (int rc = check_topk(x, n, k, "flc_topk_encode")) return rc;
   if (!idx || !val) return fail(FLC_EINVAL, "flc_topk_encode: null output");
-  size_t need = 0;
-  TopkWs w = carve_topk(ws, ws_bytes, n, k, &need);
-  if (!ws || need > ws_bytes) return fail(FLC_EWORKSPACE, "flc_topk_encode: workspace %zu < %zu", ws_bytes, need);
-  return launch_topk<false>(x, n, k, w, as_stream(stream), idx, val, nullptr, nullptr, 0, 0, 0);
+  return launch_topk<false>(x, n, k, ws, ws_bytes, as_stream(stream), idx, val, nullptr, nullptr, 0, 0, 0,
+                            "flc_topk_encode");
 }
 
 int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_t seed, uint64_t counter,
@@ -1076,10 +1316,8 @@ int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_
   if (compat_u)
     return fail(FLC_EUNSUPPORTED,
                 "flc_stacked_encode: compat RNG is composed by the caller (flc_topk_encode + flc_quant_encode)");
-  size_t need = 0;
-  TopkWs w = carve_topk(ws, ws_bytes, n, k, &need);
-  if (!ws || need > ws_bytes) return fail(FLC_EWORKSPACE, "flc_stacked_encode: workspace %zu < %zu", ws_bytes, need);
-  return launch_topk<true>(x, n, k, w, as_stream(stream), idx, nullptr, codes, norm, levels, seed, counter);
+  return launch_topk<true>(x, n, k, ws, ws_bytes, as_stream(stream), idx, nullptr, codes, norm, levels, seed, counter,
+                           "flc_stacked_encode");
 }
 
 }  // extern "C"

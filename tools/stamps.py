@@ -1,7 +1,8 @@
-"""Phase stamps of the persistent select (diagnostic build: make EXTRA=-DFLC_SELECT_STAMPS, block 0 only).
+"""Phase stamps of the persistent encode (diagnostic build: make EXTRA=-DFLC_SELECT_STAMPS, block 0 only).
 
-Stamp slots (s_memrealtime, 100 MHz): 0 start, 1 after P0, 2+2r / 3+2r before / after the barrier of
-radix round r, 14 / 15 before / after the count barrier, 13 end of compaction.
+Stamp slots (s_memrealtime, 100 MHz): filter kernel 0 start, 1 floor/ceiling, 2 HBM pass done, 3 staged +
+flushed; select kernel 4 start, 5 loads done, 6 pick, 7 in-bin lists published, 8 exchanged, 9 T and
+offsets resolved, 10 counts, 11 compaction done.
 """
 import os
 import sys
@@ -12,22 +13,23 @@ import torch
 
 from fl_sim_amd import codec
 
-n = 268_435_456
+STAMP_OFF = 175616  # byte offset of EncWs.stamps in the top-k workspace (topk.hip: carve_enc)
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
 x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 1e-3
-for it in range(5):
+names = ["sample-sel", "filter", "stage+flush", "boundary", "load", "pick0", "inbin", "x1", "local", "counts", "compact"]
+for it in range(6):
     codec.stacked_encode(x, k, 127, 1, it)
     torch.cuda.synchronize()
     ws = [t for key, t in codec._WS.items() if key[2] == "topk"][0]
-    st = ws[256:256 + 128].cpu().numpy().view(np.uint64).astype(np.int64)
+    st = ws[STAMP_OFF:STAMP_OFF + 16 * 8].cpu().numpy().view(np.uint64).astype(np.int64)
     if it < 2:
         continue
-    us = lambda a, b: (st[b] - st[a]) * 10 / 1000  # noqa: E731
-    parts = [("P0", 0, 1), ("r0 local", 1, 2), ("r0 barrier", 2, 3)]
-    r, last = 1, 3
-    while st[2 + 2 * r] > 0 and 2 + 2 * r < 13:
-        parts += [(f"r{r} local", last, 2 + 2 * r), (f"r{r} barrier", 2 + 2 * r, 3 + 2 * r)]
-        last = 3 + 2 * r
-        r += 1
-    parts += [("counts", last, 14), ("count barrier", 14, 15), ("compaction", 15, 13)]
-    print(" | ".join(f"{nm} {us(a, b):.1f}" for nm, a, b in parts), f"| total {us(0, 13):.1f} us")
+    t = st[:12].astype(np.float64)
+    prev, parts = t[0], []
+    for i in range(1, 12):
+        if t[i] > 0 and t[i] >= prev:
+            parts.append(f"{names[i - 1]} {(t[i] - prev) * 10 / 1000:.1f}")
+            prev = t[i]
+    print(" | ".join(parts), f"| total {(t[11] - t[0]) * 10 / 1000:.1f} us")
+    ws[STAMP_OFF:STAMP_OFF + 16 * 8].zero_()
