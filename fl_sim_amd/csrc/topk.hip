@@ -87,7 +87,8 @@ constexpr size_t kOffHist = al256(kOffFlags + (size_t)kMaxBlocks * kFlagStride *
 constexpr size_t kOffAcc = kOffHist + (size_t)kMaxSlots * kHistStride * 4;  // contiguous with hist (zeroed together)
 constexpr size_t kOffBlk = al256(kOffAcc + 64);
 constexpr size_t kOffStamps = al256(kOffBlk + (size_t)kMaxBlocks * 8);
-constexpr size_t kOffSample = al256(kOffStamps + 128);
+constexpr size_t kOffBlkT = al256(kOffStamps + 128);   // [kMaxBlocks][4] per-block times (diagnostic build)
+constexpr size_t kOffSample = al256(kOffBlkT + (size_t)kMaxBlocks * 32);
 constexpr size_t kOffInbin = al256(kOffSample + (size_t)kSample * 4);
 constexpr size_t kOffBlkC = al256(kOffInbin + (size_t)kMaxBlocks * kInbin * 4);
 constexpr size_t kOffStage = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // + G * kCap * 8 (keys, then indices)
@@ -103,6 +104,7 @@ struct EncWs {
   __device__ unsigned long long* acc() const { return reinterpret_cast<unsigned long long*>(base + kOffAcc); }
   __device__ unsigned long long* blk_cnt() const { return reinterpret_cast<unsigned long long*>(base + kOffBlk); }
   __device__ unsigned long long* stamps() const { return reinterpret_cast<unsigned long long*>(base + kOffStamps); }
+  __device__ unsigned long long* blkt() const { return reinterpret_cast<unsigned long long*>(base + kOffBlkT); }
   __device__ unsigned* sample() const { return reinterpret_cast<unsigned*>(base + kOffSample); }
   __device__ unsigned* inbin() const { return reinterpret_cast<unsigned*>(base + kOffInbin); }
   __device__ unsigned* blk_c() const { return reinterpret_cast<unsigned*>(base + kOffBlkC); }  // candidates / block
@@ -427,17 +429,21 @@ struct FilterCtx {
   unsigned mk;            // per thread: max candidate key
 };
 
+// a candidate into the block's LDS arrays; the band histogram, above count and max key of the stored
+// candidates are formed after the pass in one dense sweep over LDS (every lane busy), only candidates
+// beyond the LDS capacity (never stored) are binned here
 __device__ __forceinline__ void emit(FilterCtx& c, unsigned p, unsigned e, float v) {
   const unsigned raw = __float_as_uint(v);
-  if (p < (unsigned)kCap) {  // beyond: the block counts on, and later phases re-read its x range
+  if (p < (unsigned)kCap) {
     c.s_key[p] = raw;
     c.s_idx[p] = e;
+  } else {
+    const unsigned key = order_key(raw);
+    const unsigned long long rel = (unsigned long long)(key - c.t_lo);
+    if (rel >= c.width0) ++c.above;
+    else atomicAdd(&c.s_hist[(unsigned)(rel >> c.sh0)], 1u);
+    c.mk = key > c.mk ? key : c.mk;
   }
-  const unsigned key = order_key(raw);
-  const unsigned long long rel = (unsigned long long)(key - c.t_lo);
-  if (rel >= c.width0) ++c.above;
-  else atomicAdd(&c.s_hist[(unsigned)(rel >> c.sh0)], 1u);
-  c.mk = key > c.mk ? key : c.mk;
 }
 
 // ordered append from position `pos` (within a q: lane-major, then the 4 components)
@@ -634,10 +640,15 @@ __device__ __forceinline__ void cand_get(const CandSrc& c, unsigned p, unsigned&
 #define STAMP_OUT(lo, hi)                                                                        \
   if (blockIdx.x == 0 && (int)threadIdx.x >= (lo) && (int)threadIdx.x < (hi))                    \
   w.stamps()[threadIdx.x] = s_stamp[threadIdx.x]
+#define BLKT(i)                                                                                  \
+  do {                                                                                           \
+    if (threadIdx.x == 0) w.blkt()[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
 #else
 #define STAMP(i) do { } while (0)
 #define STAMP_INIT() do { } while (0)
 #define STAMP_OUT(lo, hi) do { } while (0)
+#define BLKT(i) do { } while (0)
 #endif
 
 // ------------------------------------------------------------------------------------------------
@@ -706,6 +717,7 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
   for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
   __syncthreads();
   STAMP(1);
+  BLKT(0);
 
   // ---- the HBM pass
   const float tf = floor_value(t_lo);
@@ -754,6 +766,18 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
   const unsigned C_b = base;
   __syncthreads();
   STAMP(2);
+  BLKT(1);
+  {  // band histogram / above / max of the stored candidates
+    const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
+    for (unsigned p = tid; p < nst; p += kET) {
+      const unsigned key = order_key(s_key[p]);
+      const unsigned long long rel = (unsigned long long)(key - fc.t_lo);
+      if (rel >= fc.width0) ++fc.above;
+      else atomicAdd(&s_hist[(unsigned)(rel >> fc.sh0)], 1u);
+      fc.mk = key > fc.mk ? key : fc.mk;
+    }
+    __syncthreads();
+  }
 
   // ---- staging (16-B stores) and the round-0 histogram / counts
   {
@@ -783,6 +807,7 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
     w.blk_c()[blockIdx.x] = C_b;
   }
   STAMP(3);
+  BLKT(2);
   STAMP_OUT(0, 4);
 }
 

@@ -13,7 +13,8 @@ import torch
 
 from fl_sim_amd import codec
 
-STAMP_OFF = 175616  # byte offset of EncWs.stamps in the top-k workspace (topk.hip: carve_enc)
+STAMP_OFF = 175616  # byte offset of EncWs.stamps in the top-k workspace (topk.hip: kOffStamps)
+BLKT_OFF = 175872   # kOffBlkT
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
 x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 1e-3
@@ -33,3 +34,16 @@ for it in range(6):
             prev = t[i]
     print(" | ".join(parts), f"| total {(t[11] - t[0]) * 10 / 1000:.1f} us")
     ws[STAMP_OFF:STAMP_OFF + 16 * 8].zero_()
+    if it == 5:  # per-block filter times (start of the HBM pass, its end, end of the kernel)
+        bt = ws[BLKT_OFF:BLKT_OFF + 256 * 32].cpu().numpy().view(np.uint64).astype(np.int64).reshape(256, 4)
+        G = int((bt[:, 0] > 0).sum())
+        bt = bt[:G]
+        t0 = bt[:, 0].min()
+        st_ = (bt[:, 0] - t0) * 10 / 1000
+        en_ = (bt[:, 1] - t0) * 10 / 1000
+        dur = en_ - st_
+        print(f"blocks {G}: pass start spread {st_.max():.1f} us; pass duration min {dur.min():.1f} median {np.median(dur):.1f} max {dur.max():.1f}; last end {en_.max():.1f}")
+        order = np.argsort(dur)
+        print("slowest blocks:", [(int(b), round(float(dur[b]), 1)) for b in order[-8:]])
+        xcd = np.arange(G) % 8
+        print("mean duration by blockIdx % 8:", [round(float(dur[xcd == i].mean()), 1) for i in range(8)])
