@@ -204,6 +204,27 @@ __device__ void block_select_from_top(const unsigned* h, const long long (&r)[NR
   __syncthreads();
 }
 
+// block-wide sums of N 64-bit values per thread in one LDS round (s_buf: kENW * N words)
+template <int N>
+__device__ __forceinline__ void block_sum_n(unsigned long long (&v)[N], unsigned long long* s_buf) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) s_buf[wid * N + i] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kENW; ++w) t += s_buf[w * N + i];
+    v[i] = t;
+  }
+  __syncthreads();
+}
+
 // LDS histogram add with wave aggregation: when every active lane hits the same bin (ties, narrow
 // key ranges) the wave issues ONE atomic instead of a 64-way conflicting one.
 __device__ __forceinline__ void hist_add(unsigned* h, unsigned bin, bool valid) {
@@ -262,29 +283,12 @@ struct SampleLds {
 // sample index of a thread's key slot i: 16-B runs, so the coherent read is 8 x 16 B per thread
 __device__ __forceinline__ int sample_j(int i) { return 4 * (int)threadIdx.x + 4 * kET * (i >> 2) + (i & 3); }
 
-// ascending bitonic sort of one value per lane across the wave
-__device__ __forceinline__ unsigned wave_sort_u32(unsigned v) {
-  const int lane = threadIdx.x & (kWave - 1);
-#pragma unroll
-  for (int k = 2; k <= kWave; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const unsigned o = __shfl_xor(v, j, kWave);
-      const bool up = (lane & k) == 0;
-      const bool lower = (lane & j) == 0;
-      const unsigned mn = o < v ? o : v, mx = o < v ? v : o;
-      v = (lower == up) ? mn : mx;
-    }
-  }
-  return v;
-}
-
-// Fast path (rank_lo <= 1024): B = min over waves of the wave's ceil(rank_lo / 16)-th largest lane
-// maximum, so at least rank_lo sample keys are >= B (each wave holds that many), typically ~1.4 rank_lo.
-// ONE range-adaptive 11-bit histogram of the keys in [B, max] (straight from registers) then locates
-// the bins of ranks rank_lo and rank_hi: a bin holds ~0.3 sample keys here, so the bin floor of the
-// rank_lo-th key is a floor admitting rank_lo + O(1) sample keys and the end of the rank_hi-th key's
-// bin a ceiling with fewer than rank_hi sample keys at or above it.
+// Fast path (rank_lo <= kET): B = the smallest lane maximum, so at least kET >= rank_lo sample keys are
+// >= B (one per lane); typically B sits near the 80th percentile.  An 11-bit histogram of the keys in
+// [B, max] (plain LDS atomics, from registers) locates the bins of ranks rank_lo and rank_hi; a target
+// bin holding more than a few sample keys (clustered values, ties) is refined by a second pass inside
+// it.  The floor is the floor of rank_lo's bin (>= rank_lo sample keys at or above it) and the ceiling
+// the end of rank_hi's bin (fewer than rank_hi sample keys at or above it).
 __device__ __forceinline__ bool sample_fast(const unsigned (&keys)[kSPT], int S, long long rank_lo, long long rank_hi,
                                             SampleLds& L, unsigned* s_hist, unsigned long long* s_red,
                                             unsigned* t_lo_out, unsigned long long* t_hi_out) {
@@ -292,16 +296,22 @@ __device__ __forceinline__ bool sample_fast(const unsigned (&keys)[kSPT], int S,
   unsigned m = 0;
 #pragma unroll
   for (int i = 0; i < kSPT; ++i) m = keys[i] > m ? keys[i] : m;  // invalid slots hold key 0
-  const int q = (int)((rank_lo + kENW - 1) / kENW);              // 1 <= q <= 64
-  const unsigned srt = wave_sort_u32(m);
-  const unsigned bw = __shfl(srt, kWave - q, kWave);
-  const unsigned wmx = __shfl(srt, kWave - 1, kWave);
+  unsigned wmn = m, wmx = m;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned a = __shfl_xor(wmn, o, kWave), b = __shfl_xor(wmx, o, kWave);
+    wmn = a < wmn ? a : wmn;
+    wmx = b > wmx ? b : wmx;
+  }
   if (lane == 0) {
-    L.wmin[wid] = bw;
+    L.wmin[wid] = wmn;
     L.wmax[wid] = wmx;
   }
   if (tid == 0) L.err = 0;
-  for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
+  for (int i = tid; i < kHistBins; i += kET) {
+    s_hist[i] = 0u;
+    L.hist2[i] = 0u;
+  }
   __syncthreads();
   unsigned B = 0xffffffffu, mx = 0;
 #pragma unroll
@@ -311,17 +321,42 @@ __device__ __forceinline__ bool sample_fast(const unsigned (&keys)[kSPT], int S,
   }
   const int sh = range_shift((unsigned long long)mx - B + 1ull, kHistBits);
 #pragma unroll
-  for (int i = 0; i < kSPT; ++i) {
-    const bool f = sample_j(i) < S && keys[i] >= B;
-    if (__ballot(f)) hist_add(s_hist, (keys[i] - B) >> sh, f);
-  }
+  for (int i = 0; i < kSPT; ++i)
+    if (sample_j(i) < S && keys[i] >= B) atomicAdd(&s_hist[(keys[i] - B) >> sh], 1u);
   __syncthreads();
   const bool two = rank_hi > 0;
   const long long rk[2] = {rank_lo, two ? rank_hi : 0};
   block_select_from_top<2>(s_hist, rk, L.digit, L.rem, &L.err, s_red);
   if (L.err) return false;  // block-uniform
-  *t_lo_out = B + (L.digit[0] << sh);
-  *t_hi_out = two ? (unsigned long long)B + ((unsigned long long)(L.digit[1] + 1u) << sh) : (1ull << 32);
+  const unsigned d0 = L.digit[0], d1 = two ? L.digit[1] : 0u;
+  unsigned lo0 = B + (d0 << sh), lo1 = B + (d1 << sh);
+  int sh_lo = sh, sh_hi = sh;
+  const bool ref0 = sh > 0 && s_hist[d0] > 8u, ref1 = two && sh > 0 && s_hist[d1] > 8u;  // block-uniform
+  if (ref0 || ref1) {
+    const long long r0 = L.rem[0], r1 = two ? L.rem[1] : 0;
+    const int sh2 = sh > kHistBits ? sh - kHistBits : 0;
+    const unsigned long long bw = 1ull << sh;
+    __syncthreads();
+    for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kSPT; ++i) {
+      if (sample_j(i) >= S) continue;
+      const unsigned long long rel0 = (unsigned long long)keys[i] - lo0, rel1 = (unsigned long long)keys[i] - lo1;
+      if (ref0 && keys[i] >= lo0 && rel0 < bw) atomicAdd(&s_hist[(unsigned)(rel0 >> sh2)], 1u);
+      if (ref1 && keys[i] >= lo1 && rel1 < bw) atomicAdd(&L.hist2[(unsigned)(rel1 >> sh2)], 1u);
+    }
+    __syncthreads();
+    const long long ra[1] = {ref0 ? r0 : 0}, rb[1] = {ref1 ? r1 : 0};
+    block_select_from_top<1>(s_hist, ra, &L.digit[0], &L.rem[0], &L.err, s_red);
+    block_select_from_top<1>(L.hist2, rb, &L.digit[1], &L.rem[1], &L.err, s_red);
+    if (L.err) return false;
+    if (ref0) { lo0 += L.digit[0] << sh2; sh_lo = sh2; }
+    if (ref1) { lo1 += L.digit[1] << sh2; sh_hi = sh2; }
+  }
+  *t_lo_out = lo0;
+  *t_hi_out = two ? (unsigned long long)lo1 + (1ull << sh_hi) : (1ull << 32);
+  (void)sh_lo;
   return true;
 }
 
@@ -701,8 +736,9 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
         for (int c = 0; c < 4; ++c) keys[i + c] = j + c < S ? w.sample()[j + c] : 0u;  // 0: below every key
       }
     }
+    STAMP(1);
     bool ok = false;
-    if (rank_lo <= kWave * kENW) ok = sample_fast(keys, S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
+    if (rank_lo <= kET) ok = sample_fast(keys, S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
     if (!ok) sample_general(keys, S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
     if (blockIdx.x == 0 && tid == 0) w.st()->sample_path = ok ? 0ull : 1ull;
   }
@@ -716,7 +752,7 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
   __syncthreads();  // sample scratch (aliases s_key) dead from here
   for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
   __syncthreads();
-  STAMP(1);
+  STAMP(2);
   BLKT(0);
 
   // ---- the HBM pass
@@ -765,7 +801,7 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
   }
   const unsigned C_b = base;
   __syncthreads();
-  STAMP(2);
+  STAMP(3);
   BLKT(1);
   {  // band histogram / above / max of the stored candidates
     const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
@@ -806,9 +842,9 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
     atomicAdd(&w.acc()[0], (unsigned long long)C_b);
     w.blk_c()[blockIdx.x] = C_b;
   }
-  STAMP(3);
+  STAMP(4);
   BLKT(2);
-  STAMP_OUT(0, 4);
+  STAMP_OUT(0, 5);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -829,11 +865,12 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   __shared__ unsigned long long s_glob[4];
   __shared__ unsigned long long s_ex[3];
   __shared__ SelState s_cur, s_prev;
+  __shared__ unsigned long long s_sum[kENW * 6];
   STAMP_INIT();
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * w.M;
   const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
-  STAMP(4);
+  STAMP(5);
 
   // ---- one batch of loads: this block's candidates (staging), the round-0 histogram and counts
   unsigned* hist = w.hist();
@@ -865,7 +902,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   long long A_cur = (long long)s_ex[0];
   int slot = 0;
   unsigned long long a_blk = 0;
-  STAMP(5);
+  STAMP(6);
 
   SelState& cur = s_cur;
   SelState& prev = s_prev;
@@ -936,7 +973,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   __syncthreads();
   if (tid == 0) prev = cur;
   pick_digit(w, cur, A_cur, maxkey, s_ghist, &s_err, s_red);
-  STAMP(6);
+  STAMP(7);
   unsigned long long pre = 0, tot = 0;
   bool counted = false;
   if (!fb && cur.narrowed && slot == 0) {
@@ -973,39 +1010,45 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     }
     const unsigned long long gt = block_sum<unsigned long long, kENW>((unsigned long long)gtc, s_red);
     if (tid == 0) st_mem64(&w.blk_cnt()[blockIdx.x], ((unsigned long long)s_nl << 32) | (gt & 0xffffffffull));
-    STAMP(7);
-    exchange(w, ++ep);
     STAMP(8);
-    // all-gather: per-block list sizes and counts above the bin, then the lists themselves
+    exchange(w, ++ep);
+    STAMP(9);
+    // all-gather in ONE batch of coherent loads: every block's list size and count above the bin, and
+    // all list slots (sizes are checked afterwards)
     unsigned* s_lkey = s_ghist;               // <= kInbinAll keys
     unsigned* s_lblk = s_ghist + kInbinAll;   // their blocks
     static_assert(2 * kInbinAll <= kHistBins, "in-bin list fits the histogram buffer");
     __shared__ unsigned s_nb[kMaxBlocks];
     __shared__ unsigned s_ovf, s_nall;
+    constexpr int kLW = 8;  // list words per thread per batch (G <= 256: one batch)
+    const int words = (int)gridDim.x * kInbin;
+    unsigned long long meta = 0;
+    unsigned lw[kLW];
+    if (tid < (int)gridDim.x) meta = ld_mem64(&w.blk_cnt()[tid]);
+#pragma unroll
+    for (int i = 0; i < kLW; ++i) {
+      const int j = i * kET + tid;
+      lw[i] = j < words ? ld_mem(w.inbin() + j) : 0u;
+    }
     if (tid == 0) { s_ovf = 0u; s_nall = 0u; }
     __syncthreads();
     unsigned long long my_gt = 0, pre_gt = 0;
     if (tid < (int)gridDim.x) {
-      const unsigned long long m = ld_mem64(&w.blk_cnt()[tid]);
-      const unsigned nb = (unsigned)(m >> 32);
+      const unsigned nb = (unsigned)(meta >> 32);
       s_nb[tid] = nb;
-      my_gt = m & 0xffffffffull;
+      my_gt = meta & 0xffffffffull;
       pre_gt = tid < (int)blockIdx.x ? my_gt : 0ull;
       if (nb > (unsigned)kInbin) atomicOr(&s_ovf, 1u);
     }
-    const unsigned long long gt_all = block_sum<unsigned long long, kENW>(my_gt, s_red);
-    const unsigned long long gt_pre = block_sum<unsigned long long, kENW>(pre_gt, s_red);
+    __syncthreads();
     if (s_ovf == 0u) {
-      // list words in batches of 8 per thread in flight together (G <= 256 blocks: one batch)
-      constexpr int kLW = 8;
-      const int words = (int)gridDim.x * kInbin;
       for (int c0 = 0; c0 < words; c0 += kLW * kET) {
-        unsigned lw[kLW];
+        if (c0 > 0) {  // more than 256 blocks: further batches
 #pragma unroll
-        for (int i = 0; i < kLW; ++i) {
-          const int j = c0 + i * kET + tid;
-          const int bb = j / kInbin;
-          lw[i] = (j < words && (unsigned)(j % kInbin) < s_nb[bb < (int)gridDim.x ? bb : 0]) ? ld_mem(w.inbin() + j) : 0u;
+          for (int i = 0; i < kLW; ++i) {
+            const int j = c0 + i * kET + tid;
+            lw[i] = j < words ? ld_mem(w.inbin() + j) : 0u;
+          }
         }
 #pragma unroll
         for (int i = 0; i < kLW; ++i) {
@@ -1026,6 +1069,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
         }
       }
       __syncthreads();
+      STAMP(10);
       if (s_nall <= (unsigned)kInbinAll) {  // block-uniform
         const unsigned nall = s_nall;
         // exact k-th largest among the in-bin keys: rank cur.need from the top, local radix passes
@@ -1060,6 +1104,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
           cur.need = r;
           cur.done = 1;
         }
+        STAMP(11);
         // strict / tie counts: above-the-bin counts + in-bin keys > T / == T, by block
         const unsigned T0 = lo;
         unsigned long long ps = 0, pt = 0, as = 0, at = 0;
@@ -1070,17 +1115,19 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
           at += t1;
           if (bb < blockIdx.x) { ps += s1; pt += t1; }
         }
-        const unsigned long long A_s = block_sum<unsigned long long, kENW>(as, s_red);
-        const unsigned long long A_t = block_sum<unsigned long long, kENW>(at, s_red);
-        const unsigned long long P_s = block_sum<unsigned long long, kENW>(ps, s_red);
-        const unsigned long long P_t = block_sum<unsigned long long, kENW>(pt, s_red);
-        pre = ((gt_pre + P_s) << 32) | P_t;
-        tot = ((gt_all + A_s) << 32) | A_t;
+        // the four in-bin counts are <= kInbinAll: 16-bit fields of one word
+        static_assert(kInbinAll < 65536, "16-bit count fields");
+        unsigned long long sums[3] = {as | (at << 16) | (ps << 32) | (pt << 48), my_gt, pre_gt};
+        block_sum_n<3>(sums, s_sum);
+        const unsigned long long A_s = sums[0] & 0xffffull, A_t = (sums[0] >> 16) & 0xffffull;
+        const unsigned long long P_s = (sums[0] >> 32) & 0xffffull, P_t = sums[0] >> 48;
+        pre = ((sums[2] + P_s) << 32) | P_t;
+        tot = ((sums[1] + A_s) << 32) | A_t;
         counted = true;
       }
     }
     __syncthreads();
-    STAMP(9);
+    STAMP(12);
   }
   // histogram rounds over the block's candidates until T is resolved (rare paths)
   if (!counted && cur.narrowed && !fb && slot == 0) {
@@ -1149,7 +1196,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     pre = s_glob[3];
     tot = t_all;
   }
-  STAMP(10);
+  STAMP(13);
   const long long strict_tot = (long long)(tot >> 32), ties_tot = (long long)(tot & 0xffffffffull);
   // every hist / acc read of this call happened before the last exchange: zero them for the next call
   // (my slice), and the call counter advances
@@ -1234,8 +1281,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     s_before += __popcll(ms);
     t_before += __popcll(mt);
   }
-  STAMP(11);
-  STAMP_OUT(4, 16);
+  STAMP(14);
+  STAMP_OUT(5, 16);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -18,7 +18,7 @@ BLKT_OFF = 175872   # kOffBlkT
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
 x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 1e-3
-names = ["sample-sel", "filter", "stage+flush", "boundary", "load", "pick0", "inbin", "x1", "local", "counts", "compact"]
+names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "compact"]
 for it in range(6):
     codec.stacked_encode(x, k, 127, 1, it)
     torch.cuda.synchronize()
@@ -26,13 +26,13 @@ for it in range(6):
     st = ws[STAMP_OFF:STAMP_OFF + 16 * 8].cpu().numpy().view(np.uint64).astype(np.int64)
     if it < 2:
         continue
-    t = st[:12].astype(np.float64)
+    t = st[:15].astype(np.float64)
     prev, parts = t[0], []
-    for i in range(1, 12):
+    for i in range(1, 15):
         if t[i] > 0 and t[i] >= prev:
             parts.append(f"{names[i - 1]} {(t[i] - prev) * 10 / 1000:.1f}")
             prev = t[i]
-    print(" | ".join(parts), f"| total {(t[11] - t[0]) * 10 / 1000:.1f} us")
+    print(" | ".join(parts), f"| total {(t[14] - t[0]) * 10 / 1000:.1f} us")
     ws[STAMP_OFF:STAMP_OFF + 16 * 8].zero_()
     if it == 5:  # per-block filter times (start of the HBM pass, its end, end of the kernel)
         bt = ws[BLKT_OFF:BLKT_OFF + 256 * 32].cpu().numpy().view(np.uint64).astype(np.int64).reshape(256, 4)
