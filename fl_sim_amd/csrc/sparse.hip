@@ -24,7 +24,7 @@ namespace flc {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kDecodeVariant = 40;  // V * 10 + EARLY (see launch_decode)
+constexpr int kDecodeVariant = 302;  // see launch_decode: 302 = one wave per two 1024-output tiles
 
 // tile_start[t] = first j with idx[j] >= t * TILE (t = 0 .. ntiles); idx ascending.  One thread per
 // kept entry: entry j fills the tiles between its predecessor's tile and its own.
@@ -268,6 +268,12 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave_kernel(const int* __
       acc[u] = e + 4 <= n ? *reinterpret_cast<const float4*>(out + e) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  if (dbg == 3) {  // calibration: the store stream alone
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      *reinterpret_cast<float4*>(out + t0 + 4 * (int64_t)(lane + u * kWave)) = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   unsigned lo = 0, hi = 0;
   if (dbg != 1) { lo = tile_start[blockIdx.x]; hi = tile_start[blockIdx.x + 1]; }
   if (dbg == 2) hi = lo;
@@ -302,6 +308,71 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave_kernel(const int* __
         else if (weight != 1.0f) o = weight * o;
         out[e + c] = o;
       }
+    }
+  }
+}
+
+// One-wave decode, NT tiles of 1024 outputs per wave (adjacent: one NT x 4 KB piece), every load chain
+// of the NT tiles in flight together.
+template <int MODE, int NT>
+__global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* __restrict__ idx,
+                                                                    const float* __restrict__ val,
+                                                                    const uint8_t* __restrict__ codes, float scale,
+                                                                    int levels, double step,
+                                                                    const float* __restrict__ norm_ptr, int64_t n,
+                                                                    float weight, float* __restrict__ out,
+                                                                    const unsigned* __restrict__ tile_start,
+                                                                    int64_t ntiles) {
+  constexpr int TILE = 1024;
+  __shared__ __attribute__((aligned(16))) float s_tile[NT * TILE];
+  const int lane = threadIdx.x;
+  const int64_t tb = (int64_t)blockIdx.x * NT;
+  const int64_t t0 = tb * TILE;
+  unsigned ts[NT + 1];
+#pragma unroll
+  for (int i = 0; i <= NT; ++i) ts[i] = tile_start[tb + i < ntiles ? tb + i : ntiles];
+  float4* tile4 = reinterpret_cast<float4*>(s_tile);
+#pragma unroll
+  for (int u = 0; u < 4 * NT; ++u) tile4[lane + u * kWave] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float nrm = MODE == 1 ? *norm_ptr : 0.0f;
+  // first entry per lane of every tile in flight together, the (rare) rest afterwards
+  unsigned e_idx[NT];
+  uint32_t e_raw[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const unsigned j = ts[i] + lane;
+    e_idx[i] = 0xffffffffu;
+    e_raw[i] = 0u;
+    if (j < ts[i + 1]) {
+      e_idx[i] = (unsigned)idx[j];
+      e_raw[i] = entry_raw<MODE>(val, codes, j);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    if (e_idx[i] != 0xffffffffu) {
+      const int64_t off = (int64_t)e_idx[i] - t0;
+      if (off >= 0 && off < NT * TILE) s_tile[off] = entry_value<MODE>(e_raw[i], scale, levels, step, nrm);
+    }
+    for (unsigned j = ts[i] + kWave + lane; j < ts[i + 1]; j += kWave) {
+      const int64_t off = (int64_t)(unsigned)idx[j] - t0;
+      if (off >= 0 && off < NT * TILE)
+        s_tile[off] = entry_value<MODE>(entry_raw<MODE>(val, codes, j), scale, levels, step, nrm);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int u = 0; u < 4 * NT; ++u) {
+    const int q = lane + u * kWave;
+    const int64_t e = t0 + 4 * (int64_t)q;
+    float4 v = tile4[q];
+    if (e + 4 <= n) {
+      if (weight != 1.0f) v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
+      *reinterpret_cast<float4*>(out + e) = v;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int c = 0; c < 4 && e + c < n; ++c) out[e + c] = weight != 1.0f ? weight * vv[c] : vv[c];
     }
   }
 }
@@ -546,6 +617,26 @@ int launch_decode_wave(const int32_t* idx, const float* val, const uint8_t* code
   return FLC_OK;
 }
 
+template <int MODE, int NT>
+int launch_decode_wave2(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
+                        const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws,
+                        size_t ws_bytes, hipStream_t st, const char* name) {
+  if (accumulate) return launch_decode_wave<MODE>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out,
+                                                  ws, ws_bytes, st, name);
+  const int64_t ntiles = cdiv(n, (int64_t)1024);
+  const size_t need = (size_t)(ntiles + 1) * sizeof(unsigned);
+  if (!ws || ws_bytes < need) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", name, ws_bytes, need);
+  if (!aligned16(out)) return fail(FLC_EINVAL, "%s: out must be 16-B aligned", name);
+  unsigned* tile_start = static_cast<unsigned*>(ws);
+  const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(k + 1, kThreads), 2048));
+  FLC_LAUNCH("tile_index", tile_index_kernel<10>, dim3(gi), dim3(kThreads), 0, st, idx, (long long)k,
+             (long long)ntiles, tile_start);
+  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
+  FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, NT>), dim3((unsigned)cdiv(ntiles, NT)), dim3(kWave), 0, st, idx,
+             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles);
+  return FLC_OK;
+}
+
 int64_t decode_gs_blocks() {  // resident grid: FLC_DECODE_BLOCKS or 8 blocks of 256 threads per CU
   const char* e = getenv("FLC_DECODE_BLOCKS");
   if (e && atoi(e) > 0) return atoi(e);
@@ -596,6 +687,9 @@ int launch_decode(const int32_t* idx, const float* val, const uint8_t* codes, in
   if (dv == 90) return launch_decode_stream<MODE>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out,
                                                   ws, ws_bytes, st, name);
   switch (dv) {
+    case 301: return launch_decode_wave2<MODE, 1>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
+    case 302: return launch_decode_wave2<MODE, 2>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
+    case 304: return launch_decode_wave2<MODE, 4>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
     case 300: return launch_decode_wave<MODE>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
     case 201: return launch_decode_gs<MODE, 1>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
     case 202: return launch_decode_gs<MODE, 2>(idx, val, codes, k, scale, levels, norm, n, weight, accumulate, out, ws, ws_bytes, st, name);
