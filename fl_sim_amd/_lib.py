@@ -61,6 +61,22 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p, c_size_t, c_void_p],
     ),
+    "flc_tile_index": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "flc_topk_encode_tiled": (
+        c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    ),
+    "flc_sparse_decode_tiled": (
+        c_int, [c_void_p, c_void_p, c_int64, c_float, c_int64, c_float, c_int, c_void_p, c_void_p, c_void_p]
+    ),
+    "flc_stacked_encode_tiled": (
+        c_int,
+        [c_void_p, c_int64, c_int64, c_int, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_size_t, c_void_p],
+    ),
+    "flc_stacked_decode_tiled": (
+        c_int,
+        [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p, c_void_p],
+    ),
     "flc_copy": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_scale_div": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "flc_randk_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_float, c_void_p, c_void_p]),

@@ -40,6 +40,9 @@ def _dev_f32(x: torch.Tensor, name: str = "x") -> torch.Tensor:
     return x
 
 
+TILE = 1024  # FLC_TILE (include/flcodec.h)
+
+
 def workspace(device: torch.device, nbytes: int, kind: str) -> torch.Tensor:
     """Zero-initialised workspace, cached per (device, stream, kind) and grown on demand."""
     key = (device.index if device.index is not None else torch.cuda.current_device(), _stream(device), kind)
@@ -151,21 +154,32 @@ def natural_decode(codes: torch.Tensor, n: int, out: Optional[torch.Tensor] = No
 
 
 # ------------------------------------------------------------------------------------------------ top-k
-def topk_encode(x: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Kept set of the reference Top-K (k largest signed values): (idx int32 ascending, val fp32)."""
+def _tiles(n: int, device: torch.device) -> torch.Tensor:
+    """CSR tile pointers over FLC_TILE-output tiles (include/flcodec.h)."""
+    return torch.empty((n + TILE - 1) // TILE + 1, dtype=torch.int32, device=device)
+
+
+def topk_encode(x: torch.Tensor, k: int, with_tiles: bool = False):
+    """Kept set of the reference Top-K (k largest signed values): (idx int32 ascending, val fp32), plus the
+    tile pointers of idx when ``with_tiles`` (emitted by the encoder, saving the decoder an index pass)."""
     x = _dev_f32(x).reshape(-1)
     n = x.numel()
     idx = torch.empty(k, dtype=torch.int32, device=x.device)
     val = torch.empty(k, dtype=torch.float32, device=x.device)
+    tiles = _tiles(n, x.device) if with_tiles else None
     ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
-    call("flc_topk_encode", _p(x), n, k, _p(idx), _p(val), _p(ws), ws.numel(), _stream(x.device))
-    return idx, val
+    call("flc_topk_encode_tiled", _p(x), n, k, _p(idx), _p(val), _p(tiles), _p(ws), ws.numel(), _stream(x.device))
+    return (idx, val, tiles) if with_tiles else (idx, val)
 
 
 def sparse_decode(idx: torch.Tensor, val: torch.Tensor, n: int, scale: float = 1.0, out: Optional[torch.Tensor] = None,
-                  weight: float = 1.0, accumulate: bool = False) -> torch.Tensor:
+                  weight: float = 1.0, accumulate: bool = False, tiles: Optional[torch.Tensor] = None) -> torch.Tensor:
     if out is None:
         out = torch.empty(n, dtype=torch.float32, device=val.device)
+    if tiles is not None:
+        call("flc_sparse_decode_tiled", _p(idx), _p(val), idx.numel(), scale, n, weight, int(accumulate), _p(out),
+             _p(tiles), _stream(out.device))
+        return out
     ws = workspace(out.device, _lib.size("flc_sparse_decode_workspace_size", n), "decode")
     call("flc_sparse_decode", _p(idx), _p(val), idx.numel(), scale, n, weight, int(accumulate), _p(out), _p(ws),
          ws.numel(), _stream(out.device))
@@ -174,35 +188,43 @@ def sparse_decode(idx: torch.Tensor, val: torch.Tensor, n: int, scale: float = 1
 
 @dataclass
 class StackedPacket:
-    """Wire of the stacked codec: ascending int32 indices, 8-bit (sign | level) codes, fp32 norm."""
+    """Wire of the stacked codec: ascending int32 indices, 8-bit (sign | level) codes, fp32 norm; plus the
+    encoder-emitted tile pointers of the indices (CSR over 1024-output tiles), the decoder's index."""
 
     idx: torch.Tensor
     codes: torch.Tensor
     norm: torch.Tensor
     n: int
     levels: int
+    tiles: Optional[torch.Tensor] = None
 
     @property
     def nbytes(self) -> int:
-        return 5 * self.idx.numel() + 4
+        return 5 * self.idx.numel() + 4 + (4 * self.tiles.numel() if self.tiles is not None else 0)
 
 
-def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, counter: int = 0) -> StackedPacket:
+def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, counter: int = 0,
+                   with_tiles: bool = True) -> StackedPacket:
     x = _dev_f32(x).reshape(-1)
     n = x.numel()
     idx = torch.empty(k, dtype=torch.int32, device=x.device)
     codes = torch.empty(max(k, 16), dtype=torch.uint8, device=x.device)
     norm = torch.empty(1, dtype=torch.float32, device=x.device)
+    tiles = _tiles(n, x.device) if with_tiles else None
     ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
-    call("flc_stacked_encode", _p(x), n, k, levels, seed, counter, None, _p(idx), _p(codes), _p(norm), _p(ws),
-         ws.numel(), _stream(x.device))
-    return StackedPacket(idx, codes, norm, n, levels)
+    call("flc_stacked_encode_tiled", _p(x), n, k, levels, seed, counter, None, _p(idx), _p(codes), _p(norm),
+         _p(tiles), _p(ws), ws.numel(), _stream(x.device))
+    return StackedPacket(idx, codes, norm, n, levels, tiles)
 
 
 def stacked_decode(pkt: StackedPacket, out: Optional[torch.Tensor] = None, weight: float = 1.0,
                    accumulate: bool = False) -> torch.Tensor:
     if out is None:
         out = torch.empty(pkt.n, dtype=torch.float32, device=pkt.idx.device)
+    if pkt.tiles is not None:
+        call("flc_stacked_decode_tiled", _p(pkt.idx), _p(pkt.codes), pkt.idx.numel(), pkt.levels, _p(pkt.norm), pkt.n,
+             weight, int(accumulate), _p(out), _p(pkt.tiles), _stream(out.device))
+        return out
     ws = workspace(out.device, _lib.size("flc_sparse_decode_workspace_size", pkt.n), "decode")
     call("flc_stacked_decode", _p(pkt.idx), _p(pkt.codes), pkt.idx.numel(), pkt.levels, _p(pkt.norm), pkt.n, weight,
          int(accumulate), _p(out), _p(ws), ws.numel(), _stream(out.device))

@@ -327,8 +327,8 @@ class Compressor:
                 # np.argsort(out)[:-K] is empty for K == 0 and K >= d: nothing is zeroed
                 out = codec.copy(x)
             else:
-                idx, val = codec.topk_encode(x, K)
-                out = codec.sparse_decode(idx, val, d)
+                idx, val, tiles = codec.topk_encode(x, K, with_tiles=True)
+                out = codec.sparse_decode(idx, val, d, tiles=tiles)
             self._finish(d, self.K)
             return out
         if t == CompressorType.ADAPTIVE_RANDOM_COMPRESSOR:
@@ -393,7 +393,7 @@ class Compressor:
         return codec.quant_decode(pkt)
 
     def encode(self, x: torch.Tensor) -> Any:
-        """Wire packet of ``x`` (device tensors, philox RNG): QuantPacket / (idx, val) / StackedPacket."""
+        """Wire packet of ``x`` (device tensors, philox RNG): QuantPacket / (idx, val, tiles) / StackedPacket."""
         t = self.compressorType
         if t in _STD or t in _NATD:
             kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
@@ -401,7 +401,7 @@ class Compressor:
             seed, ctr = self.philox.next()
             return codec.quant_encode(x2, kind, self.s, codec.quant_norm(x2, self.p), seed, ctr, None, want_nnz=False)
         if t == CompressorType.TOPK_COMPRESSOR:
-            return codec.topk_encode(x, int(self.K))
+            return codec.topk_encode(x, int(self.K), with_tiles=True)
         if t in _NATURAL:
             seed, ctr = self.philox.next()
             return codec.natural_encode(x, seed, ctr, None, want_nnz=False)[0]
@@ -412,8 +412,9 @@ class Compressor:
         if t in _STD or t in _NATD:
             return codec.quant_decode(packet).reshape(-1)
         if t == CompressorType.TOPK_COMPRESSOR:
-            idx, val = packet
-            return codec.sparse_decode(idx, val, int(d if d is not None else self.D))
+            idx, val = packet[0], packet[1]
+            tiles = packet[2] if len(packet) > 2 else None
+            return codec.sparse_decode(idx, val, int(d if d is not None else self.D), tiles=tiles)
         if t in _NATURAL:
             return codec.natural_decode(packet, int(d if d is not None else packet.numel()))
         raise NotImplementedError(f"decode: {t}")

@@ -617,6 +617,24 @@ int launch_decode_wave(const int32_t* idx, const float* val, const uint8_t* code
   return FLC_OK;
 }
 
+// decode over given 1024-output tile pointers (no tile_index pass): one wave per two tiles, or, when
+// accumulating, one wave per tile (its slice of `out` read first)
+template <int MODE>
+int launch_decode_tiles(const int32_t* idx, const float* val, const uint8_t* codes, float scale, int levels,
+                        const float* norm, int64_t n, float weight, int accumulate, float* out,
+                        const unsigned* tile_start, hipStream_t st, const char* name) {
+  if (!aligned16(out)) return fail(FLC_EINVAL, "%s: out must be 16-B aligned", name);
+  const int64_t ntiles = cdiv(n, (int64_t)FLC_TILE);
+  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
+  if (accumulate)
+    FLC_LAUNCH(name, (sparse_decode_wave_kernel<MODE, true>), dim3((unsigned)ntiles), dim3(kWave), 0, st, idx, val,
+               codes, scale, levels, step, norm, n, weight, out, tile_start, 0);
+  else
+    FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, 2>), dim3((unsigned)cdiv(ntiles, 2)), dim3(kWave), 0, st, idx,
+               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles);
+  return FLC_OK;
+}
+
 template <int MODE, int NT>
 int launch_decode_wave2(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
                         const float* norm, int64_t n, float weight, int accumulate, float* out, void* ws,
@@ -718,6 +736,36 @@ using namespace flc;
 extern "C" {
 
 size_t flc_sparse_decode_workspace_size(int64_t n) { return decode_ws_bytes(n); }
+
+int flc_tile_index(const int32_t* idx, int64_t k, int64_t n, uint32_t* tiles, void* stream) {
+  if (!tiles || n <= 0 || k < 0 || (k > 0 && !idx)) return fail(FLC_EINVAL, "flc_tile_index: bad arguments");
+  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_tile_index: n must be < 2^31");
+  const int64_t ntiles = cdiv(n, (int64_t)FLC_TILE);
+  const unsigned gi = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(k + 1, kThreads), 2048));
+  static_assert(FLC_TILE == 1024, "tile_index_kernel<10>");
+  FLC_LAUNCH("tile_index", tile_index_kernel<10>, dim3(gi), dim3(kThreads), 0, as_stream(stream), idx, (long long)k,
+             (long long)ntiles, tiles);
+  return FLC_OK;
+}
+
+int flc_sparse_decode_tiled(const int32_t* idx, const float* val, int64_t k, float scale, int64_t n, float weight,
+                            int accumulate, float* out, const uint32_t* tiles, void* stream) {
+  if (!out || !tiles || n <= 0 || k < 0 || (k > 0 && (!idx || !val)))
+    return fail(FLC_EINVAL, "flc_sparse_decode_tiled: bad arguments");
+  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_sparse_decode_tiled: n must be < 2^31");
+  return launch_decode_tiles<0>(idx, val, nullptr, scale, 0, nullptr, n, weight, accumulate, out, tiles,
+                                as_stream(stream), "sparse_decode");
+}
+
+int flc_stacked_decode_tiled(const int32_t* idx, const uint8_t* codes, int64_t k, int levels, const float* norm,
+                             int64_t n, float weight, int accumulate, float* out, const uint32_t* tiles, void* stream) {
+  if (!out || !norm || !tiles || n <= 0 || k < 0 || (k > 0 && (!idx || !codes)))
+    return fail(FLC_EINVAL, "flc_stacked_decode_tiled: bad arguments");
+  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_stacked_decode_tiled: n must be < 2^31");
+  if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_stacked_decode_tiled: levels must be in [1, 127]");
+  return launch_decode_tiles<1>(idx, nullptr, codes, 1.0f, levels, norm, n, weight, accumulate, out, tiles,
+                                as_stream(stream), "stacked_decode");
+}
 
 int flc_sparse_decode(const int32_t* idx, const float* val, int64_t k, float scale, int64_t n, float weight,
                       int accumulate, float* out, void* ws, size_t ws_bytes, void* stream) {

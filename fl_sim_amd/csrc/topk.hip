@@ -61,6 +61,7 @@ constexpr int kEpochStride = 32;              // exchanges per call < 32
 constexpr int kMaxBlocks = 1024;              // <= kET (per-block words are read one per thread)
 constexpr int kInbin = 32;                    // in-bin keys a block may publish (more: histogram rounds)
 constexpr int kInbinAll = 1024;               // in-bin keys of all blocks resolved locally
+constexpr int kTile = FLC_TILE;               // outputs per tile of the CSR tile pointers
 constexpr int kFlagStride = 16;               // workspace words reserved per block for flags
 
 // diagnostics and the call counter (64-bit words, memory-side atomics only)
@@ -854,11 +855,13 @@ template <bool STACKED>
 __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restrict__ x, int64_t n, long long k, EncWs w,
                                                           int* __restrict__ idx_out, float* __restrict__ val_out,
                                                           uint8_t* __restrict__ code_out, float* __restrict__ norm_out,
-                                                          int levels, double step, uint64_t seed, uint64_t counter) {
+                                                          int levels, double step, uint64_t seed, uint64_t counter,
+                                                          unsigned* __restrict__ tile_out) {
   __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
   __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
-  __shared__ unsigned s_hist[kHistBins];
-  __shared__ unsigned s_ghist[kHistBins];
+  __shared__ unsigned s_hh[2 * kHistBins];  // the round / global histograms; in the compaction: tile counts
+  unsigned* const s_hist = s_hh;
+  unsigned* const s_ghist = s_hh + kHistBins;
   __shared__ unsigned long long s_red[kENW];
   __shared__ unsigned s_mx[kENW];
   __shared__ unsigned s_err;
@@ -1230,6 +1233,12 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     if (blockIdx.x == 0 && tid == 0) *norm_out = nrm;
   }
   const bool nrm_ok = nrm > 0.0f && nrm <= 3.402823466e38f;
+  // tile pointers (CSR over FLC_TILE-output tiles): kept entries per tile of this block, counted in the
+  // compaction, scanned afterwards (block ranges are whole tiles: M is a multiple of kBlockStep)
+  const bool tiled = tile_out != nullptr;  // (the host passes null when a block spans > 2 kHistBins tiles)
+  const int ntl = (int)((b1 - b0 + kTile - 1) / kTile);
+  if (tiled)
+    for (int i = tid; i < ntl; i += kET) s_hh[i] = 0u;
   const unsigned Q = ((ncand + kENW - 1) / kENW + kWave - 1) / kWave * kWave;
   const unsigned q0 = (unsigned)wid * Q < ncand ? (unsigned)wid * Q : ncand;
   const unsigned q1 = q0 + Q < ncand ? q0 + Q : ncand;
@@ -1277,9 +1286,34 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       } else {
         val_out[pos] = __uint_as_float(raw);
       }
+      if (tiled) atomicAdd(&s_hh[(unsigned)((int64_t)id - b0) / (unsigned)kTile], 1u);
     }
     s_before += __popcll(ms);
     t_before += __popcll(mt);
+  }
+  if (tiled) {
+    constexpr int TPT = 2 * kHistBins / kET;  // tiles per thread
+    __syncthreads();
+    unsigned c[TPT];
+    unsigned long long sum = 0;
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      const int t = tid * TPT + i;
+      c[i] = t < ntl ? s_hh[t] : 0u;
+      sum += c[i];
+    }
+    unsigned long long tt;
+    unsigned long long run = block_excl_scan<unsigned long long, kENW>(sum, s_red, &tt);
+    const long long tb = (long long)(pre & 0xffffffffull);
+    run += (unsigned long long)((long long)(pre >> 32) + (tb > skip ? tb - skip : 0));  // kept before the block
+    const int64_t tile0 = b0 / kTile;
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      const int t = tid * TPT + i;
+      if (t < ntl) tile_out[tile0 + t] = (unsigned)run;
+      run += c[i];
+    }
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) tile_out[cdiv_dev(n, kTile)] = (unsigned)k;
   }
   STAMP(14);
   STAMP_OUT(5, 16);
@@ -1321,7 +1355,8 @@ int current_cus(int* dev_out) {
 
 template <bool STACKED>
 int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes, hipStream_t st, int* idx, float* val,
-                uint8_t* codes, float* norm, int levels, uint64_t seed, uint64_t counter, const char* who) {
+                uint8_t* codes, float* norm, int levels, uint64_t seed, uint64_t counter, unsigned* tiles,
+                const char* who) {
   int dev = 0;
   const int cus = current_cus(&dev);
   size_t need = 0;
@@ -1343,9 +1378,12 @@ int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes,
     else FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
   }
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
+  const bool in_kernel_tiles = tiles && g.M / kTile <= 2 * kHistBins;
   FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", topk_select_kernel<STACKED>, dim3((unsigned)g.G), dim3(kET),
-             0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter);
+             0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
+             in_kernel_tiles ? tiles : nullptr);
   if (gated) FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
+  if (tiles && !in_kernel_tiles) return flc_tile_index(idx, k, n, tiles, st);
   return FLC_OK;
 }
 
@@ -1371,17 +1409,22 @@ size_t flc_topk_workspace_size(int64_t n, int64_t k) {
   return need;
 }
 
-int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, void* ws, size_t ws_bytes,
-                    void* stream) {
+int flc_topk_encode_tiled(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, uint32_t* tiles, void* ws,
+                          size_t ws_bytes, void* stream) {
   if (int rc = check_topk(x, n, k, "flc_topk_encode")) return rc;
   if (!idx || !val) return fail(FLC_EINVAL, "flc_topk_encode: null output");
-  return launch_topk<false>(x, n, k, ws, ws_bytes, as_stream(stream), idx, val, nullptr, nullptr, 0, 0, 0,
+  return launch_topk<false>(x, n, k, ws, ws_bytes, as_stream(stream), idx, val, nullptr, nullptr, 0, 0, 0, tiles,
                             "flc_topk_encode");
 }
 
-int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_t seed, uint64_t counter,
-                       const double* compat_u, int32_t* idx, uint8_t* codes, float* norm, void* ws, size_t ws_bytes,
-                       void* stream) {
+int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, void* ws, size_t ws_bytes,
+                    void* stream) {
+  return flc_topk_encode_tiled(x, n, k, idx, val, nullptr, ws, ws_bytes, stream);
+}
+
+int flc_stacked_encode_tiled(const float* x, int64_t n, int64_t k, int levels, uint64_t seed, uint64_t counter,
+                             const double* compat_u, int32_t* idx, uint8_t* codes, float* norm, uint32_t* tiles,
+                             void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_topk(x, n, k, "flc_stacked_encode")) return rc;
   if (!idx || !codes || !norm) return fail(FLC_EINVAL, "flc_stacked_encode: null output");
   if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_stacked_encode: levels must be in [1, 127]");
@@ -1389,7 +1432,14 @@ int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_
     return fail(FLC_EUNSUPPORTED,
                 "flc_stacked_encode: compat RNG is composed by the caller (flc_topk_encode + flc_quant_encode)");
   return launch_topk<true>(x, n, k, ws, ws_bytes, as_stream(stream), idx, nullptr, codes, norm, levels, seed, counter,
-                           "flc_stacked_encode");
+                           tiles, "flc_stacked_encode");
+}
+
+int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_t seed, uint64_t counter,
+                       const double* compat_u, int32_t* idx, uint8_t* codes, float* norm, void* ws, size_t ws_bytes,
+                       void* stream) {
+  return flc_stacked_encode_tiled(x, n, k, levels, seed, counter, compat_u, idx, codes, norm, nullptr, ws, ws_bytes,
+                                  stream);
 }
 
 }  // extern "C"

@@ -118,12 +118,22 @@ int flc_natural_decode(const uint16_t* codes, int64_t n, float weight, int accum
 size_t flc_topk_workspace_size(int64_t n, int64_t k);
 int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, void* ws,
                     size_t ws_bytes, void* stream);
+/* Tile pointers (CSR row pointers over FLC_TILE-output tiles) of an ascending index stream:
+ * tiles[t] = first j with idx[j] >= t * FLC_TILE, t = 0 .. ceil(n / FLC_TILE); the encoders' *_tiled
+ * variants emit them alongside the wire (so that a decoder needs no index pass), flc_tile_index forms
+ * them from idx alone. */
+#define FLC_TILE 1024
+int flc_tile_index(const int32_t* idx, int64_t k, int64_t n, uint32_t* tiles, void* stream);
+int flc_topk_encode_tiled(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, uint32_t* tiles,
+                          void* ws, size_t ws_bytes, void* stream);
 /* dense decode of an ascending sparse stream: out[idx[j]] = scale * val[j], zeros elsewhere
  * (compressors.py:289-291, 294-295); out = weight * v, or with accumulate out = fmaf(weight, v, out)
  * over the whole vector (the fused aggregation).  Workspace: a per-tile index of the stream. */
 size_t flc_sparse_decode_workspace_size(int64_t n);
 int flc_sparse_decode(const int32_t* idx, const float* val, int64_t k, float scale, int64_t n,
                       float weight, int accumulate, float* out, void* ws, size_t ws_bytes, void* stream);
+int flc_sparse_decode_tiled(const int32_t* idx, const float* val, int64_t k, float scale, int64_t n,
+                            float weight, int accumulate, float* out, const uint32_t* tiles, void* stream);
 
 /* ------------------------------------------------------------------ stacked top-k -> 8-bit dither
  * Top-k of x (as above), then standard dithering with s = levels (<= 127), p = inf, of the k kept
@@ -132,9 +142,15 @@ int flc_sparse_decode(const int32_t* idx, const float* val, int64_t k, float sca
 int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_t seed,
                        uint64_t counter, const double* compat_u, int32_t* idx, uint8_t* codes,
                        float* norm, void* ws, size_t ws_bytes, void* stream);
+int flc_stacked_encode_tiled(const float* x, int64_t n, int64_t k, int levels, uint64_t seed,
+                             uint64_t counter, const double* compat_u, int32_t* idx, uint8_t* codes,
+                             float* norm, uint32_t* tiles, void* ws, size_t ws_bytes, void* stream);
 int flc_stacked_decode(const int32_t* idx, const uint8_t* codes, int64_t k, int levels,
                        const float* norm, int64_t n, float weight, int accumulate, float* out,
                        void* ws, size_t ws_bytes, void* stream);  /* ws: flc_sparse_decode_workspace_size */
+int flc_stacked_decode_tiled(const int32_t* idx, const uint8_t* codes, int64_t k, int levels,
+                             const float* norm, int64_t n, float weight, int accumulate, float* out,
+                             const uint32_t* tiles, void* stream);
 
 /* ------------------------------------------------------------------ other compressors
  * identical (compressors.py:273-275): out = +x;  lazy (276-283): out = x / p (fp32 division);

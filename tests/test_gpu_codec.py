@@ -272,6 +272,49 @@ def test_sparse_decode_and_accumulate():
     np.testing.assert_array_equal(acc.cpu().numpy(), e)
 
 
+@pytest.mark.parametrize("n,k", [(1000, 10), (4096, 41), (1_000_003, 10_000), (25_000_000, 250_000)])
+def test_topk_tiles_match_index_pass_and_decode(n, k):
+    """Encoder-emitted tile pointers equal the decoder-side index pass (flc_tile_index), and the tiled
+    decode equals the untiled one bit for bit (plain and accumulating)."""
+    codec = _codec()
+    g = np.random.default_rng(n)
+    x = (g.standard_normal(n) * 1e-3).astype(np.float32)
+    xd = torch.from_numpy(x).to(DEV)
+    idx, val, tiles = codec.topk_encode(xd, k, with_tiles=True)
+    ref_tiles = torch.empty_like(tiles)
+    codec.call("flc_tile_index", codec._p(idx), k, n, codec._p(ref_tiles), codec._stream(xd.device))
+    assert torch.equal(tiles, ref_tiles)
+    t = tiles.cpu().numpy().astype(np.int64)
+    i = idx.cpu().numpy().astype(np.int64)
+    assert t[-1] == k and np.all(np.diff(t) >= 0)
+    assert np.array_equal(t[:-1], np.searchsorted(i, np.arange(len(t) - 1) * codec.TILE))
+    a = codec.sparse_decode(idx, val, n, tiles=tiles)
+    b = codec.sparse_decode(idx, val, n)
+    assert torch.equal(a, b)
+    acc_a = torch.full((n,), 0.5, device=DEV)
+    acc_b = acc_a.clone()
+    codec.sparse_decode(idx, val, n, out=acc_a, weight=0.25, accumulate=True, tiles=tiles)
+    codec.sparse_decode(idx, val, n, out=acc_b, weight=0.25, accumulate=True)
+    assert torch.equal(acc_a, acc_b)
+
+
+def test_stacked_tiled_and_untiled_decode_agree():
+    codec = _codec()
+    g = np.random.default_rng(9)
+    n, k = 3_000_017, 30_000
+    x = (g.standard_normal(n) * 1e-3).astype(np.float32)
+    x[1_000_000:1_050_000] *= 100  # dense tiles (more than 64 entries per tile)
+    xd = torch.from_numpy(x).to(DEV)
+    pkt = codec.stacked_encode(xd, k, 127, seed=4, counter=2)
+    plain = codec.StackedPacket(pkt.idx, pkt.codes, pkt.norm, pkt.n, pkt.levels, None)
+    assert torch.equal(codec.stacked_decode(pkt), codec.stacked_decode(plain))
+    acc_a = torch.full((n,), -1.0, device=DEV)
+    acc_b = acc_a.clone()
+    codec.stacked_decode(pkt, out=acc_a, weight=0.5, accumulate=True)
+    codec.stacked_decode(plain, out=acc_b, weight=0.5, accumulate=True)
+    assert torch.equal(acc_a, acc_b)
+
+
 # --------------------------------------------------------------------------------------------- stacked
 @pytest.mark.parametrize("n,k,levels", [(4096, 41, 127), (1_000_000, 10_000, 127), (25_000_000, 250_000, 127),
                                         (100_000, 1000, 7)])

@@ -27,7 +27,7 @@ enc = lambda: codec.stacked_encode(x, k, 127, 1, 0)
 print("filter us", round(probe("topk_filter", enc), 1), "select us", round(probe("stacked_select", enc), 1), "sample us", round(probe("topk_sample", enc), 1), flush=True)
 pkt = enc()
 print("stacked_decode us", round(probe("stacked_decode", lambda: codec.stacked_decode(pkt, out=out)), 1), flush=True)
-print("tile_index us", round(probe("tile_index", lambda: codec.stacked_decode(pkt, out=out)), 1), flush=True)
+print("tiles in pkt:", pkt.tiles is not None, flush=True)
 def step():
     p = codec.stacked_encode(x, k, 127, 1, 0)
     codec.stacked_decode(p, out=out)
