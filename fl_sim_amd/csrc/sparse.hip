@@ -322,11 +322,21 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
                                                                     const float* __restrict__ norm_ptr, int64_t n,
                                                                     float weight, float* __restrict__ out,
                                                                     const unsigned* __restrict__ tile_start,
-                                                                    int64_t ntiles) {
+                                                                    int64_t ntiles, int64_t chunk) {
   constexpr int TILE = 1024;
   __shared__ __attribute__((aligned(16))) float s_tile[NT * TILE];
   const int lane = threadIdx.x;
-  const int64_t tb = (int64_t)blockIdx.x * NT;
+  // XCD-chunked order: the dispatcher deals workgroups round-robin to the 8 XCDs; within every run of
+  // 8 chunks, XCD x takes chunk x, so each XCD writes whole contiguous chunks (chunk = 0: plain order)
+  int64_t g = blockIdx.x;
+  if (chunk > 0) {
+    const int64_t sup = 8 * chunk, full = (int64_t)gridDim.x / sup * sup;
+    if (g < full) {
+      const int64_t x = g & 7, j = g >> 3;
+      g = (j / chunk) * sup + x * chunk + (j % chunk);
+    }
+  }
+  const int64_t tb = g * NT;
   const int64_t t0 = tb * TILE;
   unsigned ts[NT + 1];
 #pragma unroll
@@ -617,6 +627,11 @@ int launch_decode_wave(const int32_t* idx, const float* val, const uint8_t* code
   return FLC_OK;
 }
 
+int64_t decode_chunk() {  // calibration knob FLC_DECODE_CHUNK (workgroups per XCD chunk; 0: plain order)
+  const char* e = getenv("FLC_DECODE_CHUNK");
+  return e ? atoll(e) : 0;
+}
+
 // decode over given 1024-output tile pointers (no tile_index pass): one wave per two tiles, or, when
 // accumulating, one wave per tile (its slice of `out` read first)
 template <int MODE>
@@ -631,7 +646,7 @@ int launch_decode_tiles(const int32_t* idx, const float* val, const uint8_t* cod
                codes, scale, levels, step, norm, n, weight, out, tile_start, 0);
   else
     FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, 2>), dim3((unsigned)cdiv(ntiles, 2)), dim3(kWave), 0, st, idx,
-               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles);
+               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, decode_chunk());
   return FLC_OK;
 }
 
@@ -651,7 +666,7 @@ int launch_decode_wave2(const int32_t* idx, const float* val, const uint8_t* cod
              (long long)ntiles, tile_start);
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, NT>), dim3((unsigned)cdiv(ntiles, NT)), dim3(kWave), 0, st, idx,
-             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles);
+             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, decode_chunk());
   return FLC_OK;
 }
 
