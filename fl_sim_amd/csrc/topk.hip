@@ -980,28 +980,35 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   pick_digit(w, cur, A_cur, maxkey, s_ghist, &s_err, s_red);
   STAMP(7);
   unsigned long long pre = 0, tot = 0;
-  bool counted = false;
+  bool counted = false, wave_counted = false;
+  // the compaction's wave ranges: wave `wid` owns candidates [cq0, cq1) of this block
+  const unsigned cQ = ((ncand + kENW - 1) / kENW + kWave - 1) / kWave * kWave;
+  const unsigned cq0 = (unsigned)wid * cQ < ncand ? (unsigned)wid * cQ : ncand;
+  const unsigned cq1 = cq0 + cQ < ncand ? cq0 + cQ : ncand;
+  __shared__ unsigned long long s_wcnt[kENW];  // per wave range: strict << 32 | ties
   if (!fb && cur.narrowed && slot == 0) {
     // ---- in-bin exchange: every block publishes its candidates inside the chosen bin (~3 per block at
     // the headline) and its count of candidates above the bin; one exchange later every block resolves T
     // among those keys and forms its own prefix locally: no second histogram round and no separate
     // count exchange.  Falls through to the histogram rounds if any list overflows.
     __shared__ unsigned s_nl;
+    __shared__ unsigned s_mykey[kInbin], s_mywv[kInbin];
     if (tid == 0) s_nl = 0u;
     __syncthreads();
     const unsigned lo0 = cur.lo;
     const unsigned long long wd0 = cur.width;
     unsigned* my_list = w.inbin() + (size_t)blockIdx.x * kInbin;
-    unsigned gtc = 0;
-    const unsigned pend = (ncand + kET - 1) / kET * kET;
-    for (unsigned p0 = 0; p0 < pend; p0 += kET) {
-      const unsigned p = p0 + tid;
+    // scanned in the compaction's wave ranges: the count above the bin per wave range plus the wave of
+    // each of my in-bin keys give the compaction its per-wave strict / tie counts once T is known
+    unsigned gtw = 0;
+    for (unsigned p0 = cq0; p0 < cq1; p0 += kWave) {
+      const unsigned p = p0 + lane;
       unsigned raw = 0, id = 0;
-      if (p < ncand) cand_get(src, p, raw, id);
+      if (p < cq1) cand_get(src, p, raw, id);
       const unsigned key = order_key(raw);
       const unsigned long long rel = (unsigned long long)key - lo0;
-      const bool valid = p < ncand && key >= lo0 && key >= t_lo;  // (x-mode: below the floor never counts)
-      gtc += (valid && rel >= wd0) ? 1u : 0u;
+      const bool valid = p < cq1 && key >= lo0 && key >= t_lo;  // (x-mode: below the floor never counts)
+      gtw += (unsigned)__popcll(__ballot(valid && rel >= wd0));
       const bool f = valid && rel < wd0;
       const unsigned long long bm = __ballot(f);
       if (bm) {
@@ -1009,12 +1016,20 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
         if (lane == 0) base_l = atomicAdd(&s_nl, (unsigned)__popcll(bm));
         base_l = __shfl(base_l, 0, kWave);
         const unsigned q = base_l + __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
-        if (f && q < (unsigned)kInbin)  // write-through: read by other XCDs after the exchange
+        if (f && q < (unsigned)kInbin) {  // write-through: read by other XCDs after the exchange
           __hip_atomic_store(my_list + q, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_mykey[q] = key;
+          s_mywv[q] = (unsigned)wid;
+        }
       }
     }
-    const unsigned long long gt = block_sum<unsigned long long, kENW>((unsigned long long)gtc, s_red);
-    if (tid == 0) st_mem64(&w.blk_cnt()[blockIdx.x], ((unsigned long long)s_nl << 32) | (gt & 0xffffffffull));
+    if (lane == 0) s_wcnt[wid] = (unsigned long long)gtw << 32;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long gt = 0;
+      for (int v2 = 0; v2 < kENW; ++v2) gt += s_wcnt[v2] >> 32;
+      st_mem64(&w.blk_cnt()[blockIdx.x], ((unsigned long long)s_nl << 32) | (gt & 0xffffffffull));
+    }
     STAMP(8);
     exchange(w, ++ep);
     STAMP(9);
@@ -1129,6 +1144,12 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
         pre = ((sums[2] + P_s) << 32) | P_t;
         tot = ((sums[1] + A_s) << 32) | A_t;
         counted = true;
+        // (T0 >= t_lo: every key > T0 or == T0 passed the floor test of the scan above)
+        if (T0 >= t_lo && tid < (int)s_nl) {
+          const unsigned key = s_mykey[tid];
+          atomicAdd(&s_wcnt[s_mywv[tid]], (key > T0 ? (1ull << 32) : 0ull) + (key == T0 ? 1ull : 0ull));
+        }
+        wave_counted = T0 >= t_lo;
       }
     }
     __syncthreads();
@@ -1241,26 +1262,25 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   const int ntl = (int)((b1 - b0 + kTile - 1) / kTile);
   if (tiled)
     for (int i = tid; i < ntl; i += kET) s_hh[i] = 0u;
-  const unsigned Q = ((ncand + kENW - 1) / kENW + kWave - 1) / kWave * kWave;
-  const unsigned q0 = (unsigned)wid * Q < ncand ? (unsigned)wid * Q : ncand;
-  const unsigned q1 = q0 + Q < ncand ? q0 + Q : ncand;
-  // pass 1: this wave's strict / tie counts
-  unsigned ws = 0, wt = 0;
-  for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
-    const unsigned p = p0 + lane;
-    unsigned raw = 0, id = 0;
-    if (p < q1) cand_get(src, p, raw, id);
-    const unsigned key = order_key(raw);
-    ws += __popcll(__ballot(p < q1 && key > T));
-    wt += __popcll(__ballot(p < q1 && key == T));
+  const unsigned q0 = cq0, q1 = cq1;
+  if (!wave_counted) {  // pass 1: this wave's strict / tie counts (the in-bin path counted them already)
+    unsigned ws = 0, wt = 0;
+    for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
+      const unsigned p = p0 + lane;
+      unsigned raw = 0, id = 0;
+      if (p < q1) cand_get(src, p, raw, id);
+      const unsigned key = order_key(raw);
+      ws += __popcll(__ballot(p < q1 && key > T));
+      wt += __popcll(__ballot(p < q1 && key == T));
+    }
+    __syncthreads();
+    if (lane == 0) s_wcnt[wid] = ((unsigned long long)ws << 32) | wt;
   }
-  __syncthreads();
-  if (lane == 0) s_red[wid] = ((unsigned long long)ws << 32) | wt;
   __syncthreads();
   long long s_before = (long long)(pre >> 32), t_before = (long long)(pre & 0xffffffffull);
   for (int v2 = 0; v2 < wid; ++v2) {
-    s_before += (long long)(s_red[v2] >> 32);
-    t_before += (long long)(s_red[v2] & 0xffffffffull);
+    s_before += (long long)(s_wcnt[v2] >> 32);
+    t_before += (long long)(s_wcnt[v2] & 0xffffffffull);
   }
   // pass 2: keep decisions and the writes
   for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
