@@ -183,6 +183,23 @@ def main():
             "algorithmic_bytes": kernel_bytes.get(args.probe),
         }
     extra = {}
+    if probe_ms:
+        # every kernel of the step, each timed live (HIP events on its launch stream) over its own short run
+        kernels = {}
+        for name in ("topk_sample", "topk_filter", "stacked_select", "stacked_decode"):
+            _, kms = timed(step, 5, 1, world, probe=name)
+            if kms:
+                kernels[name] = round(kms * 1e3, 1)
+        extra["kernels_us"] = kernels
+        if kernels.get("stacked_decode"):
+            dms = kernels["stacked_decode"] * 1e-3
+            ach_d = kernel_bytes["stacked_decode"] / (dms * 1e-3) / 1e9
+            extra["roofline_decode"] = {
+                "kernel": "stacked_decode", "bound": "hbm", "achieved": round(ach_d, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach_d / HBM_PEAK_GBS, 4),
+                "traffic": (traffic_from_profiles().get("stacked_decode") or {}).get("bytes"),
+                "algorithmic_bytes": kernel_bytes["stacked_decode"],
+            }
     if not args.skip_extra:
         # host-resident path (north_star: client state lives on the CPU simulator): pinned host delta ->
         # H2D -> encode + decode -> D2H of the dense decoded vector; PCIe-bound, never `value`
@@ -247,9 +264,9 @@ def main():
         X3 = torch.randn(d3, generator=gen, device=dev) * 1e-3
         o3 = torch.empty(d3, dtype=torch.float32, device=dev)
 
-        def step3():
-            idx, val = codec.topk_encode(X3, k3)
-            codec.sparse_decode(idx, val, d3, out=o3)
+        def step3():  # the TopK compressor's path: encoder-emitted tile pointers, decode without an index pass
+            idx, val, tiles = codec.topk_encode(X3, k3, with_tiles=True)
+            codec.sparse_decode(idx, val, d3, out=o3, tiles=tiles)
 
         ms3, _ = timed(step3, 20, 5, world)
         ms3 = max_over_ranks(ms3, world)

@@ -15,6 +15,11 @@ from collections import defaultdict
 SHORT = {
     "topk_filter_kernel": "topk_filter",
     "sparse_decode_kernel<1": "stacked_decode",
+    "sparse_decode_wave2_kernel<1": "stacked_decode",
+    "sparse_decode_wave_kernel<1": "stacked_decode",
+    "sparse_decode_wave2_kernel<0": "sparse_decode",
+    "sparse_decode_wave_kernel<0": "sparse_decode",
+    "topk_sample_kernel": "topk_sample",
     "sparse_decode_kernel<0": "sparse_decode",
     "topk_select_kernel<true>": "stacked_select",
     "topk_select_kernel<false>": "topk_select",
