@@ -1352,11 +1352,18 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-// one select launch per device at a time: launches on different streams are ordered with an event
-// chain (stream-ordered, no host blocking), so two never compete for co-residency
+// one select launch per device at a time, so two never compete for co-residency.  While every call
+// comes on one stream, stream order is the guarantee and nothing is added (an event record after the
+// select costs the next kernel ~4 us of dispatch gap).  The first call on a second stream drains the
+// device once (the earlier stream may be gone by now, so nothing is recorded on it), and from then on
+// selects are chained with an event recorded after each one (stream-ordered, no host blocking).
 struct SelectGate {
   std::mutex mu;
   hipEvent_t last[64] = {};
+  hipStream_t first[64] = {};
+  bool used[64] = {};
+  bool multi[64] = {};
+  bool recorded[64] = {};
   int cus[64] = {};
 };
 SelectGate& gate() {
@@ -1404,15 +1411,25 @@ int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes,
   FLC_CHECK_HIP(hipStreamIsCapturing(st, &cs));
   const bool gated = cs == hipStreamCaptureStatusNone;
   if (gated) {
-    if (!gt.last[dev]) FLC_CHECK_HIP(hipEventCreateWithFlags(&gt.last[dev], hipEventDisableTiming));
-    else FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
+    if (!gt.used[dev]) {
+      gt.used[dev] = true;
+      gt.first[dev] = st;
+    } else if (!gt.multi[dev] && st != gt.first[dev]) {
+      FLC_CHECK_HIP(hipDeviceSynchronize());
+      if (!gt.last[dev]) FLC_CHECK_HIP(hipEventCreateWithFlags(&gt.last[dev], hipEventDisableTiming));
+      gt.multi[dev] = true;
+    }
+    if (gt.multi[dev] && gt.recorded[dev]) FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
   }
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   const bool in_kernel_tiles = tiles && g.M / kTile <= 2 * kHistBins;
   FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", topk_select_kernel<STACKED>, dim3((unsigned)g.G), dim3(kET),
              0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
              in_kernel_tiles ? tiles : nullptr);
-  if (gated) FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
+  if (gated && gt.multi[dev]) {
+    FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
+    gt.recorded[dev] = true;
+  }
   if (tiles && !in_kernel_tiles) return flc_tile_index(idx, k, n, tiles, st);
   return FLC_OK;
 }

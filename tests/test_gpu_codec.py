@@ -358,3 +358,25 @@ def test_stacked_full_size_1gib_properties():
     assert bool(((lv * 127 - torch.floor(y * 127)).abs() <= 1.0001).all())
     del x, masked, out
     torch.cuda.empty_cache()
+
+
+def test_stacked_encode_two_streams():
+    """Selects on two streams at once (each with its own workspace) are serialised by the library's gate
+    (first switch drains the device, then an event chain); results equal the single-stream ones."""
+    codec = _codec()
+    n, k = 3_000_000, 30_000
+    gen = torch.Generator(device=DEV).manual_seed(77)
+    xs = [torch.randn(n, generator=gen, device=DEV) * 1e-3 for _ in range(4)]
+    refs = [codec.stacked_encode(x, k, 127, seed=5, counter=i) for i, x in enumerate(xs)]
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    got = [None] * 8
+    for r in range(2):
+        for i, x in enumerate(xs):
+            with torch.cuda.stream(s1 if (i + r) % 2 == 0 else s2):
+                got[4 * r + i] = codec.stacked_encode(x, k, 127, seed=5, counter=i)
+    torch.cuda.synchronize()
+    for j, p in enumerate(got):
+        e = refs[j % 4]
+        assert torch.equal(p.idx, e.idx) and torch.equal(p.codes, e.codes) and torch.equal(p.norm, e.norm)
+        assert torch.equal(p.tiles, e.tiles)
