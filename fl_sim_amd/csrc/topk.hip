@@ -168,7 +168,7 @@ constexpr int kZeroWords = kMaxSlots * kHistStride + 16;  // hist + acc, as 32-b
 // its bins, and the thread holding rank r[j] writes digit[j] / new_rem[j].  (A wave-wide select reading
 // 32 bins per lane at a 128-B lane stride hits one bank 64 ways.)
 template <int NR>
-__device__ void block_select_from_top(const unsigned* h, const long long (&r)[NR], unsigned* digit,
+__device__ __forceinline__ void block_select_from_top(const unsigned* h, const long long (&r)[NR], unsigned* digit,
                                       long long* new_rem, unsigned* err, unsigned long long* s_red) {
   constexpr int BPT = kHistBins / kET;  // bins per thread, highest first
   static_assert(BPT * kET == kHistBins, "bins per thread");
@@ -540,7 +540,7 @@ __device__ __forceinline__ void step_process(const float4 (&v)[kStepF4], int64_t
 // `ep` (packed flags, one word per block), then one wave polls all G flags (each lane a few words per
 // round, relaxed agent-scope loads, a wave-wide vote, sleep between rounds).  No leader and no
 // contended counter: 256 arrivals on ONE word serialise at the memory-side atomic unit (measured ~5 us).
-__device__ void exchange(const EncWs& w, unsigned ep) {
+__device__ __forceinline__ void exchange(const EncWs& w, unsigned ep) {
   drain_stores();
   __syncthreads();
   const int tid = threadIdx.x;
@@ -597,25 +597,26 @@ __device__ __forceinline__ void load_hist(const EncWs& w, int r, unsigned* s_ghi
 // the k-th largest key among keys >= lo, so it stays k; the round's `A` keys above the live range
 // come first: if A >= rem the key lies above the range (re-range to [lo + width, max + 1)), otherwise
 // pick the bin of rank rem - A and narrow to it.
-__device__ void pick_digit(const EncWs& w, SelState& cur, long long A, unsigned maxkey, const unsigned* s_ghist,
+__device__ __forceinline__ void pick_digit(const EncWs& w, SelState& cur, long long A, unsigned maxkey, const unsigned* s_ghist,
                            unsigned* s_err, unsigned long long* s_red) {
   __shared__ unsigned s_digit;
   __shared__ long long s_rem;
   if (threadIdx.x == 0) *s_err = 0;
   __syncthreads();
-  SelState nx = cur;
-  nx.narrowed = 0;
+  // (the new state is written field by field by thread 0: a whole-struct copy lands in scratch)
   if (A >= cur.rem) {  // the k-th largest key is above the range (block-uniform branch)
     const unsigned long long nlo = (unsigned long long)cur.lo + cur.width;
     const unsigned long long top = (unsigned long long)maxkey + 1ull;
     const unsigned long long nw = top > nlo ? top - nlo : 0ull;
     if (nw == 0ull && threadIdx.x == 0)
       __hip_atomic_fetch_or(&w.st()->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    nx.lo = (unsigned)nlo;
-    nx.width = nw ? nw : 1ull;
-    nx.shift = range_shift(nx.width, kHistBits);
     __syncthreads();
-    if (threadIdx.x == 0) cur = nx;
+    if (threadIdx.x == 0) {
+      cur.narrowed = 0;
+      cur.lo = (unsigned)nlo;
+      cur.width = nw ? nw : 1ull;
+      cur.shift = range_shift(nw ? nw : 1ull, kHistBits);
+    }
     __syncthreads();
     return;
   }
@@ -627,19 +628,22 @@ __device__ void pick_digit(const EncWs& w, SelState& cur, long long A, unsigned 
   const long long rr = s_rem;
   if (*s_err && threadIdx.x == 0) __hip_atomic_fetch_or(&w.st()->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned nlo = cur.lo + (d << cur.shift);
-  if (cur.shift == 0) {
-    nx.T = nlo;
-    nx.need = rr;
-    nx.done = 1;
-  } else {
-    nx.lo = nlo;
-    nx.width = 1ull << cur.shift;
-    nx.shift = range_shift(nx.width, kHistBits);
-    nx.narrowed = 1;
-    nx.need = rr;
-  }
+  const int csh = cur.shift;
   __syncthreads();  // every thread has read cur, s_digit, s_rem
-  if (threadIdx.x == 0) cur = nx;
+  if (threadIdx.x == 0) {
+    cur.narrowed = 0;
+    if (csh == 0) {
+      cur.T = nlo;
+      cur.need = rr;
+      cur.done = 1;
+    } else {
+      cur.lo = nlo;
+      cur.width = 1ull << csh;
+      cur.shift = range_shift(1ull << csh, kHistBits);
+      cur.narrowed = 1;
+      cur.need = rr;
+    }
+  }
   __syncthreads();
 }
 
@@ -663,19 +667,24 @@ __device__ __forceinline__ void cand_get(const CandSrc& c, unsigned p, unsigned&
 }
 
 #ifdef FLC_SELECT_STAMPS
-// phase stamps of block 0, kept in LDS and written out at the end (slots: filter kernel 0-3, select
-// kernel 4-15; s_memrealtime, 100 MHz)
+// phase stamps of block 0, kept in LDS and written out at the end (slots: filter 0-4, select 5-15;
+// s_memrealtime, 100 MHz)
+__device__ __forceinline__ unsigned long long* stamp_lds() {
+  __shared__ unsigned long long s_stamp[16];
+  return s_stamp;
+}
 #define STAMP(i)                                                                                 \
   do {                                                                                           \
-    if (blockIdx.x == 0 && threadIdx.x == 0) s_stamp[i] = __builtin_amdgcn_s_memrealtime();      \
+    if (blockIdx.x == 0 && threadIdx.x == 0) stamp_lds()[i] = __builtin_amdgcn_s_memrealtime();  \
   } while (0)
 #define STAMP_INIT()                                                                             \
-  __shared__ unsigned long long s_stamp[16];                                                     \
-  if (threadIdx.x < 16) s_stamp[threadIdx.x] = 0ull;                                             \
-  __syncthreads()
+  do {                                                                                           \
+    if (threadIdx.x < 16) stamp_lds()[threadIdx.x] = 0ull;                                       \
+    __syncthreads();                                                                             \
+  } while (0)
 #define STAMP_OUT(lo, hi)                                                                        \
   if (blockIdx.x == 0 && (int)threadIdx.x >= (lo) && (int)threadIdx.x < (hi))                    \
-  w.stamps()[threadIdx.x] = s_stamp[threadIdx.x]
+  w.stamps()[threadIdx.x] = stamp_lds()[threadIdx.x]
 #define BLKT(i)                                                                                  \
   do {                                                                                           \
     if (threadIdx.x == 0) w.blkt()[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();     \
@@ -700,17 +709,22 @@ __global__ __launch_bounds__(256) void topk_sample_kernel(const float* __restric
 // ------------------------------------------------------------------------------------------------
 // filter kernel: floor / ceiling from the sample, the HBM pass, staging + round-0 histogram
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restrict__ x, int64_t n, EncWs w, int S,
-                                                          long long rank_lo, long long rank_hi, int take_all) {
-  __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
-  __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
-  __shared__ unsigned s_hist[kHistBins];
-  __shared__ unsigned s_wc[2][kENW];
-  __shared__ unsigned long long s_red[kENW];
-  __shared__ unsigned s_mx[kENW];
+struct FilterOut {
+  unsigned C_b;            // candidates of this block (<= kCap of them in s_key / s_idx)
+  unsigned t_lo;           // floor key
+  unsigned long long t_hi; // ceiling key (exclusive)
+};
+
+// floor / ceiling from the sample, the HBM pass into the block's LDS candidate arrays, the round-0 band
+// histogram and counts; STAGE: also the staging copy of the candidates for a separate select kernel
+template <bool STAGE>
+__device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, int64_t n, const EncWs& w, int S,
+                                                  long long rank_lo, long long rank_hi, int take_all,
+                                                  unsigned* s_key, unsigned* s_idx, unsigned* s_hist,
+                                                  unsigned (&s_wc)[2][kENW], unsigned long long* s_red,
+                                                  unsigned* s_mx) {
   SampleLds& SL = *reinterpret_cast<SampleLds*>(s_key);  // the sample phase precedes every candidate write
   static_assert(sizeof(SampleLds) <= sizeof(unsigned) * kCap, "sample scratch must fit the key array");
-  STAMP_INIT();
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * w.M;
   const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
@@ -818,8 +832,8 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
     __syncthreads();
   }
 
-  // ---- staging (16-B stores) and the round-0 histogram / counts
-  {
+  // ---- staging (16-B stores; split path only) and the round-0 histogram / counts
+  if (STAGE) {
     const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
     uint4* dk = reinterpret_cast<uint4*>(w.stage_key(blockIdx.x));
     uint4* di = reinterpret_cast<uint4*>(w.stage_idx(blockIdx.x));
@@ -843,22 +857,42 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
     if (ab) atomicAdd(&h[kHistBins], (unsigned)ab);
     atomicMax(&h[kHistBins + 1], m);
     atomicAdd(&w.acc()[0], (unsigned long long)C_b);
-    w.blk_c()[blockIdx.x] = C_b;
+    if (STAGE) w.blk_c()[blockIdx.x] = C_b;
   }
   STAMP(4);
   BLKT(2);
+  FilterOut o;
+  o.C_b = C_b;
+  o.t_lo = t_lo;
+  o.t_hi = t_hi;
+  return o;
+}
+
+__global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restrict__ x, int64_t n, EncWs w, int S,
+                                                          long long rank_lo, long long rank_hi, int take_all) {
+  __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
+  __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
+  __shared__ unsigned s_hist[kHistBins];
+  __shared__ unsigned s_wc[2][kENW];
+  __shared__ unsigned long long s_red[kENW];
+  __shared__ unsigned s_mx[kENW];
+  STAMP_INIT();
+  (void)filter_phase<true>(x, n, w, S, rank_lo, rank_hi, take_all, s_key, s_idx, s_hist, s_wc, s_red, s_mx);
   STAMP_OUT(0, 5);
 }
 
 // ------------------------------------------------------------------------------------------------
 // select kernel: the k-th largest key, the block offsets, the ordered compaction
 // ------------------------------------------------------------------------------------------------
-template <bool STACKED>
+// FUSED: the filter phase runs first in the same kernel (one exchange after it): the candidates stay in
+// LDS, so the staging round trip through HBM and a kernel boundary are gone
+template <bool STACKED, bool FUSED>
 __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restrict__ x, int64_t n, long long k, EncWs w,
                                                           int* __restrict__ idx_out, float* __restrict__ val_out,
                                                           uint8_t* __restrict__ code_out, float* __restrict__ norm_out,
                                                           int levels, double step, uint64_t seed, uint64_t counter,
-                                                          unsigned* __restrict__ tile_out) {
+                                                          unsigned* __restrict__ tile_out, int S, long long rank_lo,
+                                                          long long rank_hi, int take_all) {
   __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
   __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
   __shared__ unsigned s_hh[2 * kHistBins];  // the round / global histograms; in the compaction: tile counts
@@ -875,32 +909,49 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * w.M;
   const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
-  STAMP(5);
-
-  // ---- one batch of loads: this block's candidates (staging), the round-0 histogram and counts
   unsigned* hist = w.hist();
-  const unsigned C_b = w.blk_c()[blockIdx.x];
-  const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
-  {
-    const uint4* sk = reinterpret_cast<const uint4*>(w.stage_key(blockIdx.x));
-    const uint4* si = reinterpret_cast<const uint4*>(w.stage_idx(blockIdx.x));
-    uint4* dk = reinterpret_cast<uint4*>(s_key);
-    uint4* di = reinterpret_cast<uint4*>(s_idx);
-    for (unsigned q = tid; q < (nst + 3u) / 4u; q += kET) {
-      dk[q] = sk[q];
-      di[q] = si[q];
+  unsigned C_b;
+  unsigned ep;
+  if (FUSED) {
+    __shared__ unsigned s_wc[2][kENW];
+    if (tid == 0) s_glob[2] = ld_mem64(&w.st()->call);  // (read before any exchange of this call)
+    const FilterOut fo =
+        filter_phase<false>(x, n, w, S, rank_lo, rank_hi, take_all, s_key, s_idx, s_hist, s_wc, s_red, s_mx);
+    C_b = fo.C_b;
+    if (tid == 0) {
+      s_glob[0] = fo.t_lo;
+      s_glob[1] = fo.t_hi;
     }
-  }
-  if (tid == 0) {
-    s_glob[0] = w.st()->t_lo;
-    s_glob[1] = w.st()->t_hi;
-    s_glob[2] = ld_mem64(&w.st()->call);
+    ep = (unsigned)s_glob[2] * kEpochStride;  // (s_glob[2] was written before the filter's barriers)
+    exchange(w, ++ep);  // every block's round-0 histogram, counts and max key are in
+    STAMP(5);
+  } else {
+    // ---- one batch of loads: this block's candidates (staging), the round-0 histogram and counts
+    STAMP(5);
+    C_b = w.blk_c()[blockIdx.x];
+    const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
+    {
+      const uint4* sk = reinterpret_cast<const uint4*>(w.stage_key(blockIdx.x));
+      const uint4* si = reinterpret_cast<const uint4*>(w.stage_idx(blockIdx.x));
+      uint4* dk = reinterpret_cast<uint4*>(s_key);
+      uint4* di = reinterpret_cast<uint4*>(s_idx);
+      for (unsigned q = tid; q < (nst + 3u) / 4u; q += kET) {
+        dk[q] = sk[q];
+        di[q] = si[q];
+      }
+    }
+    if (tid == 0) {
+      s_glob[0] = w.st()->t_lo;
+      s_glob[1] = w.st()->t_hi;
+      s_glob[2] = ld_mem64(&w.st()->call);
+    }
+    ep = 0;  // set below, after the barrier
   }
   load_hist(w, 0, s_ghist, s_ex, true);  // (ends in a barrier)
   const unsigned t_lo = (unsigned)s_glob[0];
   const unsigned long long t_hi = s_glob[1];
   const unsigned call = (unsigned)s_glob[2];
-  unsigned ep = call * kEpochStride;
+  if (!FUSED) ep = call * kEpochStride;
   const unsigned long long C_tot = s_ex[2];
   const bool fb = (long long)C_tot < k;  // grid-uniform
   unsigned maxkey = (unsigned)s_ex[1];
@@ -1346,7 +1397,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     if (blockIdx.x == gridDim.x - 1 && tid == 0) tile_out[cdiv_dev(n, kTile)] = (unsigned)k;
   }
   STAMP(14);
-  STAMP_OUT(5, 16);
+  STAMP_OUT(FUSED ? 0 : 5, 16);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1403,8 +1454,10 @@ int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes,
   const SampleSetup ss = sample_setup(n, k);
   if (!ss.take_all)
     FLC_LAUNCH("topk_sample", topk_sample_kernel, dim3((unsigned)cdiv(ss.S, 256)), dim3(256), 0, st, x, n, ss.S, w);
-  FLC_LAUNCH("topk_filter", topk_filter_kernel, dim3((unsigned)g.G), dim3(kET), 0, st, x, n, w, ss.S, ss.rank_lo,
-             ss.rank_hi, ss.take_all);
+  static const bool split = getenv("FLC_TOPK_SPLIT") && atoi(getenv("FLC_TOPK_SPLIT")) != 0;  // calibration
+  if (split)
+    FLC_LAUNCH("topk_filter", topk_filter_kernel, dim3((unsigned)g.G), dim3(kET), 0, st, x, n, w, ss.S, ss.rank_lo,
+               ss.rank_hi, ss.take_all);
   SelectGate& gt = gate();
   std::lock_guard<std::mutex> lk(gt.mu);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1423,9 +1476,14 @@ int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes,
   }
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   const bool in_kernel_tiles = tiles && g.M / kTile <= 2 * kHistBins;
-  FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", topk_select_kernel<STACKED>, dim3((unsigned)g.G), dim3(kET),
-             0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
-             in_kernel_tiles ? tiles : nullptr);
+  if (split)
+    FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", (topk_select_kernel<STACKED, false>), dim3((unsigned)g.G),
+               dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
+               in_kernel_tiles ? tiles : nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
+  else
+    FLC_LAUNCH(STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true>), dim3((unsigned)g.G),
+               dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
+               in_kernel_tiles ? tiles : nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
   if (gated && gt.multi[dev]) {
     FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
     gt.recorded[dev] = true;

@@ -24,7 +24,8 @@ k = n // 100
 x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 1e-3
 out = torch.empty_like(x)
 enc = lambda: codec.stacked_encode(x, k, 127, 1, 0)
-print("filter us", round(probe("topk_filter", enc), 1), "select us", round(probe("stacked_select", enc), 1), "sample us", round(probe("topk_sample", enc), 1), flush=True)
+print("filter us", round(probe("topk_filter", enc), 1), "select us", round(probe("stacked_select", enc), 1),
+      "fused us", round(probe("stacked_encode", enc), 1), "sample us", round(probe("topk_sample", enc), 1), flush=True)
 pkt = enc()
 print("stacked_decode us", round(probe("stacked_decode", lambda: codec.stacked_decode(pkt, out=out)), 1), flush=True)
 print("tiles in pkt:", pkt.tiles is not None, flush=True)

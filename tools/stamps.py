@@ -1,8 +1,9 @@
 """Phase stamps of the persistent encode (diagnostic build: make EXTRA=-DFLC_SELECT_STAMPS, block 0 only).
 
-Stamp slots (s_memrealtime, 100 MHz): filter kernel 0 start, 1 floor/ceiling, 2 HBM pass done, 3 staged +
-flushed; select kernel 4 start, 5 loads done, 6 pick, 7 in-bin lists published, 8 exchanged, 9 T and
-offsets resolved, 10 counts, 11 compaction done.
+Stamp slots (s_memrealtime, 100 MHz): 0 start, 2 floor/ceiling, 3 HBM pass done, 4 histogram flushed
+(split path: staged); 5 select start (fused default: after the exchange that follows the filter phase),
+6 loads done, 7 pick, 8 in-bin lists published, 9 exchanged, 10 list gathered, 11 T resolved, 12 sums,
+13 counts, 14 compaction done.  FLC_TOPK_SPLIT=1 times the two-kernel path instead.
 """
 import os
 import sys
