@@ -284,15 +284,32 @@ struct SampleLds {
 // sample index of a thread's key slot i: 16-B runs, so the coherent read is 8 x 16 B per thread
 __device__ __forceinline__ int sample_j(int i) { return 4 * (int)threadIdx.x + 4 * kET * (i >> 2) + (i & 3); }
 
+// a thread's kSPT sample keys (coherent-enough plain loads: the sample kernel finished before this one)
+__device__ __forceinline__ void load_sample_keys(const unsigned* sample, int S, unsigned (&keys)[kSPT]) {
+  if (S == kSample) {  // all eight 16-B groups in flight together
+    uint4 t[kSPT / 4];
+#pragma unroll
+    for (int i = 0; i < kSPT; i += 4) t[i / 4] = *reinterpret_cast<const uint4*>(sample + sample_j(i));
+#pragma unroll
+    for (int i = 0; i < kSPT; i += 4) {
+      keys[i] = t[i / 4].x; keys[i + 1] = t[i / 4].y; keys[i + 2] = t[i / 4].z; keys[i + 3] = t[i / 4].w;
+    }
+  } else {  // small n: S = n keys
+#pragma unroll
+    for (int i = 0; i < kSPT; ++i) keys[i] = sample_j(i) < S ? sample[sample_j(i)] : 0u;  // 0: below every key
+  }
+}
+
 // Fast path (rank_lo <= kET): B = the smallest lane maximum, so at least kET >= rank_lo sample keys are
 // >= B (one per lane); typically B sits near the 80th percentile.  An 11-bit histogram of the keys in
 // [B, max] (plain LDS atomics, from registers) locates the bins of ranks rank_lo and rank_hi; a target
 // bin holding more than a few sample keys (clustered values, ties) is refined by a second pass inside
 // it.  The floor is the floor of rank_lo's bin (>= rank_lo sample keys at or above it) and the ceiling
 // the end of rank_hi's bin (fewer than rank_hi sample keys at or above it).
-__device__ __forceinline__ bool sample_fast(const unsigned (&keys)[kSPT], int S, long long rank_lo, long long rank_hi,
-                                            SampleLds& L, unsigned* s_hist, unsigned long long* s_red,
-                                            unsigned* t_lo_out, unsigned long long* t_hi_out) {
+// Two halves: the histogram (the keys' last use in registers: the caller issues the second HBM step
+// in their place) and the pick (the rare refinement re-reads the keys).
+__device__ __forceinline__ void sample_fast_hist(const unsigned (&keys)[kSPT], int S, SampleLds& L, unsigned* s_hist,
+                                                 unsigned* B_out, int* sh_out) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   unsigned m = 0;
 #pragma unroll
@@ -324,6 +341,15 @@ __device__ __forceinline__ bool sample_fast(const unsigned (&keys)[kSPT], int S,
 #pragma unroll
   for (int i = 0; i < kSPT; ++i)
     if (sample_j(i) < S && keys[i] >= B) atomicAdd(&s_hist[(keys[i] - B) >> sh], 1u);
+  *B_out = B;
+  *sh_out = sh;
+}
+
+__device__ __forceinline__ bool sample_fast_pick(const unsigned* sample, int S, long long rank_lo, long long rank_hi,
+                                                 unsigned B, int sh, SampleLds& L, unsigned* s_hist,
+                                                 unsigned long long* s_red, unsigned* t_lo_out,
+                                                 unsigned long long* t_hi_out) {
+  const int tid = threadIdx.x;
   __syncthreads();
   const bool two = rank_hi > 0;
   const long long rk[2] = {rank_lo, two ? rank_hi : 0};
@@ -331,9 +357,11 @@ __device__ __forceinline__ bool sample_fast(const unsigned (&keys)[kSPT], int S,
   if (L.err) return false;  // block-uniform
   const unsigned d0 = L.digit[0], d1 = two ? L.digit[1] : 0u;
   unsigned lo0 = B + (d0 << sh), lo1 = B + (d1 << sh);
-  int sh_lo = sh, sh_hi = sh;
+  int sh_hi = sh;
   const bool ref0 = sh > 0 && s_hist[d0] > 8u, ref1 = two && sh > 0 && s_hist[d1] > 8u;  // block-uniform
   if (ref0 || ref1) {
+    unsigned keys[kSPT];
+    load_sample_keys(sample, S, keys);
     const long long r0 = L.rem[0], r1 = two ? L.rem[1] : 0;
     const int sh2 = sh > kHistBits ? sh - kHistBits : 0;
     const unsigned long long bw = 1ull << sh;
@@ -352,17 +380,29 @@ __device__ __forceinline__ bool sample_fast(const unsigned (&keys)[kSPT], int S,
     block_select_from_top<1>(s_hist, ra, &L.digit[0], &L.rem[0], &L.err, s_red);
     block_select_from_top<1>(L.hist2, rb, &L.digit[1], &L.rem[1], &L.err, s_red);
     if (L.err) return false;
-    if (ref0) { lo0 += L.digit[0] << sh2; sh_lo = sh2; }
+    if (ref0) lo0 += L.digit[0] << sh2;
     if (ref1) { lo1 += L.digit[1] << sh2; sh_hi = sh2; }
   }
   *t_lo_out = lo0;
   *t_hi_out = two ? (unsigned long long)lo1 + (1ull << sh_hi) : (1ull << 32);
-  (void)sh_lo;
   return true;
 }
 
 // General path (any rank): two fixed 11-bit digit passes (key bits 31..21, then 20..10) per target.
-__device__ __forceinline__ void sample_general(const unsigned (&keys)[kSPT], int S, long long rank_lo, long long rank_hi,
+// The keys are re-read from the sample (L2) in each pass, 16 B at a time: the caller holds the first
+// two HBM steps in registers here, and a 32-key array on top of them would spill.
+__device__ __forceinline__ uint4 sample_group(const unsigned* sample, int S, int g) {
+  const int j = sample_j(4 * g);
+  if (S == kSample) return *reinterpret_cast<const uint4*>(sample + j);
+  uint4 t;
+  t.x = j < S ? sample[j] : 0u;
+  t.y = j + 1 < S ? sample[j + 1] : 0u;
+  t.z = j + 2 < S ? sample[j + 2] : 0u;
+  t.w = j + 3 < S ? sample[j + 3] : 0u;
+  return t;
+}
+
+__device__ __forceinline__ void sample_general(const unsigned* sample, int S, long long rank_lo, long long rank_hi,
                                                SampleLds& L, unsigned* s_hist, unsigned long long* s_red,
                                                unsigned* t_lo_out, unsigned long long* t_hi_out) {
   const int tid = threadIdx.x;
@@ -374,8 +414,15 @@ __device__ __forceinline__ void sample_general(const unsigned (&keys)[kSPT], int
   }
   if (tid == 0) L.err = 0;
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kSPT; ++i) hist_add(s_hist, keys[i] >> 21, sample_j(i) < S);
+#pragma unroll 2
+  for (int g = 0; g < kSPT / 4; ++g) {
+    const uint4 t = sample_group(sample, S, g);
+    const int j = sample_j(4 * g);
+    hist_add(s_hist, t.x >> 21, j < S);
+    hist_add(s_hist, t.y >> 21, j + 1 < S);
+    hist_add(s_hist, t.z >> 21, j + 2 < S);
+    hist_add(s_hist, t.w >> 21, j + 3 < S);
+  }
   __syncthreads();
   {
     const long long rk[2] = {rank_lo, two ? rank_hi : 0};
@@ -385,12 +432,18 @@ __device__ __forceinline__ void sample_general(const unsigned (&keys)[kSPT], int
   const long long r0 = L.rem[0], r1 = two ? L.rem[1] : 0;
   for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
   __syncthreads();
+#pragma unroll 2
+  for (int g = 0; g < kSPT / 4; ++g) {
+    const uint4 t = sample_group(sample, S, g);
+    const int j = sample_j(4 * g);
+    const unsigned kk[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
-  for (int i = 0; i < kSPT; ++i) {
-    const bool in = sample_j(i) < S;
-    const unsigned hi = keys[i] >> 21, bin = (keys[i] >> 10) & (kHistBins - 1);
-    hist_add(s_hist, bin, in && hi == d0);
-    if (two) hist_add(L.hist2, bin, in && hi == d1);
+    for (int c = 0; c < 4; ++c) {
+      const bool in = j + c < S;
+      const unsigned hi = kk[c] >> 21, bin = (kk[c] >> 10) & (kHistBins - 1);
+      hist_add(s_hist, bin, in && hi == d0);
+      if (two) hist_add(L.hist2, bin, in && hi == d1);
+    }
   }
   __syncthreads();
   {
@@ -743,23 +796,22 @@ __device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, i
     t_hi = 1ull << 32;
     if (blockIdx.x == 0 && tid == 0) w.st()->sample_path = 2ull;
   } else {
-    unsigned keys[kSPT];
-    if (S == kSample) {  // all eight 16-B groups in flight together
-      uint4 t[kSPT / 4];
-#pragma unroll
-      for (int i = 0; i < kSPT; i += 4) t[i / 4] = *reinterpret_cast<const uint4*>(w.sample() + sample_j(i));
-#pragma unroll
-      for (int i = 0; i < kSPT; i += 4) {
-        keys[i] = t[i / 4].x; keys[i + 1] = t[i / 4].y; keys[i + 2] = t[i / 4].z; keys[i + 3] = t[i / 4].w;
-      }
-    } else {  // small n: S = n keys
-#pragma unroll
-      for (int i = 0; i < kSPT; ++i) keys[i] = sample_j(i) < S ? w.sample()[sample_j(i)] : 0u;  // 0: below every key
-    }
-    step_load<false>(x, wb0, b1, lane, va);  // unconditional (clamped in-range) so no wait is merged in
     bool ok = false;
-    if (rank_lo <= kET) ok = sample_fast(keys, S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
-    if (!ok) sample_general(keys, S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
+    {
+      unsigned keys[kSPT];
+      load_sample_keys(w.sample(), S, keys);
+      // the first two steps stream while the floor / ceiling are picked (unconditional, clamped
+      // in-range loads, so no wait is merged in): the first right away, the second in the registers the
+      // keys leave free after the histogram
+      step_load<false>(x, wb0, b1, lane, va);
+      unsigned B = 0;
+      int shB = 0;
+      const bool fast = rank_lo <= kET;  // grid-uniform
+      if (fast) sample_fast_hist(keys, S, SL, s_hist, &B, &shB);
+      step_load<false>(x, wb0 + kBlockStep, b1, lane, vb);
+      if (fast) ok = sample_fast_pick(w.sample(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
+    }
+    if (!ok) sample_general(w.sample(), S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
     if (blockIdx.x == 0 && tid == 0) w.st()->sample_path = ok ? 0ull : 1ull;
   }
   // the float predicate !(v < key_value(t_lo)) equals key >= t_lo for t_lo <= key(+inf)
@@ -793,6 +845,12 @@ __device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, i
     // waits for the load), and the partial tail step is peeled off
     int s = 0;
     if (take_all && nfull > 0) step_load<true>(x, wb0, b1, lane, va);
+    if (!take_all && nfull >= 3) {  // peeled first iteration: steps 0 and 1 are in flight already
+      step_process<true>(va, wb0, b1, tf, s_wc, 0, base, fc);
+      step_load<true>(x, wb0 + 2 * kBlockStep, b1, lane, va);
+      step_process<true>(vb, wb0 + kBlockStep, b1, tf, s_wc, 1, base, fc);
+      s = 2;
+    }
     for (; s + 3 <= nfull; s += 2) {
       const int64_t wa = wb0 + (int64_t)s * kBlockStep, wbn = wa + kBlockStep;
       step_load<true>(x, wbn, b1, lane, vb);
