@@ -615,6 +615,38 @@ __device__ __forceinline__ void exchange(const EncWs& w, unsigned ep) {
   __syncthreads();
 }
 
+// Exchange with work: wave 0 raises the flag and polls as in exchange(); waves 1.. run `work()` (one
+// bounded chunk per call; false = nothing left) until wave 0 reports the exchange complete, finish the
+// chunk in hand and drain its stores.  Used to move per-candidate Philox words into the waits.
+template <typename F>
+__device__ __forceinline__ void exchange_work(const EncWs& w, unsigned ep, unsigned* s_xdone, F&& work) {
+  const int tid = threadIdx.x;
+  if (tid == 0) *s_xdone = 0u;
+  drain_stores();
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(w.flags() + blockIdx.x, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < kWave) {
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+      for (int b = tid; b < (int)gridDim.x; b += kWave)
+        ok = ok && (int)(__hip_atomic_load(w.flags() + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ep) >= 0;
+      if (__ballot(!ok) == 0ull) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {  // ~1 s: a block never arrived; flag it and let the launch drain
+        if (tid == 0) __hip_atomic_fetch_or(&w.st()->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    if (tid == 0) __hip_atomic_store(s_xdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    while (__hip_atomic_load(s_xdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      if (!work()) break;
+    drain_stores();
+  }
+  __syncthreads();
+}
+
 struct SelState {
   unsigned lo;
   unsigned long long width;
@@ -970,6 +1002,28 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   unsigned* hist = w.hist();
   unsigned C_b;
   unsigned ep;
+  // Philox words of the candidates (stacked), precomputed in exchange waits into the block's staging
+  // area (unused by the fused path; the split path has copied its staged candidates to LDS by then):
+  // chunk c = wave range c % kENW, its 64 candidates of iteration c / kENW; chunks [0, s_rnext) are
+  // complete after the exchange that ran them
+  __shared__ unsigned s_rnext, s_xdone;
+  unsigned* const rnd = w.stage_key(blockIdx.x);
+  unsigned rnd_n = 0;  // candidates covered by the chunk map (0: none)
+  auto rnd_work = [&]() -> bool {
+    unsigned c = 0;
+    if (lane == 0) c = atomicAdd(&s_rnext, 1u);
+    c = __shfl(c, 0, kWave);
+    const unsigned Qn = ((rnd_n + kENW - 1) / kENW + kWave - 1) / kWave * kWave;
+    if (c >= (Qn / kWave) * (unsigned)kENW) return false;
+    const unsigned wr = c % kENW, it = c / kENW;
+    const unsigned r0 = wr * Qn < rnd_n ? wr * Qn : rnd_n, r1 = r0 + Qn < rnd_n ? r0 + Qn : rnd_n;
+    const unsigned p = r0 + it * kWave + lane;
+    if (p < r1) {
+      const unsigned id = s_idx[p];
+      rnd[p] = pick(philox_group((uint64_t)id >> 2, seed, counter), (int)(id & 3u));
+    }
+    return true;
+  };
   if (FUSED) {
     __shared__ unsigned s_wc[2][kENW];
     if (tid == 0) s_glob[2] = ld_mem64(&w.st()->call);  // (read before any exchange of this call)
@@ -981,7 +1035,13 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       s_glob[1] = fo.t_hi;
     }
     ep = (unsigned)s_glob[2] * kEpochStride;  // (s_glob[2] was written before the filter's barriers)
-    exchange(w, ++ep);  // every block's round-0 histogram, counts and max key are in
+    if (tid == 0) s_rnext = 0u;
+    if (STACKED) {  // (x-mode blocks, C_b > kCap, have no chunks; if the call falls back, none is used)
+      rnd_n = C_b <= (unsigned)kCap ? C_b : 0u;
+      exchange_work(w, ++ep, &s_xdone, rnd_work);  // every block's round-0 histogram, counts, max are in
+    } else {
+      exchange(w, ++ep);
+    }
     STAMP(5);
   } else {
     // ---- one batch of loads: this block's candidates (staging), the round-0 histogram and counts
@@ -1004,6 +1064,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       s_glob[2] = ld_mem64(&w.st()->call);
     }
     ep = 0;  // set below, after the barrier
+    if (tid == 0) s_rnext = 0u;
   }
   load_hist(w, 0, s_ghist, s_ex, true);  // (ends in a barrier)
   const unsigned t_lo = (unsigned)s_glob[0];
@@ -1140,7 +1201,12 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       st_mem64(&w.blk_cnt()[blockIdx.x], ((unsigned long long)s_nl << 32) | (gt & 0xffffffffull));
     }
     STAMP(8);
-    exchange(w, ++ep);
+    if (STACKED) {
+      if (!FUSED) rnd_n = src.xmode ? 0u : ncand;
+      exchange_work(w, ++ep, &s_xdone, rnd_work);
+    } else {
+      exchange(w, ++ep);
+    }
     STAMP(9);
     // all-gather in ONE batch of coherent loads: every block's list size and count above the bin, and
     // all list slots (sizes are checked afterwards)
@@ -1392,9 +1458,17 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     t_before += (long long)(s_wcnt[v2] & 0xffffffffull);
   }
   // pass 2: keep decisions and the writes
+  // chunks whose Philox words were precomputed in the exchange waits (wave-uniform test per iteration)
+  // (one iteration ahead, unconditional loads at a clamped address, so no wait is merged in)
+  const unsigned rdone = (STACKED && !src.xmode && rnd_n == ncand) ? s_rnext : 0u;
+  unsigned rw_next = 0;
+  if (STACKED) rw_next = ld_mem(rnd + (q0 + lane < (unsigned)kCap ? q0 + lane : kCap - 1));
   for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
     const unsigned p = p0 + lane;
     const bool in = p < q1;
+    const bool have = ((p0 - q0) / kWave * kENW + (unsigned)wid) < rdone;
+    const unsigned rw = rw_next;
+    if (STACKED) rw_next = ld_mem(rnd + (p + kWave < (unsigned)kCap ? p + kWave : kCap - 1));
     unsigned raw = 0, id = 0;
     if (in) cand_get(src, p, raw, id);
     const unsigned key = order_key(raw);
@@ -1416,8 +1490,10 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
 #if FLC_CALIB_NOPHILOX  // calibration builds only (tools/calib_select.sh): results invalid
         const double uu = 0.5;
 #else
-        const U4 r4 = philox_group((uint64_t)id >> 2, seed, counter);
-        const double uu = u01(pick(r4, (int)(id & 3u)));
+        uint32_t r;
+        if (have) r = rw;
+        else r = pick(philox_group((uint64_t)id >> 2, seed, counter), (int)(id & 3u));
+        const double uu = u01(r);
 #endif
         const uint32_t lvl = (uint32_t)dither_level<0>(y, levels, step, uu);  // compressors.py:346-353
         const uint32_t c = nrm_ok ? (((raw >> 31) << 7) | lvl) : 1u;
@@ -1430,6 +1506,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     s_before += __popcll(ms);
     t_before += __popcll(mt);
   }
+  STAMP(14);
   if (tiled) {
     constexpr int TPT = 2 * kHistBins / kET;  // tiles per thread
     __syncthreads();
@@ -1454,7 +1531,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     }
     if (blockIdx.x == gridDim.x - 1 && tid == 0) tile_out[cdiv_dev(n, kTile)] = (unsigned)k;
   }
-  STAMP(14);
+  STAMP(15);
+  BLKT(3);
   STAMP_OUT(FUSED ? 0 : 5, 16);
 }
 

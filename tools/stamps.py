@@ -19,7 +19,7 @@ BLKT_OFF = 175872   # kOffBlkT
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
 x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 1e-3
-names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "compact"]
+names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "compact", "tiles"]
 for it in range(6):
     codec.stacked_encode(x, k, 127, 1, it)
     torch.cuda.synchronize()
@@ -27,13 +27,13 @@ for it in range(6):
     st = ws[STAMP_OFF:STAMP_OFF + 16 * 8].cpu().numpy().view(np.uint64).astype(np.int64)
     if it < 2:
         continue
-    t = st[:15].astype(np.float64)
+    t = st[:16].astype(np.float64)
     prev, parts = t[0], []
-    for i in range(1, 15):
+    for i in range(1, 16):
         if t[i] > 0 and t[i] >= prev:
             parts.append(f"{names[i - 1]} {(t[i] - prev) * 10 / 1000:.1f}")
             prev = t[i]
-    print(" | ".join(parts), f"| total {(t[14] - t[0]) * 10 / 1000:.1f} us")
+    print(" | ".join(parts), f"| total {(max(t[14], t[15]) - t[0]) * 10 / 1000:.1f} us")
     ws[STAMP_OFF:STAMP_OFF + 16 * 8].zero_()
     if it == 5:  # per-block filter times (start of the HBM pass, its end, end of the kernel)
         bt = ws[BLKT_OFF:BLKT_OFF + 256 * 32].cpu().numpy().view(np.uint64).astype(np.int64).reshape(256, 4)
@@ -48,3 +48,8 @@ for it in range(6):
         print("slowest blocks:", [(int(b), round(float(dur[b]), 1)) for b in order[-8:]])
         xcd = np.arange(G) % 8
         print("mean duration by blockIdx % 8:", [round(float(dur[xcd == i].mean()), 1) for i in range(8)])
+        if (bt[:, 3] > 0).all():  # kernel end per block (select / fused kernel)
+            fin = (bt[:, 3] - t0) * 10 / 1000
+            o = np.argsort(fin)
+            print(f"kernel end: block 0 {fin[0]:.1f} us, min {fin.min():.1f}, median {np.median(fin):.1f}, "
+                  f"max {fin.max():.1f}; last blocks:", [(int(b), round(float(fin[b]), 1)) for b in o[-6:]])
