@@ -21,7 +21,7 @@ def probe(name, fn, reps=20):
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
-x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 1e-3
+x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(int(os.environ.get("SEED", "1")))) * 1e-3
 out = torch.empty_like(x)
 enc = lambda: codec.stacked_encode(x, k, 127, 1, 0)
 print("filter us", round(probe("topk_filter", enc), 1), "select us", round(probe("stacked_select", enc), 1),

@@ -18,7 +18,8 @@ STAMP_OFF = 175616  # byte offset of EncWs.stamps in the top-k workspace (topk.h
 BLKT_OFF = 175872   # kOffBlkT
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
-x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 1e-3
+seed = int(os.environ.get("SEED", "1"))  # bench.py's headline delta: SEED=1234
+x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed)) * 1e-3
 names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "compact", "tiles"]
 for it in range(6):
     codec.stacked_encode(x, k, 127, 1, it)
@@ -27,6 +28,8 @@ for it in range(6):
     st = ws[STAMP_OFF:STAMP_OFF + 16 * 8].cpu().numpy().view(np.uint64).astype(np.int64)
     if it < 2:
         continue
+    sv = ws[:16 * 8].cpu().numpy().view(np.uint64)
+    print("state call,err,C,fb,T,maxkey,rounds,t_lo,t_hi,need,ties,strict,path:", [int(v) for v in sv[:13]])
     t = st[:16].astype(np.float64)
     prev, parts = t[0], []
     for i in range(1, 16):

@@ -23,6 +23,10 @@ SHORT = {
     "sparse_decode_kernel<0": "sparse_decode",
     "topk_select_kernel<true>": "stacked_select",
     "topk_select_kernel<false>": "topk_select",
+    "topk_select_kernel<true, true>": "stacked_encode",
+    "topk_select_kernel<false, true>": "topk_encode",
+    "topk_select_kernel<true, false>": "stacked_select",
+    "topk_select_kernel<false, false>": "topk_select",
     "topk_sample_select_kernel": "topk_sample_select",
     "topk_sample_gather_kernel": "topk_sample_gather",
     "tile_index_kernel": "tile_index",
