@@ -380,3 +380,23 @@ def test_stacked_encode_two_streams():
         e = refs[j % 4]
         assert torch.equal(p.idx, e.idx) and torch.equal(p.codes, e.codes) and torch.equal(p.norm, e.norm)
         assert torch.equal(p.tiles, e.tiles)
+
+
+def test_stacked_encode_repeated_calls_identical():
+    """Back-to-back encodes of one delta through one workspace (state carried from call to call: epochs,
+    histogram zeroing, precomputed Philox words) give identical packets and decodes."""
+    codec = _codec()
+    n, k = 40_000_000 + 4099, 400_000
+    gen = torch.Generator(device=DEV).manual_seed(99)
+    x = torch.randn(n, generator=gen, device=DEV) * 1e-3
+    ref = codec.stacked_encode(x, k, 127, seed=3, counter=7)
+    ref_out = codec.stacked_decode(ref).clone()
+    for _ in range(6):
+        p = codec.stacked_encode(x, k, 127, seed=3, counter=7)
+        assert torch.equal(p.idx, ref.idx) and torch.equal(p.codes, ref.codes) and torch.equal(p.norm, ref.norm)
+        assert torch.equal(p.tiles, ref.tiles)
+        assert torch.equal(codec.stacked_decode(p), ref_out)
+    idx, val, tiles = codec.topk_encode(x, k, with_tiles=True)
+    for _ in range(3):
+        i2, v2, t2 = codec.topk_encode(x, k, with_tiles=True)
+        assert torch.equal(i2, idx) and torch.equal(v2, val) and torch.equal(t2, tiles)

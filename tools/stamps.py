@@ -21,7 +21,7 @@ k = n // 100
 seed = int(os.environ.get("SEED", "1"))  # bench.py's headline delta: SEED=1234
 x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed)) * 1e-3
 names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "compact", "tiles"]
-for it in range(6):
+for it in range(int(os.environ.get("ITERS", "12"))):
     codec.stacked_encode(x, k, 127, 1, it)
     torch.cuda.synchronize()
     ws = [t for key, t in codec._WS.items() if key[2] == "topk"][0]
@@ -38,7 +38,7 @@ for it in range(6):
             prev = t[i]
     print(" | ".join(parts), f"| total {(max(t[14], t[15]) - t[0]) * 10 / 1000:.1f} us")
     ws[STAMP_OFF:STAMP_OFF + 16 * 8].zero_()
-    if it == 5:  # per-block filter times (start of the HBM pass, its end, end of the kernel)
+    if it == int(os.environ.get("ITERS", "12")) - 1:  # per-block filter times (start of the HBM pass, its end, end of the kernel)
         bt = ws[BLKT_OFF:BLKT_OFF + 256 * 32].cpu().numpy().view(np.uint64).astype(np.int64).reshape(256, 4)
         G = int((bt[:, 0] > 0).sum())
         bt = bt[:G]
