@@ -110,6 +110,27 @@ __device__ __forceinline__ T block_excl_scan(T v, T* lds, T* total) {
   return base + incl - v;
 }
 
+// The same with LDS-only barriers (s_waitcnt lgkmcnt(0); s_barrier): outstanding global stores and loads
+// stay in flight across it.  Only for values exchanged through LDS (defined after lds_barrier below).
+__device__ __forceinline__ void lds_barrier();
+template <typename T, int NW>
+__device__ __forceinline__ T block_excl_scan_lds(T v, T* lds, T* total) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+  const T incl = wave_incl_scan(v);
+  if (lane == kWave - 1) lds[wid] = incl;
+  lds_barrier();
+  T base = 0, tot = 0;
+#pragma unroll 4
+  for (int w = 0; w < NW; ++w) {
+    const T s = lds[w];
+    base += (w < wid) ? s : T(0);
+    tot += s;
+  }
+  lds_barrier();
+  *total = tot;
+  return base + incl - v;
+}
+
 template <typename T, int NW>
 __device__ __forceinline__ T block_sum(T v, T* lds) {
   T tot;

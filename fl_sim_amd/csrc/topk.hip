@@ -1194,7 +1194,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       }
     }
     if (lane == 0) s_wcnt[wid] = (unsigned long long)gtw << 32;
-    __syncthreads();
+    lds_barrier();  // (the list stores drain in the exchange)
     if (tid == 0) {
       unsigned long long gt = 0;
       for (int v2 = 0; v2 < kENW; ++v2) gt += s_wcnt[v2] >> 32;
@@ -1451,7 +1451,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     __syncthreads();
     if (lane == 0) s_wcnt[wid] = ((unsigned long long)ws << 32) | wt;
   }
-  __syncthreads();
+  lds_barrier();  // (LDS-only: the histogram zeroing stores need no wait)
   long long s_before = (long long)(pre >> 32), t_before = (long long)(pre & 0xffffffffull);
   for (int v2 = 0; v2 < wid; ++v2) {
     s_before += (long long)(s_wcnt[v2] >> 32);
@@ -1509,7 +1509,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   STAMP(14);
   if (tiled) {
     constexpr int TPT = 2 * kHistBins / kET;  // tiles per thread
-    __syncthreads();
+    lds_barrier();  // (LDS-only: the compaction's stores keep draining meanwhile)
     unsigned c[TPT];
     unsigned long long sum = 0;
 #pragma unroll
@@ -1519,7 +1519,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       sum += c[i];
     }
     unsigned long long tt;
-    unsigned long long run = block_excl_scan<unsigned long long, kENW>(sum, s_red, &tt);
+    unsigned long long run = block_excl_scan_lds<unsigned long long, kENW>(sum, s_red, &tt);
     const long long tb = (long long)(pre & 0xffffffffull);
     run += (unsigned long long)((long long)(pre >> 32) + (tb > skip ? tb - skip : 0));  // kept before the block
     const int64_t tile0 = b0 / kTile;
