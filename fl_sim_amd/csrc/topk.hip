@@ -62,6 +62,8 @@ constexpr int kMaxBlocks = 1024;              // <= kET (per-block words are rea
 constexpr int kInbin = 32;                    // in-bin keys a block may publish (more: histogram rounds)
 constexpr int kInbinAll = 1024;               // in-bin keys of all blocks resolved locally
 constexpr int kTile = FLC_TILE;               // outputs per tile of the CSR tile pointers
+constexpr int kTileLog = 10;
+static_assert((1 << kTileLog) == kTile, "tile size");
 constexpr int kFlagStride = 16;               // workspace words reserved per block for flags
 
 // diagnostics and the call counter (64-bit words, memory-side atomics only)
@@ -985,7 +987,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
                                                           long long rank_hi, int take_all) {
   __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
   __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
-  __shared__ unsigned s_hh[2 * kHistBins];  // the round / global histograms; in the compaction: tile counts
+  __shared__ unsigned s_hh[2 * kHistBins];  // the round / global histograms
   unsigned* const s_hist = s_hh;
   unsigned* const s_ghist = s_hh + kHistBins;
   __shared__ unsigned long long s_red[kENW];
@@ -1433,11 +1435,22 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   const bool nrm_ok = nrm > 0.0f && nrm <= 3.402823466e38f;
   // tile pointers (CSR over FLC_TILE-output tiles): kept entries per tile of this block, counted in the
   // compaction, scanned afterwards (block ranges are whole tiles: M is a multiple of kBlockStep)
-  const bool tiled = tile_out != nullptr;  // (the host passes null when a block spans > 2 kHistBins tiles)
-  const int ntl = (int)((b1 - b0 + kTile - 1) / kTile);
-  if (tiled)
-    for (int i = tid; i < ntl; i += kET) s_hh[i] = 0u;
+  // Tile pointers (CSR over FLC_TILE-output tiles) straight from the compaction, no block scan: wave w owns
+  // the tiles whose first element lies in (lo_w, hi_w], the ids just below its first candidate and at
+  // its last one (block edges at b0 - 1 and b1 - 1), and gives each the position of the first kept entry
+  // at or after the tile's start: a kept entry fills the tiles that start after the previous kept entry,
+  // and the wave's last kept entry's successor position fills the rest up to hi_w.
+  const bool tiled = tile_out != nullptr;
   const unsigned q0 = cq0, q1 = cq1;
+  const bool tile_owner = tiled && (q0 < q1 || (ncand == 0u && wid == 0));  // (wave-uniform)
+  int64_t tile_prev = -1, tile_hi = -1;  // element ids
+  if (tile_owner) {
+    unsigned r0 = 0, i0 = 0, r1 = 0, i1 = 0;
+    if (q0 > 0u) cand_get(src, q0 - 1u, r0, i0);
+    if (q1 > 0u && q1 < ncand) cand_get(src, q1 - 1u, r1, i1);
+    tile_prev = q0 == 0u ? b0 - 1 : (int64_t)i0;
+    tile_hi = q1 >= ncand ? b1 - 1 : (int64_t)i1;
+  }
   if (!wave_counted) {  // pass 1: this wave's strict / tie counts (the in-bin path counted them already)
     unsigned ws = 0, wt = 0;
     for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
@@ -1501,36 +1514,32 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       } else {
         val_out[pos] = __uint_as_float(raw);
       }
-      if (tiled) atomicAdd(&s_hh[(unsigned)((int64_t)id - b0) / (unsigned)kTile], 1u);
+    }
+    if (tile_owner) {
+      const bool kp = keep && pos >= 0 && pos < k;
+      const unsigned long long km = __ballot(kp);
+      if (km) {
+        // the previous kept entry: the nearest kept lane below, or the last kept entry before this round
+        const unsigned long long below = km & ((1ull << lane) - 1ull);
+        const int pl = below ? 63 - __clzll(below) : lane;
+        const unsigned pid = (unsigned)__shfl((int)id, pl, kWave);
+        if (kp) {
+          const int64_t prev = below ? (int64_t)pid : tile_prev;
+          for (int64_t t = (prev >> kTileLog) + 1; t <= ((int64_t)id >> kTileLog); ++t) tile_out[t] = (unsigned)pos;
+        }
+        const int hl = 63 - __clzll(km);
+        tile_prev = (int64_t)(unsigned)__shfl((int)id, hl, kWave);
+      }
     }
     s_before += __popcll(ms);
     t_before += __popcll(mt);
   }
-  STAMP(14);
-  if (tiled) {
-    constexpr int TPT = 2 * kHistBins / kET;  // tiles per thread
-    lds_barrier();  // (LDS-only: the compaction's stores keep draining meanwhile)
-    unsigned c[TPT];
-    unsigned long long sum = 0;
-#pragma unroll
-    for (int i = 0; i < TPT; ++i) {
-      const int t = tid * TPT + i;
-      c[i] = t < ntl ? s_hh[t] : 0u;
-      sum += c[i];
-    }
-    unsigned long long tt;
-    unsigned long long run = block_excl_scan_lds<unsigned long long, kENW>(sum, s_red, &tt);
-    const long long tb = (long long)(pre & 0xffffffffull);
-    run += (unsigned long long)((long long)(pre >> 32) + (tb > skip ? tb - skip : 0));  // kept before the block
-    const int64_t tile0 = b0 / kTile;
-#pragma unroll
-    for (int i = 0; i < TPT; ++i) {
-      const int t = tid * TPT + i;
-      if (t < ntl) tile_out[tile0 + t] = (unsigned)run;
-      run += c[i];
-    }
-    if (blockIdx.x == gridDim.x - 1 && tid == 0) tile_out[cdiv_dev(n, kTile)] = (unsigned)k;
+  if (tile_owner) {  // tiles after the wave's last kept entry: the next kept position
+    const long long nxt = s_before + (t_before > skip ? t_before - skip : 0);
+    for (int64_t t = (tile_prev >> kTileLog) + 1 + lane; t <= (tile_hi >> kTileLog); t += kWave) tile_out[t] = (unsigned)nxt;
+    if (blockIdx.x == gridDim.x - 1 && q1 >= ncand && lane == 0) tile_out[cdiv_dev(n, kTile)] = (unsigned)k;
   }
+  STAMP(14);
   STAMP(15);
   BLKT(3);
   STAMP_OUT(FUSED ? 0 : 5, 16);
@@ -1611,20 +1620,18 @@ int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes,
     if (gt.multi[dev] && gt.recorded[dev]) FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
   }
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
-  const bool in_kernel_tiles = tiles && g.M / kTile <= 2 * kHistBins;
   if (split)
     FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", (topk_select_kernel<STACKED, false>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
-               in_kernel_tiles ? tiles : nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
+               tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
   else
     FLC_LAUNCH(STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
-               in_kernel_tiles ? tiles : nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
+               tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
   if (gated && gt.multi[dev]) {
     FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
     gt.recorded[dev] = true;
   }
-  if (tiles && !in_kernel_tiles) return flc_tile_index(idx, k, n, tiles, st);
   return FLC_OK;
 }
 
