@@ -9,6 +9,6 @@ make -s -C $A/fl_sim_amd/csrc -j16 OUT=/tmp/libflc_A.so BUILD=/tmp/b_A > /dev/nu
 make -s -C fl_sim_amd/csrc -j16 OUT=/tmp/libflc_B.so BUILD=/tmp/b_B > /dev/null || exit 1
 for r in 1 2; do
   for v in A B; do
-    echo "== $v"; FLC_LIB=/tmp/libflc_$v.so timeout -k 10 100 python tools/calib_enc.py 2>&1 | grep -E "filter us|decode|step"
+    echo "== $v"; FLC_LIB=/tmp/libflc_$v.so SEED=1234 timeout -k 10 100 python tools/calib_enc.py 2>&1 | grep -E "filter us|decode|step"
   done
 done
