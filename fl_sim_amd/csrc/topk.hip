@@ -184,7 +184,7 @@ __device__ __forceinline__ void block_select_from_top(const unsigned* h, const l
     sum += c[i];
   }
   unsigned long long tot;
-  const long long ex = (long long)block_excl_scan<unsigned long long, kENW>(sum, s_red, &tot);
+  const long long ex = (long long)block_excl_scan_lds<unsigned long long, kENW>(sum, s_red, &tot);
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const long long rj = r[j];
@@ -204,7 +204,7 @@ __device__ __forceinline__ void block_select_from_top(const unsigned* h, const l
       *err |= 1u;
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // block-wide sums of N 64-bit values per thread in one LDS round (s_buf: kENW * N words)
@@ -332,7 +332,7 @@ __device__ __forceinline__ void sample_fast_hist(const unsigned (&keys)[kSPT], i
     s_hist[i] = 0u;
     L.hist2[i] = 0u;
   }
-  __syncthreads();
+  lds_barrier();
   unsigned B = 0xffffffffu, mx = 0;
 #pragma unroll
   for (int w = 0; w < kENW; ++w) {
@@ -352,7 +352,7 @@ __device__ __forceinline__ bool sample_fast_pick(const unsigned* sample, int S, 
                                                  unsigned long long* s_red, unsigned* t_lo_out,
                                                  unsigned long long* t_hi_out) {
   const int tid = threadIdx.x;
-  __syncthreads();
+  lds_barrier();
   const bool two = rank_hi > 0;
   const long long rk[2] = {rank_lo, two ? rank_hi : 0};
   block_select_from_top<2>(s_hist, rk, L.digit, L.rem, &L.err, s_red);
@@ -367,9 +367,9 @@ __device__ __forceinline__ bool sample_fast_pick(const unsigned* sample, int S, 
     const long long r0 = L.rem[0], r1 = two ? L.rem[1] : 0;
     const int sh2 = sh > kHistBits ? sh - kHistBits : 0;
     const unsigned long long bw = 1ull << sh;
-    __syncthreads();
+    lds_barrier();
     for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < kSPT; ++i) {
       if (sample_j(i) >= S) continue;
@@ -377,7 +377,7 @@ __device__ __forceinline__ bool sample_fast_pick(const unsigned* sample, int S, 
       if (ref0 && keys[i] >= lo0 && rel0 < bw) atomicAdd(&s_hist[(unsigned)(rel0 >> sh2)], 1u);
       if (ref1 && keys[i] >= lo1 && rel1 < bw) atomicAdd(&L.hist2[(unsigned)(rel1 >> sh2)], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     const long long ra[1] = {ref0 ? r0 : 0}, rb[1] = {ref1 ? r1 : 0};
     block_select_from_top<1>(s_hist, ra, &L.digit[0], &L.rem[0], &L.err, s_red);
     block_select_from_top<1>(L.hist2, rb, &L.digit[1], &L.rem[1], &L.err, s_red);
@@ -409,13 +409,13 @@ __device__ __forceinline__ void sample_general(const unsigned* sample, int S, lo
                                                unsigned* t_lo_out, unsigned long long* t_hi_out) {
   const int tid = threadIdx.x;
   const bool two = rank_hi > 0;
-  __syncthreads();
+  lds_barrier();
   for (int i = tid; i < kHistBins; i += kET) {
     s_hist[i] = 0u;
     L.hist2[i] = 0u;
   }
   if (tid == 0) L.err = 0;
-  __syncthreads();
+  lds_barrier();
 #pragma unroll 2
   for (int g = 0; g < kSPT / 4; ++g) {
     const uint4 t = sample_group(sample, S, g);
@@ -425,7 +425,7 @@ __device__ __forceinline__ void sample_general(const unsigned* sample, int S, lo
     hist_add(s_hist, t.z >> 21, j + 2 < S);
     hist_add(s_hist, t.w >> 21, j + 3 < S);
   }
-  __syncthreads();
+  lds_barrier();
   {
     const long long rk[2] = {rank_lo, two ? rank_hi : 0};
     block_select_from_top<2>(s_hist, rk, L.digit, L.rem, &L.err, s_red);
@@ -433,7 +433,7 @@ __device__ __forceinline__ void sample_general(const unsigned* sample, int S, lo
   const unsigned d0 = L.digit[0], d1 = two ? L.digit[1] : 0u;
   const long long r0 = L.rem[0], r1 = two ? L.rem[1] : 0;
   for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
-  __syncthreads();
+  lds_barrier();
 #pragma unroll 2
   for (int g = 0; g < kSPT / 4; ++g) {
     const uint4 t = sample_group(sample, S, g);
@@ -447,7 +447,7 @@ __device__ __forceinline__ void sample_general(const unsigned* sample, int S, lo
       if (two) hist_add(L.hist2, bin, in && hi == d1);
     }
   }
-  __syncthreads();
+  lds_barrier();
   {
     const long long ra[1] = {r0}, rb[1] = {two ? r1 : 0};
     block_select_from_top<1>(s_hist, ra, &L.digit[0], &L.rem[0], &L.err, s_red);
@@ -855,9 +855,9 @@ __device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, i
     w.st()->t_lo = t_lo;
     w.st()->t_hi = t_hi;
   }
-  __syncthreads();  // sample scratch (aliases s_key) dead from here
+  lds_barrier();  // sample scratch (aliases s_key) dead from here (LDS-only: the prefetched steps stay in flight)
   for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
-  __syncthreads();
+  lds_barrier();
   STAMP(2);
   BLKT(0);
 
