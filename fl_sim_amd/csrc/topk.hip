@@ -1474,14 +1474,20 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   // chunks whose Philox words were precomputed in the exchange waits (wave-uniform test per iteration)
   // (one iteration ahead, unconditional loads at a clamped address, so no wait is merged in)
   const unsigned rdone = (STACKED && !src.xmode && rnd_n == ncand) ? s_rnext : 0u;
-  unsigned rw_next = 0;
-  if (STACKED) rw_next = ld_mem(rnd + (q0 + lane < (unsigned)kCap ? q0 + lane : kCap - 1));
-  for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
+  // Philox words kRnd rounds ahead (a load from L2 takes longer than one round): kRnd register slots,
+  // the rounds unrolled by kRnd so each slot is a fixed register; loads at a clamped address,
+  // unconditional, so no wait is merged in
+  constexpr int kRnd = 4;
+  unsigned rq[kRnd];
+#pragma unroll
+  for (int j = 0; j < kRnd; ++j) {
+    const unsigned pa = q0 + (unsigned)(j * kWave) + lane;
+    rq[j] = STACKED ? ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1)) : 0u;
+  }
+  auto round = [&](const unsigned p0, const unsigned rw) {
     const unsigned p = p0 + lane;
     const bool in = p < q1;
     const bool have = ((p0 - q0) / kWave * kENW + (unsigned)wid) < rdone;
-    const unsigned rw = rw_next;
-    if (STACKED) rw_next = ld_mem(rnd + (p + kWave < (unsigned)kCap ? p + kWave : kCap - 1));
     unsigned raw = 0, id = 0;
     if (in) cand_get(src, p, raw, id);
     const unsigned key = order_key(raw);
@@ -1533,6 +1539,19 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     }
     s_before += __popcll(ms);
     t_before += __popcll(mt);
+  };
+  for (unsigned p00 = q0; p00 < q1; p00 += kRnd * kWave) {
+#pragma unroll
+    for (int j = 0; j < kRnd; ++j) {
+      const unsigned p0 = p00 + (unsigned)(j * kWave);
+      if (p0 >= q1) break;
+      const unsigned rw = rq[j];
+      if (STACKED) {
+        const unsigned pa = p0 + (unsigned)(kRnd * kWave) + lane;
+        rq[j] = ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1));
+      }
+      round(p0, rw);
+    }
   }
   if (tile_owner) {  // tiles after the wave's last kept entry: the next kept position
     const long long nxt = s_before + (t_before > skip ? t_before - skip : 0);
