@@ -1474,6 +1474,9 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   // chunks whose Philox words were precomputed in the exchange waits (wave-uniform test per iteration)
   // (one iteration ahead, unconditional loads at a clamped address, so no wait is merged in)
   const unsigned rdone = (STACKED && !src.xmode && rnd_n == ncand) ? s_rnext : 0u;
+#ifdef FLC_SELECT_STAMPS  // diagnostic: Philox chunks precomputed / chunks of the block
+  if (tid == 0) w.blkt()[blockIdx.x * 4 + 2] = ((unsigned long long)((cQ / kWave) * kENW) << 32) | rdone;
+#endif
   // Philox words kRnd rounds ahead (a load from L2 takes longer than one round): kRnd register slots,
   // the rounds unrolled by kRnd so each slot is a fixed register; loads at a clamped address,
   // unconditional, so no wait is merged in
@@ -1484,12 +1487,10 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     const unsigned pa = q0 + (unsigned)(j * kWave) + lane;
     rq[j] = STACKED ? ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1)) : 0u;
   }
-  auto round = [&](const unsigned p0, const unsigned rw) {
+  auto round = [&](const unsigned p0, const unsigned rw, const unsigned raw, const unsigned id) {
     const unsigned p = p0 + lane;
     const bool in = p < q1;
     const bool have = ((p0 - q0) / kWave * kENW + (unsigned)wid) < rdone;
-    unsigned raw = 0, id = 0;
-    if (in) cand_get(src, p, raw, id);
     const unsigned key = order_key(raw);
     const bool is_s = in && key > T, is_t = in && key == T;
     const unsigned long long ms = __ballot(is_s), mt = __ballot(is_t);
@@ -1533,13 +1534,17 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
           const int64_t prev = below ? (int64_t)pid : tile_prev;
           for (int64_t t = (prev >> kTileLog) + 1; t <= ((int64_t)id >> kTileLog); ++t) tile_out[t] = (unsigned)pos;
         }
-        const int hl = 63 - __clzll(km);
-        tile_prev = (int64_t)(unsigned)__shfl((int)id, hl, kWave);
+        const int hl = 63 - __clzll(km);  // (wave-uniform: a readlane, no LDS round trip)
+        tile_prev = (int64_t)(unsigned)__builtin_amdgcn_readlane((int)id, hl);
       }
     }
     s_before += __popcll(ms);
     t_before += __popcll(mt);
   };
+  // the next round's candidates are read while this one is processed (clamped index: unconditional)
+  const unsigned plast = q1 > 0u ? q1 - 1u : 0u;
+  unsigned c_raw = 0, c_id = 0;
+  if (q0 < q1) cand_get(src, q0 + lane < q1 ? q0 + lane : plast, c_raw, c_id);
   for (unsigned p00 = q0; p00 < q1; p00 += kRnd * kWave) {
 #pragma unroll
     for (int j = 0; j < kRnd; ++j) {
@@ -1550,7 +1555,12 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
         const unsigned pa = p0 + (unsigned)(kRnd * kWave) + lane;
         rq[j] = ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1));
       }
-      round(p0, rw);
+      unsigned n_raw, n_id;
+      const unsigned pn = p0 + kWave + lane;
+      cand_get(src, pn < q1 ? pn : plast, n_raw, n_id);
+      round(p0, rw, c_raw, c_id);
+      c_raw = n_raw;
+      c_id = n_id;
     }
   }
   if (tile_owner) {  // tiles after the wave's last kept entry: the next kept position

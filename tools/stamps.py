@@ -51,6 +51,10 @@ for it in range(int(os.environ.get("ITERS", "12"))):
         print("slowest blocks:", [(int(b), round(float(dur[b]), 1)) for b in order[-8:]])
         xcd = np.arange(G) % 8
         print("mean duration by blockIdx % 8:", [round(float(dur[xcd == i].mean()), 1) for i in range(8)])
+        cov = bt[:, 2]
+        done, tot = (cov & 0xffffffff).astype(np.float64), (cov >> 32).astype(np.float64)
+        frac = done / np.maximum(tot, 1)
+        print(f"philox chunks precomputed: min {frac.min():.2f} median {np.median(frac):.2f} (of {int(np.median(tot))} per block)")
         if (bt[:, 3] > 0).all():  # kernel end per block (select / fused kernel)
             fin = (bt[:, 3] - t0) * 10 / 1000
             o = np.argsort(fin)
