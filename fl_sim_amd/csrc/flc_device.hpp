@@ -1,7 +1,8 @@
 // flc_device.hpp — device-side building blocks shared by the codec kernels (gfx950 / CDNA4 only).
 //
-// Everything here is written for 64-lane wavefronts: reductions are __shfl_xor butterflies over 64
-// lanes, ballots are 64-bit, and block-level scans go through LDS one value per wave.
+// Everything here is written for 64-lane wavefronts: integer scans and reductions are DPP sequences over
+// 64 lanes (floating-point sums keep a fixed __shfl_xor butterfly), ballots are 64-bit, and block-level
+// scans go through LDS one value per wave.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -63,31 +64,77 @@ __device__ __forceinline__ uint32_t pick(const U4& v, int j) {
 // ------------------------------------------------------------------------------------------------
 // wave / block reductions (64-lane butterflies)
 // ------------------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+// Cross-lane steps are DPP moves (VALU, a few cycles) rather than __shfl (ds_bpermute through the LDS
+// pipe, ~100+ cycles each): row_shr:1/2/4/8 inside each 16-lane row, then row_bcast:15 / row_bcast:31
+// across rows (gfx9 DPP; gfx950 has no permlane16).  Lanes whose DPP source falls outside the row take
+// no part (the step's condition), so the bound / mask controls do not matter.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t w = __shfl_xor(v, o, kWave);
-    v = w > v ? w : v;
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_mov(T v) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit lanes");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, dpp_u32<CTRL>(__builtin_bit_cast(uint32_t, v)));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint64_t r = ((uint64_t)dpp_u32<CTRL>((uint32_t)(u >> 32)) << 32) | dpp_u32<CTRL>((uint32_t)u);
+    return __builtin_bit_cast(T, r);
   }
+}
+template <typename T>
+__device__ __forceinline__ T lane_bcast(T v, int l) {  // v of lane l (uniform l), as a scalar
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint32_t, v), l));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(u >> 32), l) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    return __builtin_bit_cast(T, r);
+  }
+}
+
+// inclusive prefix combine across the 64 lanes of a wave
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_scan_op(T v, Op op) {
+  const int lane = threadIdx.x & (kWave - 1), rl = lane & 15;
+  T t;
+  t = dpp_mov<0x111>(v);  // row_shr:1
+  if (rl >= 1) v = op(t, v);
+  t = dpp_mov<0x112>(v);  // row_shr:2
+  if (rl >= 2) v = op(t, v);
+  t = dpp_mov<0x114>(v);  // row_shr:4
+  if (rl >= 4) v = op(t, v);
+  t = dpp_mov<0x118>(v);  // row_shr:8
+  if (rl >= 8) v = op(t, v);
+  t = dpp_mov<0x142>(v);  // row_bcast:15
+  if ((lane & 31) >= 16) v = op(t, v);
+  t = dpp_mov<0x143>(v);  // row_bcast:31
+  if (lane >= 32) v = op(t, v);
   return v;
 }
 
-// inclusive prefix sum across the 64 lanes of a wave
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
-  const int lane = threadIdx.x & (kWave - 1);
+  return wave_incl_scan_op(v, [](T a, T b) { return a + b; });
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {  // (every lane gets the total)
+  if constexpr (__is_floating_point(T)) {
+    // floating point keeps the fixed butterfly order its results were pinned with
 #pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const T w = __shfl_up(v, o, kWave);
-    if (lane >= o) v += w;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+  } else {
+    return lane_bcast(wave_incl_scan(v), kWave - 1);
   }
-  return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  return lane_bcast(wave_incl_scan_op(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; }), kWave - 1);
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  return lane_bcast(wave_incl_scan_op(v, [](uint32_t a, uint32_t b) { return a < b ? a : b; }), kWave - 1);
 }
 
 // Block-wide exclusive scan of one value per thread; returns the exclusive prefix, *total gets the

@@ -316,13 +316,7 @@ __device__ __forceinline__ void sample_fast_hist(const unsigned (&keys)[kSPT], i
   unsigned m = 0;
 #pragma unroll
   for (int i = 0; i < kSPT; ++i) m = keys[i] > m ? keys[i] : m;  // invalid slots hold key 0
-  unsigned wmn = m, wmx = m;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned a = __shfl_xor(wmn, o, kWave), b = __shfl_xor(wmx, o, kWave);
-    wmn = a < wmn ? a : wmn;
-    wmx = b > wmx ? b : wmx;
-  }
+  const unsigned wmn = wave_min_u32(m), wmx = wave_max_u32(m);
   if (lane == 0) {
     L.wmin[wid] = wmn;
     L.wmax[wid] = wmx;
