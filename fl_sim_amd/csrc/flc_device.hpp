@@ -139,19 +139,41 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 
 // Block-wide exclusive scan of one value per thread; returns the exclusive prefix, *total gets the
 // block sum.  `lds` must hold NW = blockDim/64 entries.  Contains two __syncthreads().
+// inclusive prefix sum inside each 16-lane row (the first four steps of wave_incl_scan)
+template <typename T>
+__device__ __forceinline__ T row_incl_scan(T v) {
+  const int rl = threadIdx.x & 15;
+  T t;
+  t = dpp_mov<0x111>(v);
+  if (rl >= 1) v += t;
+  t = dpp_mov<0x112>(v);
+  if (rl >= 2) v += t;
+  t = dpp_mov<0x114>(v);
+  if (rl >= 4) v += t;
+  t = dpp_mov<0x118>(v);
+  if (rl >= 8) v += t;
+  return v;
+}
+
+// the cross-wave step of the block scans: lane w of every wave reads wave w's total (one LDS read per
+// lane instead of NW), a row scan over them, and the wave's base / the block total by readlane
+template <typename T, int NW>
+__device__ __forceinline__ void block_scan_fold(const T* lds, T* base, T* tot) {
+  static_assert(NW >= 1 && NW <= 16, "one DPP row of wave totals");
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+  const T sc = row_incl_scan(lane < NW ? lds[lane] : T(0));
+  *tot = lane_bcast(sc, NW - 1);
+  *base = wid > 0 ? lane_bcast(sc, wid > 0 ? wid - 1 : 0) : T(0);
+}
+
 template <typename T, int NW>
 __device__ __forceinline__ T block_excl_scan(T v, T* lds, T* total) {
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
   const T incl = wave_incl_scan(v);
   if (lane == kWave - 1) lds[wid] = incl;
   __syncthreads();
-  T base = 0, tot = 0;
-#pragma unroll 4
-  for (int w = 0; w < NW; ++w) {  // (partially unrolled: NW 64-bit LDS loads in flight cost 2 NW VGPRs)
-    const T s = lds[w];
-    base += (w < wid) ? s : T(0);
-    tot += s;
-  }
+  T base, tot;
+  block_scan_fold<T, NW>(lds, &base, &tot);
   __syncthreads();
   *total = tot;
   return base + incl - v;
@@ -166,13 +188,8 @@ __device__ __forceinline__ T block_excl_scan_lds(T v, T* lds, T* total) {
   const T incl = wave_incl_scan(v);
   if (lane == kWave - 1) lds[wid] = incl;
   lds_barrier();
-  T base = 0, tot = 0;
-#pragma unroll 4
-  for (int w = 0; w < NW; ++w) {
-    const T s = lds[w];
-    base += (w < wid) ? s : T(0);
-    tot += s;
-  }
+  T base, tot;
+  block_scan_fold<T, NW>(lds, &base, &tot);
   lds_barrier();
   *total = tot;
   return base + incl - v;
