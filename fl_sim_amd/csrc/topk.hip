@@ -234,7 +234,7 @@ __device__ __forceinline__ void hist_add(unsigned* h, unsigned bin, bool valid) 
   const unsigned long long act = __ballot(valid);
   if (act == 0ull) return;
   const int first = __ffsll((long long)act) - 1;
-  const unsigned b0 = __shfl(bin, first, kWave);
+  const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)bin, first);  // (uniform lane: no LDS shuffle)
   const unsigned long long same = __ballot(valid && bin == b0);
   if (same == act) {
     if ((int)(threadIdx.x & (kWave - 1)) == first) atomicAdd(&h[b0], (unsigned)__popcll(act));
@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   auto rnd_work = [&]() -> bool {
     unsigned c = 0;
     if (lane == 0) c = atomicAdd(&s_rnext, 1u);
-    c = __shfl(c, 0, kWave);
+    c = (unsigned)__builtin_amdgcn_readlane((int)c, 0);  // (lane 0 claimed: a readlane, not an LDS shuffle)
     const unsigned Qn = ((rnd_n + kENW - 1) / kENW + kWave - 1) / kWave * kWave;
     if (c >= (Qn / kWave) * (unsigned)kENW) return false;
     const unsigned wr = c % kENW, it = c / kENW;
@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       if (bm) {
         unsigned base_l = 0;
         if (lane == 0) base_l = atomicAdd(&s_nl, (unsigned)__popcll(bm));
-        base_l = __shfl(base_l, 0, kWave);
+        base_l = (unsigned)__builtin_amdgcn_readlane((int)base_l, 0);
         const unsigned q = base_l + __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
         if (f && q < (unsigned)kInbin) {  // write-through: read by other XCDs after the exchange
           __hip_atomic_store(my_list + q, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1250,7 +1250,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
           if (bm) {
             unsigned base_l = 0;
             if (lane == 0) base_l = atomicAdd(&s_nall, (unsigned)__popcll(bm));
-            base_l = __shfl(base_l, 0, kWave);
+            base_l = (unsigned)__builtin_amdgcn_readlane((int)base_l, 0);
             const unsigned q = base_l + __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
             if (v && q < (unsigned)kInbinAll) {
               s_lkey[q] = lw[i];
