@@ -236,14 +236,36 @@ def main():
             hout.copy_(out, non_blocking=True)
         torch.cuda.synchronize()
         d2h = 3 * 4 * D / (time.perf_counter() - t0) / 1e9
-        extra["e2e_host"] = {
+        extra["e2e_host_sequential"] = {
             "ms_per_step": round(ms_h, 4),
             "GB_s": round(world * stacked_bytes(D, K) / (ms_h * 1e-3) / 1e9, 1),
             "h2d_GB_s": round(h2d, 1),
             "d2h_GB_s": round(d2h, 1),
             "note": "pinned host x -> H2D -> stacked encode+decode -> D2H of the dense output; same bytes formula",
         }
-        del hx, hout
+        # the same per client through HostCodecPipeline (f3): client i+1's H2D, client i's codec and client
+        # i-1's D2H overlap (6 clients; one pinned input reused, two pinned outputs alternating)
+        from fl_sim_amd.host import HostCodecPipeline
+
+        pipe = HostCodecPipeline(D, dev)
+        hout2 = torch.empty(D, dtype=torch.float32, pin_memory=True)
+        m_cl = 6
+        pipe.run([hx] * 2, [hout, hout2], K, LEVELS, seeds=[rank] * 2)  # warm (streams, workspace)
+        pipe.synchronize()
+        barrier(world)
+        t0 = time.perf_counter()
+        pipe.run([hx] * m_cl, [hout, hout2] * (m_cl // 2), K, LEVELS, seeds=[rank] * m_cl)
+        pipe.synchronize()
+        barrier(world)
+        ms_p = max_over_ranks((time.perf_counter() - t0) * 1e3 / m_cl, world)
+        extra["e2e_host"] = {
+            "ms_per_client": round(ms_p, 4),
+            "GB_s": round(world * stacked_bytes(D, K) / (ms_p * 1e-3) / 1e9, 1),
+            "clients": m_cl,
+            "note": "pinned host deltas -> H2D / codec / D2H pipelined across clients (fl_sim_amd.host); "
+                    "fill and drain included; same bytes formula",
+        }
+        del hx, hout, hout2, pipe
     del x, out
     torch.cuda.empty_cache()
 

@@ -400,3 +400,25 @@ def test_stacked_encode_repeated_calls_identical():
     for _ in range(3):
         i2, v2, t2 = codec.topk_encode(x, k, with_tiles=True)
         assert torch.equal(i2, idx) and torch.equal(v2, val) and torch.equal(t2, tiles)
+
+
+def test_host_pipeline_matches_sequential():
+    """HostCodecPipeline (f3): pinned host deltas through H2D / codec / D2H on three streams give exactly the
+    sequential path's decoded vectors."""
+    from fl_sim_amd.host import HostCodecPipeline
+
+    codec = _codec()
+    n, k, m = 1_000_003, 10_000, 5
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    hx = [(torch.randn(n, generator=gen) * 1e-3).pin_memory() for _ in range(m)]
+    hout = [torch.empty(n, dtype=torch.float32).pin_memory() for _ in range(m)]
+    pipe = HostCodecPipeline(n, torch.device(DEV))
+    sizes = pipe.run(hx, hout, k, 127, seeds=[11] * m, counters=list(range(m)))
+    pipe.synchronize()
+    for i in range(m):
+        pkt = codec.stacked_encode(hx[i].to(DEV), k, 127, seed=11, counter=i)
+        ref = codec.stacked_decode(pkt).cpu()
+        assert torch.equal(hout[i], ref)
+        assert sizes[i] == pkt.nbytes
+    with pytest.raises(ValueError):
+        pipe.run([torch.empty(n)], [hout[0]], k)  # not pinned
