@@ -39,6 +39,41 @@ __global__ __launch_bounds__(1024) void w_ranges(float* __restrict__ y, long nch
   }
 }
 
+
+// one-wave workgroups writing NB KB each (lane-strided 1 KB store instructions, in order)
+template <int NB>
+__global__ __launch_bounds__(64) void w_wave(float* __restrict__ y) {
+  const int lane = threadIdx.x;
+  f32x4* p = (f32x4*)(y + (long)blockIdx.x * NB * 256);
+  f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < NB; ++u) p[lane + 64 * u] = z;
+}
+
+
+// one-wave workgroups writing two 4 KB pieces half the array apart (tile g and g + ntiles / 2)
+__global__ __launch_bounds__(64) void w_wave_split(float* __restrict__ y, long half_tiles) {
+  const int lane = threadIdx.x;
+  f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32x4* p = (f32x4*)(y + ((long)blockIdx.x + h * half_tiles) * 1024);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p[lane + 64 * u] = z;
+  }
+}
+// one-wave workgroups writing 8 KB with the two 4 KB halves' stores interleaved
+__global__ __launch_bounds__(64) void w_wave_8k_inter(float* __restrict__ y) {
+  const int lane = threadIdx.x;
+  f32x4* p = (f32x4*)(y + (long)blockIdx.x * 2048);
+  f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    p[lane + 64 * u] = z;
+    p[256 + lane + 64 * u] = z;
+  }
+}
+
 template <typename F>
 double timeit(F f, int reps) {
   hipEvent_t a, b;
@@ -68,6 +103,11 @@ int main() {
     rep("chunks 64KB, wave-contiguous nt", timeit([&] { w_chunks<2><<<cu, 1024>>>(y, nch); }, 20));
     rep("per-block ranges (reference)", timeit([&] { w_ranges<<<cu, 1024>>>(y, nch); }, 20));
     rep("memset", timeit([&] { CK(hipMemsetAsync(y, 0, n * 4)); }, 20));
+    rep("1-wave WG, 4 KB", timeit([&] { w_wave<4><<<n / 1024, 64>>>(y); }, 20));
+    rep("1-wave WG, 8 KB", timeit([&] { w_wave<8><<<n / 2048, 64>>>(y); }, 20));
+    rep("1-wave WG, 16 KB", timeit([&] { w_wave<16><<<n / 4096, 64>>>(y); }, 20));
+    rep("1-wave WG, 2 x 4 KB half apart", timeit([&] { w_wave_split<<<n / 2048, 64>>>(y, n / 2048); }, 20));
+    rep("1-wave WG, 8 KB halves interleaved", timeit([&] { w_wave_8k_inter<<<n / 2048, 64>>>(y); }, 20));
   }
   return 0;
 }
