@@ -422,3 +422,44 @@ def test_host_pipeline_matches_sequential():
         assert sizes[i] == pkt.nbytes
     with pytest.raises(ValueError):
         pipe.run([torch.empty(n)], [hout[0]], k)  # not pinned
+
+
+def _adversarial(name):
+    """Inputs that drive the encoder off its fast path: a floor that admits too few elements (fallback pass), a
+    region with more candidates than a block's LDS (x-mode), and massive ties at the k-th value."""
+    if name == "fallback":
+        n, S = 4_000_000, 32768
+        x = np.full(n, 1e-6, dtype=np.float32)
+        x[((np.arange(S) + 0.5) * n / S).astype(np.int64)] = 1.0
+        g = np.random.default_rng(2)
+        x[g.integers(0, n, 500_000)] = g.random(500_000).astype(np.float32) * 1e-3
+        return x, 200_000
+    if name == "skewed":
+        g = np.random.default_rng(3)
+        x = (g.standard_normal(5_000_000) * 1e-4).astype(np.float32)
+        x[1_000_000:1_100_000] *= 1000
+        return x, 50_000
+    g = np.random.default_rng(4)  # ties: a third of the vector holds the k-th value exactly
+    x = (g.standard_normal(3_000_000) * 1e-3).astype(np.float32)
+    x[g.integers(0, x.size, 1_000_000)] = np.float32(2e-3)
+    return x, 30_000
+
+
+@pytest.mark.parametrize("name", ["fallback", "skewed", "ties"])
+def test_stacked_adversarial_matches_oracle_with_tiles(name):
+    """The stacked codec off its fast path (fallback pass, x-mode blocks, heavy ties): wire, norm, tile pointers
+    and decode equal the oracle's and the index pass's."""
+    codec = _codec()
+    x, k = _adversarial(name)
+    n = x.size
+    xd = torch.from_numpy(x).to(DEV)
+    pkt = codec.stacked_encode(xd, k, 127, seed=7, counter=3)
+    u_all = ref.philox_uniforms(n, 7, 3)
+    exp_out, exp_idx, exp_codes, pn = ref.stacked(x, k, 127, lambda idx: u_all[idx])
+    assert np.array_equal(pkt.idx.cpu().numpy().astype(np.int64), exp_idx)
+    assert np.array_equal(pkt.codes[:k].cpu().numpy(), exp_codes)
+    assert pkt.norm.item() == pn
+    ref_tiles = torch.empty_like(pkt.tiles)
+    codec.call("flc_tile_index", codec._p(pkt.idx), k, n, codec._p(ref_tiles), codec._stream(xd.device))
+    assert torch.equal(pkt.tiles, ref_tiles)
+    assert gc.same_bits(codec.stacked_decode(pkt).cpu().numpy(), exp_out)
