@@ -589,6 +589,21 @@ __device__ __forceinline__ void step_process(const float4 (&v)[kStepF4], int64_t
 // `ep` (packed flags, one word per block), then one wave polls all G flags (each lane a few words per
 // round, relaxed agent-scope loads, a wave-wide vote, sleep between rounds).  No leader and no
 // contended counter: 256 arrivals on ONE word serialise at the memory-side atomic unit (measured ~5 us).
+// every block's flag at `ep` or later: all of a lane's flag loads issued together (no short-circuit, so one
+// round trip per poll rather than one per flag), then one wave-wide vote
+__device__ __forceinline__ bool all_arrived(const EncWs& w, unsigned ep) {
+  const int tid = threadIdx.x & (kWave - 1), G = (int)gridDim.x;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < kMaxBlocks / kWave; ++i) {
+    const int b = tid + i * kWave;
+    if (i * kWave >= G) break;  // (uniform)
+    const unsigned f = __hip_atomic_load(w.flags() + (b < G ? b : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ok &= b >= G || (int)(f - ep) >= 0;
+  }
+  return __ballot(!ok) == 0ull;
+}
+
 __device__ __forceinline__ void exchange(const EncWs& w, unsigned ep) {
   drain_stores();
   __syncthreads();
@@ -597,10 +612,7 @@ __device__ __forceinline__ void exchange(const EncWs& w, unsigned ep) {
   if (tid < kWave) {
     unsigned spins = 0;
     for (;;) {
-      bool ok = true;
-      for (int b = tid; b < (int)gridDim.x; b += kWave)
-        ok = ok && (int)(__hip_atomic_load(w.flags() + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ep) >= 0;
-      if (__ballot(!ok) == 0ull) break;
+      if (all_arrived(w, ep)) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 22)) {  // ~1 s: a block never arrived; flag it and let the launch drain
         if (tid == 0) __hip_atomic_fetch_or(&w.st()->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -624,10 +636,7 @@ __device__ __forceinline__ void exchange_work(const EncWs& w, unsigned ep, unsig
   if (tid < kWave) {
     unsigned spins = 0;
     for (;;) {
-      bool ok = true;
-      for (int b = tid; b < (int)gridDim.x; b += kWave)
-        ok = ok && (int)(__hip_atomic_load(w.flags() + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - ep) >= 0;
-      if (__ballot(!ok) == 0ull) break;
+      if (all_arrived(w, ep)) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 22)) {  // ~1 s: a block never arrived; flag it and let the launch drain
         if (tid == 0) __hip_atomic_fetch_or(&w.st()->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
