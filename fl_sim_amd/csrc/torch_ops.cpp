@@ -1,0 +1,371 @@
+// torch_ops.cpp — `torch.ops.flcodec.*`: the codec and aggregation entry points of include/flcodec.h registered
+// with the PyTorch dispatcher, so that graph code, torch.compile and other C++ callers
+// reach the gfx950 kernels without the ctypes layer.
+//
+// This is a thin adapter over the same C ABI (libflcodec.so, linked with rpath $ORIGIN): tensors in, tensors out,
+// every launch on the current HIP stream of the input's device, nothing synchronised.  The functional ops have
+// Meta kernels too (output shapes only), so they trace under FakeTensor.  Each op names the reference lines it
+// stands for through the C-ABI function it calls (see the header's comments).
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "flcodec.h"
+
+namespace {
+
+constexpr int64_t kTile = FLC_TILE;
+
+void check(int rc, const char* what) {
+  TORCH_CHECK(rc == FLC_OK, "flcodec: ", what, " failed with status ", rc, ": ", flc_last_error());
+}
+
+void* stream_of(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+// fp32, on a HIP device, contiguous and 16-byte aligned (the kernels' vector loads); copies once otherwise
+at::Tensor dev_f32(const at::Tensor& x, const char* name) {
+  TORCH_CHECK(x.is_cuda(), "flcodec: ", name, " must be on a HIP device (got ", x.device(), ")");
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "flcodec: ", name, " must be float32 (got ", x.scalar_type(), ")");
+  if (!x.is_contiguous() || reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 != 0) return x.contiguous().clone();
+  return x;
+}
+
+void same_device(const at::Tensor& a, const at::Tensor& b, const char* name) {
+  TORCH_CHECK(b.is_cuda() && b.device() == a.device(), "flcodec: ", name, " must be on ", a.device());
+}
+
+// Zero-filled workspace per (device, stream, kind), grown on demand (the C ABI's contract: zero once, then reuse on
+// the same stream).  Leaked on purpose: tensors must not be freed after the HIP runtime has gone at exit.
+at::Tensor workspace(const at::Tensor& like, size_t nbytes, int kind) {
+  static std::mutex mu;
+  static auto* cache = new std::map<std::tuple<int, void*, int>, at::Tensor>();
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_tuple((int)like.device().index(), stream_of(like), kind);
+  auto it = cache->find(key);
+  if (it == cache->end() || (size_t)it->second.numel() < nbytes) {
+    at::Tensor t = at::zeros({(int64_t)std::max<size_t>(nbytes, 256)}, like.options().dtype(at::kByte));
+    (*cache)[key] = t;
+    return t;
+  }
+  return it->second;
+}
+enum { kWsQuant = 0, kWsNatural = 1, kWsTopk = 2 };
+
+int code_bits(int64_t levels) {
+  TORCH_CHECK(levels >= 1, "flcodec: levels must be >= 1");
+  const int b = 1 + (int)std::ceil(std::log2((double)levels + 1.0));
+  for (int c : {2, 4, 8})
+    if (b <= c) return c;
+  TORCH_CHECK(false, "flcodec: levels=", levels, " does not fit an 8-bit code (at most 127 levels)");
+  return 0;
+}
+
+int64_t n_tiles(int64_t n) { return (n + kTile - 1) / kTile + 1; }
+
+int norm_kind(int64_t p) {
+  TORCH_CHECK(p == 0 || p == 2, "flcodec: p must be 0 (inf norm) or 2");
+  return p == 0 ? FLC_NORM_INF : FLC_NORM_L2;
+}
+
+// ------------------------------------------------------------------------------------------- stacked codec
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode(const at::Tensor& x_, int64_t k,
+                                                                            int64_t levels, int64_t seed,
+                                                                            int64_t counter) {
+  at::Tensor x = dev_f32(x_, "x").reshape({-1});
+  c10::DeviceGuard g(x.device());
+  const int64_t n = x.numel();
+  at::Tensor idx = at::empty({k}, x.options().dtype(at::kInt));
+  at::Tensor codes = at::empty({std::max<int64_t>(k, 16)}, x.options().dtype(at::kByte));
+  at::Tensor norm = at::empty({1}, x.options());
+  at::Tensor tiles = at::empty({n_tiles(n)}, x.options().dtype(at::kInt));
+  at::Tensor ws = workspace(x, flc_topk_workspace_size(n, k), kWsTopk);
+  check(flc_stacked_encode_tiled(x.data_ptr<float>(), n, k, (int)levels, (uint64_t)seed, (uint64_t)counter, nullptr,
+                                 idx.data_ptr<int32_t>(), codes.data_ptr<uint8_t>(), norm.data_ptr<float>(),
+                                 reinterpret_cast<uint32_t*>(tiles.data_ptr<int32_t>()), ws.data_ptr(),
+                                 (size_t)ws.numel(), stream_of(x)),
+        "stacked_encode");
+  return {idx, codes.narrow(0, 0, k), norm, tiles};
+}
+
+void stacked_decode_into(at::Tensor& out, const at::Tensor& idx, const at::Tensor& codes, const at::Tensor& norm,
+                         const at::Tensor& tiles, int64_t levels, double weight, bool accumulate) {
+  same_device(out, idx, "idx");
+  same_device(out, codes, "codes");
+  same_device(out, norm, "norm");
+  same_device(out, tiles, "tiles");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && codes.scalar_type() == at::kByte && norm.scalar_type() == at::kFloat &&
+                  tiles.scalar_type() == at::kInt,
+              "flcodec: stacked packet dtypes are (int32 idx, uint8 codes, fp32 norm, int32 tiles)");
+  TORCH_CHECK(idx.is_contiguous() && codes.is_contiguous() && tiles.is_contiguous(), "flcodec: packet not contiguous");
+  const int64_t n = out.numel(), k = idx.numel();
+  TORCH_CHECK(codes.numel() >= k && tiles.numel() == n_tiles(n), "flcodec: packet does not match n=", n, ", k=", k);
+  c10::DeviceGuard g(out.device());
+  check(flc_stacked_decode_tiled(idx.data_ptr<int32_t>(), codes.data_ptr<uint8_t>(), k, (int)levels,
+                                 norm.data_ptr<float>(), n, (float)weight, accumulate ? 1 : 0, out.data_ptr<float>(),
+                                 reinterpret_cast<const uint32_t*>(tiles.data_ptr<int32_t>()), stream_of(out)),
+        "stacked_decode");
+}
+
+at::Tensor stacked_decode(const at::Tensor& idx, const at::Tensor& codes, const at::Tensor& norm,
+                          const at::Tensor& tiles, int64_t n, int64_t levels, double weight) {
+  at::Tensor out = at::empty({n}, idx.options().dtype(at::kFloat));
+  stacked_decode_into(out, idx, codes, norm, tiles, levels, weight, false);
+  return out;
+}
+
+at::Tensor& stacked_decode_accumulate_(at::Tensor& out, const at::Tensor& idx, const at::Tensor& codes,
+                                       const at::Tensor& norm, const at::Tensor& tiles, int64_t levels,
+                                       double weight) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous(),
+              "flcodec: out must be a contiguous fp32 HIP tensor");
+  stacked_decode_into(out, idx, codes, norm, tiles, levels, weight, true);
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------------- top-k
+std::tuple<at::Tensor, at::Tensor, at::Tensor> topk_encode(const at::Tensor& x_, int64_t k) {
+  at::Tensor x = dev_f32(x_, "x").reshape({-1});
+  c10::DeviceGuard g(x.device());
+  const int64_t n = x.numel();
+  at::Tensor idx = at::empty({k}, x.options().dtype(at::kInt));
+  at::Tensor val = at::empty({k}, x.options());
+  at::Tensor tiles = at::empty({n_tiles(n)}, x.options().dtype(at::kInt));
+  at::Tensor ws = workspace(x, flc_topk_workspace_size(n, k), kWsTopk);
+  check(flc_topk_encode_tiled(x.data_ptr<float>(), n, k, idx.data_ptr<int32_t>(), val.data_ptr<float>(),
+                              reinterpret_cast<uint32_t*>(tiles.data_ptr<int32_t>()), ws.data_ptr(),
+                              (size_t)ws.numel(), stream_of(x)),
+        "topk_encode");
+  return {idx, val, tiles};
+}
+
+at::Tensor sparse_decode(const at::Tensor& idx, const at::Tensor& val_, const at::Tensor& tiles, int64_t n,
+                         double scale, double weight) {
+  at::Tensor val = dev_f32(val_, "val");
+  same_device(val, idx, "idx");
+  same_device(val, tiles, "tiles");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && tiles.scalar_type() == at::kInt && idx.is_contiguous() &&
+                  tiles.is_contiguous(),
+              "flcodec: idx and tiles must be contiguous int32");
+  TORCH_CHECK(idx.numel() == val.numel() && tiles.numel() == n_tiles(n), "flcodec: sparse stream does not match n");
+  c10::DeviceGuard g(val.device());
+  at::Tensor out = at::empty({n}, val.options());
+  check(flc_sparse_decode_tiled(idx.data_ptr<int32_t>(), val.data_ptr<float>(), idx.numel(), (float)scale, n,
+                                (float)weight, 0, out.data_ptr<float>(),
+                                reinterpret_cast<const uint32_t*>(tiles.data_ptr<int32_t>()), stream_of(out)),
+        "sparse_decode");
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------- dense dithering
+at::Tensor quant_norm(const at::Tensor& x_, int64_t p) {
+  at::Tensor x = dev_f32(x_, "x");
+  TORCH_CHECK(x.dim() == 2, "flcodec: quant_norm takes a [rows, d] batch");
+  c10::DeviceGuard g(x.device());
+  const int64_t rows = x.size(0), d = x.size(1);
+  at::Tensor norms = at::empty({rows}, x.options());
+  at::Tensor ws = workspace(x, flc_quant_workspace_size(rows, d), kWsQuant);
+  check(flc_quant_norm(x.data_ptr<float>(), rows, d, norm_kind(p), norms.data_ptr<float>(), ws.data_ptr(),
+                       (size_t)ws.numel(), stream_of(x)),
+        "quant_norm");
+  return norms;
+}
+
+std::tuple<at::Tensor, at::Tensor> quant_encode(const at::Tensor& x_, const at::Tensor& norms, int64_t kind,
+                                                int64_t levels, int64_t seed, int64_t counter) {
+  at::Tensor x = dev_f32(x_, "x");
+  TORCH_CHECK(x.dim() == 2, "flcodec: quant_encode takes a [rows, d] batch");
+  same_device(x, norms, "norms");
+  const int64_t rows = x.size(0), d = x.size(1);
+  TORCH_CHECK(norms.scalar_type() == at::kFloat && norms.numel() == rows && norms.is_contiguous(),
+              "flcodec: norms must be contiguous fp32 of one entry per row");
+  c10::DeviceGuard g(x.device());
+  const int bits = code_bits(levels);
+  at::Tensor codes = at::empty({std::max<int64_t>((rows * d * bits + 7) / 8, 1)}, x.options().dtype(at::kByte));
+  at::Tensor nnz = at::empty({rows}, x.options().dtype(at::kLong));
+  at::Tensor ws = workspace(x, flc_quant_workspace_size(rows, d), kWsQuant);
+  check(flc_quant_encode(x.data_ptr<float>(), rows, d, (int)kind, (int)levels, bits, norms.data_ptr<float>(),
+                         (uint64_t)seed, (uint64_t)counter, nullptr, codes.data_ptr<uint8_t>(), nnz.data_ptr<int64_t>(),
+                         ws.data_ptr(), (size_t)ws.numel(), stream_of(x)),
+        "quant_encode");
+  return {codes, nnz};
+}
+
+at::Tensor quant_decode(const at::Tensor& codes, const at::Tensor& norms, int64_t d, int64_t kind, int64_t levels) {
+  same_device(norms, codes, "codes");
+  TORCH_CHECK(codes.scalar_type() == at::kByte && codes.is_contiguous() && norms.scalar_type() == at::kFloat &&
+                  norms.is_contiguous(),
+              "flcodec: quant packet is (uint8 codes, fp32 norms)");
+  const int64_t rows = norms.numel();
+  const int bits = code_bits(levels);
+  TORCH_CHECK(codes.numel() >= (rows * d * bits + 7) / 8, "flcodec: codes too short for [", rows, ", ", d, "]");
+  c10::DeviceGuard g(norms.device());
+  at::Tensor out = at::empty({rows, d}, norms.options());
+  check(flc_quant_decode(codes.data_ptr<uint8_t>(), rows, d, (int)kind, (int)levels, bits, norms.data_ptr<float>(),
+                         nullptr, 0, out.data_ptr<float>(), stream_of(out)),
+        "quant_decode");
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------- natural compressor
+std::tuple<at::Tensor, at::Tensor> natural_encode(const at::Tensor& x_, int64_t seed, int64_t counter) {
+  at::Tensor x = dev_f32(x_, "x").reshape({-1});
+  c10::DeviceGuard g(x.device());
+  const int64_t n = x.numel();
+  at::Tensor codes = at::empty({n}, x.options().dtype(at::kShort));
+  at::Tensor nnz = at::empty({1}, x.options().dtype(at::kLong));
+  at::Tensor ws = workspace(x, flc_natural_workspace_size(n), kWsNatural);
+  check(flc_natural_encode(x.data_ptr<float>(), n, (uint64_t)seed, (uint64_t)counter, nullptr,
+                           reinterpret_cast<uint16_t*>(codes.data_ptr<int16_t>()), nnz.data_ptr<int64_t>(),
+                           ws.data_ptr(), (size_t)ws.numel(), stream_of(x)),
+        "natural_encode");
+  return {codes, nnz};
+}
+
+at::Tensor natural_decode(const at::Tensor& codes, double weight) {
+  TORCH_CHECK(codes.is_cuda() && codes.scalar_type() == at::kShort && codes.is_contiguous(),
+              "flcodec: natural codes must be contiguous int16 on a HIP device");
+  c10::DeviceGuard g(codes.device());
+  at::Tensor out = at::empty({codes.numel()}, codes.options().dtype(at::kFloat));
+  check(flc_natural_decode(reinterpret_cast<const uint16_t*>(codes.data_ptr<int16_t>()), codes.numel(),
+                           (float)weight, 0, out.data_ptr<float>(), stream_of(out)),
+        "natural_decode");
+  return out;
+}
+
+// --------------------------------------------------------------------------------------------- aggregation
+at::Tensor& weighted_sum_(at::Tensor& dst, at::TensorList srcs, at::ArrayRef<double> weights, int64_t init_mode,
+                          double beta) {
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(),
+              "flcodec: dst must be a contiguous fp32 HIP tensor");
+  TORCH_CHECK(srcs.size() == weights.size(), "flcodec: one weight per source");
+  TORCH_CHECK(init_mode >= 0 && init_mode <= 2, "flcodec: init_mode is 0 (dst*beta), 1 (zero) or 2 (keep)");
+  c10::DeviceGuard g(dst.device());
+  std::vector<at::Tensor> keep;
+  std::vector<const float*> ptrs;
+  std::vector<float> w;
+  for (size_t m = 0; m < srcs.size(); ++m) {
+    same_device(dst, srcs[m], "every source");
+    TORCH_CHECK(srcs[m].numel() == dst.numel(), "flcodec: every source must have dst's number of elements");
+    keep.push_back(dev_f32(srcs[m], "src"));
+    ptrs.push_back(keep.back().data_ptr<float>());
+    w.push_back((float)weights[m]);
+  }
+  check(flc_weighted_sum(ptrs.data(), w.data(), (int)ptrs.size(), dst.numel(), (int)init_mode, (float)beta,
+                         dst.data_ptr<float>(), stream_of(dst)),
+        "weighted_sum");
+  return dst;
+}
+
+void fedopt_step_(at::Tensor& theta, const at::Tensor& delta_, const c10::optional<at::Tensor>& v, int64_t opt,
+                  double lr, double beta2, double tau) {
+  TORCH_CHECK(theta.is_cuda() && theta.scalar_type() == at::kFloat && theta.is_contiguous(),
+              "flcodec: theta must be a contiguous fp32 HIP tensor");
+  at::Tensor delta = dev_f32(delta_, "delta");
+  same_device(theta, delta, "delta");
+  TORCH_CHECK(delta.numel() == theta.numel(), "flcodec: delta must match theta");
+  TORCH_CHECK(opt >= FLC_OPT_AVG && opt <= FLC_OPT_ADAM, "flcodec: opt is 0 avg, 1 adagrad, 2 yogi, 3 adam");
+  float* vp = nullptr;
+  if (opt != FLC_OPT_AVG) {
+    TORCH_CHECK(v.has_value(), "flcodec: adaptive optimisers need the second-moment tensor v");
+    same_device(theta, *v, "v");
+    TORCH_CHECK(v->scalar_type() == at::kFloat && v->is_contiguous() && v->numel() == theta.numel(),
+                "flcodec: v must be contiguous fp32 like theta");
+    vp = v->data_ptr<float>();
+  }
+  c10::DeviceGuard g(theta.device());
+  check(flc_fedopt_step(theta.data_ptr<float>(), delta.data_ptr<float>(), vp, theta.numel(), (int)opt, lr, beta2, tau,
+                        stream_of(theta)),
+        "fedopt_step");
+}
+
+// --------------------------------------------------------------------------------- Meta kernels (shapes only)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode_meta(const at::Tensor& x, int64_t k,
+                                                                                 int64_t, int64_t, int64_t) {
+  const int64_t n = x.numel();
+  return {at::empty({k}, x.options().dtype(at::kInt)), at::empty({k}, x.options().dtype(at::kByte)),
+          at::empty({1}, x.options().dtype(at::kFloat)), at::empty({n_tiles(n)}, x.options().dtype(at::kInt))};
+}
+at::Tensor stacked_decode_meta(const at::Tensor& idx, const at::Tensor&, const at::Tensor&, const at::Tensor&,
+                               int64_t n, int64_t, double) {
+  return at::empty({n}, idx.options().dtype(at::kFloat));
+}
+std::tuple<at::Tensor, at::Tensor, at::Tensor> topk_encode_meta(const at::Tensor& x, int64_t k) {
+  return {at::empty({k}, x.options().dtype(at::kInt)), at::empty({k}, x.options().dtype(at::kFloat)),
+          at::empty({n_tiles(x.numel())}, x.options().dtype(at::kInt))};
+}
+at::Tensor sparse_decode_meta(const at::Tensor&, const at::Tensor& val, const at::Tensor&, int64_t n, double, double) {
+  return at::empty({n}, val.options().dtype(at::kFloat));
+}
+at::Tensor quant_norm_meta(const at::Tensor& x, int64_t) { return at::empty({x.size(0)}, x.options()); }
+std::tuple<at::Tensor, at::Tensor> quant_encode_meta(const at::Tensor& x, const at::Tensor&, int64_t,
+                                                     int64_t levels, int64_t, int64_t) {
+  const int64_t rows = x.size(0), d = x.size(1);
+  return {at::empty({std::max<int64_t>((rows * d * code_bits(levels) + 7) / 8, 1)}, x.options().dtype(at::kByte)),
+          at::empty({rows}, x.options().dtype(at::kLong))};
+}
+at::Tensor quant_decode_meta(const at::Tensor&, const at::Tensor& norms, int64_t d, int64_t, int64_t) {
+  return at::empty({norms.numel(), d}, norms.options());
+}
+std::tuple<at::Tensor, at::Tensor> natural_encode_meta(const at::Tensor& x, int64_t, int64_t) {
+  return {at::empty({x.numel()}, x.options().dtype(at::kShort)), at::empty({1}, x.options().dtype(at::kLong))};
+}
+at::Tensor natural_decode_meta(const at::Tensor& codes, double) {
+  return at::empty({codes.numel()}, codes.options().dtype(at::kFloat));
+}
+
+}  // namespace
+
+TORCH_LIBRARY(flcodec, m) {
+  m.def("stacked_encode(Tensor x, int k, int levels=127, int seed=0, int counter=0) "
+        "-> (Tensor idx, Tensor codes, Tensor norm, Tensor tiles)");
+  m.def("stacked_decode(Tensor idx, Tensor codes, Tensor norm, Tensor tiles, int n, int levels=127, "
+        "float weight=1.0) -> Tensor");
+  m.def("stacked_decode_accumulate_(Tensor(a!) out, Tensor idx, Tensor codes, Tensor norm, Tensor tiles, "
+        "int levels=127, float weight=1.0) -> Tensor(a!)");
+  m.def("topk_encode(Tensor x, int k) -> (Tensor idx, Tensor val, Tensor tiles)");
+  m.def("sparse_decode(Tensor idx, Tensor val, Tensor tiles, int n, float scale=1.0, float weight=1.0) -> Tensor");
+  m.def("quant_norm(Tensor x, int p=0) -> Tensor");
+  m.def("quant_encode(Tensor x, Tensor norms, int kind, int levels, int seed=0, int counter=0) "
+        "-> (Tensor codes, Tensor nnz)");
+  m.def("quant_decode(Tensor codes, Tensor norms, int d, int kind, int levels) -> Tensor");
+  m.def("natural_encode(Tensor x, int seed=0, int counter=0) -> (Tensor codes, Tensor nnz)");
+  m.def("natural_decode(Tensor codes, float weight=1.0) -> Tensor");
+  m.def("weighted_sum_(Tensor(a!) dst, Tensor[] srcs, float[] weights, int init_mode, float beta=0.0) -> Tensor(a!)");
+  m.def("fedopt_step_(Tensor(a!) theta, Tensor delta, Tensor(b!)? v, int opt, float lr, float beta2, float tau) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
+  m.impl("stacked_encode", &stacked_encode);
+  m.impl("stacked_decode", &stacked_decode);
+  m.impl("stacked_decode_accumulate_", &stacked_decode_accumulate_);
+  m.impl("topk_encode", &topk_encode);
+  m.impl("sparse_decode", &sparse_decode);
+  m.impl("quant_norm", &quant_norm);
+  m.impl("quant_encode", &quant_encode);
+  m.impl("quant_decode", &quant_decode);
+  m.impl("natural_encode", &natural_encode);
+  m.impl("natural_decode", &natural_decode);
+  m.impl("weighted_sum_", &weighted_sum_);
+  m.impl("fedopt_step_", &fedopt_step_);
+}
+
+TORCH_LIBRARY_IMPL(flcodec, Meta, m) {
+  m.impl("stacked_encode", &stacked_encode_meta);
+  m.impl("stacked_decode", &stacked_decode_meta);
+  m.impl("topk_encode", &topk_encode_meta);
+  m.impl("sparse_decode", &sparse_decode_meta);
+  m.impl("quant_norm", &quant_norm_meta);
+  m.impl("quant_encode", &quant_encode_meta);
+  m.impl("quant_decode", &quant_decode_meta);
+  m.impl("natural_encode", &natural_encode_meta);
+  m.impl("natural_decode", &natural_decode_meta);
+}

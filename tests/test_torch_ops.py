@@ -1,0 +1,193 @@
+"""``torch.ops.flcodec.*`` (fl_sim_amd/csrc/torch_ops.cpp): the dispatcher registration of the codec and aggregation
+entry points.
+
+CPU: the library loads, every op carries its schema, the Meta kernels infer the output shapes, and a CPU tensor is
+refused (no CPU kernel, no fallback).  GPU: each op reproduces the ctypes path (``fl_sim_amd.codec``, itself checked
+against the oracle in test_gpu_codec.py) bit for bit, and the stacked op matches the oracle directly.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import compressors_ref as ref
+from tests import golden_cases as gc
+
+OPS = {
+    "stacked_encode": "flcodec::stacked_encode(Tensor x, int k, int levels=127, int seed=0, int counter=0) -> "
+                      "(Tensor idx, Tensor codes, Tensor norm, Tensor tiles)",
+    "stacked_decode": "flcodec::stacked_decode(Tensor idx, Tensor codes, Tensor norm, Tensor tiles, int n, "
+                      "int levels=127, float weight=1.) -> Tensor",
+    "stacked_decode_accumulate_": None,
+    "topk_encode": "flcodec::topk_encode(Tensor x, int k) -> (Tensor idx, Tensor val, Tensor tiles)",
+    "sparse_decode": None,
+    "quant_norm": None,
+    "quant_encode": None,
+    "quant_decode": None,
+    "natural_encode": None,
+    "natural_decode": None,
+    "weighted_sum_": None,
+    "fedopt_step_": None,
+}
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import fl_sim_amd
+
+    fl_sim_amd.load_torch_ops()
+    return torch.ops.flcodec
+
+
+def test_every_op_registered(ops):
+    for name, schema in OPS.items():
+        op = getattr(ops, name)
+        if schema is not None:
+            assert str(op.default._schema) == schema
+
+
+def test_meta_shapes(ops):
+    n, k = 100_003, 1000
+    x = torch.empty(n, device="meta")
+    idx, codes, norm, tiles = ops.stacked_encode(x, k)
+    assert (idx.shape, idx.dtype) == ((k,), torch.int32)
+    assert (codes.shape, codes.dtype) == ((k,), torch.uint8)
+    assert (norm.shape, norm.dtype) == ((1,), torch.float32)
+    assert (tiles.shape, tiles.dtype) == (((n + 1023) // 1024 + 1,), torch.int32)
+    assert ops.stacked_decode(idx, codes, norm, tiles, n).shape == (n,)
+    i2, v2, t2 = ops.topk_encode(x, k)
+    assert (v2.shape, v2.dtype, t2.shape) == ((k,), torch.float32, tiles.shape)
+    assert ops.sparse_decode(i2, v2, t2, n).shape == (n,)
+    x2 = torch.empty(3, 1000, device="meta")
+    assert ops.quant_norm(x2, 0).shape == (3,)
+    for levels, bits in ((1, 2), (3, 4), (7, 4), (8, 8), (127, 8)):
+        c, nnz = ops.quant_encode(x2, torch.empty(3, device="meta"), 0, levels)
+        assert c.shape == ((3 * 1000 * bits + 7) // 8,) and nnz.shape == (3,)
+    assert ops.quant_decode(c, torch.empty(3, device="meta"), 1000, 0, 127).shape == (3, 1000)
+    nc, nz = ops.natural_encode(x)
+    assert (nc.shape, nc.dtype, nz.dtype) == ((n,), torch.int16, torch.int64)
+    assert ops.natural_decode(nc).shape == (n,)
+
+
+def test_cpu_tensors_refused(ops):
+    with pytest.raises(NotImplementedError):
+        ops.stacked_encode(torch.zeros(64), 4)
+    with pytest.raises(NotImplementedError):
+        ops.weighted_sum_(torch.zeros(8), [torch.ones(8)], [0.5], 0)
+
+
+# ------------------------------------------------------------------------------------------------------ GPU parity
+def _x(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, generator=g) * 1e-3
+
+
+def _same(a, b):
+    a, b = a.cpu().numpy(), b.cpu().numpy()
+    return a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(4096, 41), (417_482, 4174), (1_000_003, 10_000)])
+def test_stacked_op_matches_ctypes_and_oracle(ops, n, k):
+    from fl_sim_amd import codec
+
+    x = _x(n, n)
+    xd = x.cuda()
+    idx, codes, norm, tiles = ops.stacked_encode(xd, k, 127, 7, 3)
+    pkt = codec.stacked_encode(xd, k, 127, seed=7, counter=3)
+    assert _same(idx, pkt.idx) and _same(codes, pkt.codes[:k]) and _same(norm, pkt.norm) and _same(tiles, pkt.tiles)
+    out = ops.stacked_decode(idx, codes, norm, tiles, n)
+    assert _same(out, codec.stacked_decode(pkt))
+    if n <= 417_482:
+        u = ref.philox_uniforms(n, 7, 3)
+        exp, exp_idx, exp_codes, exp_norm = ref.stacked(x.numpy(), k, 127, lambda i: u[i])
+        assert np.array_equal(idx.cpu().numpy().astype(np.int64), exp_idx)
+        assert np.array_equal(codes.cpu().numpy(), exp_codes)
+        assert gc.same_bits(out.cpu().numpy(), exp)
+    acc = torch.full((n,), 0.25, device="cuda")
+    r = ops.stacked_decode_accumulate_(acc, idx, codes, norm, tiles, 127, 0.5)
+    assert r.data_ptr() == acc.data_ptr()
+    exp_acc = torch.full((n,), 0.25, device="cuda")
+    codec.stacked_decode(pkt, out=exp_acc, weight=0.5, accumulate=True)
+    assert _same(acc, exp_acc)
+
+
+@pytest.mark.gpu
+def test_topk_and_sparse_ops(ops):
+    from fl_sim_amd import codec
+
+    n, k = 2_000_000, 20_000
+    x = _x(n, 1).cuda()
+    idx, val, tiles = ops.topk_encode(x, k)
+    e_idx, e_val, e_tiles = codec.topk_encode(x, k, with_tiles=True)
+    assert _same(idx, e_idx) and _same(val, e_val) and _same(tiles, e_tiles)
+    kept, vals = ref.topk_kept(x.cpu().numpy(), k)
+    assert np.array_equal(idx.cpu().numpy().astype(np.int64), kept)
+    out = ops.sparse_decode(idx, val, tiles, n, 2.0, 0.5)
+    assert _same(out, codec.sparse_decode(e_idx, e_val, n, scale=2.0, weight=0.5, tiles=e_tiles))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("levels", [1, 7, 127])
+@pytest.mark.parametrize("p", [0, 2])
+def test_quant_ops(ops, levels, p):
+    import math
+
+    from fl_sim_amd import codec
+
+    x = _x(4 * 10_001, levels).reshape(4, 10_001).cuda()
+    norms = ops.quant_norm(x, p)
+    assert _same(norms, codec.quant_norm(x, math.inf if p == 0 else 2))
+    codes, nnz = ops.quant_encode(x, norms, 0, levels, 5, 9)
+    pkt = codec.quant_encode(x, 0, levels, norms, seed=5, counter=9)
+    assert _same(codes, pkt.codes) and _same(nnz, pkt.nnz)
+    assert _same(ops.quant_decode(codes, norms, 10_001, 0, levels), codec.quant_decode(pkt))
+
+
+@pytest.mark.gpu
+def test_natural_ops(ops):
+    from fl_sim_amd import codec
+
+    x = _x(100_000, 3).cuda()
+    x[::7] = 0
+    codes, nnz = ops.natural_encode(x, 2, 4)
+    e_codes, e_nnz = codec.natural_encode(x, seed=2, counter=4)
+    assert _same(codes, e_codes) and _same(nnz, e_nnz)
+    assert _same(ops.natural_decode(codes, 0.5), codec.natural_decode(e_codes, x.numel(), weight=0.5))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [0, 1, 2, 3])
+def test_aggregation_ops(ops, opt):
+    from fl_sim_amd import codec
+
+    n = 417_482
+    srcs = [_x(n, 10 + i).cuda() for i in range(5)]
+    w = [float(np.float32(1.0 / (i + 2))) for i in range(5)]
+    dst = _x(n, 99).cuda()
+    exp = dst.clone()
+    r = ops.weighted_sum_(dst, srcs, w, 0, 0.3)
+    assert r.data_ptr() == dst.data_ptr()
+    codec.weighted_sum(exp, srcs, w, init_mode=0, beta=0.3)
+    assert _same(dst, exp)
+    theta, v = _x(n, 1).cuda(), _x(n, 2).cuda().abs()
+    theta2, v2 = theta.clone(), v.clone()
+    name = {0: "avg", 1: "adagrad", 2: "yogi", 3: "adam"}[opt]
+    ops.fedopt_step_(theta, dst, v if opt else None, opt, 0.1, 0.99, 1e-3)
+    codec.fedopt_step(theta2, dst, v2 if opt else None, name, 0.1, 0.99, 1e-3)
+    assert _same(theta, theta2) and _same(v, v2)
+
+
+@pytest.mark.gpu
+def test_ops_run_on_current_stream(ops):
+    """Launches follow torch's current stream (no implicit sync): a side-stream encode + decode equals the default."""
+    n, k = 1 << 20, 10_000
+    x = _x(n, 4).cuda()
+    base = ops.stacked_decode(*ops.stacked_encode(x, k, 127, 1, 1), n)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        got = ops.stacked_decode(*ops.stacked_encode(x, k, 127, 1, 1), n)
+    torch.cuda.current_stream().wait_stream(s)
+    assert _same(got, base)
