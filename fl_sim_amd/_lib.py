@@ -22,6 +22,7 @@ FLC_Q_NATURAL_DITHER = 1
 FLC_NORM_INF = 0
 FLC_NORM_L2 = 2
 FLC_OPT = {"avg": 0, "adagrad": 1, "yogi": 2, "adam": 3}
+FLC_PROX_NONE, FLC_PROX_L1, FLC_PROX_SCALE = 0, 1, 2
 
 # name -> (restype, argtypes); must list every function declared in include/flcodec.h
 SIGNATURES = {
@@ -82,6 +83,9 @@ SIGNATURES = {
     "flc_randk_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "flc_weighted_sum": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_float, c_void_p, c_void_p]),
     "flc_fedopt_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
+    "flc_feddr_combine": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_int, c_float, c_void_p]
+    ),
     "flc_probe_set": (c_int, [c_char_p]),
     "flc_probe_read": (c_int, [POINTER(c_double), POINTER(c_int64)]),
 }

@@ -8,6 +8,10 @@ subclasses unchanged (``class MyServer(AggregationMixin, FedAvgServer)``):
 * ``update_gradients``    — nodes.py:1165-1180   ``grad = Σ_m (ts_m / Σts) · g_m``
 * ``fedopt_update``       — _fedopt.py:196-265   ``δ = β0 δ + Σ_m (1-β0)/n · δ_m`` then the
                                                   avg / adagrad / yogi / adam server step
+* ``scaffold_update``     — _scaffold.py:158-167 ``θ += Σ_m lr/n · Δθ_m``, ``c += Σ_m 1/N · Δc_m``
+* ``ifca_update``         — _ifca.py:167-195     per cluster ``center += Σ_{m in cluster} 1/size · δ_m``
+                                                  (and the reference's client-id bookkeeping)
+* ``feddr_update``        — _feddr.py:166-190    ``y`` relaxation, ``x̃`` fold, ``θ = prox(c_x x̃ + c_y y)``
 
 Each tensor is folded in ONE launch (``flc_weighted_sum``): one read per message, one write, the
 fmaf chain in message order — bit-identical to the reference's sequential ``add_`` loop, which torch
@@ -17,11 +21,12 @@ the reference forms them and rounded to fp32 at the boundary, as torch does.
 
 from __future__ import annotations
 
+import math
 from typing import Iterable, List, Mapping, Optional, Sequence
 
 import torch
 
-from . import codec
+from . import _lib, codec
 
 
 def _params(ps) -> List[torch.Tensor]:
@@ -90,6 +95,95 @@ def fedopt_update(model_params: Sequence[torch.Tensor], delta_parameters: Sequen
         codec.fedopt_step(sp, dp, vp, opt if vp is not None else "avg", lr, betas[1], tau)
 
 
+def scaffold_update(model_params: Sequence[torch.Tensor], control_variates: Sequence[torch.Tensor],
+                    messages: Sequence[Mapping], lr: float, num_clients: int) -> None:
+    """_scaffold.py:158-167.  The reference interleaves the two folds per message; they touch different tensors,
+    so each tensor's fmaf chain (message order) is the same when folded in one launch per tensor."""
+    if len(messages) == 0:
+        raise ZeroDivisionError("division by zero")  # ratio_p = lr / len(messages) in the reference
+    ratio_p = lr / len(messages)
+    ratio_c = 1 / num_clients
+    for j, sp in enumerate(_params(model_params)):
+        codec.weighted_sum(sp, [_on(m["parameters_delta"][j], sp.device) for m in messages], [ratio_p] * len(messages),
+                           init_mode=2)
+    for j, cv in enumerate(control_variates):
+        codec.weighted_sum(cv, [_on(m["control_variates_delta"][j], cv.device) for m in messages],
+                           [ratio_c] * len(messages), init_mode=2)
+
+
+def ifca_update(cluster_centers: Mapping[int, dict], messages: Sequence[Mapping], num_clusters: int) -> None:
+    """_ifca.py:167-195 on ``{cluster_id: {"center_model_params": [...], "client_ids": [...]}}``, in place.
+
+    Host bookkeeping as in the reference: the round's members are listed, idle members of the previous round rejoin
+    their cluster, and each member is appended once more while its delta is folded (the reference's duplicate
+    entries are kept, so downstream code sees the same lists).  Each center tensor is folded in one launch."""
+    prev = {c: list(v["client_ids"]) for c, v in cluster_centers.items()}
+    for v in cluster_centers.values():
+        v["client_ids"] = []
+    sizes = {c: 0 for c in range(num_clusters)}
+    members: dict = {}
+    for m in messages:
+        sizes[m["cluster_id"]] += 1
+        cluster_centers[m["cluster_id"]]["client_ids"].append(m["client_id"])
+        members.setdefault(m["cluster_id"], []).append(m)
+    collected = set(i for v in cluster_centers.values() for i in v["client_ids"])
+    for c, v in cluster_centers.items():
+        v["client_ids"].extend(i for i in prev[c] if i not in collected)
+    for c, ms in members.items():
+        for j, p in enumerate(_params(cluster_centers[c]["center_model_params"])):
+            codec.weighted_sum(p, [_on(m["delta_parameters"][j], p.device) for m in ms], [1 / sizes[c]] * len(ms),
+                               init_mode=2)
+    for m in messages:
+        cluster_centers[m["cluster_id"]]["client_ids"].append(m["client_id"])
+
+
+_PROX_KIND = {"l1": "l1", "l2": "l2", "l2squared": "l2squared", "no": "none", "empty": "none", "zero": "none",
+              "none": "none", "null": "none"}
+_LINF = ("linf", "inf", "linfinity", "infinity", "linfty", "infty")
+
+
+def feddr_update(model_params: Sequence[torch.Tensor], y_params: Sequence[torch.Tensor],
+                 x_til_params: Sequence[torch.Tensor], messages: Sequence[Mapping], alpha: float, eta: float,
+                 num_clients: int, reg_type: str) -> None:
+    """_feddr.py:166-190 with the regularizer get_regularizer(reg_type, eta·N/(N+1)) builds (_feddr.py:147-150).
+
+    Per tensor: the x̃ fold (flc_weighted_sum), then one pass for the y relaxation, the combination and the
+    proximal step (flc_feddr_combine).  L1 and L2-squared proxes are fused; L2's factor needs the norm of the
+    combined θ over all tensors (an fp64 sum of squares per tensor; the reference sums fp32 per-tensor sums, so
+    this one is equal to within rounding, not bit for bit), then θ is scaled in a second pass."""
+    import re
+
+    kind = re.sub("regularizer|norm|[\\s\\_\\-]+", "", reg_type.lower())
+    if kind in _LINF:
+        raise NotImplementedError("L-infinity norm is not implemented yet")
+    if kind not in _PROX_KIND:
+        raise ValueError(f"Unknown regularizer type: {reg_type}")
+    kind = _PROX_KIND[kind]
+    coeff = eta * num_clients / (num_clients + 1)
+    total = sum([m["train_samples"] for m in messages])
+    weights = [m["train_samples"] / total for m in messages]
+    for j, xt in enumerate(x_til_params):
+        codec.weighted_sum(xt, [_on(m["x_hat_delta"][j], xt.device) for m in messages], weights, init_mode=2)
+    cx, cy = coeff / eta, 1 / (num_clients + 1)
+    if kind == "l1":
+        prox, pc = _lib.FLC_PROX_L1, coeff
+    elif kind == "l2squared":
+        prox, pc = _lib.FLC_PROX_SCALE, 1 / (1 + 2 * coeff)
+    else:
+        prox, pc = _lib.FLC_PROX_NONE, 0.0
+    ps = _params(model_params)
+    for sp, yp, xt in zip(ps, y_params, x_til_params):
+        codec.feddr_combine(sp, yp, xt, alpha, cx, cy, prox, pc)
+    if kind == "l2":
+        sq = 0.0
+        for sp in ps:
+            sq += float(codec.quant_norm(sp.reshape(1, -1), 2).item()) ** 2
+        norm = coeff * math.sqrt(sq)
+        f = max(0, 1 - coeff / norm)
+        for sp in ps:
+            codec.weighted_sum(sp, [], [], init_mode=0, beta=f)
+
+
 class AggregationMixin:
     """Mix in before a reference ``Server`` subclass to run its aggregation on the device.
 
@@ -113,3 +207,27 @@ class FedOptUpdateMixin:
         fedopt_update(list(self.model.parameters()), self.delta_parameters, self.v_parameters,
                       self._received_messages, self.config.optimizer, self.config.lr, self.config.betas,
                       self.config.tau)
+
+
+class SCAFFOLDUpdateMixin:
+    """Device ``update()`` for the reference's ``SCAFFOLDServer`` (_scaffold.py:158-167)."""
+
+    def update(self) -> None:
+        scaffold_update(list(self.model.parameters()), self._control_variates, self._received_messages,
+                        self.config.lr, len(self._clients))
+
+
+class IFCAUpdateMixin:
+    """Device ``update()`` for the reference's ``IFCAServer`` (_ifca.py:167-195)."""
+
+    def update(self) -> None:
+        ifca_update(self._cluster_centers, self._received_messages, self.config.num_clusters)
+
+
+class FedDRUpdateMixin:
+    """Device ``update()`` for the reference's ``FedDRServer`` (_feddr.py:166-190)."""
+
+    def update(self) -> None:
+        feddr_update(list(self.model.parameters()), self._y_parameters, self._x_til_parameters,
+                     self._received_messages, self.config.alpha, self.config.eta, self.config.num_clients,
+                     self.config.reg_type)

@@ -276,3 +276,15 @@ def fedopt_step(theta: torch.Tensor, delta: torch.Tensor, v: Optional[torch.Tens
                 beta2: float, tau: float) -> None:
     call("flc_fedopt_step", _p(theta), _p(delta), _p(v), theta.numel(), _lib.FLC_OPT[opt], float(lr), float(beta2),
          float(tau), _stream(theta.device))
+
+
+def feddr_combine(theta: torch.Tensor, y: torch.Tensor, x_til: torch.Tensor, alpha: float, cx: float, cy: float,
+                  prox: int, prox_c: float) -> None:
+    """y = fmaf(alpha, theta - y, y); theta = prox(cx * x_til + cy * y), in place (flc_feddr_combine)."""
+    for t, name in ((theta, "theta"), (y, "y"), (x_til, "x_til")):
+        if t.device.type != "cuda" or t.dtype != torch.float32 or not t.is_contiguous():
+            raise TypeError(f"{name} must be a contiguous fp32 HIP tensor")
+        if t.numel() != theta.numel():
+            raise ValueError("theta, y and x_til must have the same number of elements")
+    call("flc_feddr_combine", _p(theta), _p(y), _p(x_til), theta.numel(), float(alpha), float(cx), float(cy),
+         int(prox), float(prox_c), _stream(theta.device))

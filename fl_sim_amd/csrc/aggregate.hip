@@ -92,6 +92,36 @@ __global__ __launch_bounds__(kThreads) void fedopt_step_kernel(float* __restrict
   }
 }
 
+// FedDRServer.update after the x_tilde fold (_feddr.py:166-190), one pass over theta, y and x_tilde:
+//   y     = fmaf(alpha, theta - y, y)          yp.data.add_(mp.data - yp.data, alpha=alpha)   _feddr.py:169-170
+//   t     = cx * x_til + cy * y               (coeff/eta) * xtp + (1/(N+1)) * yp            _feddr.py:184-185
+//   theta = prox(t)                            regularizer.prox_eval                         _feddr.py:186-190
+// prox: FLC_PROX_NONE (NullRegularizer), FLC_PROX_L1 sign(t) * clamp(|t| - pc, min=0) (L1Norm,
+// regularizers.py:154-159), FLC_PROX_SCALE t * pc (L2NormSquared with pc = fp32(1/(1+2c)), regularizers.py:193-200;
+// L2Norm's factor needs the global norm of t first, so the host runs NONE and then scales).  Each torch op rounds
+// to fp32 on its own, so nothing here is contracted (-ffp-contract=off) except the one fmaf add_(alpha) is.
+template <int PROX>
+__global__ __launch_bounds__(kThreads) void feddr_combine_kernel(float* __restrict__ theta, float* __restrict__ y,
+                                                                 const float* __restrict__ x_til, int64_t n,
+                                                                 float alpha, float cx, float cy, float pc) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const float yo = y[i];
+    const float yn = fmaf(alpha, theta[i] - yo, yo);
+    y[i] = yn;
+    float t = cx * x_til[i] + cy * yn;
+    if (PROX == FLC_PROX_L1) {
+      float m = fabsf(t) - pc;
+      m = m < 0.f ? 0.f : m;  // clamp(min=0) keeps NaN
+      const float sg = (float)((t > 0.f) - (t < 0.f));
+      t = sg * m;
+    } else if (PROX == FLC_PROX_SCALE) {
+      t = t * pc;
+    }
+    theta[i] = t;
+  }
+}
+
 unsigned grid_for(int64_t work) {
   const int64_t g = cdiv(work, kThreads);
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 256 * 16));
@@ -160,6 +190,23 @@ int flc_fedopt_step(float* theta, const float* delta, float* v, int64_t n, int o
     default: return fail(FLC_EINVAL, "flc_fedopt_step: unknown optimiser %d", opt);
   }
 #undef FLC_FO
+  return FLC_OK;
+}
+
+int flc_feddr_combine(float* theta, float* y, const float* x_til, int64_t n, float alpha, float cx, float cy,
+                      int prox, float prox_c, void* stream) {
+  if (!theta || !y || !x_til || n < 0) return fail(FLC_EINVAL, "flc_feddr_combine: bad arguments");
+  if (n == 0) return FLC_OK;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = grid_for(n);
+#define FLC_DR(P) FLC_LAUNCH("feddr_combine", feddr_combine_kernel<P>, dim3(grid), dim3(kThreads), 0, st, theta, y, x_til, n, alpha, cx, cy, prox_c)
+  switch (prox) {
+    case FLC_PROX_NONE: FLC_DR(FLC_PROX_NONE); break;
+    case FLC_PROX_L1: FLC_DR(FLC_PROX_L1); break;
+    case FLC_PROX_SCALE: FLC_DR(FLC_PROX_SCALE); break;
+    default: return fail(FLC_EINVAL, "flc_feddr_combine: unknown prox %d", prox);
+  }
+#undef FLC_DR
   return FLC_OK;
 }
 

@@ -52,6 +52,9 @@ enum flc_quant_kind {
 };
 enum flc_norm_kind { FLC_NORM_INF = 0, FLC_NORM_L2 = 2 };
 
+/* proximal step of FedDR's regularizer (regularizers.py:146-200) */
+enum flc_prox_kind { FLC_PROX_NONE = 0, FLC_PROX_L1 = 1, FLC_PROX_SCALE = 2 };
+
 /* server optimiser of FedOptServer.update (_fedopt.py:196-265) */
 enum flc_fedopt_kind { FLC_OPT_AVG = 0, FLC_OPT_ADAGRAD = 1, FLC_OPT_YOGI = 2, FLC_OPT_ADAM = 3 };
 
@@ -177,6 +180,15 @@ int flc_weighted_sum(const float* const* srcs, const float* weights, int n_src, 
  *   adam:    v = v * beta2 + (1-beta2) * delta^2;            theta += ... */
 int flc_fedopt_step(float* theta, const float* delta, float* v, int64_t n, int opt, double lr, double beta2,
                     double tau, void* stream);
+
+/* the rest of FedDRServer.update once x_tilde holds its sample-weighted fold (flc_weighted_sum, init_mode 2,
+ * _feddr.py:172-180), one pass:
+ *   y = fmaf(alpha, theta - y, y)                       (_feddr.py:166-170)
+ *   theta = prox(cx * x_til + cy * y)                   (_feddr.py:182-190; cx = coeff/eta, cy = 1/(N+1) in fp32)
+ *   prox: NONE (NullRegularizer); L1: sign(t) * max(|t| - prox_c, 0) (L1Norm); SCALE: t * prox_c (L2NormSquared,
+ *   prox_c = 1/(1+2 coeff); L2Norm: NONE, then the host scales by max(0, 1 - 1/||theta||) with flc_weighted_sum). */
+int flc_feddr_combine(float* theta, float* y, const float* x_til, int64_t n, float alpha, float cx, float cy,
+                      int prox, float prox_c, void* stream);
 
 /* ------------------------------------------------------------------ measurement
  * Record HIP events around every launch of the kernel named `kernel_name` (NULL disables);

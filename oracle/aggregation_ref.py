@@ -3,9 +3,11 @@
 torch-CPU restatement of the reference's server aggregation, operation for operation:
 ``Server.add_parameters`` / ``avg_parameters`` / ``update_gradients`` (fl_sim/nodes.py:1116-1180)
 and ``FedOptServer.update`` with its avg/adagrad/yogi/adam tails (fl_sim/algorithms/fedopt/
-_fedopt.py:196-265).  It runs the same torch CPU kernels the reference runs (``mul_``, ``add_`` with
+_fedopt.py:196-265); the f4 variants ``SCAFFOLDServer.update`` (scaffold/_scaffold.py:158-167), ``IFCAServer.update``
+(ifca/_ifca.py:167-195) and ``FedDRServer.update`` (feddr/_feddr.py:166-190) with the regularizers' proximal steps
+(regularizers/regularizers.py:146-200).  It runs the same torch CPU kernels the reference runs (``mul_``, ``add_`` with
 ``alpha``, ``addcmul_``, ``addcdiv_``), so it rounds exactly where the reference rounds.  Pinned by
-``tests/golden/agg_*.npz``, produced by executing the reference's own method bodies
+``tests/golden/agg.npz`` and ``agg_variants.npz``, produced by executing the reference's own method bodies
 (``tests/golden/gen_golden.py``).
 """
 
@@ -66,3 +68,70 @@ def fedopt_update(params, delta_params, v_params, messages, optimizer: str, lr: 
     else:  # _fedopt.py:234-239
         for sp, dp, vp in zip(params, delta_params, v_params):
             sp.addcdiv_(dp, vp.sqrt() + tau, value=lr)
+
+
+# ------------------------------------------------------------------------------------------ f4 variants
+def scaffold_update(params, control_variates, messages, lr: float, num_clients: int) -> None:
+    ratio_p = lr / len(messages)  # _scaffold.py:160-161
+    ratio_c = 1 / num_clients
+    for m in messages:  # _scaffold.py:162-167: message order, parameters then control variates
+        add_parameters(params, m["parameters_delta"], ratio_p)
+        for cv, d in zip(control_variates, m["control_variates_delta"]):
+            cv.add_(d.detach().clone(), alpha=ratio_c)
+
+
+def ifca_update(centers: dict, messages, num_clusters: int) -> None:
+    """``centers[c] = {"center_model_params": [...], "client_ids": [...]}``, updated in place."""
+    prev = {c: list(v["client_ids"]) for c, v in centers.items()}  # _ifca.py:170
+    for v in centers.values():
+        v["client_ids"] = []
+    sizes = {c: 0 for c in range(num_clusters)}
+    for m in messages:  # _ifca.py:176-178
+        sizes[m["cluster_id"]] += 1
+        centers[m["cluster_id"]]["client_ids"].append(m["client_id"])
+    collected = [i for v in centers.values() for i in v["client_ids"]]
+    for c, v in centers.items():  # _ifca.py:182-185: idle members rejoin their cluster
+        for i in prev[c]:
+            if i not in collected:
+                v["client_ids"].append(i)
+    for m in messages:  # _ifca.py:187-195 (the client id is appended a second time, as in the reference)
+        c = m["cluster_id"]
+        for p, d in zip(centers[c]["center_model_params"], m["delta_parameters"]):
+            p.add_(d.detach().clone(), alpha=1 / sizes[c])
+        centers[c]["client_ids"].append(m["client_id"])
+
+
+def prox(params, reg_type: str, coeff: float):
+    """regularizers.py:146-200 (name normalisation of get_regularizer, regularizers.py:108)."""
+    import math
+    import re
+
+    kind = re.sub("regularizer|norm|[\\s\\_\\-]+", "", reg_type.lower())
+    if kind == "l1":
+        return [p.sign() * (p.abs() - coeff).clamp(min=0) for p in params]
+    if kind == "l2":
+        norm = coeff * math.sqrt(sum([p.pow(2).sum().item() for p in params]))
+        f = max(0, 1 - coeff / norm)
+        return [f * p for p in params]
+    if kind == "l2squared":
+        return [(1 / (1 + 2 * coeff)) * p for p in params]
+    if kind in ("no", "empty", "zero", "none", "null"):
+        return list(params)
+    if kind in ("linf", "inf", "linfinity", "infinity", "linfty", "infty"):
+        raise NotImplementedError("L-infinity norm is not implemented yet")
+    raise ValueError(f"Unknown regularizer type: {reg_type}")
+
+
+def feddr_update(params, y_params, x_til_params, messages, alpha: float, eta: float, num_clients: int,
+                 reg_type: str) -> None:
+    coeff = eta * num_clients / (num_clients + 1)  # _feddr.py:147-150
+    for yp, mp in zip(y_params, params):  # _feddr.py:169-170
+        yp.add_(mp - yp, alpha=alpha)
+    total = sum(m["train_samples"] for m in messages)
+    for m in messages:  # _feddr.py:174-180
+        for i, xt in enumerate(x_til_params):
+            xt.add_(m["x_hat_delta"][i], alpha=m["train_samples"] / total)
+    for mp, yp, xt in zip(params, y_params, x_til_params):  # _feddr.py:184-185
+        mp.copy_((coeff / eta) * xt + (1 / (num_clients + 1)) * yp)
+    for mp, p in zip(params, prox(params, reg_type, coeff)):  # _feddr.py:186-190
+        mp.copy_(p)

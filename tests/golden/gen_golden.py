@@ -14,7 +14,10 @@ Aggregation fixtures (``agg_*.npz``): FedOptServer.update (avg/adam/yogi/adagrad
 (size_aware x inertia) and update_gradients on small model shapes (full arrays) and on the
 cnn_femmist_tiny shapes of config 1 (SHA-256 of the outputs).
 
-Usage:  python tests/golden/gen_golden.py
+Variant fixtures (``agg_variants.npz``): SCAFFOLDServer.update, IFCAServer.update (centers and the
+client-id bookkeeping) and FedDRServer.update under each constructible regularizer, same shapes.
+
+Usage:  python tests/golden/gen_golden.py [all|codec|agg|variants]
 """
 
 from __future__ import annotations
@@ -297,15 +300,158 @@ def gen_aggregation():
     print("agg.npz:", len(store), "arrays")
 
 
+# --------------------------------------------------------------------- aggregation variants
+def compile_methods(rel: str, cls: str, names: Sequence[str], ns: Dict[str, Any]) -> Dict[str, types.FunctionType]:
+    """The named method bodies of ``cls`` in the reference file ``rel``, compiled from its source text."""
+    tree = ast.parse((REF / rel).read_text())
+    fns: Dict[str, types.FunctionType] = {}
+    for node in tree.body:
+        if isinstance(node, ast.ClassDef) and node.name == cls:
+            for item in node.body:
+                if isinstance(item, ast.FunctionDef) and item.name in names:
+                    item.decorator_list = []
+                    code = compile(ast.Module(body=[item], type_ignores=[]), f"{REF / rel}:{item.lineno}", "exec")
+                    local: Dict[str, Any] = {}
+                    exec(code, ns, local)
+                    fns[item.name] = local[item.name]
+    assert set(names) <= set(fns), set(names) - set(fns)
+    return fns
+
+
+def variant_namespace() -> Dict[str, Any]:
+    import copy
+    import math
+    import typing
+
+    ns: Dict[str, Any] = {"torch": torch, "np": np, "deepcopy": copy.deepcopy, "sqrt": math.sqrt,
+                          # torch_ecg.utils.misc.list_sum (absent here): concatenation of a sequence of lists
+                          "list_sum": lambda ls: sum(ls, [])}
+    ns.update({k: getattr(typing, k) for k in ("Any", "Dict", "Iterable", "List", "Optional", "Sequence")})
+    from torch.nn.parameter import Parameter
+
+    ns["Parameter"] = Parameter
+    return ns
+
+
+def reference_regularizer(reg_type: str, coeff: float):
+    """The reference regularizer class get_regularizer (regularizers.py:92-140) returns, its methods compiled from
+    source; the name normalisation is the reference's."""
+    import re
+
+    name = {"l1": "L1Norm", "l2": "L2Norm", "l2squared": "L2NormSquared", "null": "NullRegularizer",
+            "none": "NullRegularizer"}[re.sub("regularizer|norm|[\\s\\_\\-]+", "", reg_type.lower())]
+    fns = compile_methods("fl_sim/regularizers/regularizers.py", name, ("eval", "prox_eval"), variant_namespace())
+    reg = type(name, (), dict(fns))()
+    reg.coeff = coeff
+    return reg
+
+
+def variant_msgs(shapes, n, seed, keys, extra=None):
+    g = torch.Generator().manual_seed(seed)
+    msgs = []
+    for i in range(n):
+        m = {"client_id": i, "train_samples": 100 * (i + 1) + 7 * (i % 3), "metrics": {}}
+        for key in keys:
+            m[key] = [torch.randn(s, generator=g) * 1e-3 for s in shapes]
+        if extra is not None:
+            m.update(extra(i))
+        msgs.append(m)
+    return msgs
+
+
+IFCA_CLUSTER_OF = [0, 2, 0, 0, 2, 3, 0, 2, 3, 0]  # cluster 1 receives no message this round
+IFCA_PREV_IDS = {0: [0, 2, 11, 12], 1: [13, 14], 2: [1, 4, 15], 3: [5, 8]}
+FEDDR_REGS = ("l1_norm", "l2_norm", "l2_norm_squared", "none")
+SCAFFOLD_CFG = dict(lr=0.05, num_clients=20)
+FEDDR_CFG = dict(alpha=0.9, eta=0.05, num_clients=10)
+
+
+# inputs of the variant fixtures (shared with tests/test_oracle_golden.py and tests/test_gpu_aggregation.py)
+def scaffold_inputs(shapes):
+    params = [p.detach().clone() for p in make_model(shapes, 8).parameters()]
+    g = torch.Generator().manual_seed(9)
+    cvs = [torch.randn(sh, generator=g) * 1e-3 for sh in shapes]
+    return params, cvs, variant_msgs(shapes, 10, 10, ("parameters_delta", "control_variates_delta"))
+
+
+def ifca_inputs(shapes):
+    centers = {c: {"center_model_params": [p.detach().clone() for p in make_model(shapes, 20 + c).parameters()],
+                   "client_ids": list(IFCA_PREV_IDS[c])} for c in range(4)}
+    return centers, variant_msgs(shapes, 10, 11, ("delta_parameters",), lambda i: {"cluster_id": IFCA_CLUSTER_OF[i]})
+
+
+def feddr_inputs(shapes):
+    params = [p.detach().clone() for p in make_model(shapes, 30).parameters()]
+    ys = [p.detach().clone() for p in make_model(shapes, 31).parameters()]
+    xts = [p.detach().clone() for p in make_model(shapes, 32).parameters()]
+    return params, ys, xts, variant_msgs(shapes, FEDDR_CFG["num_clients"], 12, ("x_hat_delta",))
+
+
+def gen_variants():
+    ns = variant_namespace()
+    srv = compile_methods("fl_sim/nodes.py", "Server", ("add_parameters",), ns)
+    scaffold = compile_methods("fl_sim/algorithms/scaffold/_scaffold.py", "SCAFFOLDServer", ("update",), ns)["update"]
+    ifca = compile_methods("fl_sim/algorithms/ifca/_ifca.py", "IFCAServer", ("update",), ns)["update"]
+    feddr = compile_methods("fl_sim/algorithms/feddr/_feddr.py", "FedDRServer", ("update",), ns)["update"]
+
+    store: Dict[str, Any] = {}
+    for tag, shapes in (("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)):
+        full = tag == "small"
+
+        def put(key, tensors):
+            flat = torch.cat([t.detach().reshape(-1) for t in tensors]).numpy()
+            store[key + "|sha"] = np.array(sha(flat))
+            if full:
+                store[key + "|out"] = flat
+
+        # SCAFFOLDServer.update (_scaffold.py:158-167): 10 of 20 clients
+        s = types.SimpleNamespace(device=torch.device("cpu"), config=types.SimpleNamespace(lr=SCAFFOLD_CFG["lr"]),
+                                  _clients=list(range(SCAFFOLD_CFG["num_clients"])))
+        s.model = make_model(shapes, 8)
+        s.add_parameters = types.MethodType(srv["add_parameters"], s)
+        _, s._control_variates, s._received_messages = scaffold_inputs(shapes)
+        scaffold(s)
+        put(f"scaffold_{tag}|theta", list(s.model.parameters()))
+        put(f"scaffold_{tag}|cv", s._control_variates)
+
+        # IFCAServer.update (_ifca.py:167-195): 4 clusters, cluster 1 idle this round
+        s = types.SimpleNamespace(device=torch.device("cpu"), config=types.SimpleNamespace(num_clusters=4))
+        s._cluster_centers, s._received_messages = ifca_inputs(shapes)
+        ifca(s)
+        for c in range(4):
+            put(f"ifca_{tag}|center{c}", s._cluster_centers[c]["center_model_params"])
+            store[f"ifca_{tag}|ids{c}"] = np.array(s._cluster_centers[c]["client_ids"], dtype=np.int64)
+
+        # FedDRServer.update (_feddr.py:166-190) under each constructible regularizer
+        for reg in FEDDR_REGS:
+            N, eta = FEDDR_CFG["num_clients"], FEDDR_CFG["eta"]
+            s = types.SimpleNamespace(device=torch.device("cpu"),
+                                      config=types.SimpleNamespace(alpha=FEDDR_CFG["alpha"], eta=eta, num_clients=N))
+            s._regularizer = reference_regularizer(reg, eta * N / (N + 1))
+            s.model = make_model(shapes, 30)
+            _, s._y_parameters, s._x_til_parameters, s._received_messages = feddr_inputs(shapes)
+            feddr(s)
+            put(f"feddr_{reg}_{tag}|theta", list(s.model.parameters()))
+            put(f"feddr_{reg}_{tag}|y", s._y_parameters)
+            put(f"feddr_{reg}_{tag}|xtil", s._x_til_parameters)
+    np.savez_compressed(OUT / "agg_variants.npz", **store)
+    print("agg_variants.npz:", len(store), "arrays")
+
+
 def main():
     if not REF.exists():
         print("reference not present; nothing to do", file=sys.stderr)
         return 1
     torch.set_num_threads(1)
-    ref = load_reference_compressors()
-    gen_codecs(ref)
-    gen_sparse(ref)
-    gen_aggregation()
+    only = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if only in ("all", "codec"):
+        ref = load_reference_compressors()
+        gen_codecs(ref)
+        gen_sparse(ref)
+    if only in ("all", "agg"):
+        gen_aggregation()
+    if only in ("all", "variants"):
+        gen_variants()
     return 0
 
 

@@ -126,3 +126,51 @@ def test_philox_oracle_known_answer():
     c = ref.philox4x32_10([0xFFFFFFFF], [0xFFFFFFFF], [0xFFFFFFFF], [0xFFFFFFFF], np.uint32(0xFFFFFFFF),
                           np.uint32(0xFFFFFFFF))
     assert [int(v[0]) for v in c] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+
+
+# ------------------------------------------------------------------- aggregation variants
+from tests.golden.gen_golden import (  # noqa: E402
+    FEDDR_CFG, FEDDR_REGS, SCAFFOLD_CFG, feddr_inputs, ifca_inputs, scaffold_inputs)
+
+AGGV = np.load(f"{gc.GOLDEN}/agg_variants.npz", allow_pickle=False)
+
+
+def _check_v(key, ts):
+    flat = _flat(ts)
+    if key + "|out" in AGGV.files:
+        assert gc.same_bits(flat, AGGV[key + "|out"]), key
+    assert gc.sha(flat) == str(AGGV[key + "|sha"]), key
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+def test_scaffold_oracle_matches_reference(tag, shapes):
+    params, cvs, msgs = scaffold_inputs(shapes)
+    agg_ref.scaffold_update(params, cvs, msgs, SCAFFOLD_CFG["lr"], SCAFFOLD_CFG["num_clients"])
+    _check_v(f"scaffold_{tag}|theta", params)
+    _check_v(f"scaffold_{tag}|cv", cvs)
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+def test_ifca_oracle_matches_reference(tag, shapes):
+    centers, msgs = ifca_inputs(shapes)
+    agg_ref.ifca_update(centers, msgs, 4)
+    for c in range(4):
+        _check_v(f"ifca_{tag}|center{c}", centers[c]["center_model_params"])
+        assert centers[c]["client_ids"] == AGGV[f"ifca_{tag}|ids{c}"].tolist()
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+@pytest.mark.parametrize("reg", FEDDR_REGS)
+def test_feddr_oracle_matches_reference(tag, shapes, reg):
+    torch.set_num_threads(1)  # the l2 prox's norm is a torch CPU sum, as when the fixtures were made
+    params, ys, xts, msgs = feddr_inputs(shapes)
+    agg_ref.feddr_update(params, ys, xts, msgs, FEDDR_CFG["alpha"], FEDDR_CFG["eta"], FEDDR_CFG["num_clients"], reg)
+    _check_v(f"feddr_{reg}_{tag}|theta", params)
+    _check_v(f"feddr_{reg}_{tag}|y", ys)
+    _check_v(f"feddr_{reg}_{tag}|xtil", xts)
+
+
+def test_feddr_linf_raises_like_reference():
+    params, ys, xts, msgs = feddr_inputs(SMALL_SHAPES)
+    with pytest.raises(NotImplementedError):
+        agg_ref.feddr_update(params, ys, xts, msgs, 0.9, 0.05, 10, "linf_norm")
