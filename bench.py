@@ -306,6 +306,22 @@ def main():
             "GB_s": round((8 * d3 + 16 * k3) / (ms3 * 1e-3) / 1e9, 1),
             "bytes_formula": "8 * D + 16 * K",
         }
+        del o3
+        # f1: client delta formation + flatten (FedOptClient.communicate), 1 GiB of parameters in 64 tensors
+        sizes5 = [(1 << 22) + (i % 3) for i in range(63)]
+        sizes5.append((1 << 28) - sum(sizes5))
+        L5 = [torch.randn(n, generator=gen, device=dev) for n in sizes5]
+        G5 = [torch.randn(n, generator=gen, device=dev) for n in sizes5]
+        o5 = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        ms5, _ = timed(lambda: codec.delta_flatten(L5, G5, out=o5), 20, 5, world)
+        ms5 = max_over_ranks(ms5, world)
+        extra["f1_client_delta_flatten_1GiB_64_tensors"] = {
+            "ms_per_step": round(ms5, 4),
+            "GB_s": round(12 * (1 << 28) / (ms5 * 1e-3) / 1e9, 1),
+            "bytes_formula": "12 * D (8 read + 4 written)",
+        }
+        del L5, G5, o5
+        torch.cuda.empty_cache()
         if world > 1:
             from fl_sim_amd import dist as fdist
 
@@ -325,7 +341,7 @@ def main():
             ms4, _ = timed(step4, 10, 3, world)
             ms4 = max_over_ranks(ms4, world)
             extra["config4_codec_plus_rccl_reduce_25M"] = {"ms_per_step": round(ms4, 4), "clients": world}
-        del X3, o3
+        del X3
 
     cpu = None
     if rank == 0 and world == 1 and not args.skip_cpu:

@@ -288,3 +288,32 @@ def feddr_combine(theta: torch.Tensor, y: torch.Tensor, x_til: torch.Tensor, alp
             raise ValueError("theta, y and x_til must have the same number of elements")
     call("flc_feddr_combine", _p(theta), _p(y), _p(x_til), theta.numel(), float(alpha), float(cx), float(cy),
          int(prox), float(prox_c), _stream(theta.device))
+
+
+def delta_flatten(local_params: Sequence[torch.Tensor], global_params: Sequence[torch.Tensor],
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The flat client delta ``cat([l - g for l, g in zip(local, global)])`` in one pass (flc_delta_flatten):
+    FedOptClient.communicate's clone + ``add_(alpha=-1)`` (_fedopt.py:294-297) fused with the flatten the codec
+    input needs.  Returns ``out`` (allocated when None)."""
+    import ctypes
+
+    ls = [_dev_f32(t, "local") for t in local_params]
+    gs = [_dev_f32(t, "global") for t in global_params]
+    if len(ls) != len(gs):
+        raise ValueError("one global tensor per local tensor")
+    for a, b in zip(ls, gs):
+        if a.numel() != b.numel() or a.device != b.device:
+            raise ValueError("local and global tensors must match in size and device")
+    total = sum(t.numel() for t in ls)
+    dev = ls[0].device if ls else (out.device if out is not None else torch.device("cuda"))
+    if out is None:
+        out = torch.empty(total, dtype=torch.float32, device=dev)
+    elif out.device.type != "cuda" or out.dtype != torch.float32 or not out.is_contiguous() or out.numel() != total:
+        raise ValueError(f"out must be a contiguous fp32 HIP tensor of {total} elements")
+    m = max(len(ls), 1)
+    lp = (ctypes.c_void_p * m)(*[t.data_ptr() for t in ls])
+    gp = (ctypes.c_void_p * m)(*[t.data_ptr() for t in gs])
+    sz = (ctypes.c_int64 * m)(*[t.numel() for t in ls])
+    call("flc_delta_flatten", ctypes.cast(lp, ctypes.c_void_p), ctypes.cast(gp, ctypes.c_void_p),
+         ctypes.cast(sz, ctypes.c_void_p), len(ls), _p(out), _stream(dev))
+    return out

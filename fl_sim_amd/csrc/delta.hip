@@ -1,0 +1,115 @@
+// delta.hip — client delta formation + flatten for gfx950 (the delta/flatten half).
+//
+// Reference: FedOptClient.communicate (fl_sim/algorithms/fedopt/_fedopt.py:294-297) forms the delta per parameter
+// tensor as `dp = p.detach().clone()` (nodes.py:300-302) then `dp.add_(rp, alpha=-1)` — one fp32 fmaf(-1, rp, dp),
+// which equals the single-rounded difference dp - rp — and the codec then needs the tensors as ONE flat vector
+// (Compressor.compressVector takes a 1-D array).  delta_flatten does both in one pass: for tensor t,
+//   out[off_t + i] = local_t[i] - global_t[i],   off_t = n_0 + ... + n_{t-1}
+// HBM bytes per element: 8 read + 4 written (clone + add_ + cat move 28).  Each 256-thread block streams one
+// 4096-element chunk of one tensor with 16-B non-temporal loads/stores where the tensor's operands and its slot in
+// `out` are 16-B aligned (scalar accesses otherwise); a launch carries up to kMaxT tensors and their block offsets.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "flc_device.hpp"
+#include "flc_runtime.hpp"
+
+namespace flc {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;
+constexpr int64_t kChunk = (int64_t)kThreads * 4 * kUnroll;  // elements per block
+constexpr int kMaxT = 48;                                     // tensors per launch (kernel-argument budget)
+
+struct TensorPack {
+  const float* l[kMaxT];
+  const float* g[kMaxT];
+  int64_t off[kMaxT];
+  int64_t n[kMaxT];
+  int blk0[kMaxT + 1];  // first block of tensor t; blk0[nt] = grid size
+  unsigned long long vec;  // bit t: 16-B path for tensor t
+  int nt;
+};
+
+__global__ __launch_bounds__(kThreads) void delta_flatten_kernel(TensorPack p, float* __restrict__ out) {
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < p.nt && p.blk0[t + 1] <= b) ++t;  // uniform: <= kMaxT steps
+  const float* __restrict__ l = p.l[t];
+  const float* __restrict__ g = p.g[t];
+  float* __restrict__ o = out + p.off[t];
+  const int64_t n = p.n[t];
+  const int64_t c0 = (int64_t)(b - p.blk0[t]) * kChunk;
+  if ((p.vec >> t) & 1ull) {
+    const int64_t n4 = n >> 2;
+    float4 d[kUnroll];
+    bool ok[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t i4 = (c0 >> 2) + u * kThreads + threadIdx.x;
+      ok[u] = i4 < n4;
+      const int64_t j = ok[u] ? 4 * i4 : 0;
+      const float4 a = ld_stream(l + j), c = ld_stream(g + j);
+      d[u] = make_float4(a.x - c.x, a.y - c.y, a.z - c.z, a.w - c.w);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      if (ok[u]) st_stream(o + 4 * ((c0 >> 2) + u * kThreads + threadIdx.x), d[u]);
+    // the n % 4 tail, by the tensor's last block
+    const int64_t tail = n & 3;
+    if (c0 + kChunk >= n && (int64_t)threadIdx.x < tail) {
+      const int64_t i = (n4 << 2) + threadIdx.x;
+      o[i] = l[i] - g[i];
+    }
+    return;
+  }
+  for (int u = 0; u < 4 * kUnroll; ++u) {
+    const int64_t i = c0 + u * kThreads + threadIdx.x;
+    if (i < n) o[i] = l[i] - g[i];
+  }
+}
+
+}  // namespace
+}  // namespace flc
+
+using namespace flc;
+
+extern "C" {
+
+int flc_delta_flatten(const float* const* local, const float* const* global, const int64_t* sizes, int n_tensors,
+                      float* out, void* stream) {
+  if (n_tensors < 0 || (n_tensors > 0 && (!local || !global || !sizes)))
+    return fail(FLC_EINVAL, "flc_delta_flatten: bad arguments");
+  hipStream_t st = as_stream(stream);
+  int64_t off = 0;
+  for (int t0 = 0; t0 < n_tensors; t0 += kMaxT) {
+    TensorPack p{};
+    int blocks = 0;
+    p.nt = 0;
+    for (int t = t0; t < std::min(n_tensors, t0 + kMaxT); ++t) {
+      if (sizes[t] < 0) return fail(FLC_EINVAL, "flc_delta_flatten: negative size for tensor %d", t);
+      if (sizes[t] > 0 && (!local[t] || !global[t] || !out))
+        return fail(FLC_EINVAL, "flc_delta_flatten: null pointer for tensor %d", t);
+      if (sizes[t] == 0) continue;
+      const int i = p.nt++;
+      p.l[i] = local[t];
+      p.g[i] = global[t];
+      p.off[i] = off;
+      p.n[i] = sizes[t];
+      p.blk0[i] = blocks;
+      // (the 16-B path clamps idle lanes to element 0..3, so it needs n >= 4)
+      if (sizes[t] >= 4 && aligned16(local[t]) && aligned16(global[t]) && aligned16(out + off)) p.vec |= 1ull << i;
+      const int64_t nb = cdiv(sizes[t], kChunk);
+      if (blocks + nb > 0x7fffffff) return fail(FLC_EINVAL, "flc_delta_flatten: too many elements");
+      blocks += (int)nb;
+      off += sizes[t];
+    }
+    p.blk0[p.nt] = blocks;
+    if (blocks > 0) FLC_LAUNCH("delta_flatten", delta_flatten_kernel, dim3(blocks), dim3(kThreads), 0, st, p, out);
+  }
+  return FLC_OK;
+}
+
+}  // extern "C"

@@ -163,6 +163,14 @@ int flc_scale_div(const float* x, int64_t n, float p, float* out, void* stream);
 int flc_randk_apply(const float* x, int64_t n, const int32_t* idx, int64_t k, float scale, float* out,
                     void* stream);
 
+/* ------------------------------------------------------------------ client delta
+ * FedOptClient.communicate (_fedopt.py:294-297): delta_t = clone(local_t) then add_(global_t, alpha=-1), i.e.
+ * local_t - global_t per element, for each parameter tensor t; plus the flatten the codec's flat input needs.
+ * out[off_t + i] = local[t][i] - global[t][i], off_t = sizes[0] + ... + sizes[t-1].  local, global and sizes are
+ * HOST arrays (of device pointers / element counts); empty tensors are allowed. */
+int flc_delta_flatten(const float* const* local, const float* const* global, const int64_t* sizes, int n_tensors,
+                      float* out, void* stream);
+
 /* ------------------------------------------------------------------ aggregation
  * weighted sum of client tensors into dst, in message order, one fmaf per message per element:
  *   init_mode 0: dst = dst * beta   (avg_parameters' inertia, nodes.py:1158-1159;

@@ -135,3 +135,12 @@ def feddr_update(params, y_params, x_til_params, messages, alpha: float, eta: fl
         mp.copy_((coeff / eta) * xt + (1 / (num_clients + 1)) * yp)
     for mp, p in zip(params, prox(params, reg_type, coeff)):  # _feddr.py:186-190
         mp.copy_(p)
+
+
+def client_delta(local_params, cached_params):
+    """FedOptClient.communicate (_fedopt.py:294-297): detached clones of the local parameters, minus the cached
+    global ones via add_(alpha=-1)."""
+    deltas = [p.detach().clone() for p in local_params]  # nodes.py:300-302
+    for dp, rp in zip(deltas, cached_params):
+        dp.add_(rp, alpha=-1)
+    return deltas

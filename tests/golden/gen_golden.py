@@ -15,7 +15,8 @@ Aggregation fixtures (``agg_*.npz``): FedOptServer.update (avg/adam/yogi/adagrad
 cnn_femmist_tiny shapes of config 1 (SHA-256 of the outputs).
 
 Variant fixtures (``agg_variants.npz``): SCAFFOLDServer.update, IFCAServer.update (centers and the
-client-id bookkeeping) and FedDRServer.update under each constructible regularizer, same shapes.
+client-id bookkeeping), FedDRServer.update under each constructible regularizer, and FedOptClient.communicate's
+client delta, same shapes.
 
 Usage:  python tests/golden/gen_golden.py [all|codec|agg|variants]
 """
@@ -387,6 +388,14 @@ def feddr_inputs(shapes):
     return params, ys, xts, variant_msgs(shapes, FEDDR_CFG["num_clients"], 12, ("x_hat_delta",))
 
 
+def delta_inputs(shapes):
+    """(local model tensors, the round's cached global tensors) for the client-delta fixture."""
+    g = torch.Generator().manual_seed(40)
+    cached = [torch.randn(sh, generator=g) * 0.1 for sh in shapes]
+    local = [c + torch.randn(c.shape, generator=g) * 1e-3 for c in cached]
+    return local, cached
+
+
 def gen_variants():
     ns = variant_namespace()
     srv = compile_methods("fl_sim/nodes.py", "Server", ("add_parameters",), ns)
@@ -434,6 +443,20 @@ def gen_variants():
             put(f"feddr_{reg}_{tag}|theta", list(s.model.parameters()))
             put(f"feddr_{reg}_{tag}|y", s._y_parameters)
             put(f"feddr_{reg}_{tag}|xtil", s._x_til_parameters)
+        # FedOptClient.communicate (_fedopt.py:294-307): the per-tensor client delta (f1)
+        comm = compile_methods("fl_sim/algorithms/fedopt/_fedopt.py", "FedOptClient", ("communicate",),
+                               {**ns, "ClientMessage": dict})["communicate"]
+        node = compile_methods("fl_sim/nodes.py", "Node", ("get_detached_model_parameters",), ns)
+        local, cached = delta_inputs(shapes)
+        c = types.SimpleNamespace(client_id=3, _metrics={}, _cached_parameters=cached,
+                                  train_loader=types.SimpleNamespace(dataset=list(range(17))))
+        c.model = torch.nn.Module()
+        for i, t in enumerate(local):
+            c.model.register_parameter(f"p{i}", torch.nn.Parameter(t.clone()))
+        c.get_detached_model_parameters = types.MethodType(node["get_detached_model_parameters"], c)
+        server = types.SimpleNamespace(_received_messages=[])
+        comm(c, server)
+        put(f"delta_{tag}|delta", server._received_messages[0]["delta_parameters"])
     np.savez_compressed(OUT / "agg_variants.npz", **store)
     print("agg_variants.npz:", len(store), "arrays")
 

@@ -174,3 +174,11 @@ def test_feddr_linf_raises_like_reference():
     params, ys, xts, msgs = feddr_inputs(SMALL_SHAPES)
     with pytest.raises(NotImplementedError):
         agg_ref.feddr_update(params, ys, xts, msgs, 0.9, 0.05, 10, "linf_norm")
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+def test_client_delta_oracle_matches_reference(tag, shapes):
+    from tests.golden.gen_golden import delta_inputs
+
+    local, cached = delta_inputs(shapes)
+    _check_v(f"delta_{tag}|delta", agg_ref.client_delta(local, cached))
