@@ -287,7 +287,52 @@ void fedopt_step_(at::Tensor& theta, const at::Tensor& delta_, const c10::option
         "fedopt_step");
 }
 
+// ------------------------------------------------------------------------------------------- client delta (f1)
+at::Tensor delta_flatten(at::TensorList local, at::TensorList global) {
+  TORCH_CHECK(local.size() == global.size() && !local.empty(), "flcodec: one global tensor per local tensor");
+  std::vector<at::Tensor> keep;
+  std::vector<const float*> lp, gp;
+  std::vector<int64_t> sz;
+  int64_t total = 0;
+  for (size_t t = 0; t < local.size(); ++t) {
+    same_device(local[0], local[t], "every local tensor");
+    same_device(local[0], global[t], "every global tensor");
+    TORCH_CHECK(local[t].numel() == global[t].numel(), "flcodec: local and global tensor ", t, " differ in size");
+    keep.push_back(dev_f32(local[t], "local"));
+    lp.push_back(keep.back().data_ptr<float>());
+    keep.push_back(dev_f32(global[t], "global"));
+    gp.push_back(keep.back().data_ptr<float>());
+    sz.push_back(local[t].numel());
+    total += local[t].numel();
+  }
+  c10::DeviceGuard g(local[0].device());
+  at::Tensor out = at::empty({total}, local[0].options());
+  check(flc_delta_flatten(lp.data(), gp.data(), sz.data(), (int)sz.size(), total ? out.data_ptr<float>() : nullptr,
+                          stream_of(out)),
+        "delta_flatten");
+  return out;
+}
+
+void feddr_combine_(at::Tensor& theta, at::Tensor& y, const at::Tensor& x_til, double alpha, double cx, double cy,
+                    int64_t prox, double prox_c) {
+  const at::Tensor* all[3] = {&theta, &y, &x_til};
+  for (const at::Tensor* t : all) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == theta.numel(),
+                "flcodec: theta, y and x_til must be contiguous fp32 HIP tensors of one size");
+    same_device(theta, *t, "theta, y and x_til");
+  }
+  c10::DeviceGuard g(theta.device());
+  check(flc_feddr_combine(theta.data_ptr<float>(), y.data_ptr<float>(), x_til.data_ptr<float>(), theta.numel(),
+                          (float)alpha, (float)cx, (float)cy, (int)prox, (float)prox_c, stream_of(theta)),
+        "feddr_combine");
+}
+
 // --------------------------------------------------------------------------------- Meta kernels (shapes only)
+at::Tensor delta_flatten_meta(at::TensorList local, at::TensorList) {
+  int64_t total = 0;
+  for (const auto& t : local) total += t.numel();
+  return at::empty({total}, local[0].options());
+}
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode_meta(const at::Tensor& x, int64_t k,
                                                                                  int64_t, int64_t, int64_t) {
   const int64_t n = x.numel();
@@ -341,6 +386,9 @@ TORCH_LIBRARY(flcodec, m) {
   m.def("natural_decode(Tensor codes, float weight=1.0) -> Tensor");
   m.def("weighted_sum_(Tensor(a!) dst, Tensor[] srcs, float[] weights, int init_mode, float beta=0.0) -> Tensor(a!)");
   m.def("fedopt_step_(Tensor(a!) theta, Tensor delta, Tensor(b!)? v, int opt, float lr, float beta2, float tau) -> ()");
+  m.def("delta_flatten(Tensor[] theta_local, Tensor[] theta_global) -> Tensor");
+  m.def("feddr_combine_(Tensor(a!) theta, Tensor(b!) y, Tensor x_til, float alpha, float cx, float cy, int prox, "
+        "float prox_c) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
@@ -356,6 +404,8 @@ TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
   m.impl("natural_decode", &natural_decode);
   m.impl("weighted_sum_", &weighted_sum_);
   m.impl("fedopt_step_", &fedopt_step_);
+  m.impl("delta_flatten", &delta_flatten);
+  m.impl("feddr_combine_", &feddr_combine_);
 }
 
 TORCH_LIBRARY_IMPL(flcodec, Meta, m) {
@@ -368,4 +418,5 @@ TORCH_LIBRARY_IMPL(flcodec, Meta, m) {
   m.impl("quant_decode", &quant_decode_meta);
   m.impl("natural_encode", &natural_encode_meta);
   m.impl("natural_decode", &natural_decode_meta);
+  m.impl("delta_flatten", &delta_flatten_meta);
 }

@@ -28,6 +28,8 @@ OPS = {
     "natural_decode": None,
     "weighted_sum_": None,
     "fedopt_step_": None,
+    "delta_flatten": "flcodec::delta_flatten(Tensor[] theta_local, Tensor[] theta_global) -> Tensor",
+    "feddr_combine_": None,
 }
 
 
@@ -67,6 +69,8 @@ def test_meta_shapes(ops):
     nc, nz = ops.natural_encode(x)
     assert (nc.shape, nc.dtype, nz.dtype) == ((n,), torch.int16, torch.int64)
     assert ops.natural_decode(nc).shape == (n,)
+    ls = [torch.empty(s, device="meta") for s in ((16, 1, 5, 5), (16,), (10, 256))]
+    assert ops.delta_flatten(ls, ls).shape == (400 + 16 + 2560,)
 
 
 def test_cpu_tensors_refused(ops):
@@ -191,3 +195,20 @@ def test_ops_run_on_current_stream(ops):
         got = ops.stacked_decode(*ops.stacked_encode(x, k, 127, 1, 1), n)
     torch.cuda.current_stream().wait_stream(s)
     assert _same(got, base)
+
+
+@pytest.mark.gpu
+def test_delta_and_feddr_ops(ops):
+    from fl_sim_amd import _lib, codec
+
+    shapes = [(16, 1, 5, 5), (16,), (32, 16, 5, 5), (32,), (256, 1568), (256,), (10, 256), (10,)]
+    g = torch.Generator().manual_seed(3)
+    loc = [torch.randn(s, generator=g).cuda() for s in shapes]
+    glo = [torch.randn(s, generator=g).cuda() for s in shapes]
+    assert _same(ops.delta_flatten(loc, glo), codec.delta_flatten(loc, glo))
+    n = 417_482
+    th, y, xt = _x(n, 1).cuda(), _x(n, 2).cuda(), _x(n, 3).cuda()
+    th2, y2 = th.clone(), y.clone()
+    ops.feddr_combine_(th, y, xt, 0.9, 0.91, 0.09, _lib.FLC_PROX_L1, 1e-3)
+    codec.feddr_combine(th2, y2, xt, 0.9, 0.91, 0.09, _lib.FLC_PROX_L1, 1e-3)
+    assert _same(th, th2) and _same(y, y2)
