@@ -340,7 +340,33 @@ def main():
 
             ms4, _ = timed(step4, 10, 3, world)
             ms4 = max_over_ranks(ms4, world)
-            extra["config4_codec_plus_rccl_reduce_25M"] = {"ms_per_step": round(ms4, 4), "clients": world}
+
+            # the two halves on their own (per-GPU codec rate and reduce time separately):
+            # the local fold (encode + weighted decode-accumulate of this rank's clients), then the reduce
+            import torch.distributed as tdist
+
+            fold = fdist.stacked_decode_accumulate(k3, LEVELS, seed=0, counter=0)
+
+            def step4_codec():
+                acc.zero_()
+                for c in mine:
+                    fold(X3, float(w_all[c]), acc, c)
+
+            ms4c, _ = timed(step4_codec, 10, 3, world)
+            ms4c = max_over_ranks(ms4c, world)
+            ms4r, _ = timed(lambda: tdist.reduce(acc, dst=0, op=tdist.ReduceOp.SUM), 10, 3, world)
+            ms4r = max_over_ranks(ms4r, world)
+            codec_b = len(mine) * (stacked_bytes(d3, k3) + 4 * d3) + 4 * d3  # + the accumulate read, the zeroing
+            extra["config4_codec_plus_rccl_reduce_25M"] = {
+                "ms_per_step": round(ms4, 4),
+                "clients": world,
+                "codec_ms": round(ms4c, 4),
+                "codec_GB_s_per_gpu": round(codec_b / (ms4c * 1e-3) / 1e9, 1),
+                "codec_GB_s_aggregate": round(world * codec_b / (ms4c * 1e-3) / 1e9, 1),
+                "reduce_ms": round(ms4r, 4),
+                "reduce_xgmi_GB_s_per_gpu": round((world - 1) / world * 4 * d3 / (ms4r * 1e-3) / 1e9, 1),
+                "bytes_formula": "codec: n_local * (12 * D + 10 * K) + 4 * D; reduce: (N - 1) / N * 4 * D per GPU",
+            }
         del X3
 
     cpu = None
