@@ -40,16 +40,44 @@ D_HEADLINE = 268_435_456
 LEVELS = 127
 
 
-def dist_setup(n_gpus: int):
+def launch_ranks(n: int, argv) -> int:
+    """`--gpus N` without a torch.distributed environment: start N ranks as ONE child launcher.
+
+    This process has not touched the GPU (only `import torch`), and it is never replaced by another
+    program: torch.distributed.run runs as a child and its exit status is returned.
+    """
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+def dist_setup(n_gpus: int, backend: str = "nccl"):
+    """Join the process group the launcher made, pin this rank's GPU, and check the world size."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        print(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}; refusing to report a different GPU count",
+              file=sys.stderr)
+        sys.exit(3)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
+        if backend == "nccl":  # RCCL over xGMI
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+        if dist.get_world_size() != n_gpus:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, expected {n_gpus}", file=sys.stderr)
+            sys.exit(3)
+    elif backend == "nccl":
         torch.cuda.set_device(0)
     return world, rank, local
 
@@ -66,9 +94,31 @@ def max_over_ranks(v: float, world: int) -> float:
         return v
     import torch.distributed as dist
 
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    t = torch.tensor([v], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def launch_check(world: int, rank: int) -> None:
+    """Every rank reports in over the process group; rank 0 prints which ranks it saw."""
+    ranks = [rank]
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([rank], dtype=torch.int64)
+        got = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(got, t)
+        ranks = [int(g.item()) for g in got]
+        pids = [None] * world
+        dist.all_gather_object(pids, os.getpid())
+    else:
+        pids = [os.getpid()]
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": ranks, "distinct_pids": len(set(pids))}))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
 
 
 def stacked_bytes(D: int, K: int) -> int:
@@ -147,9 +197,22 @@ def main():
     ap.add_argument("--skip-extra", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--probe", default="stacked_encode", help="kernel timed live for the roofline entry")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend; gloo only with --launch-check (CPU rehearsal of the launcher)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, check the world size, print one JSON line and exit (no GPU work)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.backend != "nccl" and not args.launch_check:
+        ap.error("the benchmark itself runs on RCCL; --backend gloo is for --launch-check only")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
-    world, rank, local = dist_setup(args.gpus)
+    world, rank, local = dist_setup(args.gpus, args.backend)
+    if args.launch_check:
+        launch_check(world, rank)
+        return
     from fl_sim_amd import codec
 
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -364,8 +427,10 @@ def main():
                 "codec_GB_s_per_gpu": round(codec_b / (ms4c * 1e-3) / 1e9, 1),
                 "codec_GB_s_aggregate": round(world * codec_b / (ms4c * 1e-3) / 1e9, 1),
                 "reduce_ms": round(ms4r, 4),
-                "reduce_xgmi_GB_s_per_gpu": round((world - 1) / world * 4 * d3 / (ms4r * 1e-3) / 1e9, 1),
-                "bytes_formula": "codec: n_local * (12 * D + 10 * K) + 4 * D; reduce: (N - 1) / N * 4 * D per GPU",
+                # nccl-tests convention for reduce: busBw = algBw = bytes / time (every non-root rank's whole
+                # 4 D buffer crosses a link); the timed reduces re-reduce `acc` in place (values unused)
+                "reduce_algbw_GB_s": round(4 * d3 / (ms4r * 1e-3) / 1e9, 1),
+                "bytes_formula": "codec: n_local * (12 * D + 10 * K) + 4 * D; reduce: 4 * D (algBw = busBw)",
             }
         del X3
 
