@@ -17,9 +17,10 @@ RNG (``rng=`` constructor argument):
     index order), so outputs are bit-identical to the reference under the same seed;
   * ``"philox"``: counter-based Philox4x32-10 on the device, keyed by ``seed``; no host round trip.
 
-Extensions over the reference (documented in DESIGN.md): standard dithering accepts up to 127
-levels (the reference's ``np.arange`` table asserts for > 10), ``encode``/``decode`` expose the
-packed wire, and ``compressBatch`` runs a [clients, d] batch in one launch.
+Extensions over the reference (documented in DESIGN.md): ``Compressor(extended_levels=True)`` lets
+standard dithering take up to 127 levels (by default level counts > 10 fail the reference's
+``np.arange`` assertion, as they do there), ``encode``/``decode`` expose the packed wire, and
+``compressBatch`` runs a [clients, d] batch in one launch.
 """
 
 from __future__ import annotations
@@ -81,9 +82,12 @@ def natural_levels(levels: int) -> np.ndarray:
 class Compressor:
     """MI355X-native drop-in for the reference ``Compressor`` (compressors.py:35-419)."""
 
-    def __init__(self, compressorName: str = "", rng: str = "compat", seed: int = 0):
+    def __init__(self, compressorName: str = "", rng: str = "compat", seed: int = 0, extended_levels: bool = False):
         if rng not in ("compat", "philox"):
             raise ValueError("rng must be 'compat' or 'philox'")
+        # extension: standard dithering with 11..127 levels (8-bit codes); off by default, where such level
+        # counts fail the reference's assertion exactly as they do there
+        self.extended_levels = bool(extended_levels)
         self.__compressorName = compressorName
         self.__compressorType = CompressorType.IDENTICAL
         self.__w = 0.0
@@ -190,14 +194,20 @@ class Compressor:
         self.resetStats()
 
     def _make_std(self, name, ctype, levels, vectorNormCompressor, p):
-        if not 1 <= int(levels) <= 127:
-            raise ValueError("standard dithering supports 1..127 levels (8-bit codes)")
-        self._set(name, ctype, 0.0)
-        self.levelsValues = standard_levels(int(levels))
+        # compressors.py:154-182: the type and the table change first, then `assert self.s == levels`
+        # fails for every level count whose np.arange(0, 1.1, 1/levels) table is not levels + 1 long
+        # (all levels > 10), leaving the object half switched, as the reference does
+        self.__compressorName = name
+        self.__compressorType = ctype
+        if self.extended_levels and 1 <= int(levels) <= 127:
+            self.levelsValues = standard_levels(int(levels))  # i * (1/s): the arange table where both exist
+        else:
+            self.levelsValues = np.arange(0.0, 1.1, 1.0 / levels)
         self.s = len(self.levelsValues) - 1
         assert self.s == levels
         self.p = p
         self.vectorNormCompressor = vectorNormCompressor
+        self.__w = 0.0
         self.resetStats()
 
     def makeStandardDitheringFP64(self, levels, vectorNormCompressor, p=np.inf):
@@ -214,15 +224,15 @@ class Compressor:
         self.__w = min(dInput / (levels * levels), dInput**0.5 / levels)
 
     def _make_natd(self, name, ctype, levels, dInput, p):
-        if not 1 <= int(levels) <= 127:
-            raise ValueError("natural dithering supports 1..127 levels (8-bit codes)")
+        # compressors.py:191-221 (any level count constructs; the device codec takes up to 127)
+        self.__compressorName = name
+        self.__compressorType = ctype
         self.levelsValues = natural_levels(int(levels))
         self.s = len(self.levelsValues) - 1
         assert self.s == levels
         self.p = p
         r = min(p, 2)
-        w = 1.0 / 8.0 + (dInput ** (1.0 / r)) / (2 ** (self.s - 1)) * min(1, (dInput ** (1.0 / r)) / (2 ** (self.s - 1)))
-        self._set(name, ctype, w)
+        self.__w = 1.0 / 8.0 + (dInput ** (1.0 / r)) / (2 ** (self.s - 1)) * min(1, (dInput ** (1.0 / r)) / (2 ** (self.s - 1)))
         self.resetStats()
 
     def makeNaturalDitheringFP64(self, levels, dInput, p=np.inf):
@@ -332,7 +342,16 @@ class Compressor:
             self._finish(d, self.K)
             return out
         if t == CompressorType.ADAPTIVE_RANDOM_COMPRESSOR:
-            raise NotImplementedError("adaptive random compressor: not yet on the device path")
+            # np.random.choice(np.arange(self.D), size=1, p=|x| / sum|x|)  (compressors.py:297-301)
+            if self.D != d:
+                raise ValueError("'a' and 'p' must have same size")
+            status = int(codec.adaptive_prepare(x).item())  # numpy checks p before drawing
+            if status:
+                raise ValueError(codec.ADAPTIVE_ERRORS.get(status, "invalid probabilities"))
+            u = _rng.numpy_random_sample() if self.rng_mode == "compat" else self._philox_scalar(x.device)
+            out, _ = codec.adaptive_select(x, u)
+            self._finish(d, 1)
+            return out
         if t in _NATURAL:
             seed, ctr = self.philox.next()
             compat_u = None
@@ -347,6 +366,8 @@ class Compressor:
                 self._finish(d, 9.0 / 32.0 * d)
             return out
         if t in _STD or t in _NATD:
+            if not 1 <= self.s <= 127:
+                raise ValueError(f"the device dithering codec takes 1..127 levels (8-bit codes); s = {self.s}")
             kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
             x2 = x.reshape(1, d)
             norms = codec.quant_norm(x2, self.p)

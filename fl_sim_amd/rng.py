@@ -63,6 +63,21 @@ def numpy_shuffle_prefix(D: int, K: int) -> np.ndarray:
     return out[:kk]
 
 
+def numpy_random_sample() -> float:
+    """``np.random.random_sample()`` on numpy's global legacy RandomState (the draw ``np.random.choice``
+    makes, compressors.py:298), advancing that stream exactly as numpy would."""
+    name, key, pos, has_gauss, cached = np.random.get_state()
+    if name != "MT19937":
+        raise RuntimeError(f"unexpected numpy bit generator {name}")
+    mt = np.array(key, dtype=np.uint32)
+    p = c_int32(int(pos))
+    out = np.empty(1, dtype=np.float64)
+    _lib.call("flc_mt_random_doubles", mt.ctypes.data_as(POINTER(c_uint32)), p,
+              out.ctypes.data_as(POINTER(c_double)), 1)
+    np.random.set_state((name, mt, int(p.value), has_gauss, cached))
+    return float(out[0])
+
+
 class PhiloxStream:
     """Counter-based stream of the device kernels (Philox4x32-10 keyed by ``seed``).
 

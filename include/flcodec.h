@@ -155,6 +155,21 @@ int flc_stacked_decode_tiled(const int32_t* idx, const uint8_t* codes, int64_t k
                              const float* norm, int64_t n, float weight, int accumulate, float* out,
                              const uint32_t* tiles, void* stream);
 
+/* ------------------------------------------------------------------ adaptive random compressor
+ * (compressors.py:297-301): ind = np.random.choice(np.arange(n), size=1, p=|x| / sum|x|); out = 0,
+ * out[ind] = x[ind].  Bit-exact with numpy: S in numpy's order (8192-element buffers folded in order, each
+ * by pairwise_sum), p = fp32(|x| / S), the strictly sequential fp64 cumsum, cdf / cdf[-1] and
+ * searchsorted(u, side='right').  Two calls, because numpy validates p before it draws u:
+ *   flc_adaptive_prepare writes the check to *status (device int32): 0 ok, 1 "probabilities contain NaN",
+ *     2 "probabilities do not sum to 1" (|sum p - 1| > 3.4526698e-4);
+ *   flc_adaptive_select (same stream, same x and workspace) takes u in [0, 1) (compat mode: the legacy
+ *     np.random.random_sample() draw, see flc_mt_random_doubles) and writes out and *index (device int64);
+ *     it writes nothing when the status is non-zero.  x must be 16-byte aligned; 0 < n < 2^31. */
+size_t flc_adaptive_workspace_size(int64_t n);
+int flc_adaptive_prepare(const float* x, int64_t n, int32_t* status, void* ws, size_t ws_bytes, void* stream);
+int flc_adaptive_select(const float* x, int64_t n, double u, int64_t* index, float* out, void* ws, size_t ws_bytes,
+                        void* stream);
+
 /* ------------------------------------------------------------------ other compressors
  * identical (compressors.py:273-275): out = +x;  lazy (276-283): out = x / p (fp32 division);
  * rand-k (284-292): out = 0, out[idx[j]] = scale * x[idx[j]] (idx in any order, unique). */

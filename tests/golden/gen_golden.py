@@ -18,7 +18,11 @@ Variant fixtures (``agg_variants.npz``): SCAFFOLDServer.update
 client-id bookkeeping), FedDRServer.update under each constructible regularizer, and FedOptClient.communicate's
 client delta, same shapes.
 
-Usage:  python tests/golden/gen_golden.py [all|codec|agg|variants]
+Extra fixtures (``codec_extra.npz``, ``dropin_surface.json``): the adaptive random compressor at larger sizes and
+its error cases; the drop-in surface (name, fullName, w, is_biased, level tables, the assertion of unconstructible
+level counts) of every factory.
+
+Usage:  python tests/golden/gen_golden.py [all|codec|extra|agg|variants]
 """
 
 from __future__ import annotations
@@ -193,6 +197,121 @@ def gen_sparse(ref):
                 store[key + "|" + k] = np.array(v)
     np.savez_compressed(OUT / "codec_sparse.npz", **store)
     print("codec_sparse.npz:", len(store), "arrays")
+
+
+# ------------------------------------------------------------------------- extra codec fixtures (round 2)
+def make_heavy(D: int, seed: int) -> np.ndarray:
+    """Heavy-tailed delta (Cauchy, 20 % exact zeros): a cdf with long flat and steep stretches."""
+    g = np.random.default_rng(20_000 + seed * 104729 + D)
+    x = (g.standard_cauchy(D) * 1e-3).astype(np.float32)
+    x[g.random(D) < 0.2] = 0.0
+    return x
+
+
+ADAPTIVE_ERRORS = {
+    "zeros": np.zeros(5, dtype=np.float32),                                   # 0/0 -> NaN
+    "nan": np.array([1.0, np.nan, 2.0], dtype=np.float32),                    # NaN -> NaN
+    "inf": np.array([1.0, np.inf, 2.0], dtype=np.float32),                    # inf/inf -> NaN
+    "overflow": np.array([3e38, 3e38, 3e38, 1.0], dtype=np.float32),          # sum overflows: p = 0
+}
+
+
+def gen_extra(ref):
+    """codec_extra.npz: the adaptive random compressor at larger sizes, with zeros and heavy tails, and its
+    error cases (numpy validates p before it draws, so the streams must not move)."""
+    store: Dict[str, Any] = {}
+    mk = lambda D: (lambda c: c.makeAdaptiveRandomCompressor(D))  # noqa: E731
+    for kind, D, seed in (("adaptive_z", 65537, 0), ("adaptive_z", 1_000_003, 1), ("adaptive_z", 8192 * 3, 2),
+                          ("adaptive_heavy", 300_007, 3), ("adaptive_heavy", 4_000_000, 4)):
+        x = make_input(D, seed, zero_frac=0.05) if kind == "adaptive_z" else make_heavy(D, seed)
+        out, rec = run_codec(ref, mk(D), x, seed)
+        key = f"{kind}|{D}|{seed}"
+        store[key + "|sha_x"] = np.array(sha(x))
+        store[key + "|sha_out"] = np.array(sha(out))
+        store[key + "|index"] = np.array(np.flatnonzero(out), dtype=np.int64)
+        for k, v in rec.items():
+            store[key + "|" + k] = np.array(v)
+    for name, x in ADAPTIVE_ERRORS.items():
+        c = ref.Compressor()
+        c.makeAdaptiveRandomCompressor(len(x))
+        random.seed(9)
+        np.random.seed(9)
+        try:
+            with np.errstate(all="ignore"):
+                c.compressVector(x)
+            err = ""
+        except ValueError as e:
+            err = str(e)
+        key = f"adaptive_err|special:{name}|9"
+        store[key + "|x"] = x
+        store[key + "|error"] = np.array(err)
+        store[key + "|next_np"] = np.array(np.random.random_sample())
+        store[key + "|next_random"] = np.array(random.random())
+    np.savez_compressed(OUT / "codec_extra.npz", **store)
+    print("codec_extra.npz:", len(store), "arrays")
+
+
+def gen_surface(ref):
+    """dropin_surface.json: name, fullName, w / getW(), is_biased, compressorName and type of every factory
+    (compressors.py:58-262), and what an unconstructible level count does to the object."""
+    import json
+
+    def snap(c):
+        d = {"type": c.compressorType.value, "compressorName": c.compressorName, "w": float(c.w),
+             "getW": float(c.getW()), "is_biased": bool(c.is_biased), "is_unbiased": bool(c.is_unbiased),
+             "name": c.name, "fullName": c.fullName, "str": str(c), "repr": repr(c)}
+        if hasattr(c, "levelsValues"):
+            d["levelsValues"] = [float(v) for v in np.asarray(c.levelsValues)]
+            d["s"] = int(c.s)
+        return d
+
+    def norm_c():
+        nc = ref.Compressor("norm")
+        nc.makeIdenticalCompressor()
+        return nc
+
+    factories = {
+        "fresh": lambda c: None,
+        "identical": lambda c: c.makeIdenticalCompressor(),
+        "lazy_0.3": lambda c: c.makeLazyCompressor(0.3),
+        "lazy_0.125": lambda c: c.makeLazyCompressor(0.125),
+        "randk_7_100": lambda c: c.makeRandKCompressor(7, 100),
+        "randk_3_4096": lambda c: c.makeRandKCompressor(3, 4096),
+        "topk_41_4096": lambda c: c.makeTopKCompressor(41, 4096),
+        "natural64": lambda c: c.makeNaturalCompressorFP64(),
+        "natural32": lambda c: c.makeNaturalCompressorFP32(),
+        "adaptive_4096": lambda c: c.makeAdaptiveRandomCompressor(4096),
+        "qsgd64_4_1000": lambda c: c.makeQSGD_FP64(4, 1000),
+        "qsgd64_10_417482": lambda c: c.makeQSGD_FP64(10, 417482),
+    }
+    for L in (1, 2, 3, 5, 7, 8, 10):
+        for fp in ("64", "32"):
+            factories[f"std{fp}_{L}_inf"] = (lambda L, fp: lambda c: getattr(c, f"makeStandardDitheringFP{fp}")(
+                L, norm_c(), np.inf))(L, fp)
+        factories[f"std32_{L}_p2"] = (lambda L: lambda c: c.makeStandardDitheringFP32(L, norm_c(), 2))(L)
+    for L, dim, p in ((1, 100, np.inf), (3, 100, 2), (8, 100, np.inf), (8, 417482, 2), (16, 10, np.inf)):
+        for fp in ("64", "32"):
+            factories[f"natd{fp}_{L}_{dim}_{p}"] = (lambda L, dim, p, fp: lambda c: getattr(
+                c, f"makeNaturalDitheringFP{fp}")(L, dim, p))(L, dim, p, fp)
+    out: Dict[str, Any] = {}
+    for key, f in factories.items():
+        c = ref.Compressor("start")
+        f(c)
+        out[key] = snap(c)
+    # unconstructible standard-dithering tables (np.arange(0, 1.1, 1/L) has != L + 1 entries for L > 10):
+    # the reference raises AssertionError after it has already switched the type and the level table
+    for L in (11, 16, 127):
+        for fp in ("64", "32"):
+            c = ref.Compressor("start")
+            c.makeTopKCompressor(5, 50)
+            try:
+                getattr(c, f"makeStandardDitheringFP{fp}")(L, norm_c(), np.inf)
+                err = None
+            except AssertionError:
+                err = "AssertionError"
+            out[f"std{fp}_{L}_assert"] = {"error": err, **snap(c)}
+    (OUT / "dropin_surface.json").write_text(json.dumps(out, indent=1, sort_keys=True))
+    print("dropin_surface.json:", len(out), "cases")
 
 
 # ------------------------------------------------------------------------------------------- aggregation
@@ -471,6 +590,10 @@ def main():
         ref = load_reference_compressors()
         gen_codecs(ref)
         gen_sparse(ref)
+    if only in ("all", "extra"):
+        ref = load_reference_compressors()
+        gen_extra(ref)
+        gen_surface(ref)
     if only in ("all", "agg"):
         gen_aggregation()
     if only in ("all", "variants"):

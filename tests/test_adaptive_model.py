@@ -1,0 +1,134 @@
+"""CPU checks of the two facts the adaptive random kernels (fl_sim_amd/csrc/adaptive.hip) rest on.
+
+1. numpy's order for ``np.abs(x).sum()`` on a contiguous fp32 vector: the reduction runs over buffers of
+   np.getbufsize() = 8192 elements folded in order, each buffer summed by ``pairwise_sum`` (leaves of at
+   most 128 elements with 8 accumulators; splits at n/2 rounded down to a multiple of 8).  Restated here
+   and compared with numpy itself, bit for bit.
+2. The speculated fp64 running sum: a chunk's sequential run from a guess g shifted by (t - g) equals the
+   run from the true start t whenever (t - g) is an even multiple of the binade's spacing and both stay in
+   one binade (round-to-nearest-even commutes with such shifts).  The kernel's phase A / phase B scheme
+   is modelled here with numpy (vectorised across chunks) and must reproduce ``np.cumsum`` exactly at every
+   chunk boundary, re-running only a few chunks.
+"""
+
+import math
+import sys
+
+import numpy as np
+import pytest
+
+sys.setrecursionlimit(10_000)
+F32 = np.float32
+
+
+def pairwise_sum(a: np.ndarray) -> np.float32:
+    n = len(a)
+    if n < 8:
+        r = F32(0)
+        for v in a:
+            r = F32(r + v)
+        return r
+    if n <= 128:
+        r = [F32(v) for v in a[:8]]
+        i = 8
+        while i < n - (n % 8):
+            for j in range(8):
+                r[j] = F32(r[j] + a[i + j])
+            i += 8
+        res = F32(F32(F32(r[0] + r[1]) + F32(r[2] + r[3])) + F32(F32(r[4] + r[5]) + F32(r[6] + r[7])))
+        for v in a[i:]:
+            res = F32(res + v)
+        return res
+    n2 = n // 2
+    n2 -= n2 % 8
+    return F32(pairwise_sum(a[:n2]) + pairwise_sum(a[n2:]))
+
+
+def numpy_order_sum(a: np.ndarray) -> np.float32:
+    s = F32(0)
+    for b in range(0, len(a), 8192):
+        s = F32(s + pairwise_sum(a[b:b + 8192]))
+    return s
+
+
+@pytest.mark.parametrize("n", [1, 5, 8, 9, 127, 128, 129, 300, 1000, 8191, 8192, 8193, 16384, 20_000, 65_537])
+@pytest.mark.parametrize("scale", [1e-3, 1.0, 3e5])
+def test_numpy_sum_order(n, scale):
+    g = np.random.default_rng(n)
+    x = np.abs((g.standard_normal(n) * scale).astype(F32))
+    assert np.getbufsize() == 8192
+    assert numpy_order_sum(x).view(np.uint32) == np.abs(x).sum().view(np.uint32)
+
+
+def _binade(v: float) -> int:
+    return int(np.float64(v).view(np.uint64) >> np.uint64(52))
+
+
+def _spacing(e: int) -> float:
+    return 5e-324 if e == 0 else math.ldexp(1.0, e - 1075)
+
+
+def speculated_cumsum_ends(p: np.ndarray, chunk: int, guess: np.ndarray):
+    """The kernel's scheme: returns (exact running sum at each chunk end, number of re-run chunks)."""
+    n = len(p)
+    nq = -(-n // chunk)
+    P = np.zeros(nq * chunk)
+    P[:n] = p
+    P = P.reshape(nq, chunk)
+    ga = guess.astype(np.float64)
+    gb = np.array([g + _spacing(_binade(g)) for g in ga])
+    ea, eb = ga.copy(), gb.copy()
+    for s in range(chunk):  # phase A: every chunk's two runs, in parallel across chunks
+        ea = ea + P[:, s]
+        eb = eb + P[:, s]
+    t, reruns, ends = 0.0, 0, []
+    for j in range(nq):  # phase B
+        d = t - ga[j]
+        if d == 0.0:
+            t = ea[j]
+        else:
+            e = _binade(ga[j])
+            ok = e > 64 and _binade(t) == e
+            if ok:
+                k = d * math.ldexp(1.0, 1075 - e)
+                even = int(k) % 2 == 0
+                g, end = (ga[j], ea[j]) if even else (gb[j], eb[j])
+                cand = end + (t - g)
+                ok = _binade(g) == e and _binade(end) == e and _binade(cand) == e
+            if ok:
+                t = cand
+            else:
+                reruns += 1
+                for q in P[j]:
+                    t = t + q
+        ends.append(t)
+    return np.array(ends), reruns
+
+
+@pytest.mark.parametrize("n,dist,zero_frac", [(1 << 18, "normal", 0.0), (1_000_003, "normal", 0.05),
+                                              (1 << 20, "cauchy", 0.2), (300_001, "lognormal", 0.5),
+                                              (200_000, "spiky", 0.0)])
+def test_speculated_cumsum_is_exact(n, dist, zero_frac):
+    g = np.random.default_rng(n)
+    if dist == "normal":
+        x = g.standard_normal(n)
+    elif dist == "cauchy":
+        x = g.standard_cauchy(n)
+    elif dist == "lognormal":
+        x = g.lognormal(0, 8, n)  # many binades apart
+    else:
+        x = g.standard_normal(n) * 1e-6
+        x[g.integers(0, n, 20)] = 1e3  # a handful of elements carry nearly all the mass
+    x = x.astype(F32)
+    x[g.random(n) < zero_frac] = 0
+    ax = np.abs(x)
+    p = (ax / ax.sum()).astype(np.float64)
+    chunk = 2048
+    starts = np.arange(0, n, chunk)
+    q = np.add.reduceat(ax.astype(np.float64), starts)
+    guess = np.concatenate([[0.0], np.cumsum(q)[:-1]]) / float(ax.sum())
+    ends, reruns = speculated_cumsum_ends(p, chunk, guess)
+    cdf = np.cumsum(p)
+    want = cdf[np.minimum(starts + chunk, n) - 1]
+    assert np.array_equal(ends, want)
+    assert reruns <= 80  # about one per binade the running sum crosses

@@ -111,13 +111,13 @@ def test_sparse_compressor_matches_reference_fixture(case):
     rec = SPARSE[case]
     parts = case.split("|")
     name, seed = parts[0], int(parts[-1])
-    if name == "adaptive":
-        pytest.skip("adaptive random compressor: device path lands in a later round")
     x = gc.case_input(case, rec)
     D = len(x)
-    K = int(parts[2])
+    K = 1 if name == "adaptive" else int(parts[2])
     c = Compressor()
-    if name == "topk":
+    if name == "adaptive":
+        c.makeAdaptiveRandomCompressor(D)
+    elif name == "topk":
         c.makeTopKCompressor(K, D)
     else:
         K = max(K, 1)
