@@ -74,6 +74,19 @@ def philox_uniforms(n: int, seed: int, counter: int, start: int = 0) -> np.ndarr
     return w.astype(F64) * 2.0**-32
 
 
+def philox_uniforms_at(idx: np.ndarray, seed: int, counter: int) -> np.ndarray:
+    """u[e] for the given element indices only (same stream as philox_uniforms)."""
+    e = np.asarray(idx, dtype=np.uint64)
+    g = e >> np.uint64(2)
+    words = philox4x32_10(
+        (g & np.uint64(0xFFFFFFFF)).astype(np.uint32), (g >> np.uint64(32)).astype(np.uint32),
+        np.uint32(counter & 0xFFFFFFFF), np.uint32((counter >> 32) & 0xFFFFFFFF),
+        np.uint32(seed & 0xFFFFFFFF), np.uint32((seed >> 32) & 0xFFFFFFFF),
+    )
+    w = np.stack(words, axis=1)[np.arange(len(e)), (e & np.uint64(3)).astype(np.int64)]
+    return w.astype(F64) * 2.0**-32
+
+
 # ------------------------------------------------------------------------------------------ compressors
 def identical(x: np.ndarray):
     """compressors.py:273-275."""
@@ -98,6 +111,29 @@ def topk_kept(x: np.ndarray, K: int) -> Tuple[np.ndarray, np.ndarray]:
     """Kept set of compressors.py:293-296 under a stable argsort: (ascending idx, values)."""
     order = np.argsort(x, kind="stable")
     kept = np.sort(order[len(x) - K:]) if 0 < K < len(x) else np.arange(len(x))
+    return kept.astype(np.int64), x[kept]
+
+
+def order_keys(x: np.ndarray) -> np.ndarray:
+    """np.argsort order as uint32 keys: -0 == +0, NaN largest."""
+    b = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).copy()
+    b[b == 0x80000000] = 0
+    k = np.where(b & np.uint32(0x80000000), ~b, b | np.uint32(0x80000000)).astype(np.uint32)
+    k[np.isnan(x)] = 0xFFFFFFFF
+    return k
+
+
+def topk_kept_select(x: np.ndarray, K: int) -> Tuple[np.ndarray, np.ndarray]:
+    """topk_kept in O(n) (np.partition on order keys): every key above the K-th largest, then the
+    highest-indexed ties — the same set a stable ascending argsort keeps."""
+    n = len(x)
+    if not 0 < K < n:
+        return topk_kept(x, K)
+    keys = order_keys(x)
+    t = np.partition(keys, n - K)[n - K]
+    above = np.flatnonzero(keys > t)
+    ties = np.flatnonzero(keys == t)
+    kept = np.sort(np.concatenate([above, ties[len(ties) - (K - len(above)):]]))
     return kept.astype(np.int64), x[kept]
 
 
@@ -191,10 +227,11 @@ def natural_dithering(x, s, p, u_of, pnorm=None, fp64_stats=False):
     return out, send, pn
 
 
-def stacked(x: np.ndarray, K: int, s: int, u_of: Callable[[np.ndarray], np.ndarray]):
+def stacked(x: np.ndarray, K: int, s: int, u_of: Callable[[np.ndarray], np.ndarray], fast: bool = False):
     """Top-K then standard dithering (p = inf) of the K-sparse result — the pipeline the fused
-    flc_stacked_encode implements.  Returns (dense out, kept idx, codes (sign<<7 | level), norm)."""
-    kept, vals = topk_kept(x, K)
+    flc_stacked_encode implements.  Returns (dense out, kept idx, codes (sign<<7 | level), norm).
+    ``fast`` selects the kept set with topk_kept_select (same set, O(n))."""
+    kept, vals = (topk_kept_select if fast else topk_kept)(x, K)
     y = np.zeros_like(x)
     y[kept] = vals
     pn = F32(np.max(np.abs(y))) if len(y) else F32(0)

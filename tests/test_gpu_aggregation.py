@@ -7,6 +7,7 @@ import pytest
 import torch
 
 from oracle import aggregation_ref as agg_ref
+from oracle import compressors_ref as ref
 from tests import golden_cases as gc
 from tests.golden.gen_golden import CONFIG1_SHAPES, SMALL_SHAPES, make_model, make_msgs
 
@@ -132,6 +133,36 @@ def test_dist_fold_with_device_codec_single_rank():
         v = codec.stacked_decode(codec.stacked_encode(d, k, 127, seed=11 + c, counter=3)).cpu()
         exp.add_(v, alpha=float(np.float32(wi)))  # torch CPU add_(alpha): one fp32 fma per element
     assert np.array_equal(got.cpu().numpy().view(np.uint32), exp.numpy().view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_config3_fold_full_size_vs_oracle():
+    """BASELINE configs[3] at its real size on one rank: 8 clients x 25,000,000 fp32, w_i = ts_i / sum ts with
+    ts_i = 100 (i + 1) (nodes.py:1165-1180), each client through the stacked codec (top-k 1 % -> 8-bit dither,
+    Philox) and decoded into the partial sum with its weight fused.  Expected: the oracle's stacked codec per
+    client fed the same Philox uniforms, folded on the CPU with torch add_(alpha) in client order — the
+    reference's own fp32 fma chain.  Bit-exact."""
+    from fl_sim_amd import dist as fdist
+
+    n, k, n_cl, seed, ctr = 25_000_000, 250_000, 8, 100, 4
+    ts = [100 * (i + 1) for i in range(n_cl)]
+    w = fdist.sample_weights(ts)
+    g = np.random.default_rng(33)
+    xs = []
+    for i in range(n_cl):
+        x = (g.standard_normal(n) * 1e-3).astype(np.float32)
+        if i % 2:
+            x[g.random(n) < 0.05] = 0.0  # the "realistic" variant with exact zeros (SURVEY §8(d))
+        xs.append(x)
+    deltas = [torch.from_numpy(x).cuda() for x in xs]
+    got = fdist.aggregate_round(deltas, w, list(range(n_cl)), fdist.stacked_decode_accumulate(k, seed=seed, counter=ctr))
+    got = got.cpu().numpy()
+    exp = torch.zeros(n, dtype=torch.float32)
+    for c, (x, wi) in enumerate(zip(xs, w)):
+        dec, _, _, _ = ref.stacked(x, k, 127, lambda idx, c=c: ref.philox_uniforms_at(idx, seed + c, ctr), fast=True)
+        exp.add_(torch.from_numpy(dec), alpha=wi)
+    assert np.array_equal(got.view(np.uint32), exp.numpy().view(np.uint32))
+    assert np.count_nonzero(got) >= k  # the clients' kept sets overlap only partially
 
 
 # ------------------------------------------------------------------- aggregation variants (SURVEY §8(f) f4)
