@@ -48,6 +48,7 @@ SIGNATURES = {
     ),
     "flc_natural_decode": (c_int, [c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p]),
     "flc_topk_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "flc_topk_status": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "flc_topk_encode": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_sparse_decode_workspace_size": (c_size_t, [c_int64]),
     "flc_sparse_decode": (

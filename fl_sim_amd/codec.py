@@ -10,6 +10,7 @@ drives it directly for the device-resident measurement.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -154,6 +155,48 @@ def natural_decode(codes: torch.Tensor, n: int, out: Optional[torch.Tensor] = No
 
 
 # ------------------------------------------------------------------------------------------------ top-k
+# FLC_TOPK_CHECK=1: read the persistent encoder's sticky error word after every top-k / stacked encode
+# (one host synchronisation per call) and raise if a call lost co-residency (include/flcodec.h)
+TOPK_CHECK = os.environ.get("FLC_TOPK_CHECK", "0") not in ("", "0")
+TOPK_ERRORS = {1: "digit not found", 2: "count mismatch", 4: "exchange spin timeout"}
+
+
+def topk_status(device: Optional[torch.device] = None, reset: bool = True) -> int:
+    """The sticky error word of the top-k workspace of ``device``'s current stream (0 = every encode since
+    the last reset was exact).  Synchronises that stream."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    key = (device.index if device.index is not None else torch.cuda.current_device(), _stream(device), "topk")
+    ws = _WS.get(key)
+    if ws is None:
+        return 0
+    out = torch.empty(1, dtype=torch.int64, device=device)
+    call("flc_topk_status", _p(ws), _p(out), int(reset), _stream(device))
+    return int(out.item())
+
+
+def topk_status_all(reset: bool = True) -> Dict[Tuple[int, int], int]:
+    """{(device, stream): error word} of every cached top-k workspace.  Synchronises each device first and
+    reads on its current stream (the stream a workspace was used on may be gone)."""
+    res: Dict[Tuple[int, int], int] = {}
+    for (dev, stream, kind), ws in list(_WS.items()):
+        if kind != "topk":
+            continue
+        d = torch.device("cuda", dev)
+        torch.cuda.synchronize(d)
+        out = torch.empty(1, dtype=torch.int64, device=d)
+        call("flc_topk_status", _p(ws), _p(out), int(reset), _stream(d))
+        res[(dev, stream)] = int(out.item())
+    return res
+
+
+def _after_encode(device: torch.device) -> None:
+    if TOPK_CHECK:
+        err = topk_status(device)
+        if err:
+            bits = ", ".join(v for b, v in TOPK_ERRORS.items() if err & b)
+            raise _lib.FlcError(f"top-k encode lost co-residency or failed ({bits}); its kept set may be wrong")
+
+
 def _tiles(n: int, device: torch.device) -> torch.Tensor:
     """CSR tile pointers over FLC_TILE-output tiles (include/flcodec.h)."""
     return torch.empty((n + TILE - 1) // TILE + 1, dtype=torch.int32, device=device)
@@ -169,6 +212,7 @@ def topk_encode(x: torch.Tensor, k: int, with_tiles: bool = False):
     tiles = _tiles(n, x.device) if with_tiles else None
     ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
     call("flc_topk_encode_tiled", _p(x), n, k, _p(idx), _p(val), _p(tiles), _p(ws), ws.numel(), _stream(x.device))
+    _after_encode(x.device)
     return (idx, val, tiles) if with_tiles else (idx, val)
 
 
@@ -214,6 +258,7 @@ def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, co
     ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
     call("flc_stacked_encode_tiled", _p(x), n, k, levels, seed, counter, None, _p(idx), _p(codes), _p(norm),
          _p(tiles), _p(ws), ws.numel(), _stream(x.device))
+    _after_encode(x.device)
     return StackedPacket(idx, codes, norm, n, levels, tiles)
 
 

@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <stddef.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -1720,6 +1721,15 @@ int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_
                        void* stream) {
   return flc_stacked_encode_tiled(x, n, k, levels, seed, counter, compat_u, idx, codes, norm, nullptr, ws, ws_bytes,
                                   stream);
+}
+
+int flc_topk_status(void* ws, uint64_t* err_out, int reset, void* stream) {
+  if (!ws || !err_out) return fail(FLC_EINVAL, "flc_topk_status: null workspace or output");
+  hipStream_t st = as_stream(stream);
+  char* err_word = static_cast<char*>(ws) + kOffSt + offsetof(EncState, err);
+  FLC_CHECK_HIP(hipMemcpyAsync(err_out, err_word, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+  if (reset) FLC_CHECK_HIP(hipMemsetAsync(err_word, 0, sizeof(uint64_t), st));
+  return FLC_OK;
 }
 
 }  // extern "C"

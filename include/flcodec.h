@@ -117,7 +117,19 @@ int flc_natural_decode(const uint16_t* codes, int64_t n, float weight, int accum
 /* ------------------------------------------------------------------ top-k sparsifier
  * (compressors.py:293-296): keeps the k largest *signed* values (NaN largest, -0 == +0); among values
  * equal to the k-th largest the highest indices are kept (the order of a stable ascending argsort).
- * Output: idx[k] ascending, val[k] the kept values bit-for-bit.  Requires 0 < k < n. */
+ * Output: idx[k] ascending, val[k] the kept values bit-for-bit.  Requires 0 < k < n.
+ *
+ * Co-residency: the top-k and stacked encoders are ONE persistent launch of one 1024-thread block per CU
+ * whose blocks hand work to each other through flags in the workspace, so every block of the launch must
+ * be resident at once.  Launches of these encoders on one device are serialised by the library (stream
+ * order, or an event chain across streams; not inside a stream capture); kernels of other libraries or
+ * processes that occupy CUs for long stretches can delay a block past the bounded spin, which the kernel
+ * records in the workspace's sticky error word instead of hanging.  flc_topk_status reads that word:
+ * 0 = every call since the last reset was exact; otherwise bits 1 (digit not found), 2 (count mismatch),
+ * 4 (exchange spin timeout) mean the kept set of some call may be wrong.  Check it after calls that may
+ * have shared the device (fl_sim_amd does when FLC_TOPK_CHECK=1, and the GPU tests after every test). */
+/* *err_out (device uint64) = the workspace's sticky error word; reset != 0 clears it (stream-ordered) */
+int flc_topk_status(void* ws, uint64_t* err_out, int reset, void* stream);
 size_t flc_topk_workspace_size(int64_t n, int64_t k);
 int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, void* ws,
                     size_t ws_bytes, void* stream);

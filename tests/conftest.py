@@ -26,3 +26,20 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _topk_error_word_is_clear(request):
+    """Every GPU test ends with the persistent top-k encoder's sticky error word at 0 on every workspace it
+    used (include/flcodec.h, flc_topk_status): a lost co-residency would otherwise pass silently."""
+    yield
+    if "gpu" not in request.keywords:
+        return
+    import torch
+
+    if not torch.cuda.is_available():
+        return
+    from fl_sim_amd import codec
+
+    bad = {k: v for k, v in codec.topk_status_all(reset=True).items() if v}
+    assert not bad, f"top-k encoder error word set: {bad}"

@@ -75,3 +75,18 @@ def test_workspace_sizes_monotone():
     assert 0 < a < b
     assert _lib.size("flc_quant_workspace_size", 10, 417482) > 0
     assert _lib.size("flc_natural_workspace_size", 417482) > 0
+
+
+def test_topk_status_plumbing_without_gpu(monkeypatch):
+    """flc_topk_status validates its arguments before any HIP call; codec raises when the word is set."""
+    from fl_sim_amd import _lib, codec
+
+    lib = _lib.load()
+    assert lib.flc_topk_status(None, None, 1, None) == 1  # FLC_EINVAL
+    assert "flc_topk_status" in lib.flc_last_error().decode()
+    monkeypatch.setattr(codec, "TOPK_CHECK", True)
+    monkeypatch.setattr(codec, "topk_status", lambda device=None, reset=True: 4)
+    with pytest.raises(_lib.FlcError, match="spin timeout"):
+        codec._after_encode(None)
+    monkeypatch.setattr(codec, "topk_status", lambda device=None, reset=True: 0)
+    codec._after_encode(None)  # clean word: no error
