@@ -14,8 +14,8 @@ decode-accumulate + RCCL reduce of a 25M delta per client).  ``roofline`` is the
 (stacked_encode: the fused filter + select + compaction kernel) — its algorithmic bytes over its live
 HIP-event duration, timed in a separate short run so no event sits inside the timed steps;
 ``extra.kernels_us`` times every kernel of the step the same way and ``extra.roofline_decode`` gives
-the decode kernel's figure.  ``cpu_baseline`` times the numpy oracle on a bounded sample of the
-workload on this host.
+the decode kernel's figure.  ``cpu_baseline`` times the CPU-PyTorch path of the same workload on this
+host (all threads on the full delta, one thread on a 64 MiB sample) and, labelled apart, the numpy oracle.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--skip-extra] [--skip-cpu]
 """
@@ -155,29 +155,82 @@ def timed(fn, steps, warmup, world, probe=None):
     return (t1 - t0) * 1e3 / steps, probe_ms
 
 
-def cpu_baseline(budget_s: float = 12.0):
-    """The numpy oracle (oracle/compressors_ref.py) on a bounded sample of the headline workload."""
-    from oracle import compressors_ref as ref
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
-    n = 16_777_216  # 64 MiB sample of the 1 GiB delta, same K/D ratio
-    k = n // 100
-    g = np.random.default_rng(1234)
-    x = (g.standard_normal(n) * 1e-3).astype(np.float32)
-    reps, t_tot = 0, 0.0
-    while t_tot < budget_s and reps < 20:
+
+def _time_reps(fn, budget_s: float, max_reps: int, warm: bool = True):
+    if warm:
+        fn()  # allocator, thread pool
+    reps, tot = 0, 0.0
+    while reps < max_reps and (reps == 0 or tot < budget_s):
         t0 = time.perf_counter()
-        u = ref.philox_uniforms(n, 1, reps)
-        ref.stacked(x, k, LEVELS, lambda i: u[i])
-        t_tot += time.perf_counter() - t0
+        fn()
+        tot += time.perf_counter() - t0
         reps += 1
-    per = t_tot / reps
+    return tot / reps, reps
+
+
+def cpu_baseline():
+    """north_star's CPU baseline: the CPU-PyTorch path of the same workload (oracle/torch_ref.py: torch.topk,
+    the dithering, a dense scatter) on this host's cores, all threads on the full 1 GiB delta and one thread
+    on a 64 MiB sample; the numpy oracle (oracle/compressors_ref.py, one core) on the 64 MiB sample is kept as
+    a separately labelled field.  Rates use the same algorithmic bytes as `value` (8 D + 10 K)."""
+    from oracle import compressors_ref as ref
+    from oracle import torch_ref
+
+    threads0 = torch.get_num_threads()
+    all_threads = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = all_threads
+    gen = torch.Generator().manual_seed(1234)
+    x_full = torch.randn(D_HEADLINE, generator=gen) * 1e-3
+    n_s = 16_777_216  # 64 MiB sample, same K/D ratio
+    x_s = x_full[:n_s].clone()
+
+    torch.set_num_threads(all_threads)
+    torch_ref.stacked_step(x_s, n_s // 100, LEVELS, gen)  # warm the pool on the sample, not on 1 GiB
+    per_all, reps_all = _time_reps(lambda: torch_ref.stacked_step(x_full, D_HEADLINE // 100, LEVELS, gen), 8.0, 3,
+                                   warm=False)
+    torch.set_num_threads(1)
+    per_one, reps_one = _time_reps(lambda: torch_ref.stacked_step(x_s, n_s // 100, LEVELS, gen), 4.0, 3)
+    torch.set_num_threads(threads0)
+    del x_full
+
+    xs = x_s.numpy()
+    per_np, reps_np = _time_reps(
+        lambda: ref.stacked(xs, n_s // 100, LEVELS, lambda i: ref.philox_uniforms_at(i, 1, 0)), 4.0, 3)
+    model = cpu_model()
     return {
-        "value": round(stacked_bytes(n, k) / per / 1e9, 4),
+        "value": round(stacked_bytes(D_HEADLINE, D_HEADLINE // 100) / per_all / 1e9, 4),
         "unit": "GB/s",
-        "cores": 1,
+        "cores": all_threads,
         "kind": "port",
-        "sample": f"numpy oracle stacked top-k 1% -> 8-bit dither on D={n} (64 MiB), {reps} reps, "
-                  f"{per * 1e3:.0f} ms/rep; host has {os.cpu_count()} logical CPUs",
+        "sample": f"CPU-PyTorch stacked top-k 1% -> 8-bit dither (oracle/torch_ref.py: torch.topk + dither + dense "
+                  f"scatter) on the full 1 GiB delta, torch.set_num_threads({all_threads}) = os.cpu_count(), "
+                  f"{reps_all} reps, {per_all * 1e3:.0f} ms/rep; {model}; {affinity} CPUs in this process's "
+                  f"affinity mask",
+        "cpu_model": model,
+        "affinity_cpus": affinity,
+        "one_thread": {
+            "value": round(stacked_bytes(n_s, n_s // 100) / per_one / 1e9, 4), "unit": "GB/s", "cores": 1,
+            "sample": f"same CPU-PyTorch path, torch.set_num_threads(1), 64 MiB sample (D={n_s}), {reps_one} reps, "
+                      f"{per_one * 1e3:.0f} ms/rep",
+        },
+        "numpy_oracle_1core": {
+            "value": round(stacked_bytes(n_s, n_s // 100) / per_np / 1e9, 4), "unit": "GB/s", "cores": 1,
+            "sample": f"numpy oracle (oracle/compressors_ref.py stacked, O(n) selection) on the 64 MiB sample, "
+                      f"{reps_np} reps, {per_np * 1e3:.0f} ms/rep",
+        },
     }
 
 
