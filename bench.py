@@ -121,6 +121,18 @@ def launch_check(world: int, rank: int) -> None:
         dist.destroy_process_group()
 
 
+def settle_gpu(buf: torch.Tensor, seconds: float = 0.2) -> None:
+    """Keep the device busy for `seconds` before any warmup step (setup, untimed).  In a fresh process the
+    GPU runs steps ~5-18 of the headline 3-5 % slow (406-417 vs 394 us) even after idling 0.2 s, and not at
+    all after 0.2 s of sustained memory traffic: a power/clock transition that follows the onset of load
+    (tools/coldstart.py, profiles/r02/r02e_coldstart_steps.txt).  The driver's `--warmup 5` would otherwise
+    time exactly that transition."""
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        buf.zero_()
+        torch.cuda.synchronize()
+
+
 def stacked_bytes(D: int, K: int) -> int:
     return 8 * D + 10 * K
 
@@ -201,6 +213,9 @@ def cpu_baseline():
     torch_ref.stacked_step(x_s, n_s // 100, LEVELS, gen)  # warm the pool on the sample, not on 1 GiB
     per_all, reps_all = _time_reps(lambda: torch_ref.stacked_step(x_full, D_HEADLINE // 100, LEVELS, gen), 8.0, 3,
                                    warm=False)
+    share = min(16, all_threads)  # the GPU box's CPU share per GPU
+    torch.set_num_threads(share)
+    per_share, reps_share = _time_reps(lambda: torch_ref.stacked_step(x_s, n_s // 100, LEVELS, gen), 4.0, 3)
     torch.set_num_threads(1)
     per_one, reps_one = _time_reps(lambda: torch_ref.stacked_step(x_s, n_s // 100, LEVELS, gen), 4.0, 3)
     torch.set_num_threads(threads0)
@@ -225,6 +240,11 @@ def cpu_baseline():
             "value": round(stacked_bytes(n_s, n_s // 100) / per_one / 1e9, 4), "unit": "GB/s", "cores": 1,
             "sample": f"same CPU-PyTorch path, torch.set_num_threads(1), 64 MiB sample (D={n_s}), {reps_one} reps, "
                       f"{per_one * 1e3:.0f} ms/rep",
+        },
+        f"threads_{share}": {
+            "value": round(stacked_bytes(n_s, n_s // 100) / per_share / 1e9, 4), "unit": "GB/s", "cores": share,
+            "sample": f"same CPU-PyTorch path, torch.set_num_threads({share}), 64 MiB sample, {reps_share} reps, "
+                      f"{per_share * 1e3:.0f} ms/rep",
         },
         "numpy_oracle_1core": {
             "value": round(stacked_bytes(n_s, n_s // 100) / per_np / 1e9, 4), "unit": "GB/s", "cores": 1,
@@ -273,6 +293,7 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(D, generator=gen, device=dev) * 1e-3
     out = torch.empty(D, dtype=torch.float32, device=dev)
+    settle_gpu(out)
     ctr = [0]
 
     def step():
@@ -381,7 +402,37 @@ def main():
             "note": "pinned host deltas -> H2D / codec / D2H pipelined across clients (fl_sim_amd.host); "
                     "fill and drain included; same bytes formula",
         }
-        del hx, hout, hout2, pipe
+        # f3 with the packed wire: clients send only their wire to the host (D2H ~14.5 MB per 1 GiB client), the
+        # server copies each wire back (H2D) and decodes it into ONE device accumulator with the client's weight
+        # fused; one D2H of the aggregate per round.  PCIe carries 4 D + 2 x wire per client instead of 8 D.
+        from fl_sim_amd.host import HostWirePipeline
+
+        wp = HostWirePipeline(D, K, LEVELS, dev)
+        wires = wp.new_wires(m_cl)
+        acc = torch.empty(D, dtype=torch.float32, device=dev)
+        wts = [1.0 / m_cl] * m_cl
+        wp.encode([hx] * 2, wires[:2], seeds=[rank] * 2)  # warm (streams, workspace, pinned pages)
+        wp.decode_accumulate(wires[:2], wts[:2], acc)
+        wp.synchronize()
+        barrier(world)
+        t0 = time.perf_counter()
+        wp.encode([hx] * m_cl, wires, seeds=[rank] * m_cl, counters=list(range(m_cl)))
+        wp.decode_accumulate(wires, wts, acc)
+        wp.wait()
+        hout.copy_(acc, non_blocking=True)
+        torch.cuda.synchronize()
+        barrier(world)
+        ms_w = max_over_ranks((time.perf_counter() - t0) * 1e3 / m_cl, world)
+        extra["e2e_host_wire"] = {
+            "ms_per_client": round(ms_w, 4),
+            "GB_s": round(world * stacked_bytes(D, K) / (ms_w * 1e-3) / 1e9, 1),
+            "clients": m_cl,
+            "wire_bytes_per_client": wires[0].nbytes,
+            "note": "pinned host deltas -> H2D -> encode -> D2H of the wire only; server: H2D of each wire -> "
+                    "weighted decode-accumulate into one device accumulator -> one D2H of the aggregate "
+                    "(fl_sim_amd.host.HostWirePipeline); same bytes formula",
+        }
+        del hx, hout, hout2, pipe, wp, wires, acc
     del x, out
     torch.cuda.empty_cache()
 

@@ -424,6 +424,36 @@ def test_host_pipeline_matches_sequential():
         pipe.run([torch.empty(n)], [hout[0]], k)  # not pinned
 
 
+def test_host_wire_pipeline_equals_device_fold():
+    """f3 with the packed wire: pinned host deltas -> H2D -> encode -> D2H of the wire only; then the server's H2D of
+    each wire -> decode with the client's weight fused into one accumulator.  Equals the device-resident fold of the
+    same clients (dist.aggregate_round with the stacked decode-accumulate step) bit for bit; the wires equal the
+    device packets."""
+    from fl_sim_amd import dist as fdist
+    from fl_sim_amd.host import HostWirePipeline
+
+    codec = _codec()
+    n, k, m, seed = 3_000_017, 30_000, 5, 21
+    gen = torch.Generator(device="cpu").manual_seed(6)
+    hx = [(torch.randn(n, generator=gen) * 1e-3).pin_memory() for _ in range(m)]
+    w = fdist.sample_weights([100 * (i + 1) for i in range(m)])
+    pipe = HostWirePipeline(n, k, 127, torch.device(DEV))
+    wires = pipe.new_wires(m)
+    pipe.encode(hx, wires, seeds=[seed + i for i in range(m)], counters=[2] * m)
+    pipe.synchronize()
+    for i in range(m):
+        pkt = codec.stacked_encode(hx[i].to(DEV), k, 127, seed=seed + i, counter=2)
+        assert torch.equal(wires[i].idx, pkt.idx.cpu()) and torch.equal(wires[i].codes, pkt.codes.cpu())
+        assert torch.equal(wires[i].norm, pkt.norm.cpu()) and torch.equal(wires[i].tiles, pkt.tiles.cpu())
+        assert wires[i].nbytes == pkt.nbytes
+    acc = torch.empty(n, dtype=torch.float32, device=DEV)
+    pipe.decode_accumulate(wires, w, acc)
+    pipe.wait()
+    exp = fdist.aggregate_round([t.to(DEV) for t in hx], w, list(range(m)),
+                                fdist.stacked_decode_accumulate(k, seed=seed, counter=2))
+    assert torch.equal(acc, exp)
+
+
 def _adversarial(name):
     """Inputs that drive the encoder off its fast path: a floor that admits too few elements (fallback pass), a
     region with more candidates than a block's LDS (x-mode), and massive ties at the k-th value."""
