@@ -450,10 +450,21 @@ def main():
 
         ms2, _ = timed(step2, 50, 10, world)
         ms2 = max_over_ranks(ms2, world)
+        def step2f():  # the same round trip in two launches: norm partials, then encode (norm folded in) + decode
+            c2[0] += 1
+            codec.quant_encode_auto(X, 0, LEVELS, seed=rank, counter=c2[0])
+
+        ms2f, _ = timed(step2f, 50, 10, world)
+        ms2f = max_over_ranks(ms2f, world)
         extra["config2_quant8_10x417482"] = {
             "us_per_step": round(ms2 * 1e3, 2),
             "GB_s": round(b2 * d2 * 10 / (ms2 * 1e-3) / 1e9, 1),
-            "bytes_formula": "(8 + 8/4) * D per client",
+            "bytes_formula": "(8 + 8/4) * D per client (norm, encode, decode reading the wire: 3 launches)",
+            "fused_us_per_step": round(ms2f * 1e3, 2),
+            "fused_GB_s": round(b2 * d2 * 9 / (ms2f * 1e-3) / 1e9, 1),
+            "fused_bytes_formula": "(4 + 1 + 4) * D per client (flc_quant_encode_auto: norm partials, then the encode "
+                                   "folding the norm and writing the codes and the decoded values from registers: 2 "
+                                   "launches, the wire is not read back)",
         }
         del X
         # configs[2]: top-k 1% of a 25M delta (encode + dense decode)

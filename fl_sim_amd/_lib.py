@@ -38,6 +38,16 @@ SIGNATURES = {
         [c_void_p, c_int64, c_int64, c_int, c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
          c_void_p, c_size_t, c_void_p],
     ),
+    "flc_quant_encode_decode": (
+        c_int,
+        [c_void_p, c_int64, c_int64, c_int, c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_size_t, c_void_p],
+    ),
+    "flc_quant_encode_auto": (
+        c_int,
+        [c_void_p, c_int64, c_int64, c_int, c_int, c_int, c_int, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_size_t, c_void_p],
+    ),
     "flc_quant_decode": (
         c_int, [c_void_p, c_int64, c_int64, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
     ),

@@ -121,6 +121,46 @@ def quant_encode(x2d: torch.Tensor, kind: int, levels: int, norms: torch.Tensor,
     return QuantPacket(codes, norms, rows, d, kind, levels, bits, nnz)
 
 
+def quant_encode_decode(x2d: torch.Tensor, kind: int, levels: int, norms: torch.Tensor, seed: int = 0,
+                        counter: int = 0, compat_u: Optional[torch.Tensor] = None, want_nnz: bool = True,
+                        out: Optional[torch.Tensor] = None) -> Tuple[QuantPacket, torch.Tensor]:
+    """quant_encode and quant_decode in one pass (flc_quant_encode_decode): the same codes, and the decoded batch
+    computed from each code as it is made.  Returns (packet, decoded [rows, d])."""
+    x2d = _dev_f32(x2d)
+    rows, d = x2d.shape
+    bits = code_bits(levels)
+    codes = torch.empty(max((rows * d * bits + 7) // 8, 1), dtype=torch.uint8, device=x2d.device)
+    nnz = torch.empty(rows, dtype=torch.int64, device=x2d.device) if want_nnz else None
+    if out is None:
+        out = torch.empty(rows, d, dtype=torch.float32, device=x2d.device)
+    if compat_u is not None and compat_u.dtype != torch.float64:
+        raise TypeError("compat_u must be float64")
+    ws = workspace(x2d.device, _lib.size("flc_quant_workspace_size", rows, d), "quant")
+    call("flc_quant_encode_decode", _p(x2d), rows, d, kind, levels, bits, _p(norms), seed, counter, _p(compat_u),
+         _p(codes), _p(nnz), _p(out), _p(ws), ws.numel(), _stream(x2d.device))
+    return QuantPacket(codes, norms, rows, d, kind, levels, bits, nnz), out
+
+
+def quant_encode_auto(x2d: torch.Tensor, kind: int, levels: int, p: float = math.inf, seed: int = 0, counter: int = 0,
+                      want_nnz: bool = False, decode: bool = True):
+    """Philox mode with the norm included (flc_quant_encode_auto): norm, encode and (``decode``) the decoded batch in
+    two launches for rows of >= 2048 elements.  Returns (packet, decoded or None)."""
+    x2d = _dev_f32(x2d)
+    rows, d = x2d.shape
+    pk = _lib.FLC_NORM_INF if math.isinf(p) else (_lib.FLC_NORM_L2 if p == 2 else None)
+    if pk is None:
+        raise ValueError(f"p must be inf or 2 (got {p})")
+    bits = code_bits(levels)
+    codes = torch.empty(max((rows * d * bits + 7) // 8, 1), dtype=torch.uint8, device=x2d.device)
+    norms = torch.empty(rows, dtype=torch.float32, device=x2d.device)
+    nnz = torch.empty(rows, dtype=torch.int64, device=x2d.device) if want_nnz else None
+    out = torch.empty(rows, d, dtype=torch.float32, device=x2d.device) if decode else None
+    ws = workspace(x2d.device, _lib.size("flc_quant_workspace_size", rows, d), "quant")
+    call("flc_quant_encode_auto", _p(x2d), rows, d, kind, levels, bits, pk, seed, counter, _p(codes), _p(norms),
+         _p(nnz), _p(out), _p(ws), ws.numel(), _stream(x2d.device))
+    return QuantPacket(codes, norms, rows, d, kind, levels, bits, nnz), out
+
+
 def quant_decode(pkt: QuantPacket, out: Optional[torch.Tensor] = None, row_weights: Optional[torch.Tensor] = None,
                  accumulate: bool = False) -> torch.Tensor:
     if out is None:

@@ -376,8 +376,8 @@ class Compressor:
             if self.rng_mode == "compat":
                 cnt = int(codec.count_consumers(x2, norms).item())
                 compat_u = self._uniforms(cnt, x.device)
-            pkt = codec.quant_encode(x2, kind, self.s, norms, seed, ctr, compat_u, want_nnz=(t in _STD))
-            out = codec.quant_decode(pkt).reshape(d)
+            pkt, out = codec.quant_encode_decode(x2, kind, self.s, norms, seed, ctr, compat_u, want_nnz=(t in _STD))
+            out = out.reshape(d)
             if t in _STD:
                 pnorm = np.float32(norms.item())
                 # the norm goes through the norm compressor (compressors.py:334-337)
@@ -408,10 +408,8 @@ class Compressor:
         if t not in _STD and t not in _NATD:
             raise NotImplementedError("compressBatch: dithering compressors only")
         kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
-        norms = codec.quant_norm(X, self.p)
         seed, ctr = self.philox.next()
-        pkt = codec.quant_encode(X, kind, self.s, norms, seed, ctr, None, want_nnz=False)
-        return codec.quant_decode(pkt)
+        return codec.quant_encode_auto(X, kind, self.s, self.p, seed, ctr)[1]
 
     def encode(self, x: torch.Tensor) -> Any:
         """Wire packet of ``x`` (device tensors, philox RNG): QuantPacket / (idx, val, tiles) / StackedPacket."""

@@ -5,8 +5,8 @@
 //   norms[rows] fp32 + a flat packed code stream, BITS (2/4/8) bits per element, element i of the
 //   flattened batch at bit offset i*BITS (little-endian), code = sign << (BITS-1) | level.
 // Kernels (all HBM-streaming, no MFMA):
-//   quant_norm     per-row max|x| (exact) or fp64 sum of squares; one partial per block, folded per
-//                  row in a fixed order by quant_norm_fold -> deterministic.
+//   quant_norm     per-row max|x| (exact) or fp64 sum of squares; one partial per block, folded per row in a
+//                  fixed order (quant_norm_fold, or inside the encode: flc_quant_encode_auto) -> deterministic.
 //                  algorithmic bytes: 4 per element read.
 //   quant_count    compat mode only: consumers (x != 0) per encode chunk, then one-block scan.
 //   quant_encode   per element: y = fp32(|x| / norm), bracket [lv(s), lv(s+1)] found in fp64,
@@ -53,6 +53,24 @@ QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* nee
 // ------------------------------------------------------------------------------------------------
 // norm
 // ------------------------------------------------------------------------------------------------
+// fold of the per-block partials of a row in a fixed order (deterministic), by one wave (every lane gets it)
+template <int NORM>
+__device__ __forceinline__ float fold_row(int parts, const QuantWs& ws, int64_t row) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const unsigned long long* pr = ws.partials + row * kNormMaxParts;
+  if (NORM == FLC_NORM_INF) {
+    uint32_t m = 0;
+    for (int p = lane; p < parts; p += kWave) {
+      const uint32_t v = (uint32_t)pr[p];
+      m = v > m ? v : m;
+    }
+    return __uint_as_float(wave_max_u32(m));
+  }
+  double acc = 0.0;
+  for (int p = lane; p < parts; p += kWave) acc += __longlong_as_double(pr[p]);
+  return (float)sqrt(wave_sum(acc));
+}
+
 template <int NORM>
 __global__ __launch_bounds__(kThreads) void quant_norm_kernel(const float* __restrict__ x, int64_t d,
                                                               int parts, int64_t chunk, int vec_ok,
@@ -115,25 +133,11 @@ __global__ __launch_bounds__(kThreads) void quant_norm_kernel(const float* __res
   if (threadIdx.x == 0) ws.partials[(int64_t)row * kNormMaxParts + part] = part_bits;
 }
 
-// fold the per-block partials of each row in a fixed order (deterministic), one wave per row
+// fold of the partials in a separate launch (flc_quant_norm), one wave per row
 template <int NORM>
 __global__ __launch_bounds__(kWave) void quant_norm_fold_kernel(int parts, QuantWs ws, float* __restrict__ norms) {
-  const int row = blockIdx.x, lane = threadIdx.x;
-  const unsigned long long* pr = ws.partials + (int64_t)row * kNormMaxParts;
-  if (NORM == FLC_NORM_INF) {
-    uint32_t m = 0;
-    for (int p = lane; p < parts; p += kWave) {
-      const uint32_t v = (uint32_t)pr[p];
-      m = v > m ? v : m;
-    }
-    m = wave_max_u32(m);
-    if (lane == 0) norms[row] = __uint_as_float(m);
-  } else {
-    double acc = 0.0;
-    for (int p = lane; p < parts; p += kWave) acc += __longlong_as_double(pr[p]);
-    acc = wave_sum(acc);
-    if (lane == 0) norms[row] = (float)sqrt(acc);
-  }
+  const float v = fold_row<NORM>(parts, ws, blockIdx.x);
+  if (threadIdx.x == 0) norms[blockIdx.x] = v;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -275,14 +279,14 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(const int* __restrict_
   }
 }
 
-template <int KIND, int BITS, bool COMPAT>
+template <int KIND, int BITS, bool COMPAT, int GPB, bool DEC>
 __global__ __launch_bounds__(kThreads) void quant_encode_kernel(
     const float* __restrict__ x, int64_t n, int64_t d, int s, double step, const float* __restrict__ norms,
     uint64_t seed, uint64_t counter, const double* __restrict__ compat_u, uint8_t* __restrict__ codes,
-    long long* __restrict__ nnz, QuantWs ws) {
+    long long* __restrict__ nnz, QuantWs ws, float* __restrict__ out) {
   __shared__ long long s_scan[kNW];
   __shared__ unsigned long long s_nnz[kRowSlots];
-  const int64_t g_begin = (int64_t)blockIdx.x * kGroupsPerBlock;
+  const int64_t g_begin = (int64_t)blockIdx.x * GPB;
   const int64_t e_first = g_begin * kGroup;
   RowCursor rc{d, 0, 0};
   rc.seek(e_first);
@@ -291,7 +295,7 @@ __global__ __launch_bounds__(kThreads) void quant_encode_kernel(
   __syncthreads();
   long long running = COMPAT ? ws.chunk_offsets[blockIdx.x] : 0;
 
-  for (int it = 0; it < kGroupsPerBlock / kThreads; ++it) {
+  for (int it = 0; it < GPB / kThreads; ++it) {
     const int64_t g = g_begin + it * kThreads + threadIdx.x;
     const int64_t e0 = g * kGroup;
     const int valid = e0 >= n ? 0 : (n - e0 < kGroup ? (int)(n - e0) : kGroup);
@@ -333,11 +337,24 @@ __global__ __launch_bounds__(kThreads) void quant_encode_kernel(
     if (valid == 0) continue;
 
     uint64_t packed = 0;
+    float o[kGroup];
 #pragma unroll
     for (int j = 0; j < kGroup; ++j) {
-      if (j < valid) packed |= (uint64_t)quant_code<KIND, BITS>(v[j], nr[j], s, step, u[j]) << (j * BITS);
+      if (j < valid) {
+        const uint32_t c = quant_code<KIND, BITS>(v[j], nr[j], s, step, u[j]);
+        packed |= (uint64_t)c << (j * BITS);
+        if (DEC) o[j] = dequant<KIND, BITS>(c, nr[j], s, step);  // the decoder's value of this code
+      }
     }
     store_codes<BITS>(codes, e0, valid, packed);
+    if (DEC) {
+      if (valid == kGroup) {
+        *reinterpret_cast<float4*>(out + e0) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(out + e0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      } else {
+        for (int j = 0; j < valid; ++j) out[e0 + j] = o[j];
+      }
+    }
 
     if (nnz) {
       // rows of this group: at most a few; count nonzeros per row into LDS slots
@@ -348,6 +365,136 @@ __global__ __launch_bounds__(kThreads) void quant_encode_kernel(
           if (r < kRowSlots) atomicAdd(&s_nnz[r], 1ull);
           else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r + row_base]), 1ull);
         }
+      }
+    }
+  }
+  if (nnz) {
+    __syncthreads();
+    if (threadIdx.x < kRowSlots && s_nnz[threadIdx.x] != 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[row_base + threadIdx.x]), s_nnz[threadIdx.x]);
+  }
+}
+
+// Philox mode, one group of 8 elements per thread.  The common case — a full group inside one row — takes one
+// row lookup (one 64-bit division per thread) and one norm load; groups straddling a row boundary or the end
+// take the per-element path.  DEC also writes the decoded values (flc_quant_encode_decode).
+// FOLD (FLC_NORM_INF / FLC_NORM_L2 + 1; 0 = norms given): the block folds the norm partials of its rows itself
+// (d >= the block's span, so at most two rows) and the block holding a row's first element writes norms[row].
+template <int KIND, int BITS, bool DEC, int FOLD>
+__global__ __launch_bounds__(kThreads) void quant_encode_philox_kernel(
+    const float* __restrict__ x, int64_t n, int64_t d, int s, double step, float* __restrict__ norms, uint64_t seed,
+    uint64_t counter, uint8_t* __restrict__ codes, long long* __restrict__ nnz, float* __restrict__ out, QuantWs ws,
+    int parts) {
+  __shared__ unsigned long long s_nnz[kRowSlots];
+  __shared__ float s_norm[2];
+  const int64_t b0 = (int64_t)blockIdx.x * kThreads * kGroup;
+  const int64_t row_base = b0 / d;
+  if (nnz && threadIdx.x < kRowSlots) s_nnz[threadIdx.x] = 0;
+  if (FOLD && threadIdx.x < kWave) {
+    const int64_t rows = (n + d - 1) / d;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int64_t r = row_base + rr;
+      if (r < rows && r * d < b0 + kThreads * kGroup) {
+        const float v = fold_row<FOLD - 1>(parts, ws, r);
+        if (threadIdx.x == 0) {
+          s_norm[rr] = v;
+          if (r * d >= b0) norms[r] = v;
+        }
+      }
+    }
+  }
+  if (nnz || FOLD) __syncthreads();
+  const int64_t e0 = b0 + (int64_t)threadIdx.x * kGroup;
+  if (e0 < n) {
+    const int valid = n - e0 < kGroup ? (int)(n - e0) : kGroup;
+    float v[kGroup];
+    load_group(x, e0, valid, v);
+    const U4 a = philox_group((uint64_t)e0 >> 2, seed, counter);
+    const U4 b = philox_group(((uint64_t)e0 >> 2) + 1, seed, counter);
+    const uint32_t wd[kGroup] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const int64_t r0 = e0 / d;
+    const int64_t r_end = (r0 + 1) * d;
+    uint64_t packed = 0;
+    float o[kGroup];
+    const float nr0 = (valid == kGroup && e0 + kGroup <= r_end) ? (FOLD ? s_norm[r0 - row_base] : norms[r0]) : 0.0f;
+    if (KIND == 0 && valid == kGroup && e0 + kGroup <= r_end && norm_regular(nr0)) {
+      // standard dithering, branch-light: the fp32 decision for all 8 elements (dither_level's fast path, with
+      // u in fp32 straight from the Philox word: 1 ulp from fp32(u01), far inside the 3e-5 margin), then the
+      // exact fp64 rule for the rare elements the margin does not decide (whole-wave branch)
+      const float sf = (float)s;
+      uint32_t lvl[kGroup];
+      uint32_t slow = 0;
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        const float t = (fabsf(v[j]) / nr0) * sf;
+        const float jf = ceilf(t);
+        const float pf = jf - t;
+        const float uf = (float)wd[j] * 2.3283064365386963e-10f;
+        const bool ok = (pf > 1e-4f) & (t - (jf - 1.0f) > 1e-4f) & (fabsf(uf - pf) > 3e-5f);
+        lvl[j] = (uint32_t)(int)jf - (uf < pf ? 1u : 0u);
+        slow |= (uint32_t)(!ok && v[j] != 0.0f) << j;
+      }
+      if (slow) {
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j)
+          if ((slow >> j) & 1u) lvl[j] = (uint32_t)dither_level<0>(fabsf(v[j]) / nr0, s, step, u01(wd[j]));
+      }
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        const uint32_t c = v[j] == 0.0f ? 0u : (((__float_as_uint(v[j]) >> 31) << (BITS - 1)) | lvl[j]);
+        packed |= (uint64_t)c << (j * BITS);
+        if (DEC) o[j] = dequant<KIND, BITS>(c, nr0, s, step);
+      }
+      if (nnz) {
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) cnt += v[j] != 0.0f;
+        const int rl = (int)(r0 - row_base);
+        if (cnt) {
+          if (rl < kRowSlots) atomicAdd(&s_nnz[rl], (unsigned long long)cnt);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r0]), (unsigned long long)cnt);
+        }
+      }
+    } else if (valid == kGroup && e0 + kGroup <= r_end) {
+      const float nr = nr0;
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        const uint32_t c = quant_code<KIND, BITS>(v[j], nr, s, step, u01(wd[j]));
+        packed |= (uint64_t)c << (j * BITS);
+        if (DEC) o[j] = dequant<KIND, BITS>(c, nr, s, step);
+      }
+      if (nnz) {
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) cnt += v[j] != 0.0f;
+        const int rl = (int)(r0 - row_base);
+        if (cnt) {
+          if (rl < kRowSlots) atomicAdd(&s_nnz[rl], (unsigned long long)cnt);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r0]), (unsigned long long)cnt);
+        }
+      }
+    } else {
+      for (int j = 0; j < valid; ++j) {
+        const int64_t r = (e0 + j) / d;
+        const float nr = FOLD ? s_norm[r - row_base] : norms[r];
+        const uint32_t c = quant_code<KIND, BITS>(v[j], nr, s, step, u01(wd[j]));
+        packed |= (uint64_t)c << (j * BITS);
+        if (DEC) o[j] = dequant<KIND, BITS>(c, nr, s, step);
+        if (nnz && v[j] != 0.0f) {
+          const int rl = (int)(r - row_base);
+          if (rl < kRowSlots) atomicAdd(&s_nnz[rl], 1ull);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r]), 1ull);
+        }
+      }
+    }
+    store_codes<BITS>(codes, e0, valid, packed);
+    if (DEC) {
+      if (valid == kGroup) {
+        *reinterpret_cast<float4*>(out + e0) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(out + e0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      } else {
+        for (int j = 0; j < valid; ++j) out[e0 + j] = o[j];
       }
     }
   }
@@ -406,21 +553,24 @@ int check_quant_args(int kind, int levels, int bits) {
 
 double level_step(int levels) { return 1.0 / (double)levels; }
 
-template <int KIND, int BITS>
+template <int KIND, int BITS, bool DEC>
 int launch_encode(const float* x, int64_t n, int64_t d, int levels, const float* norms, uint64_t seed, uint64_t counter,
                   const double* compat_u, uint8_t* codes, int64_t* nnz, const QuantWs& w, int64_t nblocks,
-                  hipStream_t st) {
+                  float* out, hipStream_t st) {
+  const char* name = DEC ? "quant_encode_decode" : "quant_encode";
   const double step = level_step(levels);
   long long* nz = reinterpret_cast<long long*>(nnz);
   if (compat_u) {
-    FLC_LAUNCH("quant_count", quant_count_kernel, dim3((unsigned)nblocks), dim3(kThreads), 0, st, x, n, d, norms, w);
+    FLC_LAUNCH(DEC ? "quant_count" : "quant_count", quant_count_kernel, dim3((unsigned)nblocks), dim3(kThreads), 0, st, x, n, d, norms, w);
     FLC_LAUNCH("quant_chunk_scan", chunk_scan_kernel, dim3(1), dim3(1024), 0, st, w.chunk_counts, w.chunk_offsets,
                nblocks);
-    FLC_LAUNCH("quant_encode", (quant_encode_kernel<KIND, BITS, true>), dim3((unsigned)nblocks), dim3(kThreads), 0, st,
-               x, n, d, levels, step, norms, seed, counter, compat_u, codes, nz, w);
+    FLC_LAUNCH(name, (quant_encode_kernel<KIND, BITS, true, kGroupsPerBlock, DEC>), dim3((unsigned)nblocks),
+               dim3(kThreads), 0, st, x, n, d, levels, step, norms, seed, counter, compat_u, codes, nz, w, out);
   } else {
-    FLC_LAUNCH("quant_encode", (quant_encode_kernel<KIND, BITS, false>), dim3((unsigned)nblocks), dim3(kThreads), 0,
-               st, x, n, d, levels, step, norms, seed, counter, compat_u, codes, nz, w);
+    // philox: one group per thread, so every wave's loads are in flight at once (a small batch fills the chip)
+    const int64_t nb1 = cdiv(n, (int64_t)kGroup * kThreads);
+    FLC_LAUNCH(name, (quant_encode_philox_kernel<KIND, BITS, DEC, 0>), dim3((unsigned)nb1), dim3(kThreads), 0, st, x,
+               n, d, levels, step, const_cast<float*>(norms), seed, counter, codes, nz, out, w, 0);
   }
   return FLC_OK;
 }
@@ -483,20 +633,27 @@ int flc_quant_norm(const float* x, int64_t rows, int64_t d, int norm_p, float* n
   return FLC_OK;
 }
 
-int flc_quant_encode(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits, const float* norms,
-                     uint64_t seed, uint64_t counter, const double* compat_u, uint8_t* codes, int64_t* nnz, void* ws,
-                     size_t ws_bytes, void* stream) {
-  if (rows <= 0 || d <= 0 || !x || !norms || !codes) return fail(FLC_EINVAL, "flc_quant_encode: bad arguments");
+}  // extern "C"
+
+namespace flc {
+namespace {
+int quant_encode_entry(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits, const float* norms,
+                       uint64_t seed, uint64_t counter, const double* compat_u, uint8_t* codes, int64_t* nnz,
+                       float* out, void* ws, size_t ws_bytes, void* stream, const char* who) {
+  if (rows <= 0 || d <= 0 || !x || !norms || !codes) return fail(FLC_EINVAL, "%s: bad arguments", who);
   if (int rc = check_quant_args(kind, levels, bits)) return rc;
-  if (!aligned16(x) || !aligned16(codes)) return fail(FLC_EINVAL, "flc_quant_encode: x and codes must be 16-B aligned");
+  if (!aligned16(x) || !aligned16(codes) || (out && !aligned16(out)))
+    return fail(FLC_EINVAL, "%s: x, codes and out must be 16-B aligned", who);
   const int64_t n = rows * d;
   const int64_t nblocks = cdiv(n, (int64_t)kGroup * kGroupsPerBlock);
   size_t need = 0;
   QuantWs w = carve(ws, ws_bytes, rows, nblocks, &need);
-  if (need > ws_bytes || !ws) return fail(FLC_EWORKSPACE, "flc_quant_encode: workspace %zu < %zu", ws_bytes, need);
+  if (need > ws_bytes || !ws) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
   hipStream_t st = as_stream(stream);
   if (nnz) FLC_CHECK_HIP(hipMemsetAsync(nnz, 0, (size_t)rows * sizeof(int64_t), st));
-#define FLC_ENC(K, B) return launch_encode<K, B>(x, n, d, levels, norms, seed, counter, compat_u, codes, nnz, w, nblocks, st)
+#define FLC_ENC(K, B)                                                                                              \
+  return out ? launch_encode<K, B, true>(x, n, d, levels, norms, seed, counter, compat_u, codes, nnz, w, nblocks, out, st) \
+             : launch_encode<K, B, false>(x, n, d, levels, norms, seed, counter, compat_u, codes, nnz, w, nblocks, out, st)
   if (kind == FLC_Q_STANDARD_DITHER) {
     if (bits == 8) FLC_ENC(0, 8);
     if (bits == 4) FLC_ENC(0, 4);
@@ -507,6 +664,94 @@ int flc_quant_encode(const float* x, int64_t rows, int64_t d, int kind, int leve
     FLC_ENC(1, 2);
   }
 #undef FLC_ENC
+}
+// norm partials -> (fold) -> philox encode (+ decode), norms written by the encode
+template <int KIND, int BITS, bool DEC>
+int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p, uint64_t seed, uint64_t counter,
+                uint8_t* codes, float* norms, int64_t* nnz, float* out, const QuantWs& w, hipStream_t st) {
+  const int64_t n = rows * d;
+  int64_t parts = std::min<int64_t>(cdiv(d, 8192), kNormMaxParts);
+  const int64_t chunk = align_up((size_t)cdiv(d, parts), 4);
+  parts = cdiv(d, chunk);
+  const int vec_ok = (d % 4 == 0) && aligned16(x);
+  const bool fold_in = d >= (int64_t)kThreads * kGroup;  // a block spans at most two rows
+  const double step = level_step(levels);
+  const int64_t nb1 = cdiv(n, (int64_t)kGroup * kThreads);
+  long long* nz = reinterpret_cast<long long*>(nnz);
+  const char* name = DEC ? "quant_encode_decode" : "quant_encode";
+  if (norm_p == FLC_NORM_INF) {
+    FLC_LAUNCH("quant_norm", quant_norm_kernel<FLC_NORM_INF>, dim3((unsigned)parts, (unsigned)rows), dim3(kThreads), 0,
+               st, x, d, (int)parts, chunk, vec_ok, w);
+    if (fold_in) {
+      FLC_LAUNCH(name, (quant_encode_philox_kernel<KIND, BITS, DEC, FLC_NORM_INF + 1>), dim3((unsigned)nb1),
+                 dim3(kThreads), 0, st, x, n, d, levels, step, norms, seed, counter, codes, nz, out, w, (int)parts);
+      return FLC_OK;
+    }
+    FLC_LAUNCH("quant_norm_fold", quant_norm_fold_kernel<FLC_NORM_INF>, dim3((unsigned)rows), dim3(kWave), 0, st,
+               (int)parts, w, norms);
+  } else {
+    FLC_LAUNCH("quant_norm", quant_norm_kernel<FLC_NORM_L2>, dim3((unsigned)parts, (unsigned)rows), dim3(kThreads), 0,
+               st, x, d, (int)parts, chunk, vec_ok, w);
+    if (fold_in) {
+      FLC_LAUNCH(name, (quant_encode_philox_kernel<KIND, BITS, DEC, FLC_NORM_L2 + 1>), dim3((unsigned)nb1),
+                 dim3(kThreads), 0, st, x, n, d, levels, step, norms, seed, counter, codes, nz, out, w, (int)parts);
+      return FLC_OK;
+    }
+    FLC_LAUNCH("quant_norm_fold", quant_norm_fold_kernel<FLC_NORM_L2>, dim3((unsigned)rows), dim3(kWave), 0, st,
+               (int)parts, w, norms);
+  }
+  FLC_LAUNCH(name, (quant_encode_philox_kernel<KIND, BITS, DEC, 0>), dim3((unsigned)nb1), dim3(kThreads), 0, st, x, n,
+             d, levels, step, norms, seed, counter, codes, nz, out, w, 0);
+  return FLC_OK;
+}
+
+}  // namespace
+}  // namespace flc
+
+extern "C" {
+
+int flc_quant_encode_auto(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits, int norm_p,
+                          uint64_t seed, uint64_t counter, uint8_t* codes, float* norms, int64_t* nnz, float* out,
+                          void* ws, size_t ws_bytes, void* stream) {
+  if (rows <= 0 || d <= 0 || !x || !norms || !codes) return fail(FLC_EINVAL, "flc_quant_encode_auto: bad arguments");
+  if (rows > 65535) return fail(FLC_EINVAL, "flc_quant_encode_auto: at most 65535 rows per call");
+  if (norm_p != FLC_NORM_INF && norm_p != FLC_NORM_L2) return fail(FLC_EINVAL, "flc_quant_encode_auto: p must be inf(0) or 2");
+  if (int rc = check_quant_args(kind, levels, bits)) return rc;
+  if (!aligned16(x) || !aligned16(codes) || (out && !aligned16(out)))
+    return fail(FLC_EINVAL, "flc_quant_encode_auto: x, codes and out must be 16-B aligned");
+  size_t need = 0;
+  QuantWs w = carve(ws, ws_bytes, rows, cdiv(rows * d, (int64_t)kGroup * kGroupsPerBlock), &need);
+  if (need > ws_bytes || !ws) return fail(FLC_EWORKSPACE, "flc_quant_encode_auto: workspace %zu < %zu", ws_bytes, need);
+  hipStream_t st = as_stream(stream);
+  if (nnz) FLC_CHECK_HIP(hipMemsetAsync(nnz, 0, (size_t)rows * sizeof(int64_t), st));
+#define FLC_AUTO(K, B)                                                                                            \
+  return out ? launch_auto<K, B, true>(x, rows, d, levels, norm_p, seed, counter, codes, norms, nnz, out, w, st)   \
+             : launch_auto<K, B, false>(x, rows, d, levels, norm_p, seed, counter, codes, norms, nnz, out, w, st)
+  if (kind == FLC_Q_STANDARD_DITHER) {
+    if (bits == 8) FLC_AUTO(0, 8);
+    if (bits == 4) FLC_AUTO(0, 4);
+    FLC_AUTO(0, 2);
+  } else {
+    if (bits == 8) FLC_AUTO(1, 8);
+    if (bits == 4) FLC_AUTO(1, 4);
+    FLC_AUTO(1, 2);
+  }
+#undef FLC_AUTO
+}
+
+int flc_quant_encode(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits, const float* norms,
+                     uint64_t seed, uint64_t counter, const double* compat_u, uint8_t* codes, int64_t* nnz, void* ws,
+                     size_t ws_bytes, void* stream) {
+  return quant_encode_entry(x, rows, d, kind, levels, bits, norms, seed, counter, compat_u, codes, nnz, nullptr, ws,
+                            ws_bytes, stream, "flc_quant_encode");
+}
+
+int flc_quant_encode_decode(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits, const float* norms,
+                            uint64_t seed, uint64_t counter, const double* compat_u, uint8_t* codes, int64_t* nnz,
+                            float* out, void* ws, size_t ws_bytes, void* stream) {
+  if (!out) return fail(FLC_EINVAL, "flc_quant_encode_decode: null out");
+  return quant_encode_entry(x, rows, d, kind, levels, bits, norms, seed, counter, compat_u, codes, nnz, out, ws,
+                            ws_bytes, stream, "flc_quant_encode_decode");
 }
 
 int flc_count_consumers(const float* x, int64_t rows, int64_t d, const float* norms, int64_t* count, void* stream) {

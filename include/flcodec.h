@@ -93,6 +93,18 @@ int flc_quant_norm(const float* x, int64_t rows, int64_t d, int norm_p, float* n
 int flc_quant_encode(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits,
                      const float* norms, uint64_t seed, uint64_t counter, const double* compat_u,
                      uint8_t* codes, int64_t* nnz, void* ws, size_t ws_bytes, void* stream);
+/* encode + decode in one pass (compressVector's round trip, compressors.py:339-365 / 376-404): the codes are
+ * written exactly as flc_quant_encode writes them and out receives the value flc_quant_decode would give each code
+ * (weight 1, no accumulate), computed from the code in registers instead of reading the wire back. */
+int flc_quant_encode_decode(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits,
+                            const float* norms, uint64_t seed, uint64_t counter, const double* compat_u,
+                            uint8_t* codes, int64_t* nnz, float* out, void* ws, size_t ws_bytes, void* stream);
+/* philox mode, norm included: the per-row norm (as flc_quant_norm computes it, written to norms), the encode and,
+ * with out != NULL, the fused decode — two launches when d >= 2048 (the encode folds the norm partials itself),
+ * three otherwise. */
+int flc_quant_encode_auto(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits, int norm_p,
+                          uint64_t seed, uint64_t counter, uint8_t* codes, float* norms, int64_t* nnz, float* out,
+                          void* ws, size_t ws_bytes, void* stream);
 /* compat mode: how many uniforms the reference draws for this batch — one per element with x != 0
  * whose y = |x| / norm is not NaN (compressors.py:339-354); norms == NULL counts x != 0 (the natural
  * compressor, compressors.py:307-316).  *count is a device int64. */

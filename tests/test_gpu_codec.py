@@ -135,6 +135,48 @@ def test_sparse_compressor_matches_reference_fixture(case):
     assert np.random.random_sample() == float(rec["next_np"])
 
 
+@pytest.mark.parametrize("kind,levels", [(0, 127), (0, 7), (1, 8), (0, 1), (1, 3)])
+@pytest.mark.parametrize("rows,d,compat", [(10, 417482, False), (3, 1001, True), (1, 13, True), (2, 8192 * 3 + 5, False)])
+def test_quant_encode_decode_equals_encode_then_decode(kind, levels, rows, d, compat):
+    """flc_quant_encode_decode writes the codes flc_quant_encode writes and the values flc_quant_decode gives."""
+    codec = _codec()
+    g = np.random.default_rng(rows + d + levels)
+    x = (g.standard_normal((rows, d)) * 1e-3).astype(np.float32)
+    x[g.random((rows, d)) < 0.05] = 0
+    xd = torch.from_numpy(x).to(DEV)
+    norms = codec.quant_norm(xd)
+    u = None
+    if compat:
+        cnt = int(codec.count_consumers(xd, norms).item())
+        u = torch.from_numpy(np.random.default_rng(1).random(cnt)).to(DEV)
+    pkt = codec.quant_encode(xd, kind, levels, norms, 5, 3, u, want_nnz=True)
+    ref_out = codec.quant_decode(pkt)
+    pkt2, out2 = codec.quant_encode_decode(xd, kind, levels, norms, 5, 3, u, want_nnz=True)
+    assert torch.equal(pkt.codes, pkt2.codes) and torch.equal(pkt.nnz, pkt2.nnz)
+    assert gc.same_bits(out2.cpu().numpy(), ref_out.cpu().numpy())
+
+
+@pytest.mark.parametrize("p", [math.inf, 2])
+@pytest.mark.parametrize("kind,levels", [(0, 127), (1, 8), (0, 3)])
+@pytest.mark.parametrize("rows,d", [(10, 417482), (3, 1001), (2, 2048), (5, 4099), (1, 13)])
+def test_quant_encode_auto_equals_the_separate_calls(p, kind, levels, rows, d):
+    """flc_quant_encode_auto (norm folded inside the encode for d >= 2048) = quant_norm + encode + decode."""
+    codec = _codec()
+    g = np.random.default_rng(rows * 7 + d)
+    x = (g.standard_normal((rows, d)) * 1e-3).astype(np.float32)
+    x[g.random((rows, d)) < 0.05] = 0
+    xd = torch.from_numpy(x).to(DEV)
+    norms = codec.quant_norm(xd, p)
+    pkt = codec.quant_encode(xd, kind, levels, norms, 9, 4, None, want_nnz=True)
+    ref_out = codec.quant_decode(pkt)
+    for dec in (True, False):
+        pkt2, out2 = codec.quant_encode_auto(xd, kind, levels, p, 9, 4, want_nnz=True, decode=dec)
+        assert gc.same_bits(pkt2.norms.cpu().numpy(), norms.cpu().numpy())
+        assert torch.equal(pkt.codes, pkt2.codes) and torch.equal(pkt.nnz, pkt2.nnz)
+        if dec:
+            assert gc.same_bits(out2.cpu().numpy(), ref_out.cpu().numpy())
+
+
 # ----------------------------------------------------------------------------------------- philox mode
 @pytest.mark.parametrize("kind,levels,p", [("std", 127, math.inf), ("std", 8, math.inf), ("std", 7, 2),
                                            ("nat", 8, math.inf), ("std", 1, math.inf), ("nat", 3, 2)])
