@@ -32,6 +32,7 @@ constexpr int kNW = kThreads / kWave;
 constexpr int kGroup = 8;                  // elements per thread per step
 constexpr int kGroupsPerBlock = 1024;      // 8192 elements per block (4 steps of 256 groups)
 constexpr int kNormMaxParts = 1024;         // partial blocks per row for the norm
+constexpr int kNormChunk = 4096;            // elements per norm block (16 per thread: the whole batch in flight)
 constexpr int kRowSlots = 16;              // per-block LDS nnz slots
 
 struct QuantWs {
@@ -93,14 +94,17 @@ __global__ __launch_bounds__(kThreads) void quant_norm_kernel(const float* __res
     }
   };
   if (vec_ok) {
-    // chunk is a multiple of 4 and the row base is 16-B aligned
-    const float4* x4 = reinterpret_cast<const float4*>(xr + lo);
-    const int64_t n4 = (hi - lo) >> 2;
+    // x is 16-B aligned: a scalar head up to the next 16-B boundary of the flat batch, float4 body, scalar tail
+    const int64_t flat_lo = (int64_t)row * d + lo;
+    const int64_t head = std::min<int64_t>((4 - (flat_lo & 3)) & 3, hi - lo);
+    if (threadIdx.x < head) take(xr[lo + threadIdx.x]);
+    const float4* x4 = reinterpret_cast<const float4*>(xr + lo + head);
+    const int64_t n4 = (hi - lo - head) >> 2;
     for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
       const float4 v = x4[i];
       take(v.x); take(v.y); take(v.z); take(v.w);
     }
-    for (int64_t i = lo + (n4 << 2) + threadIdx.x; i < hi; i += kThreads) take(xr[i]);
+    for (int64_t i = lo + head + (n4 << 2) + threadIdx.x; i < hi; i += kThreads) take(xr[i]);
   } else {
     for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) take(xr[i]);
   }
@@ -613,11 +617,11 @@ int flc_quant_norm(const float* x, int64_t rows, int64_t d, int norm_p, float* n
   const int64_t nblocks = cdiv(rows * d, (int64_t)kGroup * kGroupsPerBlock);
   QuantWs w = carve(ws, ws_bytes, rows, nblocks < 1 ? 1 : nblocks, &need);
   if (need > ws_bytes || !ws) return fail(FLC_EWORKSPACE, "flc_quant_norm: workspace %zu < %zu", ws_bytes, need);
-  int64_t parts = cdiv(d, 8192);
+  int64_t parts = cdiv(d, kNormChunk);
   if (parts > kNormMaxParts) parts = kNormMaxParts;
   int64_t chunk = align_up((size_t)cdiv(d, parts), 4);
   parts = cdiv(d, chunk);
-  const int vec_ok = (d % 4 == 0) && aligned16(x);
+  const int vec_ok = aligned16(x);
   hipStream_t st = as_stream(stream);
   if (norm_p == FLC_NORM_INF) {
     FLC_LAUNCH("quant_norm", quant_norm_kernel<FLC_NORM_INF>, dim3((unsigned)parts, (unsigned)rows), dim3(kThreads), 0,
@@ -670,10 +674,10 @@ template <int KIND, int BITS, bool DEC>
 int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p, uint64_t seed, uint64_t counter,
                 uint8_t* codes, float* norms, int64_t* nnz, float* out, const QuantWs& w, hipStream_t st) {
   const int64_t n = rows * d;
-  int64_t parts = std::min<int64_t>(cdiv(d, 8192), kNormMaxParts);
+  int64_t parts = std::min<int64_t>(cdiv(d, kNormChunk), kNormMaxParts);
   const int64_t chunk = align_up((size_t)cdiv(d, parts), 4);
   parts = cdiv(d, chunk);
-  const int vec_ok = (d % 4 == 0) && aligned16(x);
+  const int vec_ok = aligned16(x);
   const bool fold_in = d >= (int64_t)kThreads * kGroup;  // a block spans at most two rows
   const double step = level_step(levels);
   const int64_t nb1 = cdiv(n, (int64_t)kGroup * kThreads);
