@@ -94,6 +94,7 @@ SIGNATURES = {
     "flc_adaptive_select": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_copy": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_scale_div": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
+    "flc_randk_keys": (c_int, [c_int64, c_uint64, c_uint64, c_void_p, c_void_p]),
     "flc_randk_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "flc_weighted_sum": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_float, c_void_p, c_void_p]),
     "flc_fedopt_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p]),

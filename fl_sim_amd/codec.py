@@ -364,6 +364,19 @@ def scale_div(x: torch.Tensor, p: float) -> torch.Tensor:
     return out
 
 
+def randk_indices(n: int, k: int, seed: int, counter: int, device: torch.device) -> torch.Tensor:
+    """Rand-K's index set in philox mode, on the device: the k largest of n Philox keys (flc_randk_keys + the top-k
+    encoder), int32 ascending.  k >= n gives every index (the reference's ``S[:K]`` of a full permutation)."""
+    if k >= n:
+        return torch.arange(n, dtype=torch.int32, device=device)
+    if k <= 0:
+        return torch.empty(0, dtype=torch.int32, device=device)
+    keys = torch.empty(n, dtype=torch.float32, device=device)
+    call("flc_randk_keys", n, seed, counter, _p(keys), _stream(device))
+    idx, _ = topk_encode(keys, k)
+    return idx
+
+
 def randk_apply(x: torch.Tensor, idx: torch.Tensor, scale: float) -> torch.Tensor:
     x = _dev_f32(x).reshape(-1)
     out = torch.empty_like(x)

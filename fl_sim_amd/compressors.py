@@ -326,8 +326,12 @@ class Compressor:
         if t == CompressorType.RANDK_COMPRESSOR:
             if self.D != d:
                 raise ValueError(f"RandK compressor built for D={self.D} applied to a vector of length {d}")
-            S = _rng.numpy_shuffle_prefix(self.D, self.K)
-            idx = torch.from_numpy(S).to(x.device)
+            if self.rng_mode == "compat":  # the reference's own permutation: numpy's legacy stream, on the host
+                S = _rng.numpy_shuffle_prefix(self.D, self.K)
+                idx = torch.from_numpy(S).to(x.device)
+            else:  # device-native: the K largest of D Philox keys (no host round trip)
+                seed, ctr = self.philox.next()
+                idx = codec.randk_indices(self.D, int(self.K), seed, ctr, x.device)
             out = codec.randk_apply(x, idx, float(np.float32(self.D / self.K)))
             self._finish(d, self.K)
             return out

@@ -514,6 +514,27 @@ __global__ __launch_bounds__(kThreads) void sparse_decode_gs_kernel(
 }
 
 // rand-k scatter: out[idx[j]] = scale * x[idx[j]] (out pre-zeroed)
+// Rand-K in philox mode: a uniformly random K-subset of [0, n) is the K largest of n i.i.d. random keys.  Key of
+// element e: the Philox word the codec's stream gives e (word e & 3 of group e >> 2), shifted right by 2 and read as
+// an fp32 bit pattern (a positive finite float: order = the word's order), so the top-k encoder selects the subset
+// (ties of the 30-bit keys broken toward higher indices, the encoder's rule).
+__global__ __launch_bounds__(kThreads) void randk_keys_kernel(int64_t n, uint64_t seed, uint64_t counter,
+                                                              float* __restrict__ keys) {
+  const int64_t ng = (n + 3) >> 2;
+  for (int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x; g < ng; g += (int64_t)gridDim.x * kThreads) {
+    const U4 w = philox_group((uint64_t)g, seed, counter);
+    const float4 v = make_float4(__uint_as_float(w.x >> 2), __uint_as_float(w.y >> 2), __uint_as_float(w.z >> 2),
+                                 __uint_as_float(w.w >> 2));
+    const int64_t e = g << 2;
+    if (e + 4 <= n) {
+      *reinterpret_cast<float4*>(keys + e) = v;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int c = 0; c < 4 && e + c < n; ++c) keys[e + c] = vv[c];
+    }
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void randk_scatter_kernel(const float* __restrict__ x, const int* __restrict__ idx,
                                                                  long long k, float scale, float* __restrict__ out) {
   for (long long j = (long long)blockIdx.x * kThreads + threadIdx.x; j < k; j += (long long)gridDim.x * kThreads) {
@@ -817,6 +838,14 @@ int flc_scale_div(const float* x, int64_t n, float p, float* out, void* stream) 
   hipStream_t st = as_stream(stream);
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 4), kThreads), 256 * 16);
   FLC_LAUNCH("scale_div", elementwise_kernel<true>, dim3(grid), dim3(kThreads), 0, st, x, n, p, out);
+  return FLC_OK;
+}
+
+int flc_randk_keys(int64_t n, uint64_t seed, uint64_t counter, float* keys, void* stream) {
+  if (!keys || n <= 0 || n >= (int64_t(1) << 31)) return fail(FLC_EINVAL, "flc_randk_keys: bad arguments");
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 4), kThreads), 256 * 16);
+  FLC_LAUNCH("randk_keys", randk_keys_kernel, dim3(grid), dim3(kThreads), 0, st, n, seed, counter, keys);
   return FLC_OK;
 }
 

@@ -201,6 +201,10 @@ int flc_copy(const float* x, int64_t n, float* out, void* stream);
 int flc_scale_div(const float* x, int64_t n, float p, float* out, void* stream);
 int flc_randk_apply(const float* x, int64_t n, const int32_t* idx, int64_t k, float scale, float* out,
                     void* stream);
+/* rand-k index set in philox mode (no host round trip): keys[e] = the Philox word of element e >> 2, as a positive
+ * fp32 bit pattern; the K largest keys (flc_topk_encode_tiled on keys) are a uniformly random K-subset, ascending.
+ * keys must be 16-B aligned. */
+int flc_randk_keys(int64_t n, uint64_t seed, uint64_t counter, float* keys, void* stream);
 
 /* ------------------------------------------------------------------ client delta
  * FedOptClient.communicate (_fedopt.py:294-297): delta_t = clone(local_t) then add_(global_t, alpha=-1), i.e.

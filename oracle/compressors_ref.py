@@ -137,6 +137,15 @@ def topk_kept_select(x: np.ndarray, K: int) -> Tuple[np.ndarray, np.ndarray]:
     return kept.astype(np.int64), x[kept]
 
 
+def randk_philox_indices(D: int, K: int, seed: int, counter: int) -> np.ndarray:
+    """The device's philox-mode rand-k set: the K largest of the keys (Philox word >> 2 as an fp32 bit pattern)."""
+    if K >= D:
+        return np.arange(D, dtype=np.int64)
+    words = (philox_uniforms(D, seed, counter) * 2.0**32).astype(np.uint64).astype(np.uint32)
+    keys = (words >> np.uint32(2)).view(np.float32)
+    return topk_kept_select(keys, K)[0]
+
+
 def topk(x: np.ndarray, K: int):
     """compressors.py:293-296, ties resolved as a stable ascending argsort (highest indices kept)."""
     out = x.copy()

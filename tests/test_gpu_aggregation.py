@@ -165,6 +165,38 @@ def test_config3_fold_full_size_vs_oracle():
     assert np.count_nonzero(got) >= k  # the clients' kept sets overlap only partially
 
 
+@pytest.mark.gpu
+def test_rccl_process_group_round_world1():
+    """The RCCL path of dist.aggregate_round (nccl backend = RCCL, device_id init as bench.py does it) on the one GPU a
+    box has: reduce and all_reduce over a world of one leave the in-rank fold unchanged (RCCL refuses two ranks on
+    one device, so N > 1 runs only in the driver's multi-GPU bench)."""
+    import socket
+
+    import torch.distributed as dist
+
+    from fl_sim_amd import dist as fdist
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        n, k = 1_000_003, 10_000
+        g = torch.Generator(device="cuda").manual_seed(8)
+        deltas = [torch.randn(n, generator=g, device="cuda") * 1e-3 for _ in range(3)]
+        w = fdist.sample_weights([100, 200, 300])
+        step = fdist.stacked_decode_accumulate(k, seed=4, counter=1)
+        single = torch.zeros(n, device="cuda")
+        for c, (d, wi) in enumerate(zip(deltas, w)):
+            step(d, wi, single, c)
+        red = fdist.aggregate_round(deltas, w, [0, 1, 2], step, out=torch.empty(n, device="cuda"), dst=0)
+        allred = fdist.aggregate_round(deltas, w, [0, 1, 2], step, out=torch.empty(n, device="cuda"), dst=None)
+        assert torch.equal(red, single) and torch.equal(allred, single)
+    finally:
+        dist.destroy_process_group()
+
+
 # ------------------------------------------------------------------- aggregation variants (SURVEY §8(f) f4)
 from tests.golden.gen_golden import (  # noqa: E402
     FEDDR_CFG, FEDDR_REGS, SCAFFOLD_CFG, feddr_inputs, ifca_inputs, scaffold_inputs)

@@ -177,6 +177,39 @@ def test_quant_encode_auto_equals_the_separate_calls(p, kind, levels, rows, d):
             assert gc.same_bits(out2.cpu().numpy(), ref_out.cpu().numpy())
 
 
+@pytest.mark.parametrize("D,K", [(4096, 41), (1_000_003, 10_000), (25_000_000, 250_000), (100, 100), (7, 3)])
+def test_randk_philox_matches_oracle(D, K):
+    """Rand-K in philox mode (compressors.py:284-292): the index set is the K largest Philox keys,
+    chosen on the device; equal to the oracle's restatement, and the Compressor output is D/K * x on that set."""
+    from fl_sim_amd import Compressor
+
+    codec = _codec()
+    idx = codec.randk_indices(D, K, 77, 5, torch.device(DEV)).cpu().numpy().astype(np.int64)
+    exp = ref.randk_philox_indices(D, K, 77, 5)
+    assert np.array_equal(idx, exp)
+    assert len(np.unique(idx)) == min(K, D)
+    if D <= 1_000_003:
+        g = np.random.default_rng(D)
+        x = (g.standard_normal(D) * 1e-3).astype(np.float32)
+        c = Compressor(rng="philox", seed=77)
+        c.philox.counter = 5
+        c.makeRandKCompressor(K, D)
+        out = c.compressVector(x)
+        want, send = ref.randk(x, K, D, exp)
+        assert gc.same_bits(out, want) and c.last_need_to_send_advance == K
+
+
+def test_randk_philox_is_uniform():
+    """Each index is kept with probability K/D: 3000 draws of K = 10 from D = 100."""
+    codec = _codec()
+    counts = np.zeros(100)
+    for c in range(3000):
+        counts[codec.randk_indices(100, 10, 3, c, torch.device(DEV)).cpu().numpy()] += 1
+    sigma = np.sqrt(3000 * 0.1 * 0.9)
+    assert np.abs(counts - 300).max() < 5 * sigma
+    assert counts.sum() == 30000
+
+
 # ----------------------------------------------------------------------------------------- philox mode
 @pytest.mark.parametrize("kind,levels,p", [("std", 127, math.inf), ("std", 8, math.inf), ("std", 7, 2),
                                            ("nat", 8, math.inf), ("std", 1, math.inf), ("nat", 3, 2)])
@@ -399,6 +432,26 @@ def test_stacked_full_size_1gib_properties():
     lv = out[idx].abs() / pkt.norm
     assert bool(((lv * 127 - torch.floor(y * 127)).abs() <= 1.0001).all())
     del x, masked, out
+    torch.cuda.empty_cache()
+
+
+def test_stacked_full_size_1gib_vs_oracle():
+    """Config 5 at its real size against the oracle, bit for bit: kept set, codes, norm and the decoded 1 GiB vector
+    (the oracle's O(n) selection and the Philox uniforms of the kept elements only, so it runs in seconds)."""
+    codec = _codec()
+    n = 268_435_456
+    k = n // 100
+    x = (np.random.default_rng(2024).standard_normal(n, dtype=np.float32) * np.float32(1e-3)).astype(np.float32)
+    x[np.random.default_rng(5).integers(0, n, n // 20)] = 0.0  # the "realistic" 5 % exact zeros
+    xd = torch.from_numpy(x).to(DEV)
+    pkt = codec.stacked_encode(xd, k, 127, seed=9, counter=3)
+    out = codec.stacked_decode(pkt).cpu().numpy()
+    exp_out, exp_idx, exp_codes, pn = ref.stacked(x, k, 127, lambda i: ref.philox_uniforms_at(i, 9, 3), fast=True)
+    assert np.array_equal(pkt.idx.cpu().numpy().astype(np.int64), exp_idx)
+    assert np.array_equal(pkt.codes[:k].cpu().numpy(), exp_codes)
+    assert pkt.norm.item() == float(pn)
+    assert gc.same_bits(out, exp_out)
+    del xd, pkt
     torch.cuda.empty_cache()
 
 
