@@ -1444,7 +1444,11 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   // its last one (block edges at b0 - 1 and b1 - 1), and gives each the position of the first kept entry
   // at or after the tile's start: a kept entry fills the tiles that start after the previous kept entry,
   // and the wave's last kept entry's successor position fills the rest up to hi_w.
+#if FLC_CALIB_NOTILES  // calibration builds only: results invalid
+  const bool tiled = false;
+#else
   const bool tiled = tile_out != nullptr;
+#endif
   const unsigned q0 = cq0, q1 = cq1;
   const bool tile_owner = tiled && (q0 < q1 || (ncand == 0u && wid == 0));  // (wave-uniform)
   int64_t tile_prev = -1, tile_hi = -1;  // element ids
@@ -1484,7 +1488,11 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
   // Philox words kRnd rounds ahead (a load from L2 takes longer than one round): kRnd register slots,
   // the rounds unrolled by kRnd so each slot is a fixed register; loads at a clamped address,
   // unconditional, so no wait is merged in
+#ifndef FLC_KRND
   constexpr int kRnd = 4;
+#else
+  constexpr int kRnd = FLC_KRND;
+#endif
   unsigned rq[kRnd];
 #pragma unroll
   for (int j = 0; j < kRnd; ++j) {
@@ -1527,20 +1535,20 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
       }
     }
     if (tile_owner) {
-      const bool kp = keep && pos >= 0 && pos < k;
-      const unsigned long long km = __ballot(kp);
-      if (km) {
-        // the previous kept entry: the nearest kept lane below, or the last kept entry before this round
-        const unsigned long long below = km & ((1ull << lane) - 1ull);
-        const int pl = below ? 63 - __clzll(below) : lane;
-        const unsigned pid = (unsigned)__shfl((int)id, pl, kWave);
-        if (kp) {
-          const int64_t prev = below ? (int64_t)pid : tile_prev;
-          for (int64_t t = (prev >> kTileLog) + 1; t <= ((int64_t)id >> kTileLog); ++t) tile_out[t] = (unsigned)pos;
-        }
-        const int hl = 63 - __clzll(km);  // (wave-uniform: a readlane, no LDS round trip)
-        tile_prev = (int64_t)(unsigned)__builtin_amdgcn_readlane((int)id, hl);
+      // tiles starting after the previous CANDIDATE (lane - 1's id by a DPP wave shift; lane 0: the last
+      // candidate of the previous round) and at or before this one get this candidate's kept-before count:
+      // the elements in between are below the floor, so the first kept entry at or after such a tile's start
+      // is the first kept entry at or after this candidate (kept or not) — no ballot / shuffle per round
+      const unsigned prev_lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(tile_prev < 0 ? 0 : tile_prev));
+      unsigned pid = (unsigned)__builtin_amdgcn_update_dpp((int)prev_lo, (int)id, 0x138, 0xf, 0xf, false);  // wave_shr:1
+      const int64_t prev = lane == 0 ? tile_prev : (int64_t)pid;
+      if (in) {
+        const long long before = sb + (tb > skip ? tb - skip : 0);  // kept entries before this candidate
+        for (int64_t t = (prev >> kTileLog) + 1; t <= ((int64_t)id >> kTileLog); ++t) tile_out[t] = (unsigned)before;
       }
+      const unsigned long long im = __ballot(in);
+      const int hl = 63 - __clzll(im);  // (wave-uniform)
+      tile_prev = (int64_t)(unsigned)__builtin_amdgcn_readlane((int)id, hl);
     }
     s_before += __popcll(ms);
     t_before += __popcll(mt);
