@@ -498,6 +498,29 @@ def main():
             "GB_s": round(12 * (1 << 28) / (ms5 * 1e-3) / 1e9, 1),
             "bytes_formula": "12 * D (8 read + 4 written)",
         }
+        # f1, second half: the client step = delta formation + stacked encode; two passes (delta_flatten writes the
+        # flat delta, the encode reads it) against the delta formed inside the encoder's read (stacked_encode_delta)
+        k5 = (1 << 28) // 100
+        c5 = [0]
+
+        def step5_two():
+            c5[0] += 1
+            codec.stacked_encode(codec.delta_flatten(L5, G5, out=o5), k5, LEVELS, seed=rank, counter=c5[0])
+
+        def step5_fused():
+            c5[0] += 1
+            codec.stacked_encode_delta(L5, G5, k5, LEVELS, seed=rank, counter=c5[0])
+
+        ms5t, _ = timed(step5_two, 10, 3, world)
+        ms5f, _ = timed(step5_fused, 10, 3, world)
+        ms5t, ms5f = max_over_ranks(ms5t, world), max_over_ranks(ms5f, world)
+        extra["f1_client_step_delta_plus_encode_1GiB_64_tensors"] = {
+            "two_pass_ms": round(ms5t, 4),
+            "fused_ms": round(ms5f, 4),
+            "fused_GB_s": round((8 * (1 << 28) + 5 * k5) / (ms5f * 1e-3) / 1e9, 1),
+            "bytes_formula": "8 * D read (local + global) + 5 * K wire written",
+            "plain_encode_us": (extra.get("kernels_us") or {}).get("stacked_encode"),
+        }
         del L5, G5, o5
         torch.cuda.empty_cache()
         from fl_sim_amd import dist as fdist

@@ -302,6 +302,40 @@ def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, co
     return StackedPacket(idx, codes, norm, n, levels, tiles)
 
 
+def stacked_encode_delta(local_params: Sequence[torch.Tensor], global_params: Sequence[torch.Tensor], k: int,
+                         levels: int = 127, seed: int = 0, counter: int = 0) -> StackedPacket:
+    """The stacked encode of the client delta ``cat([l - g for l, g in zip(local, global)])`` with the delta formed in
+    the encoder's read pass (flc_stacked_encode_delta): the flat delta is never written.  Same packet as
+    ``stacked_encode(delta_flatten(local, global), ...)``."""
+    import ctypes
+
+    ls = [t if (t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 4 == 0) else t.contiguous().float()
+          for t in local_params]
+    gs = [t if (t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 4 == 0) else t.contiguous().float()
+          for t in global_params]
+    if len(ls) != len(gs) or not ls:
+        raise ValueError("one global tensor per local tensor, at least one")
+    for a, b in zip(ls, gs):
+        if a.numel() != b.numel() or a.device != b.device or a.device.type != "cuda":
+            raise ValueError("local and global tensors must be HIP tensors of matching sizes")
+    dev = ls[0].device
+    n = sum(t.numel() for t in ls)
+    m = len(ls)
+    lp = (ctypes.c_void_p * m)(*[t.data_ptr() for t in ls])
+    gp = (ctypes.c_void_p * m)(*[t.data_ptr() for t in gs])
+    sz = (ctypes.c_int64 * m)(*[t.numel() for t in ls])
+    idx = torch.empty(k, dtype=torch.int32, device=dev)
+    codes = torch.empty(max(k, 16), dtype=torch.uint8, device=dev)
+    norm = torch.empty(1, dtype=torch.float32, device=dev)
+    tiles = _tiles(n, dev)
+    ws = workspace(dev, _lib.size("flc_stacked_encode_delta_workspace_size", n, k, m), "topk")
+    call("flc_stacked_encode_delta", ctypes.cast(lp, ctypes.c_void_p), ctypes.cast(gp, ctypes.c_void_p),
+         ctypes.cast(sz, ctypes.c_void_p), m, k, levels, seed, counter, _p(idx), _p(codes), _p(norm), _p(tiles), _p(ws),
+         ws.numel(), _stream(dev))
+    _after_encode(dev)
+    return StackedPacket(idx, codes, norm, n, levels, tiles)
+
+
 def stacked_decode(pkt: StackedPacket, out: Optional[torch.Tensor] = None, weight: float = 1.0,
                    accumulate: bool = False) -> torch.Tensor:
     if out is None:

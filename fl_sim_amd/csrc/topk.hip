@@ -38,7 +38,9 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "flc_device.hpp"
 #include "flc_runtime.hpp"
@@ -461,24 +463,121 @@ __device__ __forceinline__ void sample_general(const unsigned* sample, int S, lo
 // ------------------------------------------------------------------------------------------------
 // filter
 // ------------------------------------------------------------------------------------------------
-// one wave's 2048-element step: 8 float4 per lane (q-major: lane l, step q -> elements 256q + 4l + c).
-// A partial step (the last block only) clamps each float4 to the last one holding valid data
-// (16-B aligned, so it never crosses a page); `lim` masks everything past the range end.
-template <bool FULL>
-__device__ __forceinline__ void step_load(const float* __restrict__ x, int64_t wb, int64_t end, int lane,
-                                          float4 (&v)[kStepF4]) {
-  if (FULL) {
+// Sources of the filter's elements.  A wave step covers SF * 256 elements: SF float4 per lane, q-major (lane l,
+// step slot q -> elements 256q + 4l + c).  FlatSrc reads one fp32 vector; DeltaSrc forms the client delta
+// local - global of a list of parameter tensors on the fly (FedOptClient.communicate, _fedopt.py:294-297, fused
+// into the encode's read: nothing is written), two float4 per slot, so it runs SF = 2 to keep the same
+// registers and bytes in flight per wave as FlatSrc's SF = 4.
+struct FlatSrc {
+  static constexpr int SF = 4;
+  const float* x;
+  struct Step {
+    float4 v[SF];
+    __device__ __forceinline__ float4 val(int q) const { return v[q]; }
+  };
+  struct Cursor {};
+  __device__ __forceinline__ float get(int64_t e) const { return x[e]; }
+  // a partial step (the last block only) clamps each float4 to the last one holding valid data (16-B aligned, so it
+  // never crosses a page); `lim` masks everything past the range end
+  template <bool FULL>
+  __device__ __forceinline__ void load(Cursor&, int64_t wb, int64_t end, int lane, Step& st) const {
+    if (FULL) {
 #pragma unroll
-    for (int q = 0; q < kStepF4; ++q) v[q] = ld_stream(x + wb + 256 * q + 4 * lane);
-  } else {
-    const int64_t last4 = (end - 1) & ~(int64_t)3;
+      for (int q = 0; q < SF; ++q) st.v[q] = ld_stream(x + wb + 256 * q + 4 * lane);
+    } else {
+      const int64_t last4 = (end - 1) & ~(int64_t)3;
 #pragma unroll
-    for (int q = 0; q < kStepF4; ++q) {
-      const int64_t e = wb + 256 * q + 4 * lane;
-      v[q] = *reinterpret_cast<const float4*>(x + (e < last4 ? e : (last4 >= 0 ? last4 : 0)));
+      for (int q = 0; q < SF; ++q) {
+        const int64_t e = wb + 256 * q + 4 * lane;
+        st.v[q] = *reinterpret_cast<const float4*>(x + (e < last4 ? e : (last4 >= 0 ? last4 : 0)));
+      }
     }
   }
-}
+};
+
+// device-side table of DeltaSrc's tensors (in the workspace): off[t] = first flat index of tensor t,
+// off[nseg] = n; lp / gp = the tensors' local / global parameter pointers
+struct SegTab {
+  const long long* off;
+  const float* const* lp;
+  const float* const* gp;
+  int nseg;
+};
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B aligned 16-B access
+
+struct DeltaSrc {
+  static constexpr int SF = 2;
+  SegTab t;
+  struct Step {
+    float4 l[SF], g[SF];
+    __device__ __forceinline__ float4 val(int q) const {  // local - global, one rounding (torch add_(alpha=-1))
+      return make_float4(l[q].x - g[q].x, l[q].y - g[q].y, l[q].z - g[q].z, l[q].w - g[q].w);
+    }
+  };
+  // the wave's current tensor (wave-uniform: kept in SGPRs)
+  struct Cursor {
+    long long lo = 1, hi = 0;
+    const float* l = nullptr;
+    const float* g = nullptr;
+  };
+  __device__ __forceinline__ int seg_of(int64_t e) const {  // off[s] <= e < off[s + 1]
+    int lo = 0, hi = t.nseg;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (t.off[mid] <= e) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  }
+  __device__ __forceinline__ float get(int64_t e) const {
+    const int sg = seg_of(e);
+    const int64_t r = e - t.off[sg];
+    return t.lp[sg][r] - t.gp[sg][r];
+  }
+  __device__ __forceinline__ void seek(Cursor& c, int64_t wb) const {
+    if (wb >= c.lo && wb < c.hi) return;
+    const int sg = __builtin_amdgcn_readfirstlane(seg_of(wb));
+    c.lo = t.off[sg];
+    c.hi = t.off[sg + 1];
+    c.l = t.lp[sg];
+    c.g = t.gp[sg];
+  }
+  template <bool FULL>
+  __device__ __forceinline__ void load(Cursor& c, int64_t wb, int64_t end, int lane, Step& st) const {
+    seek(c, wb);
+    const int64_t span_end = wb + 256 * SF;
+    if ((FULL || span_end <= end) && span_end <= c.hi) {  // the whole wave step inside one tensor (wave-uniform)
+      const float* l = c.l + (wb - c.lo) + 4 * lane;
+      const float* g = c.g + (wb - c.lo) + 4 * lane;
+#pragma unroll
+      for (int q = 0; q < SF; ++q) {
+        const f32x4u a = __builtin_nontemporal_load(reinterpret_cast<const f32x4u*>(l + 256 * q));
+        const f32x4u b = __builtin_nontemporal_load(reinterpret_cast<const f32x4u*>(g + 256 * q));
+        st.l[q] = make_float4(a.x, a.y, a.z, a.w);
+        st.g[q] = make_float4(b.x, b.y, b.z, b.w);
+      }
+    } else {  // a tensor boundary or the range end inside the step: element by element
+#pragma unroll
+      for (int q = 0; q < SF; ++q) {
+        float a[4], b[4];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          const int64_t e = wb + 256 * q + 4 * lane + cc;
+          a[cc] = 0.0f;
+          b[cc] = 0.0f;
+          if (e < end) {
+            const int sg = seg_of(e);
+            const int64_t r = e - t.off[sg];
+            a[cc] = t.lp[sg][r];
+            b[cc] = t.gp[sg][r];
+          }
+        }
+        st.l[q] = make_float4(a[0], a[1], a[2], a[3]);
+        st.g[q] = make_float4(b[0], b[1], b[2], b[3]);
+      }
+    }
+  }
+};
 
 template <bool FULL>
 __device__ __forceinline__ bool in_span(int o, int lim) { return FULL || o < lim; }
@@ -492,13 +591,13 @@ __device__ __forceinline__ void cand4(const float4& v, float tf, int o, int lim,
   f3 = is_cand(v.w, tf) && in_span<FULL>(o + 3, lim);
 }
 
-template <bool FULL>
-__device__ __forceinline__ unsigned step_count(const float4 (&v)[kStepF4], float tf, int lim, int lane) {
+template <bool FULL, class Step, int SF>
+__device__ __forceinline__ unsigned step_count(const Step& v, float tf, int lim, int lane) {
   unsigned cnt = 0;
 #pragma unroll
-  for (int q = 0; q < kStepF4; ++q) {
+  for (int q = 0; q < SF; ++q) {
     bool f0, f1, f2, f3;
-    cand4<FULL>(v[q], tf, 256 * q + 4 * lane, lim, f0, f1, f2, f3);
+    cand4<FULL>(v.val(q), tf, 256 * q + 4 * lane, lim, f0, f1, f2, f3);
     cnt += __popcll(__ballot(f0)) + __popcll(__ballot(f1)) + __popcll(__ballot(f2)) + __popcll(__ballot(f3));
   }
   return cnt;
@@ -533,13 +632,14 @@ __device__ __forceinline__ void emit(FilterCtx& c, unsigned p, unsigned e, float
 }
 
 // ordered append from position `pos` (within a q: lane-major, then the 4 components)
-template <bool FULL>
-__device__ __forceinline__ void step_write(const float4 (&v)[kStepF4], float tf, int lim, int lane, unsigned wbu,
+template <bool FULL, class Step, int SF>
+__device__ __forceinline__ void step_write(const Step& st, float tf, int lim, int lane, unsigned wbu,
                                            unsigned pos, FilterCtx& c) {
 #pragma unroll
-  for (int q = 0; q < kStepF4; ++q) {
+  for (int q = 0; q < SF; ++q) {
     bool f0, f1, f2, f3;
-    cand4<FULL>(v[q], tf, 256 * q + 4 * lane, lim, f0, f1, f2, f3);
+    const float4 vq = st.val(q);
+    cand4<FULL>(vq, tf, 256 * q + 4 * lane, lim, f0, f1, f2, f3);
     const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
     if ((m0 | m1 | m2 | m3) != 0ull) {
       unsigned p = pos;
@@ -549,10 +649,10 @@ __device__ __forceinline__ void step_write(const float4 (&v)[kStepF4], float tf,
       p = __builtin_amdgcn_mbcnt_hi((unsigned)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m3, p));
       if (f0 | f1 | f2 | f3) {
         const unsigned e = wbu + (unsigned)(256 * q + 4 * lane);
-        if (f0) { emit(c, p, e + 0u, v[q].x); ++p; }
-        if (f1) { emit(c, p, e + 1u, v[q].y); ++p; }
-        if (f2) { emit(c, p, e + 2u, v[q].z); ++p; }
-        if (f3) emit(c, p, e + 3u, v[q].w);
+        if (f0) { emit(c, p, e + 0u, vq.x); ++p; }
+        if (f1) { emit(c, p, e + 1u, vq.y); ++p; }
+        if (f2) { emit(c, p, e + 2u, vq.z); ++p; }
+        if (f3) emit(c, p, e + 3u, vq.w);
       }
       pos += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
     }
@@ -560,12 +660,13 @@ __device__ __forceinline__ void step_write(const float4 (&v)[kStepF4], float tf,
 }
 
 // one block step: count, exchange the 16 wave counts through LDS, append in index order
-template <bool FULL>
-__device__ __forceinline__ void step_process(const float4 (&v)[kStepF4], int64_t wb, int64_t end, float tf,
+template <bool FULL, class Step, int SF>
+__device__ __forceinline__ void step_process(const Step& v, int64_t wb, int64_t end, float tf,
                                              unsigned (&s_wc)[2][kENW], int par, unsigned& base, FilterCtx& c) {
+  constexpr int span = SF * 256;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
-  const int lim = FULL ? kWaveSpan : (int)(end > wb ? (end - wb < kWaveSpan ? end - wb : kWaveSpan) : 0);
-  const unsigned cnt = step_count<FULL>(v, tf, lim, lane);
+  const int lim = FULL ? span : (int)(end > wb ? (end - wb < span ? end - wb : span) : 0);
+  const unsigned cnt = step_count<FULL, Step, SF>(v, tf, lim, lane);
   if (lane == 0) s_wc[par][wid] = cnt;
   lds_barrier();
   unsigned pre = 0, tot = 0;
@@ -579,7 +680,7 @@ __device__ __forceinline__ void step_process(const float4 (&v)[kStepF4], int64_t
   // stops the compiler from reusing the count pass's compares)
   float tf2 = tf;
   asm volatile("" : "+v"(tf2));
-  if (cnt != 0u) step_write<FULL>(v, tf2, lim, lane, (unsigned)wb, base + pre, c);
+  if (cnt != 0u) step_write<FULL, Step, SF>(v, tf2, lim, lane, (unsigned)wb, base + pre, c);
   base += tot;
 }
 
@@ -740,16 +841,18 @@ __device__ __forceinline__ void pick_digit(const EncWs& w, SelState& cur, long l
 
 // candidate p of this block: its LDS array, or (fallback, or more candidates than kCap) the block's x
 // range itself — every element, since no later phase keeps an element below the floor anyway
+template <class Src>
 struct CandSrc {
   const unsigned* s_key;
   const unsigned* s_idx;
-  const float* x;
+  Src x;
   int64_t b0;
   bool xmode;
 };
-__device__ __forceinline__ void cand_get(const CandSrc& c, unsigned p, unsigned& raw, unsigned& id) {
+template <class Src>
+__device__ __forceinline__ void cand_get(const CandSrc<Src>& c, unsigned p, unsigned& raw, unsigned& id) {
   if (c.xmode) {
-    raw = __float_as_uint(c.x[c.b0 + p]);
+    raw = __float_as_uint(c.x.get(c.b0 + p));
     id = (unsigned)(c.b0 + p);
   } else {
     raw = c.s_key[p];
@@ -790,11 +893,12 @@ __device__ __forceinline__ unsigned long long* stamp_lds() {
 // ------------------------------------------------------------------------------------------------
 // sample kernel
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void topk_sample_kernel(const float* __restrict__ x, int64_t n, int S, EncWs w) {
+template <class Src>
+__global__ __launch_bounds__(256) void topk_sample_kernel(Src x, int64_t n, int S, EncWs w) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= S) return;
   const int64_t pos = (S == n) ? (int64_t)j : (int64_t)(((double)j + 0.5) * (double)n / (double)S);
-  w.sample()[j] = order_key(__float_as_uint(x[pos < n ? pos : n - 1]));
+  w.sample()[j] = order_key(__float_as_uint(x.get(pos < n ? pos : n - 1)));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -808,8 +912,8 @@ struct FilterOut {
 
 // floor / ceiling from the sample, the HBM pass into the block's LDS candidate arrays, the round-0 band
 // histogram and counts; STAGE: also the staging copy of the candidates for a separate select kernel
-template <bool STAGE>
-__device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, int64_t n, const EncWs& w, int S,
+template <bool STAGE, class Src>
+__device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const EncWs& w, int S,
                                                   long long rank_lo, long long rank_hi, int take_all,
                                                   unsigned* s_key, unsigned* s_idx, unsigned* s_hist,
                                                   unsigned (&s_wc)[2][kENW], unsigned long long* s_red,
@@ -819,14 +923,19 @@ __device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, i
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * w.M;
   const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
-  const int nsteps = (int)cdiv_dev(b1 - b0, (int64_t)kBlockStep);
+  constexpr int SF = Src::SF;
+  constexpr int64_t kWS = SF * 256;         // elements per wave step
+  constexpr int64_t kBS = kENW * kWS;       // elements per block step (M is a multiple of it)
+  using Step = typename Src::Step;
+  const int nsteps = (int)cdiv_dev(b1 - b0, kBS);
   STAMP(0);
 
   // ---- floor / ceiling (identical in every block); the first step of the HBM pass is already in flight
   // meanwhile (issued after the sample keys, so waiting for the keys does not wait for it)
-  float4 va[kStepF4], vb[kStepF4];
-  const int64_t wb0 = b0 + (int64_t)wid * kWaveSpan;
-  const int nfull = (int)((b1 - b0) / kBlockStep);
+  Step va, vb;
+  typename Src::Cursor cur;
+  const int64_t wb0 = b0 + (int64_t)wid * kWS;
+  const int nfull = (int)((b1 - b0) / kBS);
   unsigned t_lo;
   unsigned long long t_hi;
   if (take_all) {
@@ -841,12 +950,12 @@ __device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, i
       // the first two steps stream while the floor / ceiling are picked (unconditional, clamped
       // in-range loads, so no wait is merged in): the first right away, the second in the registers the
       // keys leave free after the histogram
-      step_load<false>(x, wb0, b1, lane, va);
+      x.template load<false>(cur, wb0, b1, lane, va);
       unsigned B = 0;
       int shB = 0;
       const bool fast = rank_lo <= kET;  // grid-uniform
       if (fast) sample_fast_hist(keys, S, SL, s_hist, &B, &shB);
-      step_load<false>(x, wb0 + kBlockStep, b1, lane, vb);
+      x.template load<false>(cur, wb0 + kBS, b1, lane, vb);
       if (fast) ok = sample_fast_pick(w.sample(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
     }
     if (!ok) sample_general(w.sample(), S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
@@ -882,34 +991,34 @@ __device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, i
     // (a conditional prefetch makes the compiler copy the loaded registers on a side path, and the copy
     // waits for the load), and the partial tail step is peeled off
     int s = 0;
-    if (take_all && nfull > 0) step_load<true>(x, wb0, b1, lane, va);
+    if (take_all && nfull > 0) x.template load<true>(cur, wb0, b1, lane, va);
     if (!take_all && nfull >= 3) {  // peeled first iteration: steps 0 and 1 are in flight already
-      step_process<true>(va, wb0, b1, tf, s_wc, 0, base, fc);
-      step_load<true>(x, wb0 + 2 * kBlockStep, b1, lane, va);
-      step_process<true>(vb, wb0 + kBlockStep, b1, tf, s_wc, 1, base, fc);
+      step_process<true, Step, SF>(va, wb0, b1, tf, s_wc, 0, base, fc);
+      x.template load<true>(cur, wb0 + 2 * kBS, b1, lane, va);
+      step_process<true, Step, SF>(vb, wb0 + kBS, b1, tf, s_wc, 1, base, fc);
       s = 2;
     }
     for (; s + 3 <= nfull; s += 2) {
-      const int64_t wa = wb0 + (int64_t)s * kBlockStep, wbn = wa + kBlockStep;
-      step_load<true>(x, wbn, b1, lane, vb);
-      step_process<true>(va, wa, b1, tf, s_wc, 0, base, fc);
-      step_load<true>(x, wbn + kBlockStep, b1, lane, va);
-      step_process<true>(vb, wbn, b1, tf, s_wc, 1, base, fc);
+      const int64_t wa = wb0 + (int64_t)s * kBS, wbn = wa + kBS;
+      x.template load<true>(cur, wbn, b1, lane, vb);
+      step_process<true, Step, SF>(va, wa, b1, tf, s_wc, 0, base, fc);
+      x.template load<true>(cur, wbn + kBS, b1, lane, va);
+      step_process<true, Step, SF>(vb, wbn, b1, tf, s_wc, 1, base, fc);
     }
     if (s + 2 == nfull) {
-      const int64_t wa = wb0 + (int64_t)s * kBlockStep, wbn = wa + kBlockStep;
-      step_load<true>(x, wbn, b1, lane, vb);
-      step_process<true>(va, wa, b1, tf, s_wc, 0, base, fc);
-      step_process<true>(vb, wbn, b1, tf, s_wc, 1, base, fc);
+      const int64_t wa = wb0 + (int64_t)s * kBS, wbn = wa + kBS;
+      x.template load<true>(cur, wbn, b1, lane, vb);
+      step_process<true, Step, SF>(va, wa, b1, tf, s_wc, 0, base, fc);
+      step_process<true, Step, SF>(vb, wbn, b1, tf, s_wc, 1, base, fc);
       s += 2;
     } else if (s + 1 == nfull) {
-      step_process<true>(va, wb0 + (int64_t)s * kBlockStep, b1, tf, s_wc, 0, base, fc);
+      step_process<true, Step, SF>(va, wb0 + (int64_t)s * kBS, b1, tf, s_wc, 0, base, fc);
       ++s;
     }
     if (s < nsteps) {  // the partial last step of the last block
-      const int64_t wa = wb0 + (int64_t)s * kBlockStep;
-      step_load<false>(x, wa, b1, lane, va);
-      step_process<false>(va, wa, b1, tf, s_wc, s & 1, base, fc);
+      const int64_t wa = wb0 + (int64_t)s * kBS;
+      x.template load<false>(cur, wa, b1, lane, va);
+      step_process<false, Step, SF>(va, wa, b1, tf, s_wc, s & 1, base, fc);
     }
   }
   const unsigned C_b = base;
@@ -964,7 +1073,8 @@ __device__ __forceinline__ FilterOut filter_phase(const float* __restrict__ x, i
   return o;
 }
 
-__global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restrict__ x, int64_t n, EncWs w, int S,
+template <class Src>
+__global__ __launch_bounds__(kET) void topk_filter_kernel(Src x, int64_t n, EncWs w, int S,
                                                           long long rank_lo, long long rank_hi, int take_all) {
   __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
   __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
@@ -982,8 +1092,8 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(const float* __restric
 // ------------------------------------------------------------------------------------------------
 // FUSED: the filter phase runs first in the same kernel (one exchange after it): the candidates stay in
 // LDS, so the staging round trip through HBM and a kernel boundary are gone
-template <bool STACKED, bool FUSED>
-__global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restrict__ x, int64_t n, long long k, EncWs w,
+template <bool STACKED, bool FUSED, class Src>
+__global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long long k, EncWs w,
                                                           int* __restrict__ idx_out, float* __restrict__ val_out,
                                                           uint8_t* __restrict__ code_out, float* __restrict__ norm_out,
                                                           int levels, double step, uint64_t seed, uint64_t counter,
@@ -1098,7 +1208,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(const float* __restric
     cur.need = 0;
     prev = cur;
   }
-  CandSrc src;
+  CandSrc<Src> src;
   src.s_key = s_key;
   src.s_idx = s_idx;
   src.x = x;
@@ -1627,8 +1737,8 @@ int current_cus(int* dev_out) {
   return device_cus(dev);
 }
 
-template <bool STACKED>
-int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes, hipStream_t st, int* idx, float* val,
+template <bool STACKED, class Src>
+int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, hipStream_t st, int* idx, float* val,
                 uint8_t* codes, float* norm, int levels, uint64_t seed, uint64_t counter, unsigned* tiles,
                 const char* who) {
   int dev = 0;
@@ -1639,10 +1749,10 @@ int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes,
   const EncGeom g = enc_geometry(n, cus);
   const SampleSetup ss = sample_setup(n, k);
   if (!ss.take_all)
-    FLC_LAUNCH("topk_sample", topk_sample_kernel, dim3((unsigned)cdiv(ss.S, 256)), dim3(256), 0, st, x, n, ss.S, w);
+    FLC_LAUNCH("topk_sample", topk_sample_kernel<Src>, dim3((unsigned)cdiv(ss.S, 256)), dim3(256), 0, st, x, n, ss.S, w);
   static const bool split = getenv("FLC_TOPK_SPLIT") && atoi(getenv("FLC_TOPK_SPLIT")) != 0;  // calibration
   if (split)
-    FLC_LAUNCH("topk_filter", topk_filter_kernel, dim3((unsigned)g.G), dim3(kET), 0, st, x, n, w, ss.S, ss.rank_lo,
+    FLC_LAUNCH("topk_filter", topk_filter_kernel<Src>, dim3((unsigned)g.G), dim3(kET), 0, st, x, n, w, ss.S, ss.rank_lo,
                ss.rank_hi, ss.take_all);
   SelectGate& gt = gate();
   std::lock_guard<std::mutex> lk(gt.mu);
@@ -1662,11 +1772,11 @@ int launch_topk(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes,
   }
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   if (split)
-    FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", (topk_select_kernel<STACKED, false>), dim3((unsigned)g.G),
+    FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", (topk_select_kernel<STACKED, false, Src>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
                tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
   else
-    FLC_LAUNCH(STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true>), dim3((unsigned)g.G),
+    FLC_LAUNCH(STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true, Src>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
                tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
   if (gated && gt.multi[dev]) {
@@ -1702,7 +1812,7 @@ int flc_topk_encode_tiled(const float* x, int64_t n, int64_t k, int32_t* idx, fl
                           size_t ws_bytes, void* stream) {
   if (int rc = check_topk(x, n, k, "flc_topk_encode")) return rc;
   if (!idx || !val) return fail(FLC_EINVAL, "flc_topk_encode: null output");
-  return launch_topk<false>(x, n, k, ws, ws_bytes, as_stream(stream), idx, val, nullptr, nullptr, 0, 0, 0, tiles,
+  return launch_topk<false>(FlatSrc{x}, n, k, ws, ws_bytes, as_stream(stream), idx, val, nullptr, nullptr, 0, 0, 0, tiles,
                             "flc_topk_encode");
 }
 
@@ -1720,8 +1830,8 @@ int flc_stacked_encode_tiled(const float* x, int64_t n, int64_t k, int levels, u
   if (compat_u)
     return fail(FLC_EUNSUPPORTED,
                 "flc_stacked_encode: compat RNG is composed by the caller (flc_topk_encode + flc_quant_encode)");
-  return launch_topk<true>(x, n, k, ws, ws_bytes, as_stream(stream), idx, nullptr, codes, norm, levels, seed, counter,
-                           tiles, "flc_stacked_encode");
+  return launch_topk<true>(FlatSrc{x}, n, k, ws, ws_bytes, as_stream(stream), idx, nullptr, codes, norm, levels, seed,
+                           counter, tiles, "flc_stacked_encode");
 }
 
 int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_t seed, uint64_t counter,
@@ -1729,6 +1839,52 @@ int flc_stacked_encode(const float* x, int64_t n, int64_t k, int levels, uint64_
                        void* stream) {
   return flc_stacked_encode_tiled(x, n, k, levels, seed, counter, compat_u, idx, codes, norm, nullptr, ws, ws_bytes,
                                   stream);
+}
+
+// the delta encoder's tensor table sits after the encoder's own workspace
+size_t delta_table_bytes(int n_tensors) { return align_up((size_t)(n_tensors + 1) * 8 + (size_t)n_tensors * 16, 256); }
+
+size_t flc_stacked_encode_delta_workspace_size(int64_t n, int64_t k, int n_tensors) {
+  return align_up(flc_topk_workspace_size(n, k), 256) + delta_table_bytes(n_tensors < 0 ? 0 : n_tensors);
+}
+
+int flc_stacked_encode_delta(const float* const* local, const float* const* global, const int64_t* sizes,
+                             int n_tensors, int64_t k, int levels, uint64_t seed, uint64_t counter, int32_t* idx,
+                             uint8_t* codes, float* norm, uint32_t* tiles, void* ws, size_t ws_bytes, void* stream) {
+  if (n_tensors <= 0 || !local || !global || !sizes) return fail(FLC_EINVAL, "flc_stacked_encode_delta: bad arguments");
+  if (!idx || !codes || !norm) return fail(FLC_EINVAL, "flc_stacked_encode_delta: null output");
+  if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_stacked_encode_delta: levels must be in [1, 127]");
+  std::vector<long long> off((size_t)n_tensors + 1, 0);
+  for (int t = 0; t < n_tensors; ++t) {
+    if (sizes[t] < 0 || (sizes[t] > 0 && (!local[t] || !global[t])))
+      return fail(FLC_EINVAL, "flc_stacked_encode_delta: bad tensor %d", t);
+    if ((reinterpret_cast<uintptr_t>(local[t]) | reinterpret_cast<uintptr_t>(global[t])) & 3u)
+      return fail(FLC_EINVAL, "flc_stacked_encode_delta: tensor %d is not 4-B aligned", t);
+    off[t + 1] = off[t] + sizes[t];
+  }
+  const int64_t n = off[n_tensors];
+  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_stacked_encode_delta: n must be < 2^31");
+  if (k <= 0 || k >= n)
+    return fail(FLC_EINVAL, "flc_stacked_encode_delta: need 0 < k < n (got k=%lld, n=%lld)", (long long)k, (long long)n);
+  const size_t enc = align_up(flc_topk_workspace_size(n, k), 256);
+  if (!ws || ws_bytes < enc + delta_table_bytes(n_tensors))
+    return fail(FLC_EWORKSPACE, "flc_stacked_encode_delta: workspace %zu < %zu", ws_bytes,
+                enc + delta_table_bytes(n_tensors));
+  // table: off[n_tensors + 1] (int64), then the local pointers, then the global pointers
+  std::vector<char> host(delta_table_bytes(n_tensors), 0);
+  std::memcpy(host.data(), off.data(), off.size() * 8);
+  std::memcpy(host.data() + off.size() * 8, local, (size_t)n_tensors * 8);
+  std::memcpy(host.data() + off.size() * 8 + (size_t)n_tensors * 8, global, (size_t)n_tensors * 8);
+  char* tab = static_cast<char*>(ws) + enc;
+  hipStream_t st = as_stream(stream);
+  FLC_CHECK_HIP(hipMemcpyAsync(tab, host.data(), host.size(), hipMemcpyHostToDevice, st));
+  DeltaSrc src;
+  src.t.off = reinterpret_cast<const long long*>(tab);
+  src.t.lp = reinterpret_cast<const float* const*>(tab + off.size() * 8);
+  src.t.gp = reinterpret_cast<const float* const*>(tab + off.size() * 8 + (size_t)n_tensors * 8);
+  src.t.nseg = n_tensors;
+  return launch_topk<true>(src, n, k, ws, enc, st, idx, nullptr, codes, norm, levels, seed, counter, tiles,
+                           "flc_stacked_encode_delta");
 }
 
 int flc_topk_status(void* ws, uint64_t* err_out, int reset, void* stream) {

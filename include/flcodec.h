@@ -194,6 +194,17 @@ int flc_adaptive_prepare(const float* x, int64_t n, int32_t* status, void* ws, s
 int flc_adaptive_select(const float* x, int64_t n, double u, int64_t* index, float* out, void* ws, size_t ws_bytes,
                         void* stream);
 
+/* the stacked encoder fused with the client delta (f1): x = local - global formed in the encoder's HBM pass
+ * (FedOptClient.communicate, _fedopt.py:294-297: clone + add_(alpha=-1) per parameter tensor, then the flatten the
+ * codec's flat input needs, nodes.py:300-302) — the flat delta is never written.  local, global and sizes are HOST
+ * arrays (of device pointers / element counts, like flc_delta_flatten); tensors must be 4-B aligned; the element
+ * order is the concatenation.  The output is bit-identical to flc_stacked_encode_tiled of the flattened delta.
+ * The workspace holds the encoder's plus a tensor table (copied from the host arrays, so not graph-capturable). */
+size_t flc_stacked_encode_delta_workspace_size(int64_t n, int64_t k, int n_tensors);
+int flc_stacked_encode_delta(const float* const* local, const float* const* global, const int64_t* sizes,
+                             int n_tensors, int64_t k, int levels, uint64_t seed, uint64_t counter, int32_t* idx,
+                             uint8_t* codes, float* norm, uint32_t* tiles, void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------ other compressors
  * identical (compressors.py:273-275): out = +x;  lazy (276-283): out = x / p (fp32 division);
  * rand-k (284-292): out = 0, out[idx[j]] = scale * x[idx[j]] (idx in any order, unique). */

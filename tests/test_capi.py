@@ -90,3 +90,25 @@ def test_topk_status_plumbing_without_gpu(monkeypatch):
         codec._after_encode(None)
     monkeypatch.setattr(codec, "topk_status", lambda device=None, reset=True: 0)
     codec._after_encode(None)  # clean word: no error
+
+
+def test_stacked_encode_delta_validates_without_gpu():
+    """flc_stacked_encode_delta rejects bad tensor tables before touching the device."""
+    from fl_sim_amd import _lib
+
+    lib = _lib.load()
+    P = ctypes.c_void_p * 2
+    S = ctypes.c_int64 * 2
+    good = P(16, 32)
+    assert lib.flc_stacked_encode_delta(None, None, None, 0, 1, 127, 0, 0, 16, 16, 16, None, 16, 1 << 30, None) == 1
+    # misaligned tensor pointer
+    rc = lib.flc_stacked_encode_delta(ctypes.cast(P(18, 32), ctypes.c_void_p), ctypes.cast(good, ctypes.c_void_p),
+                                      ctypes.cast(S(100, 100), ctypes.c_void_p), 2, 10, 127, 0, 0, 16, 16, 16, None, 16,
+                                      1 << 30, None)
+    assert rc == 1 and "aligned" in lib.flc_last_error().decode()
+    # k out of range
+    rc = lib.flc_stacked_encode_delta(ctypes.cast(good, ctypes.c_void_p), ctypes.cast(good, ctypes.c_void_p),
+                                      ctypes.cast(S(100, 100), ctypes.c_void_p), 2, 200, 127, 0, 0, 16, 16, 16, None, 16,
+                                      1 << 30, None)
+    assert rc == 1 and "0 < k < n" in lib.flc_last_error().decode()
+    assert lib.flc_stacked_encode_delta_workspace_size(1000, 10, 8) > lib.flc_topk_workspace_size(1000, 10)

@@ -73,3 +73,77 @@ def test_delta_flatten_then_stacked_codec():
     exp, exp_idx, _, _ = ref.stacked(x, k, 127, lambda i: u[i])
     assert np.array_equal(pkt.idx.cpu().numpy().astype(np.int64), exp_idx)
     assert gc.same_bits(out, exp)
+
+
+# ---------------------------------------------------------------------- f1: the delta fused into the encode read
+def _same_packet(a, b):
+    k = a.idx.numel()
+    return (torch.equal(a.idx, b.idx) and torch.equal(a.codes[:k], b.codes[:k]) and torch.equal(a.norm, b.norm)
+            and torch.equal(a.tiles, b.tiles))
+
+
+def test_stacked_encode_delta_matches_reference_delta_and_oracle():
+    """flc_stacked_encode_delta on the config-1 parameter list: the packet of the reference's own delta
+    (agg_variants.npz fixture, FedOptClient.communicate) through the oracle's stacked codec, bit for bit."""
+    from fl_sim_amd import codec
+    from oracle import compressors_ref as ref
+
+    local, cached = delta_inputs(CONFIG1_SHAPES)
+    x = _expected(local, cached)
+    assert gc.sha(x) == str(AGGV["delta_config1|delta|sha"])
+    n = x.size
+    k = n // 100
+    pkt = codec.stacked_encode_delta([t.cuda() for t in local], [t.cuda() for t in cached], k, 127, seed=3, counter=9)
+    exp, exp_idx, exp_codes, pn = ref.stacked(x, k, 127, lambda i: ref.philox_uniforms_at(i, 3, 9), fast=True)
+    assert np.array_equal(pkt.idx.cpu().numpy().astype(np.int64), exp_idx)
+    assert np.array_equal(pkt.codes[:k].cpu().numpy(), exp_codes) and pkt.norm.item() == float(pn)
+    assert gc.same_bits(codec.stacked_decode(pkt).cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("sizes", [[1, 7, 3, 100_000, 5], [4097, 4095, 4096, 8193, 0, 16384 * 3 + 1],
+                                   [1_000_003], list(range(1, 400)), [16384 * 16 + 3] * 9])
+def test_stacked_encode_delta_equals_flatten_then_encode(sizes):
+    """Odd sizes (tensor boundaries inside wave steps, not 16-B aligned in the flat space), many tensors, empty
+    tensors: the same packet as delta_flatten + stacked_encode."""
+    from fl_sim_amd import codec
+
+    g = torch.Generator(device="cuda").manual_seed(len(sizes))
+    cached = [torch.randn(n, generator=g, device="cuda") for n in sizes]
+    local = [c + torch.randn(c.shape, generator=g, device="cuda") * 1e-3 for c in cached]
+    n = sum(sizes)
+    k = max(1, n // 100)
+    a = codec.stacked_encode_delta(local, cached, k, 127, seed=5, counter=2)
+    b = codec.stacked_encode(codec.delta_flatten(local, cached), k, 127, seed=5, counter=2)
+    assert _same_packet(a, b)
+
+
+def test_stacked_encode_delta_misaligned_views():
+    from fl_sim_amd import codec
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    base_l = torch.randn(3_000_011, generator=g, device="cuda")
+    base_g = torch.randn(3_000_011, generator=g, device="cuda")
+    local = [base_l[1:1_000_001], base_l[1_000_003:2_500_003], base_l[2_500_006:3_000_011]]
+    cached = [base_g[2:1_000_002], base_g[1_000_000:2_500_000], base_g[2_500_006:3_000_011]]
+    n = sum(t.numel() for t in local)
+    a = codec.stacked_encode_delta(local, cached, n // 100, 127, seed=1, counter=1)
+    b = codec.stacked_encode(codec.delta_flatten(local, cached), n // 100, 127, seed=1, counter=1)
+    assert _same_packet(a, b)
+
+
+def test_stacked_encode_delta_1gib_in_64_tensors():
+    """The bench's f1 configuration (1 GiB of parameters in 64 tensors): the same packet as the two-pass path."""
+    from fl_sim_amd import codec
+
+    sizes = [(1 << 22) + (i % 3) for i in range(63)]
+    sizes.append((1 << 28) - sum(sizes))
+    g = torch.Generator(device="cuda").manual_seed(64)
+    cached = [torch.randn(n, generator=g, device="cuda") * 0.1 for n in sizes]
+    local = [c + torch.randn(c.shape, generator=g, device="cuda") * 1e-3 for c in cached]
+    k = (1 << 28) // 100
+    a = codec.stacked_encode_delta(local, cached, k, 127, seed=2, counter=6)
+    flat = codec.delta_flatten(local, cached)
+    b = codec.stacked_encode(flat, k, 127, seed=2, counter=6)
+    assert _same_packet(a, b)
+    del flat, local, cached
+    torch.cuda.empty_cache()
