@@ -423,19 +423,21 @@ __global__ __launch_bounds__(kThreads) void quant_encode_philox_kernel(
     float o[kGroup];
     const float nr0 = (valid == kGroup && e0 + kGroup <= r_end) ? (FOLD ? s_norm[r0 - row_base] : norms[r0]) : 0.0f;
     if (KIND == 0 && valid == kGroup && e0 + kGroup <= r_end && norm_regular(nr0)) {
-      // standard dithering, branch-light: the fp32 decision for all 8 elements (dither_level's fast path, with
-      // u in fp32 straight from the Philox word: 1 ulp from fp32(u01), far inside the 3e-5 margin), then the
-      // exact fp64 rule for the rare elements the margin does not decide (whole-wave branch)
-      const float sf = (float)s;
+      // standard dithering, branch-light: an fp32 decision for all 8 elements, then the exact fp64 rule for the rare
+      // elements its margins do not decide (whole-wave branch).  No division: t' = |x| * fp32(s / norm) is within
+      // 2^-23 t <= 1.6e-5 of s|x|/norm, and the reference's t = fp32(|x| / norm) * s within 7.6e-6 of it, so
+      // |t' - t| < 2.4e-5 and the same holds for p = ceil(t) - t (the subtraction is exact); u in fp32 straight
+      // from the Philox word is within 6e-8 of u.  Margins 1e-4 (bracket) and 5e-5 (u vs p) cover that.
+      const float rs = (float)s / nr0;
       uint32_t lvl[kGroup];
       uint32_t slow = 0;
 #pragma unroll
       for (int j = 0; j < kGroup; ++j) {
-        const float t = (fabsf(v[j]) / nr0) * sf;
+        const float t = fabsf(v[j]) * rs;
         const float jf = ceilf(t);
         const float pf = jf - t;
         const float uf = (float)wd[j] * 2.3283064365386963e-10f;
-        const bool ok = (pf > 1e-4f) & (t - (jf - 1.0f) > 1e-4f) & (fabsf(uf - pf) > 3e-5f);
+        const bool ok = (pf > 1e-4f) & (t - (jf - 1.0f) > 1e-4f) & (fabsf(uf - pf) > 5e-5f);
         lvl[j] = (uint32_t)(int)jf - (uf < pf ? 1u : 0u);
         slow |= (uint32_t)(!ok && v[j] != 0.0f) << j;
       }
