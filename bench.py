@@ -485,6 +485,20 @@ def main():
             "bytes_formula": "8 * D + 16 * K",
         }
         del o3
+        # a7: adaptive random (np.random.choice with p = |x| / sum|x|) on the 25M delta, device u (philox mode)
+        def step_ar():
+            codec.adaptive_prepare(X3)
+            codec.adaptive_select(X3, 0.37)
+
+        ms_ar, _ = timed(step_ar, 10, 3, world)
+        ms_ar = max_over_ranks(ms_ar, world)
+        extra["adaptive_random_25M"] = {
+            "ms_per_call": round(ms_ar, 4),
+            "GB_s": round(8 * d3 / (ms_ar * 1e-3) / 1e9, 1),
+            "bytes_formula": "8 * D (two reads of x: the buffer sums and the speculated cumsum) + 4 * D output",
+            "note": "bit-exact numpy order: pairwise fp32 sum per 8192-element buffer, speculated exact fp64 cumsum "
+                    "(DESIGN.md 3.5); the numpy reference takes ~0.3 s for this call",
+        }
         # f1: client delta formation + flatten (FedOptClient.communicate), 1 GiB of parameters in 64 tensors
         sizes5 = [(1 << 22) + (i % 3) for i in range(63)]
         sizes5.append((1 << 28) - sum(sizes5))
