@@ -494,8 +494,8 @@ def main():
         ms_ar = max_over_ranks(ms_ar, world)
         extra["adaptive_random_25M"] = {
             "ms_per_call": round(ms_ar, 4),
-            "GB_s": round(8 * d3 / (ms_ar * 1e-3) / 1e9, 1),
-            "bytes_formula": "8 * D (two reads of x: the buffer sums and the speculated cumsum) + 4 * D output",
+            "GB_s": round(12 * d3 / (ms_ar * 1e-3) / 1e9, 1),
+            "bytes_formula": "12 * D: two reads of x (the buffer sums, the speculated cumsum) + the dense output",
             "note": "bit-exact numpy order: pairwise fp32 sum per 8192-element buffer, speculated exact fp64 cumsum "
                     "(DESIGN.md 3.5); the numpy reference takes ~0.3 s for this call",
         }
