@@ -58,7 +58,7 @@ at::Tensor workspace(const at::Tensor& like, size_t nbytes, int kind) {
   }
   return it->second;
 }
-enum { kWsQuant = 0, kWsNatural = 1, kWsTopk = 2 };
+enum { kWsQuant = 0, kWsNatural = 1, kWsTopk = 2, kWsAdaptive = 3 };
 
 int code_bits(int64_t levels) {
   TORCH_CHECK(levels >= 1, "flcodec: levels must be >= 1");
@@ -327,7 +327,102 @@ void feddr_combine_(at::Tensor& theta, at::Tensor& y, const at::Tensor& x_til, d
         "feddr_combine");
 }
 
+// ------------------------------------------------------------------------------------- round-2 entry points
+// the stacked encode of the client delta formed in the encoder's read (flc_stacked_encode_delta)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode_delta(at::TensorList local,
+                                                                                  at::TensorList global, int64_t k,
+                                                                                  int64_t levels, int64_t seed,
+                                                                                  int64_t counter) {
+  TORCH_CHECK(!local.empty() && local.size() == global.size(), "flcodec: one global tensor per local tensor");
+  std::vector<at::Tensor> keep;
+  std::vector<const float*> lp, gp;
+  std::vector<int64_t> sz;
+  int64_t n = 0;
+  for (size_t t = 0; t < local.size(); ++t) {
+    same_device(local[0], local[t], "local tensors");
+    same_device(local[0], global[t], "global tensors");
+    TORCH_CHECK(local[t].numel() == global[t].numel(), "flcodec: local and global tensor ", t, " differ in size");
+    keep.push_back(dev_f32(local[t], "local"));
+    lp.push_back(keep.back().data_ptr<float>());
+    keep.push_back(dev_f32(global[t], "global"));
+    gp.push_back(keep.back().data_ptr<float>());
+    sz.push_back(local[t].numel());
+    n += local[t].numel();
+  }
+  const at::Tensor& x = local[0];
+  c10::DeviceGuard g(x.device());
+  at::Tensor idx = at::empty({k}, x.options().dtype(at::kInt));
+  at::Tensor codes = at::empty({std::max<int64_t>(k, 16)}, x.options().dtype(at::kByte));
+  at::Tensor norm = at::empty({1}, x.options().dtype(at::kFloat));
+  at::Tensor tiles = at::empty({n_tiles(n)}, x.options().dtype(at::kInt));
+  at::Tensor ws = workspace(x, flc_stacked_encode_delta_workspace_size(n, k, (int)sz.size()), kWsTopk);
+  check(flc_stacked_encode_delta(lp.data(), gp.data(), sz.data(), (int)sz.size(), k, (int)levels, (uint64_t)seed,
+                                 (uint64_t)counter, idx.data_ptr<int32_t>(), codes.data_ptr<uint8_t>(),
+                                 norm.data_ptr<float>(), reinterpret_cast<uint32_t*>(tiles.data_ptr<int32_t>()),
+                                 ws.data_ptr(), (size_t)ws.numel(), stream_of(x)),
+        "stacked_encode_delta");
+  return {idx, codes.narrow(0, 0, k), norm, tiles};
+}
+
+// philox dithering with the norm included and the decode fused (flc_quant_encode_auto)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> quant_encode_auto(const at::Tensor& x_, int64_t kind, int64_t levels,
+                                                                 int64_t p, int64_t seed, int64_t counter) {
+  at::Tensor x = dev_f32(x_, "x");
+  TORCH_CHECK(x.dim() == 2, "flcodec: quant_encode_auto takes a [rows, d] batch");
+  c10::DeviceGuard g(x.device());
+  const int64_t rows = x.size(0), d = x.size(1);
+  const int bits = code_bits(levels);
+  at::Tensor codes = at::empty({std::max<int64_t>((rows * d * bits + 7) / 8, 1)}, x.options().dtype(at::kByte));
+  at::Tensor norms = at::empty({rows}, x.options());
+  at::Tensor out = at::empty({rows, d}, x.options());
+  at::Tensor ws = workspace(x, flc_quant_workspace_size(rows, d), kWsQuant);
+  check(flc_quant_encode_auto(x.data_ptr<float>(), rows, d, (int)kind, (int)levels, bits, norm_kind(p), (uint64_t)seed,
+                              (uint64_t)counter, codes.data_ptr<uint8_t>(), norms.data_ptr<float>(), nullptr,
+                              out.data_ptr<float>(), ws.data_ptr(), (size_t)ws.numel(), stream_of(x)),
+        "quant_encode_auto");
+  return {codes, norms, out};
+}
+
+// adaptive random with the uniform given (flc_adaptive_prepare + flc_adaptive_select): (out, index, status);
+// status != 0 is numpy's ValueError (1: p contains NaN, 2: p does not sum to 1) and then out is all zero
+std::tuple<at::Tensor, at::Tensor, at::Tensor> adaptive_random(const at::Tensor& x_, double u) {
+  at::Tensor x = dev_f32(x_, "x").reshape({-1});
+  c10::DeviceGuard g(x.device());
+  const int64_t n = x.numel();
+  TORCH_CHECK(n > 0, "flcodec: adaptive_random of an empty vector");
+  at::Tensor status = at::empty({1}, x.options().dtype(at::kInt));
+  at::Tensor index = at::zeros({1}, x.options().dtype(at::kLong));
+  at::Tensor out = at::empty({n}, x.options());
+  at::Tensor ws = workspace(x, flc_adaptive_workspace_size(n), kWsAdaptive);
+  check(flc_adaptive_prepare(x.data_ptr<float>(), n, status.data_ptr<int32_t>(), ws.data_ptr(), (size_t)ws.numel(),
+                             stream_of(x)),
+        "adaptive_prepare");
+  check(flc_adaptive_select(x.data_ptr<float>(), n, u, index.data_ptr<int64_t>(), out.data_ptr<float>(), ws.data_ptr(),
+                            (size_t)ws.numel(), stream_of(x)),
+        "adaptive_select");
+  return {out, index, status};
+}
+
 // --------------------------------------------------------------------------------- Meta kernels (shapes only)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode_delta_meta(at::TensorList local,
+                                                                                       at::TensorList, int64_t k,
+                                                                                       int64_t, int64_t, int64_t) {
+  int64_t n = 0;
+  for (const auto& t : local) n += t.numel();
+  const auto o = local[0].options();
+  return {at::empty({k}, o.dtype(at::kInt)), at::empty({k}, o.dtype(at::kByte)), at::empty({1}, o.dtype(at::kFloat)),
+          at::empty({n_tiles(n)}, o.dtype(at::kInt))};
+}
+std::tuple<at::Tensor, at::Tensor, at::Tensor> quant_encode_auto_meta(const at::Tensor& x, int64_t, int64_t levels,
+                                                                      int64_t, int64_t, int64_t) {
+  const int64_t rows = x.size(0), d = x.size(1);
+  return {at::empty({std::max<int64_t>((rows * d * code_bits(levels) + 7) / 8, 1)}, x.options().dtype(at::kByte)),
+          at::empty({rows}, x.options()), at::empty({rows, d}, x.options())};
+}
+std::tuple<at::Tensor, at::Tensor, at::Tensor> adaptive_random_meta(const at::Tensor& x, double) {
+  return {at::empty({x.numel()}, x.options()), at::empty({1}, x.options().dtype(at::kLong)),
+          at::empty({1}, x.options().dtype(at::kInt))};
+}
 at::Tensor delta_flatten_meta(at::TensorList local, at::TensorList) {
   int64_t total = 0;
   for (const auto& t : local) total += t.numel();
@@ -389,6 +484,11 @@ TORCH_LIBRARY(flcodec, m) {
   m.def("delta_flatten(Tensor[] theta_local, Tensor[] theta_global) -> Tensor");
   m.def("feddr_combine_(Tensor(a!) theta, Tensor(b!) y, Tensor x_til, float alpha, float cx, float cy, int prox, "
         "float prox_c) -> ()");
+  m.def("stacked_encode_delta(Tensor[] theta_local, Tensor[] theta_global, int k, int levels=127, int seed=0, "
+        "int counter=0) -> (Tensor idx, Tensor codes, Tensor norm, Tensor tiles)");
+  m.def("quant_encode_auto(Tensor x, int kind, int levels, int p=0, int seed=0, int counter=0) "
+        "-> (Tensor codes, Tensor norms, Tensor decoded)");
+  m.def("adaptive_random(Tensor x, float u) -> (Tensor out, Tensor index, Tensor status)");
 }
 
 TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
@@ -406,6 +506,9 @@ TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
   m.impl("fedopt_step_", &fedopt_step_);
   m.impl("delta_flatten", &delta_flatten);
   m.impl("feddr_combine_", &feddr_combine_);
+  m.impl("stacked_encode_delta", &stacked_encode_delta);
+  m.impl("quant_encode_auto", &quant_encode_auto);
+  m.impl("adaptive_random", &adaptive_random);
 }
 
 TORCH_LIBRARY_IMPL(flcodec, Meta, m) {
@@ -419,4 +522,7 @@ TORCH_LIBRARY_IMPL(flcodec, Meta, m) {
   m.impl("natural_encode", &natural_encode_meta);
   m.impl("natural_decode", &natural_decode_meta);
   m.impl("delta_flatten", &delta_flatten_meta);
+  m.impl("stacked_encode_delta", &stacked_encode_delta_meta);
+  m.impl("quant_encode_auto", &quant_encode_auto_meta);
+  m.impl("adaptive_random", &adaptive_random_meta);
 }
