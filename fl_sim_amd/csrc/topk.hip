@@ -1607,7 +1607,11 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
 #pragma unroll
   for (int j = 0; j < kRnd; ++j) {
     const unsigned pa = q0 + (unsigned)(j * kWave) + lane;
+#if FLC_CALIB_NORQ  // calibration builds only: results invalid
+    rq[j] = pa;
+#else
     rq[j] = STACKED ? ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1)) : 0u;
+#endif
   }
   auto round = [&](const unsigned p0, const unsigned rw, const unsigned raw, const unsigned id) {
     const unsigned p = p0 + lane;
@@ -1675,7 +1679,11 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
       const unsigned rw = rq[j];
       if (STACKED) {
         const unsigned pa = p0 + (unsigned)(kRnd * kWave) + lane;
+#if FLC_CALIB_NORQ
+        rq[j] = pa;
+#else
         rq[j] = ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1));
+#endif
       }
       unsigned n_raw, n_id;
       const unsigned pn = p0 + kWave + lane;
