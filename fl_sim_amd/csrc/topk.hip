@@ -955,6 +955,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
       int shB = 0;
       const bool fast = rank_lo <= kET;  // grid-uniform
       if (fast) sample_fast_hist(keys, S, SL, s_hist, &B, &shB);
+      STAMP(1);
       x.template load<false>(cur, wb0 + kBS, b1, lane, vb);
       if (fast) ok = sample_fast_pick(w.sample(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
     }
@@ -1287,10 +1288,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     // scanned in the compaction's wave ranges: the count above the bin per wave range plus the wave of
     // each of my in-bin keys give the compaction its per-wave strict / tie counts once T is known
     unsigned gtw = 0;
-    for (unsigned p0 = cq0; p0 < cq1; p0 += kWave) {
-      const unsigned p = p0 + lane;
-      unsigned raw = 0, id = 0;
-      if (p < cq1) cand_get(src, p, raw, id);
+    auto scan_one = [&](const unsigned p, const unsigned raw) {
       const unsigned key = order_key(raw);
       const unsigned long long rel = (unsigned long long)key - lo0;
       const bool valid = p < cq1 && key >= lo0 && key >= t_lo;  // (x-mode: below the floor never counts)
@@ -1307,6 +1305,29 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
           s_mykey[q] = key;
           s_mywv[q] = (unsigned)wid;
         }
+      }
+    };
+    if (!src.xmode) {
+      // LDS candidates: 4 rounds of reads at clamped indices issued together, then scanned
+      const unsigned wq0 = (unsigned)__builtin_amdgcn_readfirstlane((int)cq0);
+      const unsigned wq1 = (unsigned)__builtin_amdgcn_readfirstlane((int)cq1);
+      const unsigned pl = wq1 > 0u ? wq1 - 1u : 0u;
+      for (unsigned p00 = wq0; p00 < wq1; p00 += 4u * kWave) {
+        unsigned r4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned p = p00 + (unsigned)(j * kWave) + lane;
+          r4[j] = s_key[p < wq1 ? p : pl];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) scan_one(p00 + (unsigned)(j * kWave) + lane, r4[j]);
+      }
+    } else {
+      for (unsigned p0 = cq0; p0 < cq1; p0 += kWave) {
+        const unsigned p = p0 + lane;
+        unsigned raw = 0, id = 0;
+        if (p < cq1) cand_get(src, p, raw, id);
+        scan_one(p, raw);
       }
     }
     if (lane == 0) s_wcnt[wid] = (unsigned long long)gtw << 32;
@@ -1588,9 +1609,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     s_before += (long long)(s_wcnt[v2] >> 32);
     t_before += (long long)(s_wcnt[v2] & 0xffffffffull);
   }
-  // pass 2: keep decisions and the writes
+  // pass 2: keep decisions, then the writes
   // chunks whose Philox words were precomputed in the exchange waits (wave-uniform test per iteration)
-  // (one iteration ahead, unconditional loads at a clamped address, so no wait is merged in)
   const unsigned rdone = (STACKED && !src.xmode && rnd_n == ncand) ? s_rnext : 0u;
 #ifdef FLC_SELECT_STAMPS  // diagnostic: Philox chunks precomputed / chunks of the block
   if (tid == 0) w.blkt()[blockIdx.x * 4 + 2] = ((unsigned long long)((cQ / kWave) * kENW) << 32) | rdone;
@@ -1603,102 +1623,177 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
 #else
   constexpr int kRnd = FLC_KRND;
 #endif
-  unsigned rq[kRnd];
-#pragma unroll
-  for (int j = 0; j < kRnd; ++j) {
-    const unsigned pa = q0 + (unsigned)(j * kWave) + lane;
-#if FLC_CALIB_NORQ  // calibration builds only: results invalid
-    rq[j] = pa;
-#else
-    rq[j] = STACKED ? ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1)) : 0u;
-#endif
-  }
-  auto round = [&](const unsigned p0, const unsigned rw, const unsigned raw, const unsigned id) {
-    const unsigned p = p0 + lane;
-    const bool in = p < q1;
-    const bool have = ((p0 - q0) / kWave * kENW + (unsigned)wid) < rdone;
-    const unsigned key = order_key(raw);
-    const bool is_s = in && key > T, is_t = in && key == T;
-    const unsigned long long ms = __ballot(is_s), mt = __ballot(is_t);
-    const long long sb = s_before + __builtin_amdgcn_mbcnt_hi((unsigned)(ms >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ms, 0u));
-    const long long tb = t_before + __builtin_amdgcn_mbcnt_hi((unsigned)(mt >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mt, 0u));
-    const bool keep = is_s || (is_t && tb >= skip);
-    const long long pos = sb + (tb > skip ? tb - skip : 0);
-#if FLC_CALIB_NOWRITE  // calibration builds only: results invalid
-    if (keep && pos == -5) {
-#else
-    if (keep && pos >= 0 && pos < k) {
-#endif
-      idx_out[pos] = (int)id;
-      if (STACKED) {
-        const float v = __uint_as_float(raw);
-        const float y = nrm_ok ? fabsf(v) / nrm : 0.0f;  // compressors.py:344
+  // the code byte of a kept candidate (stacked): compressors.py:344-353 on |v| / norm
+  // No division on the common path: t' = |v| * fp32(s / norm) and u = fp32(word) * 2^-32 decide whenever
+  // they clear the margins of quant.hip's encode (1e-4 from a level, 5e-5 between u and p; valid for s <= 127,
+  // the argument written there); the rest take the exact fp64 rule on fp32(|v| / norm).
+  const bool fast_ok = nrm_ok && levels <= 127;
+  const float rs = fast_ok ? (float)levels / nrm : 0.0f;
+  auto code_of = [&](const unsigned raw, const unsigned id, const bool have, const unsigned rw) -> unsigned {
+    const float v = __uint_as_float(raw);
 #if FLC_CALIB_NOPHILOX  // calibration builds only (tools/calib_select.sh): results invalid
-        const double uu = 0.5;
+    const uint32_t r = 0x80000000u;
 #else
-        uint32_t r;
-        if (have) r = rw;
-        else r = pick(philox_group((uint64_t)id >> 2, seed, counter), (int)(id & 3u));
-        const double uu = u01(r);
+    uint32_t r;
+    if (have) r = rw;
+    else r = pick(philox_group((uint64_t)id >> 2, seed, counter), (int)(id & 3u));
 #endif
-        const uint32_t lvl = (uint32_t)dither_level<0>(y, levels, step, uu);  // compressors.py:346-353
-        const uint32_t c = nrm_ok ? (((raw >> 31) << 7) | lvl) : 1u;
-        code_out[pos] = (uint8_t)((v != 0.0f) ? c : 0u);
-      } else {
-        val_out[pos] = __uint_as_float(raw);
-      }
+    uint32_t lvl;
+    const float t = fabsf(v) * rs;
+    const float jf = ceilf(t);
+    const float pf = jf - t;
+    const float uf = (float)r * 2.3283064365386963e-10f;
+    if (fast_ok && (pf > 1e-4f) & (t - (jf - 1.0f) > 1e-4f) & (fabsf(uf - pf) > 5e-5f)) {
+      lvl = (uint32_t)(int)jf - (uf < pf ? 1u : 0u);
+    } else {
+      const float y = nrm_ok ? fabsf(v) / nrm : 0.0f;  // compressors.py:344
+      lvl = (uint32_t)dither_level<0>(y, levels, step, u01(r));  // compressors.py:346-353
     }
-    if (tile_owner) {
-      // tiles starting after the previous CANDIDATE (lane - 1's id by a DPP wave shift; lane 0: the last
-      // candidate of the previous round) and at or before this one get this candidate's kept-before count:
-      // the elements in between are below the floor, so the first kept entry at or after such a tile's start
-      // is the first kept entry at or after this candidate (kept or not) — no ballot / shuffle per round
-      const unsigned prev_lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(tile_prev < 0 ? 0 : tile_prev));
-      unsigned pid = (unsigned)__builtin_amdgcn_update_dpp((int)prev_lo, (int)id, 0x138, 0xf, 0xf, false);  // wave_shr:1
-      const int64_t prev = lane == 0 ? tile_prev : (int64_t)pid;
-      if (in) {
-        const long long before = sb + (tb > skip ? tb - skip : 0);  // kept entries before this candidate
-        for (int64_t t = (prev >> kTileLog) + 1; t <= ((int64_t)id >> kTileLog); ++t) tile_out[t] = (unsigned)before;
-      }
-      const unsigned long long im = __ballot(in);
+    const uint32_t c = nrm_ok ? (((raw >> 31) << 7) | lvl) : 1u;
+    return (v != 0.0f) ? c : 0u;
+  };
+  // tiles starting after the previous kept entry (lane - 1's id by a DPP wave shift; lane 0: `tile_prev`)
+  // and at or before this one get this entry's position: the first kept entry at or after such a tile's
+  // start.  Every candidate between two kept entries is dropped, so kept entries alone define the tiles.
+  auto tiles_of = [&](const bool v, const unsigned id, const long long pos) {
+    const unsigned prev_lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(tile_prev < 0 ? 0 : tile_prev));
+    const unsigned pid = (unsigned)__builtin_amdgcn_update_dpp((int)prev_lo, (int)id, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    const int64_t prev = lane == 0 ? tile_prev : (int64_t)pid;
+    if (v)
+      for (int64_t t = (prev >> kTileLog) + 1; t <= ((int64_t)id >> kTileLog); ++t) tile_out[t] = (unsigned)pos;
+    const unsigned long long im = __ballot(v);
+    if (im) {
       const int hl = 63 - __clzll(im);  // (wave-uniform)
       tile_prev = (int64_t)(unsigned)__builtin_amdgcn_readlane((int)id, hl);
     }
-    s_before += __popcll(ms);
-    t_before += __popcll(mt);
   };
-  // the next round's candidates are read while this one is processed (clamped index: unconditional)
   const unsigned plast = q1 > 0u ? q1 - 1u : 0u;
-  unsigned c_raw = 0, c_id = 0;
-  if (q0 < q1) cand_get(src, q0 + lane < q1 ? q0 + lane : plast, c_raw, c_id);
-  for (unsigned p00 = q0; p00 < q1; p00 += kRnd * kWave) {
+  if (!src.xmode) {
+    // LDS candidates: pass 2 touches no memory but LDS and the Philox words.  Kept entries are staged in
+    // place, wave range order (a kept entry's slot q0 + (kept before it in the range) <= its own index, and
+    // the next round's candidates, read before this round's slots are written, lie past them), then
+    // written out with the tile pointers in a second loop: no stores in the decision loop, so the
+    // Philox-word loads kRnd rounds ahead keep counted waits instead of draining every store each round.
+    const unsigned wq0 = (unsigned)__builtin_amdgcn_readfirstlane((int)q0);
+    const unsigned wq1 = (unsigned)__builtin_amdgcn_readfirstlane((int)q1);
+    const long long kept0 = s_before + (t_before > skip ? t_before - skip : 0);  // position of my first kept entry
+    unsigned nk = 0;  // kept entries staged (wave-uniform)
+    unsigned* const st_id = const_cast<unsigned*>(src.s_idx);
+    unsigned* const st_cw = const_cast<unsigned*>(src.s_key);
+    unsigned rq[kRnd];
 #pragma unroll
     for (int j = 0; j < kRnd; ++j) {
-      const unsigned p0 = p00 + (unsigned)(j * kWave);
-      if (p0 >= q1) break;
-      const unsigned rw = rq[j];
-      if (STACKED) {
-        const unsigned pa = p0 + (unsigned)(kRnd * kWave) + lane;
-#if FLC_CALIB_NORQ
-        rq[j] = pa;
+      const unsigned pa = wq0 + (unsigned)(j * kWave) + lane;
+#if FLC_CALIB_NORQ  // calibration builds only: results invalid
+      rq[j] = pa;
 #else
-        rq[j] = ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1));
+      rq[j] = STACKED ? ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1)) : 0u;
 #endif
+    }
+    unsigned c_raw = 0, c_id = 0;
+    {
+      const unsigned pc = wq0 + lane < wq1 ? wq0 + lane : plast;
+      c_raw = src.s_key[pc];
+      c_id = src.s_idx[pc];
+    }
+    for (unsigned p00 = wq0; p00 < wq1; p00 += kRnd * kWave) {
+#pragma unroll
+      for (int j = 0; j < kRnd; ++j) {  // (rounds past q1: no lane in, nothing kept)
+        const unsigned p0 = p00 + (unsigned)(j * kWave);
+        const unsigned rw = rq[j];
+        if (STACKED) {
+          const unsigned pa = p0 + (unsigned)(kRnd * kWave) + lane;
+#if FLC_CALIB_NORQ
+          rq[j] = pa;
+#else
+          rq[j] = ld_mem(rnd + (pa < (unsigned)kCap ? pa : kCap - 1));
+#endif
+        }
+        const unsigned pn = p0 + kWave + lane < wq1 ? p0 + kWave + lane : plast;
+        const unsigned n_raw = src.s_key[pn], n_id = src.s_idx[pn];
+        const unsigned p = p0 + lane;
+        const bool in = p < wq1;
+        const unsigned key = order_key(c_raw);
+        const bool is_s = in && key > T, is_t = in && key == T;
+        const unsigned long long ms = __ballot(is_s), mt = __ballot(is_t);
+        const long long tb = t_before + __builtin_amdgcn_mbcnt_hi((unsigned)(mt >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mt, 0u));
+        const bool keep = is_s || (is_t && tb >= skip);
+        const unsigned long long km = __ballot(keep);
+        if (keep) {
+          const unsigned slot = wq0 + nk + __builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
+          const bool have = ((p0 - wq0) / kWave * kENW + (unsigned)wid) < rdone;
+          st_id[slot] = c_id;
+          st_cw[slot] = STACKED ? code_of(c_raw, c_id, have, rw) : c_raw;
+        }
+        nk += (unsigned)__popcll(km);
+        s_before += __popcll(ms);
+        t_before += __popcll(mt);
+        c_raw = n_raw;
+        c_id = n_id;
       }
+    }
+    STAMP(14);
+    // write-out: positions kept0 + i, i < nk, contiguous per wave
+    for (unsigned i0 = 0; i0 < nk; i0 += kWave) {
+      const unsigned i = i0 + lane;
+      const bool v = i < nk;
+      const unsigned id = v ? st_id[wq0 + i] : 0u, cw = v ? st_cw[wq0 + i] : 0u;
+      const long long pos = kept0 + (long long)i;
+#if !FLC_CALIB_NOWRITE
+      if (v && pos >= 0 && pos < k) {
+        idx_out[pos] = (int)id;
+        if (STACKED) code_out[pos] = (uint8_t)cw;
+        else val_out[pos] = __uint_as_float(cw);
+      }
+#endif
+      if (tile_owner) tiles_of(v, id, pos);
+    }
+  } else {
+    // x-mode (fallback, or more candidates than LDS holds): candidates from x, writes in the loop
+    unsigned rq[kRnd];
+#pragma unroll
+    for (int j = 0; j < kRnd; ++j) rq[j] = 0u;
+    auto round = [&](const unsigned p0, const unsigned rw, const unsigned raw, const unsigned id) {
+      const unsigned p = p0 + lane;
+      const bool in = p < q1;
+      const unsigned key = order_key(raw);
+      const bool is_s = in && key > T, is_t = in && key == T;
+      const unsigned long long ms = __ballot(is_s), mt = __ballot(is_t);
+      const long long sb = s_before + __builtin_amdgcn_mbcnt_hi((unsigned)(ms >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ms, 0u));
+      const long long tb = t_before + __builtin_amdgcn_mbcnt_hi((unsigned)(mt >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mt, 0u));
+      const bool keep = is_s || (is_t && tb >= skip);
+      const long long pos = sb + (tb > skip ? tb - skip : 0);
+#if FLC_CALIB_NOWRITE  // calibration builds only: results invalid
+      if (keep && pos == -5) {
+#else
+      if (keep && pos >= 0 && pos < k) {
+#endif
+        idx_out[pos] = (int)id;
+        if (STACKED) code_out[pos] = (uint8_t)code_of(raw, id, false, rw);
+        else val_out[pos] = __uint_as_float(raw);
+      }
+      if (tile_owner) tiles_of(in, id, pos);  // (pos of a dropped candidate: the kept entries before it)
+      s_before += __popcll(ms);
+      t_before += __popcll(mt);
+    };
+    // the next round's candidates are read while this one is processed (clamped index: unconditional)
+    unsigned c_raw = 0, c_id = 0;
+    if (q0 < q1) cand_get(src, q0 + lane < q1 ? q0 + lane : plast, c_raw, c_id);
+    for (unsigned p0 = q0; p0 < q1; p0 += kWave) {
       unsigned n_raw, n_id;
       const unsigned pn = p0 + kWave + lane;
       cand_get(src, pn < q1 ? pn : plast, n_raw, n_id);
-      round(p0, rw, c_raw, c_id);
+      round(p0, rq[0], c_raw, c_id);
       c_raw = n_raw;
       c_id = n_id;
     }
+    STAMP(14);
   }
   if (tile_owner) {  // tiles after the wave's last kept entry: the next kept position
     const long long nxt = s_before + (t_before > skip ? t_before - skip : 0);
     for (int64_t t = (tile_prev >> kTileLog) + 1 + lane; t <= (tile_hi >> kTileLog); t += kWave) tile_out[t] = (unsigned)nxt;
     if (blockIdx.x == gridDim.x - 1 && q1 >= ncand && lane == 0) tile_out[cdiv_dev(n, kTile)] = (unsigned)k;
   }
-  STAMP(14);
   STAMP(15);
   BLKT(3);
   STAMP_OUT(FUSED ? 0 : 5, 16);

@@ -1,9 +1,9 @@
 """Phase stamps of the persistent encode (diagnostic build: make EXTRA=-DFLC_SELECT_STAMPS, block 0 only).
 
-Stamp slots (s_memrealtime, 100 MHz): 0 start, 2 floor/ceiling, 3 HBM pass done, 4 histogram flushed
+Stamp slots (s_memrealtime, 100 MHz): 0 start, 1 sample keys histogrammed, 2 floor/ceiling, 3 HBM pass done, 4 histogram flushed
 (split path: staged); 5 select start (fused default: after the exchange that follows the filter phase),
 6 loads done, 7 pick, 8 in-bin lists published, 9 exchanged, 10 list gathered, 11 T resolved, 12 sums,
-13 counts, 14 compaction done.  FLC_TOPK_SPLIT=1 times the two-kernel path instead.
+13 counts, 14 keep decisions staged (x-mode: compaction done), 15 written out with the tile pointers.  FLC_TOPK_SPLIT=1 times the two-kernel path instead.
 """
 import os
 import sys
@@ -20,7 +20,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
 seed = int(os.environ.get("SEED", "1"))  # bench.py's headline delta: SEED=1234
 x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed)) * 1e-3
-names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "compact", "tiles"]
+names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "decide", "write+tiles"]
 for it in range(int(os.environ.get("ITERS", "12"))):
     codec.stacked_encode(x, k, 127, 1, it)
     torch.cuda.synchronize()
