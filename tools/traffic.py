@@ -21,12 +21,15 @@ SHORT = {
     "sparse_decode_wave_kernel<0": "sparse_decode",
     "topk_sample_kernel": "topk_sample",
     "sparse_decode_kernel<0": "sparse_decode",
+    "topk_select_kernel<true, true, flc::(anonymous namespace)::DeltaSrc>": "stacked_encode_delta",
+    "topk_select_kernel<true, true, flc::(anonymous namespace)::FlatSrc>": "stacked_encode",
+    "topk_select_kernel<false, true, flc::(anonymous namespace)::FlatSrc>": "topk_encode",
     "topk_select_kernel<true>": "stacked_select",
     "topk_select_kernel<false>": "topk_select",
     "topk_select_kernel<true, true>": "stacked_encode",
     "topk_select_kernel<false, true>": "topk_encode",
-    "topk_select_kernel<true, false>": "stacked_select",
-    "topk_select_kernel<false, false>": "topk_select",
+    "topk_select_kernel<true, false": "stacked_select",
+    "topk_select_kernel<false, false": "topk_select",
     "topk_sample_select_kernel": "topk_sample_select",
     "topk_sample_gather_kernel": "topk_sample_gather",
     "tile_index_kernel": "tile_index",
