@@ -588,6 +588,24 @@ def main():
             # nccl-tests convention for reduce: busBw = algBw = bytes / time (every non-root rank's whole 4 D
             # buffer crosses a link); the timed reduces re-reduce `acc` in place (values unused)
             line4["reduce_algbw_GB_s"] = round(4 * d3 / (ms4r * 1e-3) / 1e9, 1)
+        # the same round with the packed wire as the only exchange (SURVEY §8(e)'s sparse alternative): each rank
+        # encodes its clients into wire records, ONE all_gather of the records, the fold of all 8 clients in
+        # client order in one pass on rank 0 (bit-identical to the single-device fold at every N)
+        wc4 = fdist.StackedWireCodec(d3, k3, LEVELS, seed=0, counter=0)
+
+        def step4w():
+            c4[0] += 1
+            wc4.counter = c4[0]
+            fdist.aggregate_round_wire([X3] * len(mine), w_all, n_cl4, wc4, out=acc, dst=0, device=dev)
+
+        ms4w, _ = timed(step4w, 10, 3, world)
+        ms4w = max_over_ranks(ms4w, world)
+        per4 = -(-n_cl4 // world)
+        line4["wire_ms_per_step"] = round(ms4w, 4)
+        line4["wire_record_bytes"] = wc4.stride
+        line4["wire_gather_bytes_per_rank"] = per4 * wc4.stride
+        line4["wire_bytes_formula"] = ("codec: n_local * (4 * D + 5 * K + tiles) written as records; all_gather: "
+                                       "world * ceil(8 / world) records; fold: 4 * D written + 8 records read")
         extra["config4_codec_plus_rccl_reduce_25M"] = line4
         del acc
         del X3

@@ -95,6 +95,11 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p, c_void_p],
     ),
+    "flc_stacked_wire_layout": (c_size_t, [c_int64, c_int64, c_void_p]),
+    "flc_stacked_fold_wires": (
+        c_int,
+        [c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int64, c_int64, c_int, c_int, c_void_p, c_void_p],
+    ),
     "flc_adaptive_workspace_size": (c_size_t, [c_int64]),
     "flc_adaptive_prepare": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_adaptive_select": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

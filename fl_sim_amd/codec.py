@@ -287,14 +287,58 @@ class StackedPacket:
         return 5 * self.idx.numel() + 4 + (4 * self.tiles.numel() if self.tiles is not None else 0)
 
 
+_WIRE_LAYOUT = {}
+
+
+def stacked_wire_layout(n: int, k: int):
+    """(record bytes, {"norm", "idx", "codes", "tiles"} byte offsets) of the packed stacked wire
+    (flc_stacked_wire_layout): one contiguous record per client whose layout depends on (n, k) only."""
+    import ctypes
+
+    key = (int(n), int(k))
+    r = _WIRE_LAYOUT.get(key)
+    if r is None:
+        off = (ctypes.c_int64 * 4)()
+        total = _lib.size("flc_stacked_wire_layout", int(n), int(k), ctypes.cast(off, ctypes.c_void_p))
+        if total == 0:
+            raise ValueError(f"bad wire shape n={n}, k={k}")
+        r = (int(total), dict(zip(("norm", "idx", "codes", "tiles"), (int(v) for v in off))))
+        _WIRE_LAYOUT[key] = r
+    return r
+
+
+def wire_packet(record: torch.Tensor, n: int, k: int, levels: int = 127) -> StackedPacket:
+    """The StackedPacket whose tensors are views into one packed wire record (a uint8 HIP tensor of at least
+    ``stacked_wire_layout(n, k)[0]`` bytes, 16-B aligned)."""
+    stride, off = stacked_wire_layout(n, k)
+    if record.dtype != torch.uint8 or record.device.type != "cuda" or not record.is_contiguous():
+        raise TypeError("a wire record is a contiguous uint8 HIP tensor")
+    rec = record.reshape(-1)
+    if rec.numel() < stride or rec.data_ptr() % 16 != 0:
+        raise ValueError(f"a wire record needs {stride} bytes, 16-B aligned")
+    ntiles = (n + TILE - 1) // TILE + 1
+    return StackedPacket(rec[off["idx"]:off["idx"] + 4 * k].view(torch.int32),
+                         rec[off["codes"]:off["codes"] + max(k, 16)],
+                         rec[off["norm"]:off["norm"] + 4].view(torch.float32), int(n), int(levels),
+                         rec[off["tiles"]:off["tiles"] + 4 * ntiles].view(torch.int32))
+
+
 def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, counter: int = 0,
-                   with_tiles: bool = True) -> StackedPacket:
+                   with_tiles: bool = True, wire: Optional[torch.Tensor] = None) -> StackedPacket:
+    """Stacked top-k -> 8-bit dithering encode.  ``wire``: a packed wire record (see :func:`wire_packet`) to write
+    the packet into; the returned packet's tensors are then views of it."""
     x = _dev_f32(x).reshape(-1)
     n = x.numel()
-    idx = torch.empty(k, dtype=torch.int32, device=x.device)
-    codes = torch.empty(max(k, 16), dtype=torch.uint8, device=x.device)
-    norm = torch.empty(1, dtype=torch.float32, device=x.device)
-    tiles = _tiles(n, x.device) if with_tiles else None
+    if wire is not None:
+        if wire.device != x.device:
+            raise ValueError("the wire record must be on the input's device")
+        pk = wire_packet(wire, n, k, levels)
+        idx, codes, norm, tiles = pk.idx, pk.codes, pk.norm, pk.tiles
+    else:
+        idx = torch.empty(k, dtype=torch.int32, device=x.device)
+        codes = torch.empty(max(k, 16), dtype=torch.uint8, device=x.device)
+        norm = torch.empty(1, dtype=torch.float32, device=x.device)
+        tiles = _tiles(n, x.device) if with_tiles else None
     ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
     call("flc_stacked_encode_tiled", _p(x), n, k, levels, seed, counter, None, _p(idx), _p(codes), _p(norm),
          _p(tiles), _p(ws), ws.numel(), _stream(x.device))
@@ -347,6 +391,38 @@ def stacked_decode(pkt: StackedPacket, out: Optional[torch.Tensor] = None, weigh
     ws = workspace(out.device, _lib.size("flc_sparse_decode_workspace_size", pkt.n), "decode")
     call("flc_stacked_decode", _p(pkt.idx), _p(pkt.codes), pkt.idx.numel(), pkt.levels, _p(pkt.norm), pkt.n, weight,
          int(accumulate), _p(out), _p(ws), ws.numel(), _stream(out.device))
+    return out
+
+
+def stacked_fold_wires(wires: torch.Tensor, slots: Sequence[int], weights: Sequence[float], n: int, k: int,
+                       levels: int = 127, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """Server fold of many clients' packed wires in one pass (flc_stacked_fold_wires):
+    ``out = (out if accumulate else +0)``, then ``out = fmaf(weights[c], decode(wires[slots[c]]), out)`` for c in
+    order — bit-identical to zeroing ``out`` and calling ``stacked_decode(..., weight, accumulate=True)`` per client.
+    ``wires``: uint8 HIP tensor [records, stride] (or flat, records of ``stacked_wire_layout(n, k)[0]`` bytes)."""
+    import ctypes
+
+    stride, _ = stacked_wire_layout(n, k)
+    if wires.dtype != torch.uint8 or wires.device.type != "cuda" or not wires.is_contiguous():
+        raise TypeError("wires must be a contiguous uint8 HIP tensor")
+    if wires.dim() == 2:
+        stride = wires.shape[1]
+    nrec = wires.numel() // stride
+    if len(slots) != len(weights) or not slots:
+        raise ValueError("one weight per slot, at least one")
+    if min(slots) < 0 or max(slots) >= nrec:
+        raise ValueError(f"slots must index the {nrec} records")
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs an out tensor")
+        out = torch.empty(n, dtype=torch.float32, device=wires.device)
+    elif out.device != wires.device or out.dtype != torch.float32 or not out.is_contiguous() or out.numel() != n:
+        raise ValueError(f"out must be a contiguous fp32 tensor of {n} elements on {wires.device}")
+    m = len(slots)
+    sl = (ctypes.c_int32 * m)(*[int(v) for v in slots])
+    wt = (ctypes.c_float * m)(*[float(v) for v in weights])
+    call("flc_stacked_fold_wires", _p(wires), stride, ctypes.cast(sl, ctypes.c_void_p), ctypes.cast(wt, ctypes.c_void_p),
+         m, n, k, levels, int(accumulate), _p(out), _stream(out.device))
     return out
 
 

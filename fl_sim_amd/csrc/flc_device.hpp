@@ -313,4 +313,12 @@ __device__ __forceinline__ int level_lower_bound(float yf, int s, double step) {
   }
 }
 
+// decoded value of a stacked-codec code byte (sign << 7 | level) with the kept set's norm (compressors.py:357:
+// fp32(fp32(lv) * sign) * norm); a non-regular norm decodes every nonzero code to NaN
+__device__ __forceinline__ float stacked_dequant(uint32_t code, int levels, double step, float nrm) {
+  if (!(nrm > 0.0f && nrm <= 3.402823466e38f)) return code == 0u ? 0.0f : __uint_as_float(0x7fc00000u);
+  const float lv = (float)level_value<0>((int)(code & 127u), levels, step);
+  return ((code >> 7) ? -lv : lv) * nrm;
+}
+
 }  // namespace flc

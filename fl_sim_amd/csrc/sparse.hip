@@ -127,9 +127,7 @@ __device__ __forceinline__ uint32_t entry_raw(const float* __restrict__ val, con
 template <int MODE>
 __device__ __forceinline__ float entry_value(uint32_t raw, float scale, int levels, double step, float nrm) {
   if (MODE == 0) return scale * __uint_as_float(raw);
-  if (!(nrm > 0.0f && nrm <= 3.402823466e38f)) return raw == 0u ? 0.0f : __uint_as_float(0x7fc00000u);
-  const float lv = (float)level_value<0>((int)(raw & 127u), levels, step);
-  return ((raw >> 7) ? -lv : lv) * nrm;  // compressors.py:357
+  return stacked_dequant(raw, levels, step, nrm);  // compressors.py:357
 }
 
 // Streaming decode: persistent blocks, block b owns the contiguous tiles [b * tpb, (b + 1) * tpb) of

@@ -1,0 +1,258 @@
+// wire.hip — the stacked codec's packed wire and the server-side fold of many clients' wires in one pass (gfx950).
+//
+// Packed wire (one contiguous, 256-B-aligned record per client; the layout is a function of (n, k) only, so a
+// [clients, stride] byte tensor can be all-gathered over RCCL or copied over PCIe as one piece):
+//   [0, 4)                     norm       fp32, the kept set's max |value| (compressors.py:344's pnorm at p = inf)
+//   [16, 16 + 4k)              idx        int32, ascending
+//   [codes, codes + max(k,16)) codes      u8, sign << 7 | level
+//   [tiles, tiles + 4(T+1))    tiles      u32 CSR pointers over FLC_TILE-output tiles (T = ceil(n / FLC_TILE))
+// The encoder writes it directly (flc_stacked_encode_tiled with the four pointers inside the record).
+//
+// Fold (flc_stacked_fold_wires): out = fmaf(w_c, decode(wire_c), out) for c = 0 .. m-1 in order, every element,
+// every client — the server's sequential fold (nodes.py:1165-1180, _fedopt.py:202-208) in ONE
+// pass over `out` instead of one decode-accumulate pass (read + write of 4n bytes) per client.  One 64-lane wave
+// per 1024-output tile keeps its slice of the accumulator in registers; per client the tile's kept entries are
+// scattered into a 4 KB LDS tile, read back densely (zeros included: fmaf(w, +0, acc) is applied exactly as the
+// dense per-client fold applies it), and the scattered slots are cleared again.  All clients' entries of the tile
+// are loaded in one batch (a wave prefix over the clients' counts) before the ordered fold; tiles holding more than
+// 128 entries over all clients take a per-client loop.  Bytes: 4n written (+ 4n read when accumulating) + the
+// wires' 5 B per kept entry and tile pointers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "flc_device.hpp"
+#include "flc_runtime.hpp"
+
+namespace flc {
+namespace {
+
+constexpr int kMaxWires = 64;  // clients per launch (more: chained launches, accumulating)
+
+struct WireLayout {
+  long long norm, idx, codes, tiles;
+};
+struct FoldArgs {
+  float w[kMaxWires];
+  int slot[kMaxWires];  // record index (in units of the stride) of the c-th client in fold order
+};
+
+WireLayout wire_layout(int64_t n, int64_t k, size_t* total) {
+  WireLayout L;
+  L.norm = 0;
+  L.idx = 16;
+  L.codes = (long long)align_up((size_t)(16 + 4 * k), 16);
+  L.tiles = (long long)align_up((size_t)L.codes + (size_t)std::max<int64_t>(k, 16), 16);
+  const int64_t ntiles = cdiv(n < 1 ? 1 : n, (int64_t)FLC_TILE);
+  *total = align_up((size_t)L.tiles + 4 * (size_t)(ntiles + 1), 256);
+  return L;
+}
+
+__global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t* __restrict__ wires, int64_t stride,
+                                                                   WireLayout L, FoldArgs a, int nw, int levels,
+                                                                   double step, int64_t n, int acc_in,
+                                                                   float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float s_tile[FLC_TILE];
+  float4* tile4 = reinterpret_cast<float4*>(s_tile);
+  const int lane = threadIdx.x;
+  const int64_t t = blockIdx.x;
+  const int64_t t0 = t * FLC_TILE;
+  // the tile's slice of the accumulator: lane owns float4 q = lane + 64 u
+  float4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (acc_in) {
+      if (e + 4 <= n) {
+        v = *reinterpret_cast<const float4*>(out + e);
+      } else {
+        if (e < n) v.x = out[e];
+        if (e + 1 < n) v.y = out[e + 1];
+        if (e + 2 < n) v.z = out[e + 2];
+      }
+    }
+    acc[u] = v;
+    tile4[lane + u * kWave] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // client `lane`'s record, entry range in this tile and norm (lanes >= nw: empty)
+  const uint8_t* rec = nullptr;
+  unsigned lo = 0, cnt = 0;
+  float nrm = 0.0f, wl = 0.0f;
+  if (lane < nw) {
+    rec = wires + (int64_t)a.slot[lane] * stride;
+    wl = a.w[lane];
+    const unsigned* tiles = reinterpret_cast<const unsigned*>(rec + L.tiles);
+    lo = tiles[t];
+    cnt = tiles[t + 1] - lo;
+    nrm = *reinterpret_cast<const float*>(rec + L.norm);
+  }
+  const unsigned incl = wave_incl_scan(cnt);
+  const unsigned excl = incl - cnt;
+  const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+
+  if (total <= 2u * kWave) {
+    // fast path: every entry of the tile over all clients in registers (g = lane, lane + 64), one load batch
+    int cg[2] = {-1, -1};
+    unsigned off[2] = {0u, 0u};
+    float val[2] = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const unsigned g = (unsigned)lane + (unsigned)(r * kWave);
+      int c = -1;
+      for (int cc = 0; cc < nw; ++cc) {  // (uniform loop; the client whose range holds g)
+        const unsigned ec = (unsigned)__builtin_amdgcn_readlane((int)excl, cc);
+        const unsigned nc = (unsigned)__builtin_amdgcn_readlane((int)cnt, cc);
+        if (g >= ec && g < ec + nc) c = cc;
+      }
+      cg[r] = g < total ? c : -1;
+    }
+    // the owning client's record / range / norm by lane shuffles, then the loads (one batch)
+    unsigned idx_raw[2] = {0u, 0u}, code[2] = {0u, 0u};
+    float nr[2] = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int src = cg[r] < 0 ? 0 : cg[r];
+      const unsigned lo_c = (unsigned)__shfl((int)lo, src, kWave);
+      const unsigned ex_c = (unsigned)__shfl((int)excl, src, kWave);
+      const unsigned long long rp = (unsigned long long)(uintptr_t)rec;
+      const unsigned rlo = (unsigned)__shfl((int)(unsigned)rp, src, kWave);
+      const unsigned rhi = (unsigned)__shfl((int)(unsigned)(rp >> 32), src, kWave);
+      nr[r] = __shfl(nrm, src, kWave);
+      if (cg[r] >= 0) {
+        const uint8_t* rc = reinterpret_cast<const uint8_t*>((uintptr_t)(((unsigned long long)rhi << 32) | rlo));
+        const unsigned j = lo_c + ((unsigned)lane + (unsigned)(r * kWave) - ex_c);
+        idx_raw[r] = reinterpret_cast<const unsigned*>(rc + L.idx)[j];
+        code[r] = rc[L.codes + j];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int64_t o = (int64_t)idx_raw[r] - t0;
+      if (cg[r] >= 0 && (o < 0 || o >= FLC_TILE)) cg[r] = -1;  // (a malformed wire: ignored, never out of the tile)
+      off[r] = (unsigned)(o < 0 ? 0 : (o >= FLC_TILE ? 0 : o));
+      val[r] = stacked_dequant(code[r], levels, step, nr[r]);
+    }
+    for (int c = 0; c < nw; ++c) {  // the ordered fold
+      const float wc = __shfl(wl, c, kWave);
+      const bool any = __builtin_amdgcn_readlane((int)cnt, c) != 0;
+      if (any) {
+        if (cg[0] == c) s_tile[off[0]] = val[0];
+        if (cg[1] == c) s_tile[off[1]] = val[1];
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 v = tile4[lane + u * kWave];
+          acc[u] = make_float4(fmaf(wc, v.x, acc[u].x), fmaf(wc, v.y, acc[u].y), fmaf(wc, v.z, acc[u].z),
+                               fmaf(wc, v.w, acc[u].w));
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (cg[0] == c) s_tile[off[0]] = 0.0f;
+        if (cg[1] == c) s_tile[off[1]] = 0.0f;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          acc[u] = make_float4(fmaf(wc, 0.0f, acc[u].x), fmaf(wc, 0.0f, acc[u].y), fmaf(wc, 0.0f, acc[u].z),
+                               fmaf(wc, 0.0f, acc[u].w));
+      }
+    }
+  } else {
+    // dense tiles (skewed inputs): per client, its entries in rounds of 64, scattered, folded, cleared
+    for (int c = 0; c < nw; ++c) {
+      const float wc = __shfl(wl, c, kWave);
+      const unsigned lo_c = (unsigned)__builtin_amdgcn_readlane((int)lo, c);
+      const unsigned n_c = (unsigned)__builtin_amdgcn_readlane((int)cnt, c);
+      const float nr_c = __shfl(nrm, c, kWave);
+      const unsigned long long rp = (unsigned long long)(uintptr_t)rec;
+      const unsigned rlo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)rp, c);
+      const unsigned rhi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(rp >> 32), c);
+      const uint8_t* rc = reinterpret_cast<const uint8_t*>((uintptr_t)(((unsigned long long)rhi << 32) | rlo));
+      const unsigned* ix = reinterpret_cast<const unsigned*>(rc + L.idx);
+      const uint8_t* cd = rc + L.codes;
+      for (unsigned j = lo_c + lane; j < lo_c + n_c; j += kWave) {
+        const int64_t o = (int64_t)ix[j] - t0;
+        if (o >= 0 && o < FLC_TILE) s_tile[o] = stacked_dequant(cd[j], levels, step, nr_c);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = tile4[lane + u * kWave];
+        acc[u] = make_float4(fmaf(wc, v.x, acc[u].x), fmaf(wc, v.y, acc[u].y), fmaf(wc, v.z, acc[u].z),
+                             fmaf(wc, v.w, acc[u].w));
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (unsigned j = lo_c + lane; j < lo_c + n_c; j += kWave) {
+        const int64_t o = (int64_t)ix[j] - t0;
+        if (o >= 0 && o < FLC_TILE) s_tile[o] = 0.0f;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
+    if (e + 4 <= n) {
+      *reinterpret_cast<float4*>(out + e) = acc[u];
+    } else {
+      if (e < n) out[e] = acc[u].x;
+      if (e + 1 < n) out[e + 1] = acc[u].y;
+      if (e + 2 < n) out[e + 2] = acc[u].z;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace flc
+
+using namespace flc;
+
+extern "C" {
+
+size_t flc_stacked_wire_layout(int64_t n, int64_t k, int64_t* offsets) {
+  if (n <= 0 || k < 0) return 0;
+  size_t total = 0;
+  const WireLayout L = wire_layout(n, k, &total);
+  if (offsets) {
+    offsets[0] = L.norm;
+    offsets[1] = L.idx;
+    offsets[2] = L.codes;
+    offsets[3] = L.tiles;
+  }
+  return total;
+}
+
+int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slots, const float* weights, int n_wires,
+                           int64_t n, int64_t k, int levels, int accumulate, float* out, void* stream) {
+  if (!wires || !slots || !weights || !out || n_wires < 1 || n <= 0 || k < 0)
+    return fail(FLC_EINVAL, "flc_stacked_fold_wires: bad arguments");
+  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_stacked_fold_wires: n must be < 2^31");
+  if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_stacked_fold_wires: levels must be in [1, 127]");
+  size_t need = 0;
+  const WireLayout L = wire_layout(n, k, &need);
+  if (stride < (int64_t)need || stride % 16 != 0)
+    return fail(FLC_EINVAL, "flc_stacked_fold_wires: stride %lld < record size %zu (or not 16-B aligned)",
+                (long long)stride, need);
+  if (!aligned16(wires) || !aligned16(out)) return fail(FLC_EINVAL, "flc_stacked_fold_wires: 16-B aligned buffers required");
+  for (int c = 0; c < n_wires; ++c)
+    if (slots[c] < 0) return fail(FLC_EINVAL, "flc_stacked_fold_wires: slot %d is negative", c);
+  hipStream_t st = as_stream(stream);
+  const int64_t ntiles = cdiv(n, (int64_t)FLC_TILE);
+  const double step = 1.0 / (double)levels;
+  for (int c0 = 0; c0 < n_wires; c0 += kMaxWires) {
+    const int nw = std::min(kMaxWires, n_wires - c0);
+    FoldArgs a;
+    for (int c = 0; c < kMaxWires; ++c) {
+      a.w[c] = c < nw ? weights[c0 + c] : 0.0f;
+      a.slot[c] = c < nw ? slots[c0 + c] : 0;
+    }
+    FLC_LAUNCH("stacked_fold_wires", stacked_fold_wires_kernel, dim3((unsigned)ntiles), dim3(kWave), 0, st,
+               static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, (c0 > 0 || accumulate) ? 1 : 0,
+               out);
+  }
+  return FLC_OK;
+}
+
+}  // extern "C"

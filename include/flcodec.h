@@ -179,6 +179,23 @@ int flc_stacked_decode_tiled(const int32_t* idx, const uint8_t* codes, int64_t k
                              const float* norm, int64_t n, float weight, int accumulate, float* out,
                              const uint32_t* tiles, void* stream);
 
+/* Packed wire: one client's stacked wire as ONE contiguous record whose layout depends on (n, k) only, so that
+ * a [clients, stride] byte buffer moves as one piece (RCCL all-gather, PCIe copy).  Returns the record size
+ * (a multiple of 256 B; 0 for bad arguments) and, if offsets != NULL, the byte offsets of
+ * offsets[0] norm (fp32), [1] idx (int32[k]), [2] codes (u8[max(k,16)]), [3] tiles (u32[ceil(n/FLC_TILE)+1]).
+ * flc_stacked_encode_tiled writes a record when given those four pointers inside it. */
+size_t flc_stacked_wire_layout(int64_t n, int64_t k, int64_t* offsets);
+/* Fold of many clients' wires into one vector in ONE pass over out (the server's weighted aggregation,
+ * nodes.py:1165-1180 / _fedopt.py:202-208, fused with the decode):
+ *   out = (accumulate ? out : +0);  for c = 0 .. n_wires-1:  out = fmaf(weights[c], decode(record slots[c]), out)
+ * elementwise, in that order — bit-identical to n_wires flc_stacked_decode_tiled(weight, accumulate=1) calls on a
+ * zeroed (or the given) out.  wires: records of `stride` bytes (>= flc_stacked_wire_layout(n, k), 16-B multiple),
+ * record index slots[c] holds client c; slots and weights are HOST arrays.  Replaces SURVEY §8(e)'s dense reduce
+ * when the records are all-gathered: every rank folds all clients in client order, so the result does not depend on
+ * the number of GPUs. */
+int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slots, const float* weights,
+                           int n_wires, int64_t n, int64_t k, int levels, int accumulate, float* out, void* stream);
+
 /* ------------------------------------------------------------------ adaptive random compressor
  * (compressors.py:297-301): ind = np.random.choice(np.arange(n), size=1, p=|x| / sum|x|); out = 0,
  * out[ind] = x[ind].  Bit-exact with numpy: S in numpy's order (8192-element buffers folded in order, each

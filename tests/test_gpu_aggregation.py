@@ -157,11 +157,15 @@ def test_config3_fold_full_size_vs_oracle():
     deltas = [torch.from_numpy(x).cuda() for x in xs]
     got = fdist.aggregate_round(deltas, w, list(range(n_cl)), fdist.stacked_decode_accumulate(k, seed=seed, counter=ctr))
     got = got.cpu().numpy()
+    # the packed-wire round (records + one-pass fold of all clients) on the same inputs
+    got_w = fdist.aggregate_round_wire(deltas, w, n_cl, fdist.StackedWireCodec(n, k, seed=seed, counter=ctr))
+    got_w = got_w.cpu().numpy()
     exp = torch.zeros(n, dtype=torch.float32)
     for c, (x, wi) in enumerate(zip(xs, w)):
         dec, _, _, _ = ref.stacked(x, k, 127, lambda idx, c=c: ref.philox_uniforms_at(idx, seed + c, ctr), fast=True)
         exp.add_(torch.from_numpy(dec), alpha=wi)
     assert np.array_equal(got.view(np.uint32), exp.numpy().view(np.uint32))
+    assert np.array_equal(got_w.view(np.uint32), exp.numpy().view(np.uint32))
     assert np.count_nonzero(got) >= k  # the clients' kept sets overlap only partially
 
 
