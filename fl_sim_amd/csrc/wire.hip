@@ -15,11 +15,14 @@
 // scattered into a 4 KB LDS tile, read back densely (zeros included: fmaf(w, +0, acc) is applied exactly as the
 // dense per-client fold applies it), and the scattered slots are cleared again.  All clients' entries of the tile
 // are loaded in one batch (a wave prefix over the clients' counts) before the ordered fold; tiles holding more than
-// 128 entries over all clients take a per-client loop.  Bytes: 4n written (+ 4n read when accumulating) + the
+// 128 entries over all clients take a per-client loop.  Sparse variant (a fold from +0 with finite weights, the
+// aggregation round's case): the accumulator lives in the LDS tile and only the kept entries are fma'd, in client
+// order — exact, because such an accumulator never holds -0, so fmaf(w, +0, acc) == acc everywhere else.  Bytes: 4n written (+ 4n read when accumulating) + the
 // wires' 5 B per kept entry and tile pointers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 
 #include "flc_device.hpp"
 #include "flc_runtime.hpp"
@@ -48,6 +51,7 @@ WireLayout wire_layout(int64_t n, int64_t k, size_t* total) {
   return L;
 }
 
+template <bool SPARSE>
 __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t* __restrict__ wires, int64_t stride,
                                                                    WireLayout L, FoldArgs a, int nw, int levels,
                                                                    double step, int64_t n, int acc_in,
@@ -73,7 +77,8 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
       }
     }
     acc[u] = v;
-    tile4[lane + u * kWave] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // dense: a zero tile per client; sparse: the accumulator itself lives in the LDS tile
+    tile4[lane + u * kWave] = SPARSE ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   // client `lane`'s record, entry range in this tile and norm (lanes >= nw: empty)
   const uint8_t* rec = nullptr;
@@ -133,7 +138,20 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
       off[r] = (unsigned)(o < 0 ? 0 : (o >= FLC_TILE ? 0 : o));
       val[r] = stacked_dequant(code[r], levels, step, nr[r]);
     }
-    for (int c = 0; c < nw; ++c) {  // the ordered fold
+    if (SPARSE) {
+      // the accumulator in LDS, updated at the kept entries only (see the launch: +0 start, finite weights, so
+      // fmaf(w, +0, acc) == acc for every element no entry touches)
+      for (int c = 0; c < nw; ++c) {
+        const float wc = __shfl(wl, c, kWave);
+        if (cg[0] == c) s_tile[off[0]] = fmaf(wc, val[0], s_tile[off[0]]);
+        if (cg[1] == c) s_tile[off[1]] = fmaf(wc, val[1], s_tile[off[1]]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = tile4[lane + u * kWave];
+    }
+    for (int c = 0; c < (SPARSE ? 0 : nw); ++c) {  // the ordered fold
       const float wc = __shfl(wl, c, kWave);
       const bool any = __builtin_amdgcn_readlane((int)cnt, c) != 0;
       if (any) {
@@ -170,6 +188,15 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
       const uint8_t* rc = reinterpret_cast<const uint8_t*>((uintptr_t)(((unsigned long long)rhi << 32) | rlo));
       const unsigned* ix = reinterpret_cast<const unsigned*>(rc + L.idx);
       const uint8_t* cd = rc + L.codes;
+      if (SPARSE) {
+        for (unsigned j = lo_c + lane; j < lo_c + n_c; j += kWave) {
+          const int64_t o = (int64_t)ix[j] - t0;
+          if (o >= 0 && o < FLC_TILE) s_tile[o] = fmaf(wc, stacked_dequant(cd[j], levels, step, nr_c), s_tile[o]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        continue;
+      }
       for (unsigned j = lo_c + lane; j < lo_c + n_c; j += kWave) {
         const int64_t o = (int64_t)ix[j] - t0;
         if (o >= 0 && o < FLC_TILE) s_tile[o] = stacked_dequant(cd[j], levels, step, nr_c);
@@ -189,6 +216,10 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (SPARSE) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = tile4[lane + u * kWave];
     }
   }
 #pragma unroll
@@ -241,6 +272,11 @@ int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slo
   hipStream_t st = as_stream(stream);
   const int64_t ntiles = cdiv(n, (int64_t)FLC_TILE);
   const double step = 1.0 / (double)levels;
+  // Sparse fold: starting from +0 the accumulator never holds -0 (an fma yields -0 only from -0 + -0), so with
+  // finite weights fmaf(w, +0, acc) == acc exactly and only the kept entries change it.  Otherwise (accumulating
+  // into a given vector, or a non-finite weight) every element takes every client's fma.
+  bool sparse = !accumulate;
+  for (int c = 0; c < n_wires; ++c) sparse = sparse && std::isfinite(weights[c]);
   for (int c0 = 0; c0 < n_wires; c0 += kMaxWires) {
     const int nw = std::min(kMaxWires, n_wires - c0);
     FoldArgs a;
@@ -248,9 +284,13 @@ int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slo
       a.w[c] = c < nw ? weights[c0 + c] : 0.0f;
       a.slot[c] = c < nw ? slots[c0 + c] : 0;
     }
-    FLC_LAUNCH("stacked_fold_wires", stacked_fold_wires_kernel, dim3((unsigned)ntiles), dim3(kWave), 0, st,
-               static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, (c0 > 0 || accumulate) ? 1 : 0,
-               out);
+    const int acc_in = (c0 > 0 || accumulate) ? 1 : 0;
+    if (sparse)
+      FLC_LAUNCH("stacked_fold_wires", stacked_fold_wires_kernel<true>, dim3((unsigned)ntiles), dim3(kWave), 0, st,
+                 static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, acc_in, out);
+    else
+      FLC_LAUNCH("stacked_fold_wires", stacked_fold_wires_kernel<false>, dim3((unsigned)ntiles), dim3(kWave), 0, st,
+                 static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, acc_in, out);
   }
   return FLC_OK;
 }

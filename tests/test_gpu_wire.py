@@ -104,3 +104,14 @@ def test_wire_round_world1_equals_dense_round():
     dense = fdist.aggregate_round(deltas, w, list(range(n_cl)), fdist.stacked_decode_accumulate(k, seed=9, counter=2))
     wired = fdist.aggregate_round_wire(deltas, w, n_cl, fdist.StackedWireCodec(n, k, seed=9, counter=2))
     assert np.array_equal(_bits(wired), _bits(dense))
+
+
+def test_fold_wires_nonfinite_weight_takes_every_fma():
+    """A non-finite weight turns fmaf(w, +0, acc) into NaN everywhere: the fold must then apply every client's fma to
+    every element (the dense variant), like the per-client chain does."""
+    n, k = 70_001, 700
+    recs = _records([_x(n, 90 + i) for i in range(3)], k, seeds=[1, 2, 3])
+    for weights in ([0.5, float("inf"), 0.25], [float("nan"), 1.0, 1.0], [-0.0, 0.0, 2.0]):
+        exp = _fold_ref(recs, [0, 1, 2], weights, n, k, torch.zeros(n, device="cuda"))
+        got = codec.stacked_fold_wires(recs, [0, 1, 2], weights, n, k)
+        assert np.array_equal(_bits(got), _bits(exp))
