@@ -104,16 +104,22 @@ class HostCodecPipeline:
 
 # ------------------------------------------------------------------------------------------- packed wire (f3)
 class HostWire:
-    """One client's stacked-codec wire in pinned host memory: ascending int32 indices, 8-bit (sign | level) codes,
-    the fp32 norm and the CSR tile pointers of the indices (the decoder's index).  ``nbytes`` is what crosses PCIe
-    (compressors.py:406-408 count the same payload as ``really_need_to_send_components``)."""
+    """One client's stacked-codec wire in pinned host memory, as ONE packed record (flc_stacked_wire_layout):
+    the fp32 norm, ascending int32 indices, 8-bit (sign | level) codes and the CSR tile pointers of the indices
+    (the decoder's index) at fixed offsets, so that it crosses PCIe in one copy.  ``idx`` / ``codes`` / ``norm`` /
+    ``tiles`` are views of the record.  ``nbytes`` is the payload (compressors.py:406-408 count the same as
+    ``really_need_to_send_components``); ``record.numel()`` adds the alignment padding."""
 
     def __init__(self, n: int, k: int, levels: int):
         self.n, self.k, self.levels = int(n), int(k), int(levels)
-        self.idx = torch.empty(self.k, dtype=torch.int32, pin_memory=True)
-        self.codes = torch.empty(max(self.k, 16), dtype=torch.uint8, pin_memory=True)
-        self.norm = torch.empty(1, dtype=torch.float32, pin_memory=True)
-        self.tiles = torch.empty((self.n + codec.TILE - 1) // codec.TILE + 1, dtype=torch.int32, pin_memory=True)
+        stride, off = codec.stacked_wire_layout(self.n, self.k)
+        self.record = torch.empty(stride, dtype=torch.uint8, pin_memory=True)
+        nt = (self.n + codec.TILE - 1) // codec.TILE + 1
+        r = self.record
+        self.norm = r[off["norm"]:off["norm"] + 4].view(torch.float32)
+        self.idx = r[off["idx"]:off["idx"] + 4 * self.k].view(torch.int32)
+        self.codes = r[off["codes"]:off["codes"] + max(self.k, 16)]
+        self.tiles = r[off["tiles"]:off["tiles"] + 4 * nt].view(torch.int32)
 
     @property
     def nbytes(self) -> int:
@@ -123,34 +129,28 @@ class HostWire:
 class HostWirePipeline:
     """The client -> server path with only the packed wire on the return link.
 
-    Client side (``encode``): pinned dense delta -> H2D -> stacked encode -> D2H of the WIRE only (~5 bytes per kept
-    entry + tile pointers: 14.5 MB per 1 GiB client at k = 1 %), instead of the dense decoded vector.  Server side
-    (``decode_accumulate``): H2D of each client's wire -> stacked decode with the client's weight fused
-    (``acc = fmaf(w_i, decode_i, acc)``, message order) into one device accumulator.  Copies and kernels of
-    neighbouring clients overlap on three streams; ordering is by events only.  The accumulated result equals the
-    device-resident fold of the same clients bit for bit (same kernels, seeds, counters and order).
+    Client side (``encode``): pinned dense delta -> H2D -> stacked encode straight into a device wire record -> ONE D2H
+    copy of the record (~14.5 MB per 1 GiB client at k = 1 %), instead of the dense decoded vector.  Server side
+    (``decode_accumulate``): one H2D copy per client's record into a device record buffer, then ONE pass over the
+    accumulator folding every client with its weight in message order (flc_stacked_fold_wires:
+    ``acc = fmaf(w_i, decode_i, acc)``).  Client copies and kernels overlap on three streams; ordering is by events only.
+    The accumulated result equals the device-resident fold of the same clients bit for bit (same kernels, seeds,
+    counters and order).
     """
 
     def __init__(self, n: int, k: int, levels: int = 127, device: Optional[torch.device] = None):
         self.n, self.k, self.levels = int(n), int(k), int(levels)
         self.device = _device(device)
+        self.stride = codec.stacked_wire_layout(self.n, self.k)[0]
         self.x = [torch.empty(self.n, dtype=torch.float32, device=self.device) for _ in range(2)]
-        self.pk = [None, None]
+        self.rec = [torch.empty(self.stride, dtype=torch.uint8, device=self.device) for _ in range(2)]
         self.s_h2d = torch.cuda.Stream(self.device)
         self.s_comp = torch.cuda.Stream(self.device)
         self.s_d2h = torch.cuda.Stream(self.device)
         self.in_free = [None, None]
         self.wire_free = [None, None]
         self._last = None
-        # server side: two device wire buffers
-        self.dw = [self._device_wire() for _ in range(2)]
-        self.dw_free = [None, None]
-
-    def _device_wire(self):
-        d = self.device
-        return (torch.empty(self.k, dtype=torch.int32, device=d), torch.empty(max(self.k, 16), dtype=torch.uint8, device=d),
-                torch.empty(1, dtype=torch.float32, device=d),
-                torch.empty((self.n + codec.TILE - 1) // codec.TILE + 1, dtype=torch.int32, device=d))
+        self.srv = None  # server side: the device record buffer, grown on demand
 
     def new_wires(self, m: int) -> List[HostWire]:
         return [HostWire(self.n, self.k, self.levels) for _ in range(m)]
@@ -185,19 +185,15 @@ class HostWirePipeline:
             with torch.cuda.stream(self.s_comp):
                 self.s_comp.wait_event(loaded)
                 if self.wire_free[b] is not None:
-                    self.s_comp.wait_event(self.wire_free[b])  # the packet buffers of b drained to the host
-                pkt = codec.stacked_encode(self.x[b], self.k, self.levels, seed=seeds[i], counter=counters[i])
-                self.pk[b] = pkt
+                    self.s_comp.wait_event(self.wire_free[b])  # record b drained to the host
+                codec.stacked_encode(self.x[b], self.k, self.levels, seed=seeds[i], counter=counters[i],
+                                     wire=self.rec[b])
                 done = torch.cuda.Event()
                 done.record(self.s_comp)
                 self.in_free[b] = done
             with torch.cuda.stream(self.s_d2h):
                 self.s_d2h.wait_event(done)
-                w = wires[i]
-                w.idx.copy_(pkt.idx, non_blocking=True)
-                w.codes.copy_(pkt.codes, non_blocking=True)
-                w.norm.copy_(pkt.norm, non_blocking=True)
-                w.tiles.copy_(pkt.tiles, non_blocking=True)
+                wires[i].record.copy_(self.rec[b], non_blocking=True)
                 drained = torch.cuda.Event()
                 drained.record(self.s_d2h)
                 self.wire_free[b] = drained
@@ -207,34 +203,34 @@ class HostWirePipeline:
                           zero: bool = True) -> torch.Tensor:
         """Server side: ``acc = (0 if zero else acc)``, then ``acc = fmaf(weights[i], decode(wires[i]), acc)`` in
         order.  ``acc`` is a device fp32 tensor of n elements.  Asynchronous on the pipeline's compute stream."""
-        if len(weights) != len(wires):
-            raise ValueError("one weight per wire")
+        if len(weights) != len(wires) or not wires:
+            raise ValueError("one weight per wire, at least one")
         if acc.device != self.device or acc.dtype != torch.float32 or acc.numel() != self.n or not acc.is_contiguous():
             raise ValueError(f"acc must be a contiguous fp32 tensor of {self.n} elements on {self.device}")
+        for i, w in enumerate(wires):
+            if (w.n, w.k) != (self.n, self.k):
+                raise ValueError(f"wires[{i}] has the wrong shape")
+        m = len(wires)
         self._start()
         self.s_h2d.wait_stream(self.s_d2h)  # wires this pipeline produced have reached the host
+        if self.srv is None or self.srv.shape[0] < m:
+            self.srv = torch.empty(m, self.stride, dtype=torch.uint8, device=self.device)
+        srv = self.srv
+        srv.record_stream(self.s_h2d)
+        with torch.cuda.stream(self.s_h2d):
+            self.s_h2d.wait_stream(self.s_comp)  # the previous fold has read the record buffer
+            for i, w in enumerate(wires):
+                srv[i].copy_(w.record, non_blocking=True)
+            loaded = torch.cuda.Event()
+            loaded.record(self.s_h2d)
         acc.record_stream(self.s_comp)
-        if zero:
-            with torch.cuda.stream(self.s_comp):
-                acc.zero_()
-        for i, (w, wt) in enumerate(zip(wires, weights)):
-            b = i % 2
-            dw = self.dw[b]
-            with torch.cuda.stream(self.s_h2d):
-                if self.dw_free[b] is not None:
-                    self.s_h2d.wait_event(self.dw_free[b])
-                for dst, src in zip(dw, (w.idx, w.codes, w.norm, w.tiles)):
-                    dst.copy_(src, non_blocking=True)
-                loaded = torch.cuda.Event()
-                loaded.record(self.s_h2d)
-            with torch.cuda.stream(self.s_comp):
-                self.s_comp.wait_event(loaded)
-                pkt = codec.StackedPacket(dw[0], dw[1], dw[2], self.n, self.levels, dw[3])
-                codec.stacked_decode(pkt, out=acc, weight=float(wt), accumulate=True)
-                done = torch.cuda.Event()
-                done.record(self.s_comp)
-                self.dw_free[b] = done
-                self._last = done
+        with torch.cuda.stream(self.s_comp):
+            self.s_comp.wait_event(loaded)
+            codec.stacked_fold_wires(srv, list(range(m)), [float(v) for v in weights], self.n, self.k, self.levels,
+                                     out=acc, accumulate=not zero)
+            done = torch.cuda.Event()
+            done.record(self.s_comp)
+            self._last = done
         return acc
 
     def synchronize(self):
