@@ -96,6 +96,57 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode(const 
   return {idx, codes.narrow(0, 0, k), norm, tiles};
 }
 
+// packed wire records (flc_stacked_wire_layout): the encode straight into one record, and the one-pass fold of many
+at::Tensor stacked_encode_wire(const at::Tensor& x_, int64_t k, int64_t levels, int64_t seed, int64_t counter) {
+  at::Tensor x = dev_f32(x_, "x").reshape({-1});
+  c10::DeviceGuard g(x.device());
+  const int64_t n = x.numel();
+  int64_t off[4];
+  const size_t stride = flc_stacked_wire_layout(n, k, off);
+  TORCH_CHECK(stride > 0, "flcodec: bad wire shape n=", n, ", k=", k);
+  at::Tensor rec = at::empty({(int64_t)stride}, x.options().dtype(at::kByte));
+  uint8_t* r = rec.data_ptr<uint8_t>();
+  at::Tensor ws = workspace(x, flc_topk_workspace_size(n, k), kWsTopk);
+  check(flc_stacked_encode_tiled(x.data_ptr<float>(), n, k, (int)levels, (uint64_t)seed, (uint64_t)counter, nullptr,
+                                 reinterpret_cast<int32_t*>(r + off[1]), r + off[2], reinterpret_cast<float*>(r + off[0]),
+                                 reinterpret_cast<uint32_t*>(r + off[3]), ws.data_ptr(), (size_t)ws.numel(),
+                                 stream_of(x)),
+        "stacked_encode_wire");
+  return rec;
+}
+
+at::Tensor stacked_fold_wires(const at::Tensor& wires, at::IntArrayRef slots, at::ArrayRef<double> weights, int64_t n,
+                              int64_t k, int64_t levels, const c10::optional<at::Tensor>& out_, bool accumulate) {
+  TORCH_CHECK(wires.is_cuda() && wires.scalar_type() == at::kByte && wires.is_contiguous(),
+              "flcodec: wires must be a contiguous uint8 HIP tensor");
+  TORCH_CHECK(slots.size() == weights.size() && !slots.empty(), "flcodec: one weight per slot, at least one");
+  const int64_t stride = wires.dim() == 2 ? wires.size(1) : (int64_t)flc_stacked_wire_layout(n, k, nullptr);
+  TORCH_CHECK(stride > 0, "flcodec: bad wire shape n=", n, ", k=", k);
+  const int64_t nrec = wires.numel() / stride;
+  std::vector<int32_t> sl(slots.size());
+  std::vector<float> wt(weights.size());
+  for (size_t c = 0; c < slots.size(); ++c) {
+    TORCH_CHECK(slots[c] >= 0 && slots[c] < nrec, "flcodec: slot ", slots[c], " outside the ", nrec, " records");
+    sl[c] = (int32_t)slots[c];
+    wt[c] = (float)weights[c];
+  }
+  at::Tensor out;
+  if (out_.has_value()) {
+    out = *out_;
+    same_device(out, wires, "wires");
+    TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == n,
+                "flcodec: out must be a contiguous fp32 tensor of n elements");
+  } else {
+    TORCH_CHECK(!accumulate, "flcodec: accumulate needs an out tensor");
+    out = at::empty({n}, wires.options().dtype(at::kFloat));
+  }
+  c10::DeviceGuard g(wires.device());
+  check(flc_stacked_fold_wires(wires.data_ptr(), stride, sl.data(), wt.data(), (int)sl.size(), n, k, (int)levels,
+                               accumulate ? 1 : 0, out.data_ptr<float>(), stream_of(out)),
+        "stacked_fold_wires");
+  return out;
+}
+
 void stacked_decode_into(at::Tensor& out, const at::Tensor& idx, const at::Tensor& codes, const at::Tensor& norm,
                          const at::Tensor& tiles, int64_t levels, double weight, bool accumulate) {
   same_device(out, idx, "idx");
@@ -434,6 +485,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode_meta(c
   return {at::empty({k}, x.options().dtype(at::kInt)), at::empty({k}, x.options().dtype(at::kByte)),
           at::empty({1}, x.options().dtype(at::kFloat)), at::empty({n_tiles(n)}, x.options().dtype(at::kInt))};
 }
+at::Tensor stacked_encode_wire_meta(const at::Tensor& x, int64_t k, int64_t, int64_t, int64_t) {
+  return at::empty({(int64_t)flc_stacked_wire_layout(x.numel(), k, nullptr)}, x.options().dtype(at::kByte));
+}
+at::Tensor stacked_fold_wires_meta(const at::Tensor& wires, at::IntArrayRef, at::ArrayRef<double>, int64_t n, int64_t,
+                                   int64_t, const c10::optional<at::Tensor>&, bool) {
+  return at::empty({n}, wires.options().dtype(at::kFloat));
+}
 at::Tensor stacked_decode_meta(const at::Tensor& idx, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                                int64_t n, int64_t, double) {
   return at::empty({n}, idx.options().dtype(at::kFloat));
@@ -489,6 +547,9 @@ TORCH_LIBRARY(flcodec, m) {
   m.def("quant_encode_auto(Tensor x, int kind, int levels, int p=0, int seed=0, int counter=0) "
         "-> (Tensor codes, Tensor norms, Tensor decoded)");
   m.def("adaptive_random(Tensor x, float u) -> (Tensor out, Tensor index, Tensor status)");
+  m.def("stacked_encode_wire(Tensor x, int k, int levels=127, int seed=0, int counter=0) -> Tensor");
+  m.def("stacked_fold_wires(Tensor wires, int[] slots, float[] weights, int n, int k, int levels=127, "
+        "Tensor? out=None, bool accumulate=False) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
@@ -509,6 +570,8 @@ TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
   m.impl("stacked_encode_delta", &stacked_encode_delta);
   m.impl("quant_encode_auto", &quant_encode_auto);
   m.impl("adaptive_random", &adaptive_random);
+  m.impl("stacked_encode_wire", &stacked_encode_wire);
+  m.impl("stacked_fold_wires", &stacked_fold_wires);
 }
 
 TORCH_LIBRARY_IMPL(flcodec, Meta, m) {
@@ -525,4 +588,6 @@ TORCH_LIBRARY_IMPL(flcodec, Meta, m) {
   m.impl("stacked_encode_delta", &stacked_encode_delta_meta);
   m.impl("quant_encode_auto", &quant_encode_auto_meta);
   m.impl("adaptive_random", &adaptive_random_meta);
+  m.impl("stacked_encode_wire", &stacked_encode_wire_meta);
+  m.impl("stacked_fold_wires", &stacked_fold_wires_meta);
 }

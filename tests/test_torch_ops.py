@@ -35,6 +35,9 @@ OPS = {
                             "Tensor tiles)",
     "quant_encode_auto": None,
     "adaptive_random": "flcodec::adaptive_random(Tensor x, float u) -> (Tensor out, Tensor index, Tensor status)",
+    "stacked_encode_wire": "flcodec::stacked_encode_wire(Tensor x, int k, int levels=127, int seed=0, int counter=0) "
+                           "-> Tensor",
+    "stacked_fold_wires": None,
 }
 
 
@@ -247,3 +250,34 @@ def test_round2_ops_match_codec(ops):
     out, ind, st = ops.adaptive_random(x, 0.25)
     exp_out, _, exp_ind = ref.adaptive_random(x.cpu().numpy(), x.numel(), 0.25)
     assert int(st.item()) == 0 and int(ind.item()) == exp_ind and gc.same_bits(out.cpu().numpy(), exp_out)
+
+
+def test_wire_ops_meta_shapes(ops):
+    from fl_sim_amd import codec
+
+    rec = ops.stacked_encode_wire(torch.empty(5000, device="meta"), 50)
+    assert rec.shape == (codec.stacked_wire_layout(5000, 50)[0],) and rec.dtype == torch.uint8
+    out = ops.stacked_fold_wires(torch.empty(3, rec.numel(), dtype=torch.uint8, device="meta"), [2, 0], [0.5, 0.25],
+                                 5000, 50)
+    assert out.shape == (5000,) and out.dtype == torch.float32
+
+
+@pytest.mark.gpu
+def test_wire_ops_match_codec(ops):
+    from fl_sim_amd import codec
+
+    n, k = 300_007, 3_000
+    g = torch.Generator(device="cuda").manual_seed(21)
+    xs = [torch.randn(n, generator=g, device="cuda") * 1e-3 for _ in range(3)]
+    recs = torch.stack([ops.stacked_encode_wire(x, k, 127, 5 + i, 2) for i, x in enumerate(xs)])
+    stride = recs.shape[1]
+    ref_recs = torch.empty(3, stride, dtype=torch.uint8, device="cuda")
+    for i, x in enumerate(xs):
+        codec.stacked_encode(x, k, 127, seed=5 + i, counter=2, wire=ref_recs[i])
+    for i in range(3):  # the payload bytes (padding is never written)
+        a, b = codec.wire_packet(recs[i], n, k), codec.wire_packet(ref_recs[i], n, k)
+        assert torch.equal(a.idx, b.idx) and torch.equal(a.codes[:k], b.codes[:k]) and torch.equal(a.tiles, b.tiles)
+        assert torch.equal(a.norm, b.norm)
+    got = ops.stacked_fold_wires(recs, [1, 2, 0], [0.25, 0.5, 0.125], n, k)
+    exp = codec.stacked_fold_wires(ref_recs, [1, 2, 0], [0.25, 0.5, 0.125], n, k)
+    assert torch.equal(got.view(torch.int32), exp.view(torch.int32))
