@@ -42,7 +42,8 @@ enum flc_status {
   FLC_EINVAL = 1,       /* bad argument (sizes, levels, bits, null pointer) */
   FLC_EHIP = 2,         /* HIP runtime error */
   FLC_EWORKSPACE = 3,   /* workspace too small */
-  FLC_EUNSUPPORTED = 4  /* valid request this build does not implement */
+  FLC_EUNSUPPORTED = 4, /* valid request this build does not implement */
+  FLC_ECOMM = 5         /* RCCL error, or RCCL could not be loaded */
 };
 
 /* dense quantizer families (compressors.py:327-404) */
@@ -195,6 +196,25 @@ size_t flc_stacked_wire_layout(int64_t n, int64_t k, int64_t* offsets);
  * the number of GPUs. */
 int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slots, const float* weights,
                            int n_wires, int64_t n, int64_t k, int levels, int accumulate, float* out, void* stream);
+
+/* ------------------------------------------------------------------ multi-GPU exchange (RCCL over xGMI)
+ * For callers outside torch; one process per GPU.  RCCL is the NCCL API on ROCm, loaded
+ * on first use (librccl.so.1; inside a torch process, torch's own).  The round's exchange is either
+ *   flc_rccl_reduce: sum of the ranks' fp32 partial sums to `root` (the dense round; the cross-rank summation order is
+ *     RCCL's, so the result matches one device to 1e-6 * sum|w_i d_i|), or
+ *   flc_rccl_allgather: every rank's block of packed wire records to every rank (recv = nranks * bytes_per_rank, rank
+ *     order), then flc_stacked_fold_wires over all clients in client order (bit-identical to one device at any N).
+ * flc_comm_unique_id on one rank, its flc_comm_id_bytes() bytes shipped to the others out of band, then
+ * flc_comm_init on every rank (collective; `device` >= 0 selects the HIP device first).  Collectives are
+ * stream-ordered and asynchronous like every other call. */
+size_t flc_comm_id_bytes(void);
+int flc_comm_unique_id(void* id_out);
+int flc_comm_init(const void* id, int nranks, int rank, int device, void** comm_out);
+int flc_comm_size(void* comm, int* nranks, int* rank);
+int flc_comm_destroy(void* comm);
+int flc_rccl_reduce(const float* send, float* recv, int64_t n, int root, void* comm, void* stream);
+int flc_rccl_allreduce(const float* send, float* recv, int64_t n, void* comm, void* stream);
+int flc_rccl_allgather(const void* send, void* recv, int64_t bytes_per_rank, void* comm, void* stream);
 
 /* ------------------------------------------------------------------ adaptive random compressor
  * (compressors.py:297-301): ind = np.random.choice(np.arange(n), size=1, p=|x| / sum|x|); out = 0,

@@ -112,3 +112,22 @@ def test_stacked_encode_delta_validates_without_gpu():
                                       1 << 30, None)
     assert rc == 1 and "0 < k < n" in lib.flc_last_error().decode()
     assert lib.flc_stacked_encode_delta_workspace_size(1000, 10, 8) > lib.flc_topk_workspace_size(1000, 10)
+
+
+def test_rccl_entries_validate_without_gpu():
+    """The RCCL entries (flc_comm_* / flc_rccl_*) check their arguments before RCCL is touched; the unique id is
+    RCCL's 128 bytes."""
+    import ctypes
+
+    lib = _lib.load()
+    assert _lib.size("flc_comm_id_bytes") == 128
+    h = ctypes.c_void_p()
+    assert lib.flc_comm_init(None, 1, 0, -1, ctypes.byref(h)) == 1
+    uid = ctypes.create_string_buffer(128)
+    assert lib.flc_comm_init(ctypes.cast(uid, ctypes.c_void_p), 2, 2, -1, ctypes.byref(h)) == 1  # rank >= nranks
+    n, r = ctypes.c_int(), ctypes.c_int()
+    assert lib.flc_comm_size(None, ctypes.byref(n), ctypes.byref(r)) == 1
+    assert lib.flc_rccl_reduce(None, None, 5, 0, None, None) == 1
+    assert lib.flc_rccl_allreduce(None, None, 5, None, None) == 1
+    assert lib.flc_rccl_allgather(None, None, 0, None, None) == 1
+    assert lib.flc_comm_destroy(None) == 0  # destroying nothing is a no-op
