@@ -58,7 +58,8 @@ def test_encode_into_record_equals_plain_packet(n, k):
     assert np.array_equal(_bits(out_a), _bits(out_b))
 
 
-@pytest.mark.parametrize("n,k,m", [(4099, 41, 1), (4099, 41, 3), (1_000_003, 10_000, 8), (65_536, 655, 70)])
+@pytest.mark.parametrize("n,k,m", [(5, 2, 3), (1023, 10, 2), (4099, 41, 1), (4099, 41, 3), (1_000_003, 10_000, 8),
+                                   (65_536, 655, 70)])
 def test_fold_wires_equals_sequential_decode_accumulate(n, k, m):
     xs = [_x(n, 10 + i, zeros=bool(i % 2)) for i in range(m)]
     recs = _records(xs, k, seeds=list(range(m)))
@@ -115,3 +116,11 @@ def test_fold_wires_nonfinite_weight_takes_every_fma():
         exp = _fold_ref(recs, [0, 1, 2], weights, n, k, torch.zeros(n, device="cuda"))
         got = codec.stacked_fold_wires(recs, [0, 1, 2], weights, n, k)
         assert np.array_equal(_bits(got), _bits(exp))
+
+
+def test_fold_wires_flat_buffer_equals_2d():
+    n, k = 50_001, 500
+    recs = _records([_x(n, 60 + i) for i in range(3)], k, seeds=[4, 5, 6])
+    a = codec.stacked_fold_wires(recs, [2, 1, 0], [0.5, 0.25, 0.125], n, k)
+    b = codec.stacked_fold_wires(recs.reshape(-1), [2, 1, 0], [0.5, 0.25, 0.125], n, k)
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
