@@ -1630,6 +1630,9 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   const bool fast_ok = nrm_ok && levels <= 127;
   const float rs = fast_ok ? (float)levels / nrm : 0.0f;
   auto code_of = [&](const unsigned raw, const unsigned id, const bool have, const unsigned rw) -> unsigned {
+#if FLC_CALIB_NOCODE  // calibration builds only: results invalid
+    return (raw >> 24) ^ rw;
+#endif
     const float v = __uint_as_float(raw);
 #if FLC_CALIB_NOPHILOX  // calibration builds only (tools/calib_select.sh): results invalid
     const uint32_t r = 0x80000000u;
