@@ -347,6 +347,22 @@ def main():
                 "algorithmic_bytes": kernel_bytes["stacked_decode"],
             }
     if not args.skip_extra:
+        # SURVEY §8(d)'s "realistic" variant of the headline input: 5 % exact zeros (the dithering's zero path,
+        # zeros among the candidates); same step, same bytes formula
+        xz = x.clone()
+        xz[torch.rand(D, generator=gen, device=dev) < 0.05] = 0.0
+        cz = [0]
+
+        def step_z():
+            cz[0] += 1
+            pkt = codec.stacked_encode(xz, K, LEVELS, seed=rank, counter=cz[0])
+            codec.stacked_decode(pkt, out=out)
+
+        msz, _ = timed(step_z, args.steps, args.warmup, world)
+        msz = max_over_ranks(msz, world)
+        extra["headline_5pct_zeros"] = {"ms_per_step": round(msz, 5),
+                                        "GB_s": round(world * stacked_bytes(D, K) / (msz * 1e-3) / 1e9, 1)}
+        del xz
         # host-resident path (north_star: client state lives on the CPU simulator): pinned host delta ->
         # H2D -> encode + decode -> D2H of the dense decoded vector; PCIe-bound, never `value`
         hx = torch.empty(D, dtype=torch.float32, pin_memory=True)
