@@ -103,7 +103,9 @@ static_assert(sizeof(EncState) <= 128, "state block");
 
 struct EncWs {
   char* base;
-  int64_t M;  // elements per block range (multiple of kBlockStep)
+  int64_t M;      // elements per block range (multiple of kBlockStep)
+  size_t off_ovf; // byte offset of the candidate overflow area: per block 2 * ovf words (keys, then indices)
+  unsigned ovf;   // candidates per block kept in HBM beyond the LDS's kCap (0: none)
   __device__ EncState* st() const { return reinterpret_cast<EncState*>(base + kOffSt); }
   __device__ unsigned* flags() const { return reinterpret_cast<unsigned*>(base + kOffFlags); }
   __device__ unsigned* hist() const { return reinterpret_cast<unsigned*>(base + kOffHist); }
@@ -118,6 +120,10 @@ struct EncWs {
     return reinterpret_cast<unsigned*>(base + kOffStage) + (size_t)b * 2 * kCap;
   }
   __device__ unsigned* stage_idx(int b) const { return stage_key(b) + kCap; }
+  __device__ unsigned* ovf_key(int b) const {
+    return reinterpret_cast<unsigned*>(base + off_ovf) + (size_t)b * 2 * ovf;
+  }
+  __device__ unsigned* ovf_idx(int b) const { return ovf_key(b) + ovf; }
 };
 
 struct EncGeom {
@@ -152,12 +158,29 @@ SampleSetup sample_setup(int64_t n, int64_t k) {
   return s;
 }
 
-EncWs carve_enc(void* ws, int64_t n, int cus, size_t* need) {
+// Candidates beyond a block's LDS (kCap) go to an HBM overflow area sized from the expected count: the floor
+// admits about rank_lo / S of the elements, so a block holds ~(rank_lo / S) * M candidates; twice that (for skew)
+// beyond kCap, capped at kMaxOvf.  Blocks past kCap + ovf re-read their range instead (x-mode).  At k = 1 % the
+// area is empty up to 1 GiB inputs (M = 1 Mi: ~13 K candidates per block) and lets 2-8 GiB inputs keep their
+// candidates instead of re-reading x.
+constexpr int64_t kMaxOvf = 1ll << 17;
+SampleSetup sample_setup(int64_t n, int64_t k);
+unsigned ovf_capacity(int64_t n, int64_t k, int64_t M) {
+  const SampleSetup ss = sample_setup(n, k);
+  const double frac = ss.take_all ? 1.0 : std::min(1.0, (double)ss.rank_lo / (double)ss.S);
+  int64_t want = (int64_t)std::ceil(2.0 * frac * (double)M) + 4096 - kCap;
+  want = std::min<int64_t>(std::min<int64_t>(want, kMaxOvf), M);
+  return want > 0 ? (unsigned)align_up((size_t)want, 64) : 0u;
+}
+
+EncWs carve_enc(void* ws, int64_t n, int64_t k, int cus, size_t* need) {
   EncWs w;
   w.base = static_cast<char*>(ws);
   const EncGeom g = enc_geometry(n, cus);
   w.M = g.M;
-  *need = kOffStage + (size_t)g.G * kCap * 8;
+  w.ovf = ovf_capacity(n, k, g.M);
+  w.off_ovf = al256(kOffStage + (size_t)g.G * kCap * 8);
+  *need = w.off_ovf + (size_t)g.G * w.ovf * 8;
   return w;
 }
 constexpr int kZeroWords = kMaxSlots * kHistStride + 16;  // hist + acc, as 32-bit words
@@ -606,6 +629,9 @@ __device__ __forceinline__ unsigned step_count(const Step& v, float tf, int lim,
 struct FilterCtx {
   unsigned* s_key;
   unsigned* s_idx;
+  unsigned* g_key;  // the block's HBM overflow (candidates kCap .. kCap + gcap - 1)
+  unsigned* g_idx;
+  unsigned gcap;
   unsigned* s_hist;
   unsigned t_lo;
   unsigned long long width0;  // t_hi - t_lo
@@ -616,13 +642,17 @@ struct FilterCtx {
 
 // a candidate into the block's LDS arrays; the band histogram, above count and max key of the stored
 // candidates are formed after the pass in one dense sweep over LDS (every lane busy), only candidates
-// beyond the LDS capacity (never stored) are binned here
+// beyond the LDS capacity are binned here (and kept in the HBM overflow while it has room)
 __device__ __forceinline__ void emit(FilterCtx& c, unsigned p, unsigned e, float v) {
   const unsigned raw = __float_as_uint(v);
   if (p < (unsigned)kCap) {
     c.s_key[p] = raw;
     c.s_idx[p] = e;
   } else {
+    if (p - (unsigned)kCap < c.gcap) {
+      c.g_key[p - kCap] = raw;
+      c.g_idx[p - kCap] = e;
+    }
     const unsigned key = order_key(raw);
     const unsigned long long rel = (unsigned long long)(key - c.t_lo);
     if (rel >= c.width0) ++c.above;
@@ -845,18 +875,24 @@ template <class Src>
 struct CandSrc {
   const unsigned* s_key;
   const unsigned* s_idx;
+  unsigned* g_key;  // the HBM overflow: candidates kCap.. (gmode)
+  unsigned* g_idx;
   Src x;
   int64_t b0;
   bool xmode;
+  bool gmode;       // more candidates than LDS holds, all of them in LDS + the overflow
 };
 template <class Src>
 __device__ __forceinline__ void cand_get(const CandSrc<Src>& c, unsigned p, unsigned& raw, unsigned& id) {
   if (c.xmode) {
     raw = __float_as_uint(c.x.get(c.b0 + p));
     id = (unsigned)(c.b0 + p);
-  } else {
+  } else if (!c.gmode || p < (unsigned)kCap) {
     raw = c.s_key[p];
     id = c.s_idx[p];
+  } else {  // (written by this block's waves in the filter pass, before the exchange that followed it)
+    raw = ld_mem(c.g_key + (p - kCap));
+    id = ld_mem(c.g_idx + (p - kCap));
   }
 }
 
@@ -980,6 +1016,9 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   FilterCtx fc;
   fc.s_key = s_key;
   fc.s_idx = s_idx;
+  fc.gcap = STAGE ? 0u : w.ovf;  // (the split path stages LDS only)
+  fc.g_key = w.ovf_key(blockIdx.x);
+  fc.g_idx = w.ovf_idx(blockIdx.x);
   fc.s_hist = s_hist;
   fc.t_lo = t_lo;
   fc.width0 = t_hi - t_lo;
@@ -1214,7 +1253,11 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   src.s_idx = s_idx;
   src.x = x;
   src.b0 = b0;
-  src.xmode = fb || C_b > (unsigned)kCap;  // block-uniform
+  src.g_key = w.ovf_key(blockIdx.x);
+  src.g_idx = w.ovf_idx(blockIdx.x);
+  const unsigned gcap = FUSED ? w.ovf : 0u;
+  src.xmode = fb || C_b > (unsigned)kCap + gcap;  // block-uniform
+  src.gmode = !src.xmode && C_b > (unsigned)kCap;
   const unsigned ncand = src.xmode ? (unsigned)(b1 - b0) : C_b;
 
   auto flush = [&](int sl, unsigned above_t, unsigned mk_t) {
@@ -1307,7 +1350,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
         }
       }
     };
-    if (!src.xmode) {
+    if (!src.xmode && !src.gmode) {
       // LDS candidates: 4 rounds of reads at clamped indices issued together, then scanned
       const unsigned wq0 = (unsigned)__builtin_amdgcn_readfirstlane((int)cq0);
       const unsigned wq1 = (unsigned)__builtin_amdgcn_readfirstlane((int)cq1);
@@ -1671,7 +1714,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     }
   };
   const unsigned plast = q1 > 0u ? q1 - 1u : 0u;
-  if (!src.xmode) {
+  if (!src.xmode && !src.gmode) {
     // LDS candidates: pass 2 touches no memory but LDS and the Philox words.  Kept entries are staged in
     // place, wave range order (a kept entry's slot q0 + (kept before it in the range) <= its own index, and
     // the next round's candidates, read before this round's slots are written, lie past them), then
@@ -1752,7 +1795,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
       if (tile_owner) tiles_of(v, id, pos);
     }
   } else {
-    // x-mode (fallback, or more candidates than LDS holds): candidates from x, writes in the loop
+    // x-mode (fallback, or more candidates than LDS + the HBM overflow hold: candidates from x) and g-mode (LDS +
+    // overflow): candidates through cand_get, writes in the loop
     unsigned rq[kRnd];
 #pragma unroll
     for (int j = 0; j < kRnd; ++j) rq[j] = 0u;
@@ -1850,7 +1894,7 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
   int dev = 0;
   const int cus = current_cus(&dev);
   size_t need = 0;
-  EncWs w = carve_enc(ws, n, cus, &need);
+  EncWs w = carve_enc(ws, n, k, cus, &need);
   if (!ws || need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
   const EncGeom g = enc_geometry(n, cus);
   const SampleSetup ss = sample_setup(n, k);
@@ -1908,9 +1952,8 @@ using namespace flc;
 extern "C" {
 
 size_t flc_topk_workspace_size(int64_t n, int64_t k) {
-  (void)k;
   size_t need = 0;
-  (void)carve_enc(nullptr, n < 1 ? 1 : n, current_cus(nullptr), &need);
+  (void)carve_enc(nullptr, n < 1 ? 1 : n, k < 1 ? 1 : k, current_cus(nullptr), &need);
   return need;
 }
 

@@ -455,6 +455,28 @@ def test_stacked_full_size_1gib_vs_oracle():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("n,frac", [(33_554_439, 0.15), (20_000_011, 0.30)])
+def test_encode_hbm_overflow_vs_oracle(n, frac):
+    """More candidates per block than its LDS holds (kCap = 16384): the blocks keep the rest in the workspace's HBM
+    overflow (g-mode) instead of re-reading x — n = 32 M at k = 15 % (~20 K candidates per block) and 20 M at
+    k = 30 % (~24 K).  Top-k and stacked encodes against the oracle, bit for bit."""
+    codec = _codec()
+    k = int(n * frac)
+    x = (np.random.default_rng(31).standard_normal(n, dtype=np.float32) * np.float32(1e-3)).astype(np.float32)
+    xd = torch.from_numpy(x).to(DEV)
+    idx, val, tiles = codec.topk_encode(xd, k, with_tiles=True)
+    exp_idx, exp_val = ref.topk_kept_select(x, k)
+    assert np.array_equal(idx.cpu().numpy().astype(np.int64), exp_idx)
+    assert gc.same_bits(val.cpu().numpy(), exp_val)
+    pkt = codec.stacked_encode(xd, k, 127, seed=4, counter=8)
+    _, e_idx, e_codes, pn = ref.stacked(x, k, 127, lambda i: ref.philox_uniforms_at(i, 4, 8), fast=True)
+    assert np.array_equal(pkt.idx.cpu().numpy().astype(np.int64), e_idx)
+    assert np.array_equal(pkt.codes[:k].cpu().numpy(), e_codes)
+    assert pkt.norm.item() == float(pn)
+    del xd, pkt
+    torch.cuda.empty_cache()
+
+
 def test_stacked_encode_two_streams():
     """Selects on two streams at once (each with its own workspace) are serialised by the library's gate
     (first switch drains the device, then an event chain); results equal the single-stream ones."""
