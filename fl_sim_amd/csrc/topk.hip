@@ -643,9 +643,11 @@ struct FilterCtx {
 // a candidate into the block's LDS arrays; the band histogram, above count and max key of the stored
 // candidates are formed after the pass in one dense sweep over LDS (every lane busy), only candidates
 // beyond the LDS capacity are binned here (and kept in the HBM overflow while it has room)
+// (OVF = false: the caller has checked that the whole step lands below kCap — the hot path, LDS stores only)
+template <bool OVF>
 __device__ __forceinline__ void emit(FilterCtx& c, unsigned p, unsigned e, float v) {
   const unsigned raw = __float_as_uint(v);
-  if (p < (unsigned)kCap) {
+  if (!OVF || p < (unsigned)kCap) {
     c.s_key[p] = raw;
     c.s_idx[p] = e;
   } else {
@@ -662,7 +664,7 @@ __device__ __forceinline__ void emit(FilterCtx& c, unsigned p, unsigned e, float
 }
 
 // ordered append from position `pos` (within a q: lane-major, then the 4 components)
-template <bool FULL, class Step, int SF>
+template <bool FULL, class Step, int SF, bool OVF>
 __device__ __forceinline__ void step_write(const Step& st, float tf, int lim, int lane, unsigned wbu,
                                            unsigned pos, FilterCtx& c) {
 #pragma unroll
@@ -679,10 +681,10 @@ __device__ __forceinline__ void step_write(const Step& st, float tf, int lim, in
       p = __builtin_amdgcn_mbcnt_hi((unsigned)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m3, p));
       if (f0 | f1 | f2 | f3) {
         const unsigned e = wbu + (unsigned)(256 * q + 4 * lane);
-        if (f0) { emit(c, p, e + 0u, vq.x); ++p; }
-        if (f1) { emit(c, p, e + 1u, vq.y); ++p; }
-        if (f2) { emit(c, p, e + 2u, vq.z); ++p; }
-        if (f3) emit(c, p, e + 3u, vq.w);
+        if (f0) { emit<OVF>(c, p, e + 0u, vq.x); ++p; }
+        if (f1) { emit<OVF>(c, p, e + 1u, vq.y); ++p; }
+        if (f2) { emit<OVF>(c, p, e + 2u, vq.z); ++p; }
+        if (f3) emit<OVF>(c, p, e + 3u, vq.w);
       }
       pos += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
     }
@@ -710,7 +712,12 @@ __device__ __forceinline__ void step_process(const Step& v, int64_t wb, int64_t 
   // stops the compiler from reusing the count pass's compares)
   float tf2 = tf;
   asm volatile("" : "+v"(tf2));
-  if (cnt != 0u) step_write<FULL, Step, SF>(v, tf2, lim, lane, (unsigned)wb, base + pre, c);
+  if (cnt != 0u) {
+    if (base + tot <= (unsigned)kCap)  // (block-uniform) the step lands in LDS: no overflow code on the hot path
+      step_write<FULL, Step, SF, false>(v, tf2, lim, lane, (unsigned)wb, base + pre, c);
+    else
+      step_write<FULL, Step, SF, true>(v, tf2, lim, lane, (unsigned)wb, base + pre, c);
+  }
   base += tot;
 }
 
