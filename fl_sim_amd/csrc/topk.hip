@@ -638,7 +638,17 @@ struct FilterCtx {
   int sh0;
   unsigned above;         // per thread: candidates >= t_hi
   unsigned mk;            // per thread: max candidate key
+  unsigned swept;         // (block-uniform) LDS candidates [0, swept) already in the band histogram
 };
+
+// one LDS candidate into the band histogram / above count / max key
+__device__ __forceinline__ void band_bin(FilterCtx& c, unsigned p) {
+  const unsigned key = order_key(c.s_key[p]);
+  const unsigned long long rel = (unsigned long long)(key - c.t_lo);
+  if (rel >= c.width0) ++c.above;
+  else atomicAdd(&c.s_hist[(unsigned)(rel >> c.sh0)], 1u);
+  c.mk = key > c.mk ? key : c.mk;
+}
 
 // a candidate into the block's LDS arrays; the band histogram, above count and max key of the stored
 // candidates are formed after the pass in one dense sweep over LDS (every lane busy), only candidates
@@ -701,6 +711,14 @@ __device__ __forceinline__ void step_process(const Step& v, int64_t wb, int64_t 
   const unsigned cnt = step_count<FULL, Step, SF>(v, tf, lim, lane);
   if (lane == 0) s_wc[par][wid] = cnt;
   lds_barrier();
+#if !FLC_BAND_AFTER_PASS
+  {  // the band histogram of the earlier steps' LDS candidates (their writes are visible after this barrier),
+     // binned while this step's loads are in flight: the post-pass sweep is left with the last step's
+    const unsigned s1 = base < (unsigned)kCap ? base : (unsigned)kCap;
+    for (unsigned p = c.swept + threadIdx.x; p < s1; p += kET) band_bin(c, p);
+    c.swept = s1;
+  }
+#endif
   unsigned pre = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < kENW; ++w) {
@@ -1032,6 +1050,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   fc.sh0 = range_shift(fc.width0, kHistBits);
   fc.above = 0;
   fc.mk = 0;
+  fc.swept = 0;
   unsigned base = 0;
   {
     // full block steps in a two-deep software pipeline; every load in the loop body is unconditional
@@ -1074,13 +1093,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   BLKT(1);
   {  // band histogram / above / max of the stored candidates
     const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
-    for (unsigned p = tid; p < nst; p += kET) {
-      const unsigned key = order_key(s_key[p]);
-      const unsigned long long rel = (unsigned long long)(key - fc.t_lo);
-      if (rel >= fc.width0) ++fc.above;
-      else atomicAdd(&s_hist[(unsigned)(rel >> fc.sh0)], 1u);
-      fc.mk = key > fc.mk ? key : fc.mk;
-    }
+    for (unsigned p = fc.swept + tid; p < nst; p += kET) band_bin(fc, p);
     __syncthreads();
   }
 
