@@ -38,6 +38,12 @@ for it in range(int(os.environ.get("ITERS", "12"))):
             prev = t[i]
     print(" | ".join(parts), f"| total {(max(t[14], t[15]) - t[0]) * 10 / 1000:.1f} us")
     ws[STAMP_OFF:STAMP_OFF + 16 * 8].zero_()
+    if os.environ.get("XCD_EVERY"):  # per-call mean pass duration per XCD (blockIdx % 8), and the max block
+        bt = ws[BLKT_OFF:BLKT_OFF + 256 * 32].cpu().numpy().view(np.uint64).astype(np.int64).reshape(256, 4)
+        G = int((bt[:, 0] > 0).sum())
+        d = (bt[:G, 1] - bt[:G, 0]) * 10 / 1000
+        print("xcd means", [round(float(d[np.arange(G) % 8 == i].mean()), 1) for i in range(8)],
+              "median", round(float(np.median(d)), 1), "max", round(float(d.max()), 1), "argmax", int(d.argmax()))
     if it == int(os.environ.get("ITERS", "12")) - 1:  # per-block filter times (start of the HBM pass, its end, end of the kernel)
         bt = ws[BLKT_OFF:BLKT_OFF + 256 * 32].cpu().numpy().view(np.uint64).astype(np.int64).reshape(256, 4)
         G = int((bt[:, 0] > 0).sum())
