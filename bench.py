@@ -618,6 +618,20 @@ def main():
         ms4w = max_over_ranks(ms4w, world)
         per4 = -(-n_cl4 // world)
         line4["wire_ms_per_step"] = round(ms4w, 4)
+        if len(mine) > 1:
+            # the same round with one encode launch per client instead of the rank's clients in one batched launch
+            # (flc_stacked_encode_batch: each client's select on its share of the CUs)
+            class _OneByOne:
+                stride, n = wc4.stride, wc4.n
+                encode_into, fold = wc4.encode_into, wc4.fold
+
+            def step4w1():
+                c4[0] += 1
+                wc4.counter = c4[0]
+                fdist.aggregate_round_wire([X3] * len(mine), w_all, n_cl4, _OneByOne, out=acc, dst=0, device=dev)
+
+            ms4w1, _ = timed(step4w1, 10, 3, world)
+            line4["wire_ms_per_step_one_launch_per_client"] = round(max_over_ranks(ms4w1, world), 4)
         line4["wire_record_bytes"] = wc4.stride
         line4["wire_gather_bytes_per_rank"] = per4 * wc4.stride
         line4["wire_bytes_formula"] = ("codec: n_local * (4 * D + 5 * K + tiles) written as records; all_gather: "

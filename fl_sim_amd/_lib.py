@@ -75,6 +75,12 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_int, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
          c_void_p, c_void_p, c_size_t, c_void_p],
     ),
+    "flc_stacked_encode_batch_workspace_size": (c_size_t, [c_int64, c_int64, c_int]),
+    "flc_stacked_encode_batch": (
+        c_int,
+        [c_void_p, c_int, c_int64, c_int64, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_size_t, c_void_p],
+    ),
     "flc_stacked_decode": (
         c_int,
         [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p, c_size_t, c_void_p],
@@ -149,6 +155,8 @@ def load() -> ctypes.CDLL:
             )
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("FLC_LIB") and not hasattr(lib, name):
+                continue  # (a calibration build of an older revision, A/B runs only: its missing entries stay unbound)
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

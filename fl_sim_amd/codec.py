@@ -199,19 +199,23 @@ def natural_decode(codes: torch.Tensor, n: int, out: Optional[torch.Tensor] = No
 # (one host synchronisation per call) and raise if a call lost co-residency (include/flcodec.h)
 TOPK_CHECK = os.environ.get("FLC_TOPK_CHECK", "0") not in ("", "0")
 TOPK_ERRORS = {1: "digit not found", 2: "count mismatch", 4: "exchange spin timeout"}
+_TOPK_KINDS = ("topk", "topk_batch")  # single-client and batched encoder workspaces (never shared)
 
 
 def topk_status(device: Optional[torch.device] = None, reset: bool = True) -> int:
     """The sticky error word of the top-k workspace of ``device``'s current stream (0 = every encode since
     the last reset was exact).  Synchronises that stream."""
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
-    key = (device.index if device.index is not None else torch.cuda.current_device(), _stream(device), "topk")
-    ws = _WS.get(key)
-    if ws is None:
-        return 0
-    out = torch.empty(1, dtype=torch.int64, device=device)
-    call("flc_topk_status", _p(ws), _p(out), int(reset), _stream(device))
-    return int(out.item())
+    err = 0
+    for kind in _TOPK_KINDS:
+        key = (device.index if device.index is not None else torch.cuda.current_device(), _stream(device), kind)
+        ws = _WS.get(key)
+        if ws is None:
+            continue
+        out = torch.empty(1, dtype=torch.int64, device=device)
+        call("flc_topk_status", _p(ws), _p(out), int(reset), _stream(device))
+        err |= int(out.item())
+    return err
 
 
 def topk_status_all(reset: bool = True) -> Dict[Tuple[int, int], int]:
@@ -219,13 +223,13 @@ def topk_status_all(reset: bool = True) -> Dict[Tuple[int, int], int]:
     reads on its current stream (the stream a workspace was used on may be gone)."""
     res: Dict[Tuple[int, int], int] = {}
     for (dev, stream, kind), ws in list(_WS.items()):
-        if kind != "topk":
+        if kind not in _TOPK_KINDS:
             continue
         d = torch.device("cuda", dev)
         torch.cuda.synchronize(d)
         out = torch.empty(1, dtype=torch.int64, device=d)
         call("flc_topk_status", _p(ws), _p(out), int(reset), _stream(d))
-        res[(dev, stream)] = int(out.item())
+        res[(dev, stream)] = res.get((dev, stream), 0) | int(out.item())
     return res
 
 
@@ -344,6 +348,46 @@ def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, co
          _p(tiles), _p(ws), ws.numel(), _stream(x.device))
     _after_encode(x.device)
     return StackedPacket(idx, codes, norm, n, levels, tiles)
+
+
+def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, seeds: Sequence[int] = (),
+                         counter: int = 0, with_tiles: bool = True,
+                         wires: Optional[Sequence[torch.Tensor]] = None) -> List[StackedPacket]:
+    """The stacked encode of many clients' flat deltas (all of one size) in one launch (flc_stacked_encode_batch):
+    packet c equals ``stacked_encode(xs[c], k, levels, seeds[c], counter)`` bit for bit.  ``wires``: one packed wire
+    record per client to write into (the packets are then views of them)."""
+    import ctypes
+
+    xs = [_dev_f32(x).reshape(-1) for x in xs]
+    if not xs:
+        return []
+    n, dev = xs[0].numel(), xs[0].device
+    if any(x.numel() != n or x.device != dev for x in xs):
+        raise ValueError("a batched encode takes clients of one size on one device")
+    C = len(xs)
+    seeds = list(seeds) if len(seeds) else [0] * C
+    if len(seeds) != C:
+        raise ValueError("one seed per client")
+    if wires is not None:
+        if len(wires) != C:
+            raise ValueError("one wire record per client")
+        pks = [wire_packet(r, n, k, levels) for r in wires]
+    else:
+        pks = [StackedPacket(torch.empty(k, dtype=torch.int32, device=dev),
+                             torch.empty(max(k, 16), dtype=torch.uint8, device=dev),
+                             torch.empty(1, dtype=torch.float32, device=dev), n, levels,
+                             _tiles(n, dev) if with_tiles else None) for _ in range(C)]
+    arr = lambda vals: (ctypes.c_void_p * C)(*vals)  # noqa: E731
+    ws = workspace(dev, _lib.size("flc_stacked_encode_batch_workspace_size", n, k, C), "topk_batch")
+    call("flc_stacked_encode_batch", ctypes.cast(arr([x.data_ptr() for x in xs]), ctypes.c_void_p), C, n, k, levels,
+         ctypes.cast((ctypes.c_uint64 * C)(*[int(s) for s in seeds]), ctypes.c_void_p), counter,
+         ctypes.cast(arr([p.idx.data_ptr() for p in pks]), ctypes.c_void_p),
+         ctypes.cast(arr([p.codes.data_ptr() for p in pks]), ctypes.c_void_p),
+         ctypes.cast(arr([p.norm.data_ptr() for p in pks]), ctypes.c_void_p),
+         ctypes.cast(arr([p.tiles.data_ptr() for p in pks]), ctypes.c_void_p) if pks[0].tiles is not None else None,
+         _p(ws), ws.numel(), _stream(dev))
+    _after_encode(dev)
+    return pks
 
 
 def stacked_encode_delta(local_params: Sequence[torch.Tensor], global_params: Sequence[torch.Tensor], k: int,

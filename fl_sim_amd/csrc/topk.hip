@@ -101,11 +101,19 @@ constexpr size_t kOffStage = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // + G *
 static_assert(kOffAcc % 8 == 0, "acc words are 64-bit");
 static_assert(sizeof(EncState) <= 128, "state block");
 
+// A batched call (flc_stacked_encode_batch) runs one independent select per client in one launch: client g owns
+// blocks [g * nb, (g + 1) * nb) and its own header (st ... blkC, at base + g * kOffStage) and staging / overflow
+// area (at var + g * vstride); `bid` / `nb` are the block's index and the block count of its own select (for a
+// single call: blockIdx.x and gridDim.x).  Every select ORs its error bits into `errp` (group 0's word).
 struct EncWs {
-  char* base;
+  char* base;     // the header (fixed offsets kOffSt .. kOffStage)
+  char* var;      // staging area, then the overflow area
   int64_t M;      // elements per block range (multiple of kBlockStep)
-  size_t off_ovf; // byte offset of the candidate overflow area: per block 2 * ovf words (keys, then indices)
+  size_t off_ovf; // byte offset from `var` of the candidate overflow area: per block 2 * ovf words (keys, indices)
   unsigned ovf;   // candidates per block kept in HBM beyond the LDS's kCap (0: none)
+  int bid, nb;    // this block's index in its select, the blocks of its select (set in the kernel prologue)
+  size_t vstride; // batched: bytes between two clients' staging / overflow areas
+  unsigned long long* errp;
   __device__ EncState* st() const { return reinterpret_cast<EncState*>(base + kOffSt); }
   __device__ unsigned* flags() const { return reinterpret_cast<unsigned*>(base + kOffFlags); }
   __device__ unsigned* hist() const { return reinterpret_cast<unsigned*>(base + kOffHist); }
@@ -116,12 +124,10 @@ struct EncWs {
   __device__ unsigned* sample() const { return reinterpret_cast<unsigned*>(base + kOffSample); }
   __device__ unsigned* inbin() const { return reinterpret_cast<unsigned*>(base + kOffInbin); }
   __device__ unsigned* blk_c() const { return reinterpret_cast<unsigned*>(base + kOffBlkC); }  // candidates / block
-  __device__ unsigned* stage_key(int b) const {
-    return reinterpret_cast<unsigned*>(base + kOffStage) + (size_t)b * 2 * kCap;
-  }
+  __device__ unsigned* stage_key(int b) const { return reinterpret_cast<unsigned*>(var) + (size_t)b * 2 * kCap; }
   __device__ unsigned* stage_idx(int b) const { return stage_key(b) + kCap; }
   __device__ unsigned* ovf_key(int b) const {
-    return reinterpret_cast<unsigned*>(base + off_ovf) + (size_t)b * 2 * ovf;
+    return reinterpret_cast<unsigned*>(var + off_ovf) + (size_t)b * 2 * ovf;
   }
   __device__ unsigned* ovf_idx(int b) const { return ovf_key(b) + ovf; }
 };
@@ -173,14 +179,29 @@ unsigned ovf_capacity(int64_t n, int64_t k, int64_t M) {
   return want > 0 ? (unsigned)align_up((size_t)want, 64) : 0u;
 }
 
+// staging + overflow bytes of one select over n elements with `cus` blocks at most
+size_t enc_var_bytes(int64_t n, int64_t k, int cus, EncGeom* geo, unsigned* ovf, size_t* off_ovf) {
+  const EncGeom g = enc_geometry(n, cus);
+  const unsigned o = ovf_capacity(n, k, g.M);
+  const size_t oo = al256((size_t)g.G * kCap * 8);
+  if (geo) *geo = g;
+  if (ovf) *ovf = o;
+  if (off_ovf) *off_ovf = oo;
+  return al256(oo + (size_t)g.G * o * 8);
+}
+
 EncWs carve_enc(void* ws, int64_t n, int64_t k, int cus, size_t* need) {
   EncWs w;
   w.base = static_cast<char*>(ws);
-  const EncGeom g = enc_geometry(n, cus);
+  w.var = w.base + kOffStage;
+  EncGeom g;
+  const size_t vb = enc_var_bytes(n, k, cus, &g, &w.ovf, &w.off_ovf);
   w.M = g.M;
-  w.ovf = ovf_capacity(n, k, g.M);
-  w.off_ovf = al256(kOffStage + (size_t)g.G * kCap * 8);
-  *need = w.off_ovf + (size_t)g.G * w.ovf * 8;
+  w.bid = 0;
+  w.nb = g.G;
+  w.vstride = 0;
+  w.errp = reinterpret_cast<unsigned long long*>(w.base + kOffSt + offsetof(EncState, err));
+  *need = kOffStage + vb;
   return w;
 }
 constexpr int kZeroWords = kMaxSlots * kHistStride + 16;  // hist + acc, as 32-bit words
@@ -749,7 +770,7 @@ __device__ __forceinline__ void step_process(const Step& v, int64_t wb, int64_t 
 // every block's flag at `ep` or later: all of a lane's flag loads issued together (no short-circuit, so one
 // round trip per poll rather than one per flag), then one wave-wide vote
 __device__ __forceinline__ bool all_arrived(const EncWs& w, unsigned ep) {
-  const int tid = threadIdx.x & (kWave - 1), G = (int)gridDim.x;
+  const int tid = threadIdx.x & (kWave - 1), G = w.nb;
   bool ok = true;
 #pragma unroll
   for (int i = 0; i < kMaxBlocks / kWave; ++i) {
@@ -765,14 +786,14 @@ __device__ __forceinline__ void exchange(const EncWs& w, unsigned ep) {
   drain_stores();
   __syncthreads();
   const int tid = threadIdx.x;
-  if (tid == 0) __hip_atomic_store(w.flags() + blockIdx.x, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(w.flags() + w.bid, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid < kWave) {
     unsigned spins = 0;
     for (;;) {
       if (all_arrived(w, ep)) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 22)) {  // ~1 s: a block never arrived; flag it and let the launch drain
-        if (tid == 0) __hip_atomic_fetch_or(&w.st()->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_fetch_or(w.errp, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -789,14 +810,14 @@ __device__ __forceinline__ void exchange_work(const EncWs& w, unsigned ep, unsig
   if (tid == 0) *s_xdone = 0u;
   drain_stores();
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(w.flags() + blockIdx.x, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(w.flags() + w.bid, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid < kWave) {
     unsigned spins = 0;
     for (;;) {
       if (all_arrived(w, ep)) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 22)) {  // ~1 s: a block never arrived; flag it and let the launch drain
-        if (tid == 0) __hip_atomic_fetch_or(&w.st()->err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_fetch_or(w.errp, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -856,7 +877,7 @@ __device__ __forceinline__ void pick_digit(const EncWs& w, SelState& cur, long l
     const unsigned long long top = (unsigned long long)maxkey + 1ull;
     const unsigned long long nw = top > nlo ? top - nlo : 0ull;
     if (nw == 0ull && threadIdx.x == 0)
-      __hip_atomic_fetch_or(&w.st()->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(w.errp, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (threadIdx.x == 0) {
       cur.narrowed = 0;
@@ -873,7 +894,7 @@ __device__ __forceinline__ void pick_digit(const EncWs& w, SelState& cur, long l
   }
   const unsigned d = s_digit;
   const long long rr = s_rem;
-  if (*s_err && threadIdx.x == 0) __hip_atomic_fetch_or(&w.st()->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (*s_err && threadIdx.x == 0) __hip_atomic_fetch_or(w.errp, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned nlo = cur.lo + (d << cur.shift);
   const int csh = cur.shift;
   __syncthreads();  // every thread has read cur, s_digit, s_rem
@@ -955,11 +976,33 @@ __device__ __forceinline__ unsigned long long* stamp_lds() {
 // sample kernel
 // ------------------------------------------------------------------------------------------------
 template <class Src>
-__global__ __launch_bounds__(256) void topk_sample_kernel(Src x, int64_t n, int S, EncWs w) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void sample_one(const Src& x, int64_t n, int S, const EncWs& w, int j) {
   if (j >= S) return;
   const int64_t pos = (S == n) ? (int64_t)j : (int64_t)(((double)j + 0.5) * (double)n / (double)S);
   w.sample()[j] = order_key(__float_as_uint(x.get(pos < n ? pos : n - 1)));
+}
+
+template <class Src>
+__global__ __launch_bounds__(256) void topk_sample_kernel(Src x, int64_t n, int S, EncWs w) {
+  sample_one(x, n, S, w, blockIdx.x * 256 + threadIdx.x);
+}
+
+// one client of a batched call (flc_stacked_encode_batch): its input, Philox seed and outputs
+struct BatchEntry {
+  const float* x;
+  uint64_t seed;
+  int* idx;
+  uint8_t* codes;
+  float* norm;
+  unsigned* tiles;
+};
+
+// batched: `per` blocks sample each client into its own header
+__global__ __launch_bounds__(256) void topk_sample_batch_kernel(const BatchEntry* __restrict__ tab, int64_t n, int S,
+                                                                EncWs w, int per) {
+  const int g = (int)blockIdx.x / per;
+  w.base += (size_t)g * kOffStage;
+  sample_one(FlatSrc{tab[g].x}, n, S, w, ((int)blockIdx.x - g * per) * 256 + (int)threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -982,7 +1025,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   SampleLds& SL = *reinterpret_cast<SampleLds*>(s_key);  // the sample phase precedes every candidate write
   static_assert(sizeof(SampleLds) <= sizeof(unsigned) * kCap, "sample scratch must fit the key array");
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
-  const int64_t b0 = (int64_t)blockIdx.x * w.M;
+  const int64_t b0 = (int64_t)w.bid * w.M;
   const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
   constexpr int SF = Src::SF;
   constexpr int64_t kWS = SF * 256;         // elements per wave step
@@ -1002,7 +1045,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   if (take_all) {
     t_lo = 0u;
     t_hi = 1ull << 32;
-    if (blockIdx.x == 0 && tid == 0) w.st()->sample_path = 2ull;
+    if (w.bid == 0 && tid == 0) w.st()->sample_path = 2ull;
   } else {
     bool ok = false;
     {
@@ -1021,12 +1064,12 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
       if (fast) ok = sample_fast_pick(w.sample(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
     }
     if (!ok) sample_general(w.sample(), S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
-    if (blockIdx.x == 0 && tid == 0) w.st()->sample_path = ok ? 0ull : 1ull;
+    if (w.bid == 0 && tid == 0) w.st()->sample_path = ok ? 0ull : 1ull;
   }
   // the float predicate !(v < key_value(t_lo)) equals key >= t_lo for t_lo <= key(+inf)
   if (t_lo > 0xff800000u) t_lo = 0xff800000u;
   if (t_hi <= (unsigned long long)t_lo || t_hi > (1ull << 32)) t_hi = 1ull << 32;
-  if (blockIdx.x == 0 && tid == 0) {
+  if (w.bid == 0 && tid == 0) {
     w.st()->t_lo = t_lo;
     w.st()->t_hi = t_hi;
   }
@@ -1042,8 +1085,8 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   fc.s_key = s_key;
   fc.s_idx = s_idx;
   fc.gcap = STAGE ? 0u : w.ovf;  // (the split path stages LDS only)
-  fc.g_key = w.ovf_key(blockIdx.x);
-  fc.g_idx = w.ovf_idx(blockIdx.x);
+  fc.g_key = w.ovf_key(w.bid);
+  fc.g_idx = w.ovf_idx(w.bid);
   fc.s_hist = s_hist;
   fc.t_lo = t_lo;
   fc.width0 = t_hi - t_lo;
@@ -1100,8 +1143,8 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   // ---- staging (16-B stores; split path only) and the round-0 histogram / counts
   if (STAGE) {
     const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
-    uint4* dk = reinterpret_cast<uint4*>(w.stage_key(blockIdx.x));
-    uint4* di = reinterpret_cast<uint4*>(w.stage_idx(blockIdx.x));
+    uint4* dk = reinterpret_cast<uint4*>(w.stage_key(w.bid));
+    uint4* di = reinterpret_cast<uint4*>(w.stage_idx(w.bid));
     const uint4* sk = reinterpret_cast<const uint4*>(s_key);
     const uint4* si = reinterpret_cast<const uint4*>(s_idx);
     for (unsigned q = tid; q < (nst + 3u) / 4u; q += kET) {
@@ -1122,7 +1165,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
     if (ab) atomicAdd(&h[kHistBins], (unsigned)ab);
     atomicMax(&h[kHistBins + 1], m);
     atomicAdd(&w.acc()[0], (unsigned long long)C_b);
-    if (STAGE) w.blk_c()[blockIdx.x] = C_b;
+    if (STAGE) w.blk_c()[w.bid] = C_b;
   }
   STAMP(4);
   BLKT(2);
@@ -1143,6 +1186,8 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(Src x, int64_t n, EncW
   __shared__ unsigned long long s_red[kENW];
   __shared__ unsigned s_mx[kENW];
   STAMP_INIT();
+  w.bid = (int)blockIdx.x;
+  w.nb = (int)gridDim.x;
   (void)filter_phase<true>(x, n, w, S, rank_lo, rank_hi, take_all, s_key, s_idx, s_hist, s_wc, s_red, s_mx);
   STAMP_OUT(0, 5);
 }
@@ -1152,13 +1197,33 @@ __global__ __launch_bounds__(kET) void topk_filter_kernel(Src x, int64_t n, EncW
 // ------------------------------------------------------------------------------------------------
 // FUSED: the filter phase runs first in the same kernel (one exchange after it): the candidates stay in
 // LDS, so the staging round trip through HBM and a kernel boundary are gone
-template <bool STACKED, bool FUSED, class Src>
+// BATCH (stacked, fused, flat input only): blocks [g * w.nb, (g + 1) * w.nb) run client g's select with its own
+// header, staging area, input, seed and outputs (tab[g]); the selects never exchange with each other
+template <bool STACKED, bool FUSED, class Src, bool BATCH = false>
 __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long long k, EncWs w,
                                                           int* __restrict__ idx_out, float* __restrict__ val_out,
                                                           uint8_t* __restrict__ code_out, float* __restrict__ norm_out,
                                                           int levels, double step, uint64_t seed, uint64_t counter,
                                                           unsigned* __restrict__ tile_out, int S, long long rank_lo,
-                                                          long long rank_hi, int take_all) {
+                                                          long long rank_hi, int take_all,
+                                                          const BatchEntry* __restrict__ tab = nullptr) {
+  if constexpr (BATCH) {
+    static_assert(STACKED && FUSED, "batched selects are the fused stacked encode");
+    const int g = (int)blockIdx.x / w.nb;  // (w.nb: blocks per client, set by the host)
+    w.bid = (int)blockIdx.x - g * w.nb;
+    w.base += (size_t)g * kOffStage;
+    w.var += (size_t)g * w.vstride;
+    const BatchEntry e = tab[g];
+    x = Src{e.x};
+    seed = e.seed;
+    idx_out = e.idx;
+    code_out = e.codes;
+    norm_out = e.norm;
+    tile_out = e.tiles;
+  } else {
+    w.bid = (int)blockIdx.x;
+    w.nb = (int)gridDim.x;
+  }
   __shared__ __attribute__((aligned(16))) unsigned s_key[kCap];
   __shared__ __attribute__((aligned(16))) unsigned s_idx[kCap];
   __shared__ unsigned s_hh[2 * kHistBins];  // the round / global histograms
@@ -1173,7 +1238,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   __shared__ unsigned long long s_sum[kENW * 6];
   STAMP_INIT();
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
-  const int64_t b0 = (int64_t)blockIdx.x * w.M;
+  const int64_t b0 = (int64_t)w.bid * w.M;
   const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
   unsigned* hist = w.hist();
   unsigned C_b;
@@ -1183,7 +1248,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   // chunk c = wave range c % kENW, its 64 candidates of iteration c / kENW; chunks [0, s_rnext) are
   // complete after the exchange that ran them
   __shared__ unsigned s_rnext, s_xdone;
-  unsigned* const rnd = w.stage_key(blockIdx.x);
+  unsigned* const rnd = w.stage_key(w.bid);
   unsigned rnd_n = 0;  // candidates covered by the chunk map (0: none)
   auto rnd_work = [&]() -> bool {
     unsigned c = 0;
@@ -1222,11 +1287,11 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   } else {
     // ---- one batch of loads: this block's candidates (staging), the round-0 histogram and counts
     STAMP(5);
-    C_b = w.blk_c()[blockIdx.x];
+    C_b = w.blk_c()[w.bid];
     const unsigned nst = C_b < (unsigned)kCap ? C_b : (unsigned)kCap;
     {
-      const uint4* sk = reinterpret_cast<const uint4*>(w.stage_key(blockIdx.x));
-      const uint4* si = reinterpret_cast<const uint4*>(w.stage_idx(blockIdx.x));
+      const uint4* sk = reinterpret_cast<const uint4*>(w.stage_key(w.bid));
+      const uint4* si = reinterpret_cast<const uint4*>(w.stage_idx(w.bid));
       uint4* dk = reinterpret_cast<uint4*>(s_key);
       uint4* di = reinterpret_cast<uint4*>(s_idx);
       for (unsigned q = tid; q < (nst + 3u) / 4u; q += kET) {
@@ -1273,8 +1338,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   src.s_idx = s_idx;
   src.x = x;
   src.b0 = b0;
-  src.g_key = w.ovf_key(blockIdx.x);
-  src.g_idx = w.ovf_idx(blockIdx.x);
+  src.g_key = w.ovf_key(w.bid);
+  src.g_idx = w.ovf_idx(w.bid);
   const unsigned gcap = FUSED ? w.ovf : 0u;
   src.xmode = fb || C_b > (unsigned)kCap + gcap;  // block-uniform
   src.gmode = !src.xmode && C_b > (unsigned)kCap;
@@ -1347,7 +1412,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     __syncthreads();
     const unsigned lo0 = cur.lo;
     const unsigned long long wd0 = cur.width;
-    unsigned* my_list = w.inbin() + (size_t)blockIdx.x * kInbin;
+    unsigned* my_list = w.inbin() + (size_t)w.bid * kInbin;
     // scanned in the compaction's wave ranges: the count above the bin per wave range plus the wave of
     // each of my in-bin keys give the compaction its per-wave strict / tie counts once T is known
     unsigned gtw = 0;
@@ -1398,7 +1463,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     if (tid == 0) {
       unsigned long long gt = 0;
       for (int v2 = 0; v2 < kENW; ++v2) gt += s_wcnt[v2] >> 32;
-      st_mem64(&w.blk_cnt()[blockIdx.x], ((unsigned long long)s_nl << 32) | (gt & 0xffffffffull));
+      st_mem64(&w.blk_cnt()[w.bid], ((unsigned long long)s_nl << 32) | (gt & 0xffffffffull));
     }
     STAMP(8);
     if (STACKED) {
@@ -1416,10 +1481,10 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     __shared__ unsigned s_nb[kMaxBlocks];
     __shared__ unsigned s_ovf, s_nall;
     constexpr int kLW = 8;  // list words per thread per batch (G <= 256: one batch)
-    const int words = (int)gridDim.x * kInbin;
+    const int words = w.nb * kInbin;
     unsigned long long meta = 0;
     unsigned lw[kLW];
-    if (tid < (int)gridDim.x) meta = ld_mem64(&w.blk_cnt()[tid]);
+    if (tid < w.nb) meta = ld_mem64(&w.blk_cnt()[tid]);
 #pragma unroll
     for (int i = 0; i < kLW; ++i) {
       const int j = i * kET + tid;
@@ -1428,11 +1493,11 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     if (tid == 0) { s_ovf = 0u; s_nall = 0u; }
     __syncthreads();
     unsigned long long my_gt = 0, pre_gt = 0;
-    if (tid < (int)gridDim.x) {
+    if (tid < w.nb) {
       const unsigned nb = (unsigned)(meta >> 32);
       s_nb[tid] = nb;
       my_gt = meta & 0xffffffffull;
-      pre_gt = tid < (int)blockIdx.x ? my_gt : 0ull;
+      pre_gt = tid < w.bid ? my_gt : 0ull;
       if (nb > (unsigned)kInbin) atomicOr(&s_ovf, 1u);
     }
     __syncthreads();
@@ -1449,7 +1514,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
         for (int i = 0; i < kLW; ++i) {
           const int j = c0 + i * kET + tid;
           const int bb = j / kInbin;
-          const bool v = j < words && (unsigned)(j % kInbin) < s_nb[bb < (int)gridDim.x ? bb : 0];
+          const bool v = j < words && (unsigned)(j % kInbin) < s_nb[bb < w.nb ? bb : 0];
           const unsigned long long bm = __ballot(v);
           if (bm) {
             unsigned base_l = 0;
@@ -1508,7 +1573,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
           const unsigned long long s1 = key > T0 ? 1ull : 0ull, t1 = key == T0 ? 1ull : 0ull;
           as += s1;
           at += t1;
-          if (bb < blockIdx.x) { ps += s1; pt += t1; }
+          if (bb < w.bid) { ps += s1; pt += t1; }
         }
         // the four in-bin counts are <= kInbinAll: 16-bit fields of one word
         static_assert(kInbinAll < 65536, "16-bit count fields");
@@ -1561,8 +1626,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     pick_digit(w, cur, (long long)s_ex[0], maxkey, s_ghist, &s_err, s_red);
   }
   __syncthreads();
-  if (!cur.done && blockIdx.x == 0 && tid == 0)
-    __hip_atomic_fetch_or(&w.st()->err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!cur.done && w.bid == 0 && tid == 0)
+    __hip_atomic_fetch_or(w.errp, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned T = cur.T;
   const long long need = cur.need;
   if (!counted) {
@@ -1587,12 +1652,12 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
       }
     }
     const unsigned long long both = block_sum<unsigned long long, kENW>(cnt, s_red) + (slot == 0 ? 0ull : (a_blk << 32));
-    if (tid == 0) st_mem64(&w.blk_cnt()[blockIdx.x], both);
+    if (tid == 0) st_mem64(&w.blk_cnt()[w.bid], both);
     exchange(w, ++ep);
-    const unsigned long long v = tid < (int)gridDim.x ? ld_mem64(&w.blk_cnt()[tid]) : 0ull;
+    const unsigned long long v = tid < w.nb ? ld_mem64(&w.blk_cnt()[tid]) : 0ull;
     unsigned long long t_all;
     const unsigned long long ex = block_excl_scan<unsigned long long, kENW>(v, s_red, &t_all);
-    if (tid == (int)blockIdx.x) s_glob[3] = ex;
+    if (tid == w.bid) s_glob[3] = ex;
     __syncthreads();
     pre = s_glob[3];
     tot = t_all;
@@ -1603,11 +1668,11 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   // (my slice), and the call counter advances
   {
     unsigned* z = hist;
-    const int per = (kZeroWords + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int z0 = (int)blockIdx.x * per, z1 = z0 + per < kZeroWords ? z0 + per : kZeroWords;
+    const int per = (kZeroWords + w.nb - 1) / w.nb;
+    const int z0 = w.bid * per, z1 = z0 + per < kZeroWords ? z0 + per : kZeroWords;
     for (int i = z0 + tid; i < z1; i += kET) z[i] = 0u;
   }
-  if (blockIdx.x == 0 && tid == 0) {
+  if (w.bid == 0 && tid == 0) {
     (void)__hip_atomic_fetch_add(&w.st()->call, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     EncState* st = w.st();
     st->C = C_tot;
@@ -1619,7 +1684,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     st->ties = (unsigned long long)ties_tot;
     st->strict = (unsigned long long)strict_tot;
     if (strict_tot + need != k || need > ties_tot)
-      __hip_atomic_fetch_or(&st->err, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(w.errp, 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
   // ---- ordered compaction: wave `wid` owns candidates [wid * Q, (wid + 1) * Q) of this block
@@ -1628,7 +1693,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   if (STACKED) {
     const float a = fabsf(key_value(maxkey)), b = fabsf(key_value(T));
     nrm = (isnan(a) || isnan(b)) ? __uint_as_float(0x7fc00000u) : (a > b ? a : b);
-    if (blockIdx.x == 0 && tid == 0) *norm_out = nrm;
+    if (w.bid == 0 && tid == 0) *norm_out = nrm;
   }
   const bool nrm_ok = nrm > 0.0f && nrm <= 3.402823466e38f;
   // tile pointers (CSR over FLC_TILE-output tiles): kept entries per tile of this block, counted in the
@@ -1859,7 +1924,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   if (tile_owner) {  // tiles after the wave's last kept entry: the next kept position
     const long long nxt = s_before + (t_before > skip ? t_before - skip : 0);
     for (int64_t t = (tile_prev >> kTileLog) + 1 + lane; t <= (tile_hi >> kTileLog); t += kWave) tile_out[t] = (unsigned)nxt;
-    if (blockIdx.x == gridDim.x - 1 && q1 >= ncand && lane == 0) tile_out[cdiv_dev(n, kTile)] = (unsigned)k;
+    if (w.bid == w.nb - 1 && q1 >= ncand && lane == 0) tile_out[cdiv_dev(n, kTile)] = (unsigned)k;
   }
   STAMP(15);
   BLKT(3);
@@ -1949,6 +2014,88 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
     FLC_LAUNCH(STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true, Src>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
                tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
+  if (gated && gt.multi[dev]) {
+    FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
+    gt.recorded[dev] = true;
+  }
+  return FLC_OK;
+}
+
+// Batched stacked encode: the clients in chunks of at most `cus` (one select of cus / chunk blocks each, all in one
+// launch, so every block of the launch is co-resident: one per CU); chunks run one after another on the stream.
+// Workspace: [chunk headers of kOffStage][chunk staging / overflow areas of vstride][the entry table]; the headers'
+// state, flags and histograms are zeroed at the start of every call.
+struct BatchGeom {
+  int chunk;       // clients per launch
+  EncGeom g;       // one client's select geometry
+  unsigned ovf;
+  size_t off_ovf;  // from the client's staging area
+  size_t vstride;
+  size_t table_off, need;
+};
+
+BatchGeom batch_geometry(int64_t n, int64_t k, int n_clients, int cus) {
+  BatchGeom b;
+  b.chunk = std::max(1, std::min(n_clients, cus));
+  b.vstride = enc_var_bytes(n, k, std::max(1, cus / b.chunk), &b.g, &b.ovf, &b.off_ovf);
+  b.table_off = (size_t)b.chunk * (kOffStage + b.vstride);
+  b.need = b.table_off + al256((size_t)std::max(n_clients, 1) * sizeof(BatchEntry));
+  return b;
+}
+
+int launch_topk_batch(const std::vector<BatchEntry>& ents, int64_t n, int64_t k, int levels, uint64_t counter,
+                      void* ws, size_t ws_bytes, hipStream_t st, const char* who) {
+  int dev = 0;
+  const int cus = current_cus(&dev);
+  const int C = (int)ents.size();
+  const BatchGeom bg = batch_geometry(n, k, C, cus);
+  if (!ws || bg.need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, bg.need);
+  char* base = static_cast<char*>(ws);
+  BatchEntry* tab = reinterpret_cast<BatchEntry*>(base + bg.table_off);
+  FLC_CHECK_HIP(hipMemcpyAsync(tab, ents.data(), ents.size() * sizeof(BatchEntry), hipMemcpyHostToDevice, st));
+  // each call starts its headers from zero (state, flags, histograms): no history is carried between calls, so the
+  // header / staging split may move with the client count
+  FLC_CHECK_HIP(hipMemset2DAsync(base, kOffStage, 0, kOffBlk, (size_t)bg.chunk, st));
+  EncWs w;
+  w.base = base;
+  w.var = base + (size_t)bg.chunk * kOffStage;
+  w.M = bg.g.M;
+  w.off_ovf = bg.off_ovf;
+  w.ovf = bg.ovf;
+  w.bid = 0;
+  w.nb = bg.g.G;
+  w.vstride = bg.vstride;
+  w.errp = reinterpret_cast<unsigned long long*>(base + kOffSt + offsetof(EncState, err));
+  const SampleSetup ss = sample_setup(n, k);
+  const double step = 1.0 / (double)levels;
+  SelectGate& gt = gate();
+  std::lock_guard<std::mutex> lk(gt.mu);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  FLC_CHECK_HIP(hipStreamIsCapturing(st, &cs));
+  const bool gated = cs == hipStreamCaptureStatusNone;
+  if (gated) {
+    if (!gt.used[dev]) {
+      gt.used[dev] = true;
+      gt.first[dev] = st;
+    } else if (!gt.multi[dev] && st != gt.first[dev]) {
+      FLC_CHECK_HIP(hipDeviceSynchronize());
+      if (!gt.last[dev]) FLC_CHECK_HIP(hipEventCreateWithFlags(&gt.last[dev], hipEventDisableTiming));
+      gt.multi[dev] = true;
+    }
+    if (gt.multi[dev] && gt.recorded[dev]) FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
+  }
+  for (int c0 = 0; c0 < C; c0 += bg.chunk) {
+    const int cn = std::min(bg.chunk, C - c0);
+    const BatchEntry* t = tab + c0;
+    if (!ss.take_all) {
+      const int per = (int)cdiv(ss.S, 256);
+      FLC_LAUNCH("topk_sample_batch", topk_sample_batch_kernel, dim3((unsigned)(cn * per)), dim3(256), 0, st, t, n, ss.S,
+                 w, per);
+    }
+    FLC_LAUNCH("stacked_encode_batch", (topk_select_kernel<true, true, FlatSrc, true>),
+               dim3((unsigned)(cn * bg.g.G)), dim3(kET), 0, st, FlatSrc{nullptr}, n, (long long)k, w, nullptr, nullptr,
+               nullptr, nullptr, levels, step, 0ull, counter, nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, t);
+  }
   if (gated && gt.multi[dev]) {
     FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
     gt.recorded[dev] = true;
@@ -2054,6 +2201,25 @@ int flc_stacked_encode_delta(const float* const* local, const float* const* glob
   src.t.nseg = n_tensors;
   return launch_topk<true>(src, n, k, ws, enc, st, idx, nullptr, codes, norm, levels, seed, counter, tiles,
                            "flc_stacked_encode_delta");
+}
+
+size_t flc_stacked_encode_batch_workspace_size(int64_t n, int64_t k, int n_clients) {
+  return batch_geometry(n < 1 ? 1 : n, k < 1 ? 1 : k, n_clients < 1 ? 1 : n_clients, current_cus(nullptr)).need;
+}
+
+int flc_stacked_encode_batch(const float* const* xs, int n_clients, int64_t n, int64_t k, int levels,
+                             const uint64_t* seeds, uint64_t counter, int32_t* const* idx, uint8_t* const* codes,
+                             float* const* norm, uint32_t* const* tiles, void* ws, size_t ws_bytes, void* stream) {
+  const char* who = "flc_stacked_encode_batch";
+  if (n_clients <= 0 || !xs || !seeds || !idx || !codes || !norm) return fail(FLC_EINVAL, "%s: bad arguments", who);
+  if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "%s: levels must be in [1, 127]", who);
+  std::vector<BatchEntry> ents((size_t)n_clients);
+  for (int c = 0; c < n_clients; ++c) {
+    if (int rc = check_topk(xs[c], n, k, who)) return rc;
+    if (!idx[c] || !codes[c] || !norm[c]) return fail(FLC_EINVAL, "%s: null output of client %d", who, c);
+    ents[c] = BatchEntry{xs[c], seeds[c], idx[c], codes[c], norm[c], tiles ? tiles[c] : nullptr};
+  }
+  return launch_topk_batch(ents, n, k, levels, counter, ws, ws_bytes, as_stream(stream), who);
 }
 
 int flc_topk_status(void* ws, uint64_t* err_out, int reset, void* stream) {

@@ -118,6 +118,14 @@ class StackedWireCodec:
 
         codec.stacked_encode(delta, self.k, self.levels, seed=self.seed + client, counter=self.counter, wire=record)
 
+    def encode_many_into(self, deltas: Sequence[torch.Tensor], records: torch.Tensor, clients: Sequence[int]) -> None:
+        """All of this rank's clients in one batched launch (flc_stacked_encode_batch): records[j] equals
+        ``encode_into(deltas[j], records[j], clients[j])`` bit for bit."""
+        from . import codec
+
+        codec.stacked_encode_batch(deltas, self.k, self.levels, seeds=[self.seed + c for c in clients],
+                                   counter=self.counter, wires=[records[j] for j in range(len(deltas))])
+
     def fold(self, records: torch.Tensor, slots: Sequence[int], weights: Sequence[float],
              out: torch.Tensor) -> None:
         from . import codec
@@ -156,8 +164,11 @@ def aggregate_round_wire(deltas: Sequence[torch.Tensor], weights: Sequence[float
         raise ValueError("need a device when this rank owns no client and no `out` is given")
     per = -(-n_clients // world)
     send = torch.empty(per, wire.stride, dtype=torch.uint8, device=dev)  # (padding bytes are never read)
-    for j, d in enumerate(deltas):
-        wire.encode_into(d, send[j], mine[j])
+    if len(deltas) > 1 and hasattr(wire, "encode_many_into"):  # the rank's clients in one launch
+        wire.encode_many_into(deltas, send, mine)
+    else:
+        for j, d in enumerate(deltas):
+            wire.encode_into(d, send[j], mine[j])
     if multi:
         recs = torch.empty(world * per, wire.stride, dtype=torch.uint8, device=dev)
         if dist.get_backend(group) == "gloo":  # (gloo: the list form)

@@ -242,6 +242,21 @@ int flc_stacked_encode_delta(const float* const* local, const float* const* glob
                              int n_tensors, int64_t k, int levels, uint64_t seed, uint64_t counter, int32_t* idx,
                              uint8_t* codes, float* norm, uint32_t* tiles, void* ws, size_t ws_bytes, void* stream);
 
+/* the stacked encoder over many clients of one round in one launch (the clients a rank encodes before the fold,
+ * nodes.py:706-713 / _fedopt.py:295-308 once per client): client c's packet is bit-identical to
+ * flc_stacked_encode_tiled(xs[c], n, k, levels, seeds[c], counter, ...) into idx[c], codes[c], norm[c], tiles[c]
+ * (tiles may be NULL: no tile pointers; the four pointers of a wire record make client c's record).  All clients
+ * have the same n and k; xs, seeds, idx, codes, norm and tiles are HOST arrays of n_clients entries (device
+ * pointers / seeds).  The device's CUs are split among up to #CU clients per launch (one independent select of
+ * #CU / clients blocks each, its own header, no exchange across clients); more clients run in further launches on
+ * the stream.  The workspace is used afresh by every call (its headers are zeroed in the stream), so it needs no
+ * zeroing by the caller, but must not be shared with single-client calls.  flc_topk_status(ws) reports the errors
+ * of every client's select. */
+size_t flc_stacked_encode_batch_workspace_size(int64_t n, int64_t k, int n_clients);
+int flc_stacked_encode_batch(const float* const* xs, int n_clients, int64_t n, int64_t k, int levels,
+                             const uint64_t* seeds, uint64_t counter, int32_t* const* idx, uint8_t* const* codes,
+                             float* const* norm, uint32_t* const* tiles, void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------ other compressors
  * identical (compressors.py:273-275): out = +x;  lazy (276-283): out = x / p (fp32 division);
  * rand-k (284-292): out = 0, out[idx[j]] = scale * x[idx[j]] (idx in any order, unique). */

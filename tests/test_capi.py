@@ -114,6 +114,38 @@ def test_stacked_encode_delta_validates_without_gpu():
     assert lib.flc_stacked_encode_delta_workspace_size(1000, 10, 8) > lib.flc_topk_workspace_size(1000, 10)
 
 
+def test_stacked_encode_batch_validates_without_gpu():
+    """flc_stacked_encode_batch rejects bad client tables before touching the device; its workspace grows with the
+    client count."""
+    from fl_sim_amd import _lib
+
+    lib = _lib.load()
+    P = ctypes.c_void_p * 2
+    U = ctypes.c_uint64 * 2
+    c = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+    good, seeds = P(16, 32), U(1, 2)
+    assert lib.flc_stacked_encode_batch(None, 2, 100, 10, 127, None, 0, None, None, None, None, 16, 1 << 30,
+                                        None) == 1
+    rc = lib.flc_stacked_encode_batch(c(good), 0, 100, 10, 127, c(seeds), 0, c(good), c(good), c(good), None, 16,
+                                      1 << 30, None)
+    assert rc == 1 and "bad arguments" in lib.flc_last_error().decode()
+    rc = lib.flc_stacked_encode_batch(c(good), 2, 100, 10, 200, c(seeds), 0, c(good), c(good), c(good), None, 16,
+                                      1 << 30, None)
+    assert rc == 1 and "levels" in lib.flc_last_error().decode()
+    rc = lib.flc_stacked_encode_batch(c(P(16, 40)), 2, 100, 10, 127, c(seeds), 0, c(good), c(good), c(good), None, 16,
+                                      1 << 30, None)  # client 1's input not 16-B aligned
+    assert rc == 1 and "aligned" in lib.flc_last_error().decode()
+    rc = lib.flc_stacked_encode_batch(c(good), 2, 100, 100, 127, c(seeds), 0, c(good), c(good), c(good), None, 16,
+                                      1 << 30, None)
+    assert rc == 1 and "0 < k < n" in lib.flc_last_error().decode()
+    rc = lib.flc_stacked_encode_batch(c(good), 2, 100, 10, 127, c(seeds), 0, c(P(16, 0)), c(good), c(good), None, 16,
+                                      1 << 30, None)
+    assert rc == 1 and "null output of client 1" in lib.flc_last_error().decode()
+    a = lib.flc_stacked_encode_batch_workspace_size(1 << 20, 1 << 10, 2)
+    b = lib.flc_stacked_encode_batch_workspace_size(1 << 20, 1 << 10, 8)
+    assert 0 < a < b
+
+
 def test_rccl_entries_validate_without_gpu():
     """The RCCL entries (flc_comm_* / flc_rccl_*) check their arguments before RCCL is touched; the unique id is
     RCCL's 128 bytes."""

@@ -1,0 +1,96 @@
+"""GPU parity of the batched stacked encode (flc_stacked_encode_batch): the clients of one round encoded in one
+launch, each client's select on its own share of the CUs, equal bit for bit to one single-client encode per client
+(stacked_encode, itself pinned against the oracle in test_gpu_codec.py) — plain packets and packed wire records,
+more clients than CUs (chunked launches), the take-all sample path, skewed and tied inputs, and the configs[3]
+workload (8 clients x 25M) through the packed-wire round against the per-client round."""
+
+import pytest
+import torch
+
+from fl_sim_amd import codec
+from fl_sim_amd import dist as fdist
+
+pytestmark = pytest.mark.gpu
+
+
+def _x(n, seed, kind="randn"):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(n, generator=g, device="cuda") * 1e-3
+    if kind == "zeros":
+        x[torch.rand(n, generator=g, device="cuda") < 0.3] = 0.0
+    elif kind == "ties":  # few distinct values: the k-th value is tied many times
+        x = torch.round(x * 4e3) / 4e3
+    elif kind == "skew":
+        x[: min(n, 5000)] += 1.0
+    return x
+
+
+def _same(a: codec.StackedPacket, b: codec.StackedPacket, what=""):
+    assert torch.equal(a.idx, b.idx), f"idx differ {what}"
+    assert torch.equal(a.codes[: a.idx.numel()], b.codes[: b.idx.numel()]), f"codes differ {what}"
+    assert torch.equal(a.norm, b.norm), f"norm differs {what}"
+    if a.tiles is not None and b.tiles is not None:
+        assert torch.equal(a.tiles, b.tiles), f"tiles differ {what}"
+
+
+@pytest.mark.parametrize("n,k,C", [(70_001, 700, 1), (70_001, 700, 3), (1_000_003, 10_000, 8), (4_194_304, 41_943, 2),
+                                   (250_000, 2_500, 17)])
+def test_batch_equals_single_encodes(n, k, C):
+    kinds = ["randn", "zeros", "ties", "skew"]
+    xs = [_x(n, 100 + c, kinds[c % 4]) for c in range(C)]
+    seeds = [7 + 3 * c for c in range(C)]
+    pks = codec.stacked_encode_batch(xs, k, 127, seeds=seeds, counter=11)
+    for c in range(C):
+        _same(pks[c], codec.stacked_encode(xs[c], k, 127, seed=seeds[c], counter=11), f"client {c}")
+    assert codec.topk_status() == 0
+
+
+def test_batch_more_clients_than_cus():
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    C, n, k = cus + 44, 5_000, 50
+    xs = [_x(n, c, "randn" if c % 3 else "ties") for c in range(C)]
+    pks = codec.stacked_encode_batch(xs, k, 127, seeds=list(range(C)), counter=2)
+    for c in range(0, C, 7):
+        _same(pks[c], codec.stacked_encode(xs[c], k, 127, seed=c, counter=2), f"client {c}")
+    _same(pks[-1], codec.stacked_encode(xs[-1], k, 127, seed=C - 1, counter=2), "last client")
+
+
+def test_batch_take_all_and_repeat_calls():
+    # k close to n: the sample admits everything (take-all path); then the same workspace with other shapes
+    for (n, k, C) in [(1_000, 999, 4), (300_001, 3_000, 6), (2_048, 1, 5), (300_001, 3_000, 2)]:
+        xs = [_x(n, 7 * c + n % 97) for c in range(C)]
+        pks = codec.stacked_encode_batch(xs, k, 127, seeds=[c for c in range(C)], counter=n % 13)
+        for c in range(C):
+            _same(pks[c], codec.stacked_encode(xs[c], k, 127, seed=c, counter=n % 13), f"n={n} client {c}")
+    assert codec.topk_status() == 0
+
+
+def test_batch_into_wire_records_and_fold():
+    n, k, C = 2_000_000, 20_000, 5
+    xs = [_x(n, 40 + c, "zeros" if c == 2 else "randn") for c in range(C)]
+    stride, _ = codec.stacked_wire_layout(n, k)
+    recs = torch.zeros(C, stride, dtype=torch.uint8, device="cuda")
+    ref = torch.zeros_like(recs)
+    codec.stacked_encode_batch(xs, k, 127, seeds=[5 + c for c in range(C)], counter=3, wires=list(recs))
+    for c in range(C):
+        codec.stacked_encode(xs[c], k, 127, seed=5 + c, counter=3, wire=ref[c])
+    for c in range(C):
+        _same(codec.wire_packet(recs[c], n, k), codec.wire_packet(ref[c], n, k), f"record {c}")
+    w = [0.1 * (c + 1) for c in range(C)]
+    a = codec.stacked_fold_wires(recs, list(range(C)), w, n, k, 127)
+    b = codec.stacked_fold_wires(ref, list(range(C)), w, n, k, 127)
+    assert torch.equal(a, b)
+
+
+def test_config3_wire_round_batched_equals_per_client():
+    # configs[3]: 8 clients x 25M fp32, w_i = ts_i / sum ts with ts_i = 100 (i + 1); one rank owns all 8
+    n, k, C = 25_000_000, 250_000, 8
+    xs = [_x(n, 300 + c) for c in range(C)]
+    w = fdist.sample_weights([100 * (i + 1) for i in range(C)])
+    wc = fdist.StackedWireCodec(n, k, 127, seed=0, counter=9)
+    got = fdist.aggregate_round_wire(xs, w, C, wc)
+    ref = torch.zeros(n, dtype=torch.float32, device="cuda")
+    for c in range(C):
+        pk = codec.stacked_encode(xs[c], k, 127, seed=c, counter=9)
+        codec.stacked_decode(pk, out=ref, weight=float(w[c]), accumulate=True)
+    assert torch.equal(got, ref)
