@@ -58,7 +58,7 @@ at::Tensor workspace(const at::Tensor& like, size_t nbytes, int kind) {
   }
   return it->second;
 }
-enum { kWsQuant = 0, kWsNatural = 1, kWsTopk = 2, kWsAdaptive = 3 };
+enum { kWsQuant = 0, kWsNatural = 1, kWsTopk = 2, kWsAdaptive = 3, kWsTopkBatch = 4 };
 
 int code_bits(int64_t levels) {
   TORCH_CHECK(levels >= 1, "flcodec: levels must be >= 1");
@@ -97,6 +97,46 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode(const 
 }
 
 // packed wire records (flc_stacked_wire_layout): the encode straight into one record, and the one-pass fold of many
+// every client's packed wire record from one batched launch (flc_stacked_encode_batch): row c equals
+// stacked_encode_wire(xs[c], k, levels, seeds[c], counter)
+at::Tensor stacked_encode_batch_wire(at::TensorList xs_, int64_t k, int64_t levels, at::IntArrayRef seeds,
+                                     int64_t counter) {
+  TORCH_CHECK(!xs_.empty(), "flcodec: stacked_encode_batch_wire needs at least one client");
+  TORCH_CHECK(seeds.size() == xs_.size(), "flcodec: one seed per client");
+  std::vector<at::Tensor> xs;
+  for (const auto& t : xs_) xs.push_back(dev_f32(t, "xs").reshape({-1}));
+  c10::DeviceGuard g(xs[0].device());
+  const int64_t n = xs[0].numel();
+  const int C = (int)xs.size();
+  for (const auto& t : xs)
+    TORCH_CHECK(t.numel() == n && t.device() == xs[0].device(), "flcodec: clients of one size on one device");
+  int64_t off[4];
+  const size_t stride = flc_stacked_wire_layout(n, k, off);
+  TORCH_CHECK(stride > 0, "flcodec: bad wire shape n=", n, ", k=", k);
+  at::Tensor recs = at::empty({(int64_t)C, (int64_t)stride}, xs[0].options().dtype(at::kByte));
+  uint8_t* r0 = recs.data_ptr<uint8_t>();
+  std::vector<const float*> xp;
+  std::vector<uint64_t> sd;
+  std::vector<int32_t*> ip;
+  std::vector<uint8_t*> cp;
+  std::vector<float*> np_;
+  std::vector<uint32_t*> tp;
+  for (int c = 0; c < C; ++c) {
+    uint8_t* r = r0 + (size_t)c * stride;
+    xp.push_back(xs[c].data_ptr<float>());
+    sd.push_back((uint64_t)seeds[c]);
+    ip.push_back(reinterpret_cast<int32_t*>(r + off[1]));
+    cp.push_back(r + off[2]);
+    np_.push_back(reinterpret_cast<float*>(r + off[0]));
+    tp.push_back(reinterpret_cast<uint32_t*>(r + off[3]));
+  }
+  at::Tensor ws = workspace(xs[0], flc_stacked_encode_batch_workspace_size(n, k, C), kWsTopkBatch);
+  check(flc_stacked_encode_batch(xp.data(), C, n, k, (int)levels, sd.data(), (uint64_t)counter, ip.data(), cp.data(),
+                                 np_.data(), tp.data(), ws.data_ptr(), (size_t)ws.numel(), stream_of(xs[0])),
+        "stacked_encode_batch_wire");
+  return recs;
+}
+
 at::Tensor stacked_encode_wire(const at::Tensor& x_, int64_t k, int64_t levels, int64_t seed, int64_t counter) {
   at::Tensor x = dev_f32(x_, "x").reshape({-1});
   c10::DeviceGuard g(x.device());
@@ -485,6 +525,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> stacked_encode_meta(c
   return {at::empty({k}, x.options().dtype(at::kInt)), at::empty({k}, x.options().dtype(at::kByte)),
           at::empty({1}, x.options().dtype(at::kFloat)), at::empty({n_tiles(n)}, x.options().dtype(at::kInt))};
 }
+at::Tensor stacked_encode_batch_wire_meta(at::TensorList xs, int64_t k, int64_t, at::IntArrayRef, int64_t) {
+  TORCH_CHECK(!xs.empty(), "flcodec: stacked_encode_batch_wire needs at least one client");
+  return at::empty({(int64_t)xs.size(), (int64_t)flc_stacked_wire_layout(xs[0].numel(), k, nullptr)},
+                   xs[0].options().dtype(at::kByte));
+}
 at::Tensor stacked_encode_wire_meta(const at::Tensor& x, int64_t k, int64_t, int64_t, int64_t) {
   return at::empty({(int64_t)flc_stacked_wire_layout(x.numel(), k, nullptr)}, x.options().dtype(at::kByte));
 }
@@ -548,6 +593,7 @@ TORCH_LIBRARY(flcodec, m) {
         "-> (Tensor codes, Tensor norms, Tensor decoded)");
   m.def("adaptive_random(Tensor x, float u) -> (Tensor out, Tensor index, Tensor status)");
   m.def("stacked_encode_wire(Tensor x, int k, int levels=127, int seed=0, int counter=0) -> Tensor");
+  m.def("stacked_encode_batch_wire(Tensor[] xs, int k, int levels, int[] seeds, int counter=0) -> Tensor");
   m.def("stacked_fold_wires(Tensor wires, int[] slots, float[] weights, int n, int k, int levels=127, "
         "Tensor? out=None, bool accumulate=False) -> Tensor");
 }
@@ -571,6 +617,7 @@ TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
   m.impl("quant_encode_auto", &quant_encode_auto);
   m.impl("adaptive_random", &adaptive_random);
   m.impl("stacked_encode_wire", &stacked_encode_wire);
+  m.impl("stacked_encode_batch_wire", &stacked_encode_batch_wire);
   m.impl("stacked_fold_wires", &stacked_fold_wires);
 }
 
@@ -589,5 +636,6 @@ TORCH_LIBRARY_IMPL(flcodec, Meta, m) {
   m.impl("quant_encode_auto", &quant_encode_auto_meta);
   m.impl("adaptive_random", &adaptive_random_meta);
   m.impl("stacked_encode_wire", &stacked_encode_wire_meta);
+  m.impl("stacked_encode_batch_wire", &stacked_encode_batch_wire_meta);
   m.impl("stacked_fold_wires", &stacked_fold_wires_meta);
 }

@@ -38,6 +38,8 @@ OPS = {
     "stacked_encode_wire": "flcodec::stacked_encode_wire(Tensor x, int k, int levels=127, int seed=0, int counter=0) "
                            "-> Tensor",
     "stacked_fold_wires": None,
+    "stacked_encode_batch_wire": "flcodec::stacked_encode_batch_wire(Tensor[] xs, int k, int levels, int[] seeds, "
+                                 "int counter=0) -> Tensor",
 }
 
 
@@ -260,6 +262,8 @@ def test_wire_ops_meta_shapes(ops):
     out = ops.stacked_fold_wires(torch.empty(3, rec.numel(), dtype=torch.uint8, device="meta"), [2, 0], [0.5, 0.25],
                                  5000, 50)
     assert out.shape == (5000,) and out.dtype == torch.float32
+    recs = ops.stacked_encode_batch_wire([torch.empty(5000, device="meta")] * 4, 50, 127, [1, 2, 3, 4])
+    assert recs.shape == (4, rec.numel()) and recs.dtype == torch.uint8
 
 
 @pytest.mark.gpu
@@ -281,3 +285,18 @@ def test_wire_ops_match_codec(ops):
     got = ops.stacked_fold_wires(recs, [1, 2, 0], [0.25, 0.5, 0.125], n, k)
     exp = codec.stacked_fold_wires(ref_recs, [1, 2, 0], [0.25, 0.5, 0.125], n, k)
     assert torch.equal(got.view(torch.int32), exp.view(torch.int32))
+
+
+@pytest.mark.gpu
+def test_batch_wire_op_matches_codec(ops):
+    from fl_sim_amd import codec
+
+    n, k = 300_007, 3_000
+    g = torch.Generator(device="cuda").manual_seed(22)
+    xs = [torch.randn(n, generator=g, device="cuda") * 1e-3 for _ in range(5)]
+    recs = ops.stacked_encode_batch_wire(xs, k, 127, [9 + i for i in range(5)], 4)
+    for i, x in enumerate(xs):
+        a = codec.wire_packet(recs[i], n, k)
+        b = codec.stacked_encode(x, k, 127, seed=9 + i, counter=4)
+        assert torch.equal(a.idx, b.idx) and torch.equal(a.codes[:k], b.codes[:k]) and torch.equal(a.tiles, b.tiles)
+        assert torch.equal(a.norm, b.norm)
