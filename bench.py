@@ -580,8 +580,11 @@ def main():
 
         def step4_codec():
             acc.zero_()
-            for c in mine:
-                fold(X3, float(w_all[c]), acc, c)
+            if len(mine) > 1:  # the rank's clients encoded in one batched launch, as aggregate_round does
+                fold.many([X3] * len(mine), [w_all[c] for c in mine], acc, mine)
+            else:
+                for c in mine:
+                    fold(X3, float(w_all[c]), acc, c)
 
         ms4c, _ = timed(step4_codec, 10, 3, world)
         ms4c = max_over_ranks(ms4c, world)

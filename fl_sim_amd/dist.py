@@ -58,6 +58,15 @@ def stacked_decode_accumulate(k: int, levels: int = 127, seed: int = 0, counter:
         pkt = codec.stacked_encode(delta, k, levels, seed=seed + client, counter=counter)
         codec.stacked_decode(pkt, out=acc, weight=weight, accumulate=True)
 
+    def many(deltas: Sequence[torch.Tensor], weights: Sequence[float], acc: torch.Tensor,
+             clients: Sequence[int]) -> None:
+        """The rank's clients encoded in one batched launch, then decoded into ``acc`` in client order: the same
+        packets and the same fmaf chain as one ``step`` per client."""
+        pkts = codec.stacked_encode_batch(deltas, k, levels, seeds=[seed + c for c in clients], counter=counter)
+        for pkt, w in zip(pkts, weights):
+            codec.stacked_decode(pkt, out=acc, weight=float(w), accumulate=True)
+
+    step.many = many
     return step
 
 
@@ -78,10 +87,15 @@ def aggregate_round(deltas: Sequence[torch.Tensor], weights: Sequence[float], cl
         out = torch.zeros_like(deltas[0])
     else:
         out.zero_()
-    for d, w, c in zip(deltas, weights, clients):
+    for d in deltas:
         if d.shape != out.shape or d.dtype != torch.float32:
             raise ValueError("every delta must be a flat fp32 tensor shaped like `out`")
-        step(d, float(w), out, c)
+    many = getattr(step, "many", None)
+    if many is not None and len(deltas) > 1:  # a codec that encodes the rank's clients in one launch
+        many(deltas, weights, out, clients)
+    else:
+        for d, w, c in zip(deltas, weights, clients):
+            step(d, float(w), out, c)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         if dst is None:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
