@@ -1,8 +1,9 @@
 """GPU parity of the batched stacked encode (flc_stacked_encode_batch): the clients of one round encoded in one
 launch, each client's select on its own share of the CUs, equal bit for bit to one single-client encode per client
 (stacked_encode, itself pinned against the oracle in test_gpu_codec.py) — plain packets and packed wire records,
-more clients than CUs (chunked launches), the take-all sample path, skewed and tied inputs, and the configs[3]
-workload (8 clients x 25M) through the packed-wire round against the per-client round."""
+more clients than CUs (chunked launches), the take-all sample path, skewed and tied inputs, the HBM overflow
+(g-mode) and range re-read (x-mode) paths and NaN, and the configs[3] workload (8 clients x 25M) through the
+packed-wire round against the per-client round."""
 
 import pytest
 import torch
@@ -28,7 +29,7 @@ def _x(n, seed, kind="randn"):
 def _same(a: codec.StackedPacket, b: codec.StackedPacket, what=""):
     assert torch.equal(a.idx, b.idx), f"idx differ {what}"
     assert torch.equal(a.codes[: a.idx.numel()], b.codes[: b.idx.numel()]), f"codes differ {what}"
-    assert torch.equal(a.norm, b.norm), f"norm differs {what}"
+    assert torch.equal(a.norm.view(torch.int32), b.norm.view(torch.int32)), f"norm differs {what}"  # (NaN: bits)
     if a.tiles is not None and b.tiles is not None:
         assert torch.equal(a.tiles, b.tiles), f"tiles differ {what}"
 
@@ -94,3 +95,22 @@ def test_config3_wire_round_batched_equals_per_client():
         pk = codec.stacked_encode(xs[c], k, 127, seed=c, counter=9)
         codec.stacked_decode(pk, out=ref, weight=float(w[c]), accumulate=True)
     assert torch.equal(got, ref)
+
+
+def test_batch_overflow_modes_and_nan():
+    # g-mode (candidates past a block's LDS kept in the HBM overflow: 15 % kept, ~40 K candidates per block), x-mode
+    # (one block's range holds all the large values: more candidates than LDS + overflow, the range re-read) and a NaN
+    # (the largest key, always kept) — each in one client of a batch, the other clients plain
+    n, k = 32_000_000, 4_800_000
+    xs = [_x(n, 500), _x(n, 501, "zeros")]
+    pks = codec.stacked_encode_batch(xs, k, 127, seeds=[3, 4], counter=6)
+    for c in range(2):
+        _same(pks[c], codec.stacked_encode(xs[c], k, 127, seed=3 + c, counter=6), f"g-mode client {c}")
+    n, k = 2_000_000, 20_000
+    xs = [_x(n, 510), _x(n, 511), _x(n, 512)]
+    xs[1][:30_000] += 1.0
+    xs[2][5] = float("nan")
+    pks = codec.stacked_encode_batch(xs, k, 127, seeds=[1, 2, 3], counter=8)
+    for c in range(3):
+        _same(pks[c], codec.stacked_encode(xs[c], k, 127, seed=1 + c, counter=8), f"x-mode/NaN client {c}")
+    assert codec.topk_status() == 0
