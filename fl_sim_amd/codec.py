@@ -44,6 +44,19 @@ def _dev_f32(x: torch.Tensor, name: str = "x") -> torch.Tensor:
 TILE = 1024  # FLC_TILE (include/flcodec.h)
 
 
+_WS_SIZE: Dict[tuple, int] = {}
+
+
+def _ws_size(name: str, *args) -> int:
+    """A workspace-size entry point's result, memoised per device (a pure function of its arguments and the
+    device's CU count): one ctypes call fewer per encode."""
+    key = (torch.cuda.current_device(), name) + args
+    v = _WS_SIZE.get(key)
+    if v is None:
+        v = _WS_SIZE[key] = _lib.size(name, *args)
+    return v
+
+
 def workspace(device: torch.device, nbytes: int, kind: str) -> torch.Tensor:
     """Zero-initialised workspace, cached per (device, stream, kind) and grown on demand."""
     key = (device.index if device.index is not None else torch.cuda.current_device(), _stream(device), kind)
@@ -328,11 +341,22 @@ def wire_packet(record: torch.Tensor, n: int, k: int, levels: int = 127) -> Stac
 
 
 def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, counter: int = 0,
-                   with_tiles: bool = True, wire: Optional[torch.Tensor] = None) -> StackedPacket:
+                   with_tiles: bool = True, wire: Optional[torch.Tensor] = None,
+                   out: Optional[StackedPacket] = None) -> StackedPacket:
     """Stacked top-k -> 8-bit dithering encode.  ``wire``: a packed wire record (see :func:`wire_packet`) to write
-    the packet into; the returned packet's tensors are then views of it."""
+    the packet into; the returned packet's tensors are then views of it.  ``out``: a packet of the same (n, k) whose
+    tensors are overwritten (no allocation per call); it is returned."""
     x = _dev_f32(x).reshape(-1)
     n = x.numel()
+    if out is not None:
+        if out.n != n or out.idx.numel() != k or out.idx.device != x.device or (with_tiles and out.tiles is None):
+            raise ValueError("`out` must be a packet of the same n and k on the input's device")
+        pk = StackedPacket(out.idx, out.codes, out.norm, n, levels, out.tiles if with_tiles else None)
+        ws = workspace(x.device, _ws_size("flc_topk_workspace_size", n, k), "topk")
+        call("flc_stacked_encode_tiled", _p(x), n, k, levels, seed, counter, None, _p(pk.idx), _p(pk.codes),
+             _p(pk.norm), _p(pk.tiles), _p(ws), ws.numel(), _stream(x.device))
+        _after_encode(x.device)
+        return pk
     if wire is not None:
         if wire.device != x.device:
             raise ValueError("the wire record must be on the input's device")
@@ -343,7 +367,7 @@ def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, co
         codes = torch.empty(max(k, 16), dtype=torch.uint8, device=x.device)
         norm = torch.empty(1, dtype=torch.float32, device=x.device)
         tiles = _tiles(n, x.device) if with_tiles else None
-    ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
+    ws = workspace(x.device, _ws_size("flc_topk_workspace_size", n, k), "topk")
     call("flc_stacked_encode_tiled", _p(x), n, k, levels, seed, counter, None, _p(idx), _p(codes), _p(norm),
          _p(tiles), _p(ws), ws.numel(), _stream(x.device))
     _after_encode(x.device)

@@ -21,6 +21,10 @@ SHORT = {
     "sparse_decode_wave_kernel<0": "sparse_decode",
     "topk_sample_kernel": "topk_sample",
     "sparse_decode_kernel<0": "sparse_decode",
+    "topk_select_kernel<true, true, flc::(anonymous namespace)::FlatSrc, true>": "stacked_encode_batch",
+    "topk_select_kernel<true, true, flc::(anonymous namespace)::DeltaSrc, false>": "stacked_encode_delta",
+    "topk_select_kernel<true, true, flc::(anonymous namespace)::FlatSrc, false>": "stacked_encode",
+    "topk_select_kernel<false, true, flc::(anonymous namespace)::FlatSrc, false>": "topk_encode",
     "topk_select_kernel<true, true, flc::(anonymous namespace)::DeltaSrc>": "stacked_encode_delta",
     "topk_select_kernel<true, true, flc::(anonymous namespace)::FlatSrc>": "stacked_encode",
     "topk_select_kernel<false, true, flc::(anonymous namespace)::FlatSrc>": "topk_encode",
