@@ -610,3 +610,21 @@ def test_stacked_adversarial_matches_oracle_with_tiles(name):
     codec.call("flc_tile_index", codec._p(pkt.idx), k, n, codec._p(ref_tiles), codec._stream(xd.device))
     assert torch.equal(pkt.tiles, ref_tiles)
     assert gc.same_bits(codec.stacked_decode(pkt).cpu().numpy(), exp_out)
+
+
+def test_stacked_encode_into_reused_packet():
+    """stacked_encode(out=packet) overwrites the packet's tensors with the same result as a fresh encode."""
+    from fl_sim_amd import codec
+
+    n, k = 1_000_003, 10_000
+    g = torch.Generator(device="cuda").manual_seed(77)
+    xa = torch.randn(n, generator=g, device="cuda") * 1e-3
+    xb = torch.randn(n, generator=g, device="cuda") * 1e-3
+    pk = codec.stacked_encode(xa, k, 127, seed=1, counter=1)
+    got = codec.stacked_encode(xb, k, 127, seed=2, counter=3, out=pk)
+    ref = codec.stacked_encode(xb, k, 127, seed=2, counter=3)
+    assert got.idx.data_ptr() == pk.idx.data_ptr()
+    assert torch.equal(got.idx, ref.idx) and torch.equal(got.codes[:k], ref.codes[:k])
+    assert torch.equal(got.norm, ref.norm) and torch.equal(got.tiles, ref.tiles)
+    with pytest.raises(ValueError):
+        codec.stacked_encode(xb[:-1], k, 127, out=pk)
