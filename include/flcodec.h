@@ -251,7 +251,8 @@ int flc_stacked_encode_delta(const float* const* local, const float* const* glob
  * #CU / clients blocks each, its own header, no exchange across clients); more clients run in further launches on
  * the stream.  The workspace is used afresh by every call (its headers are zeroed in the stream), so it needs no
  * zeroing by the caller, but must not be shared with single-client calls.  flc_topk_status(ws) reports the errors
- * of every client's select. */
+ * of every client's select.  The client table is copied from the host arrays into the workspace, so the call is not
+ * graph-capturable (like flc_stacked_encode_delta). */
 size_t flc_stacked_encode_batch_workspace_size(int64_t n, int64_t k, int n_clients);
 int flc_stacked_encode_batch(const float* const* xs, int n_clients, int64_t n, int64_t k, int levels,
                              const uint64_t* seeds, uint64_t counter, int32_t* const* idx, uint8_t* const* codes,
