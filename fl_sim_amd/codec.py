@@ -375,41 +375,68 @@ def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, co
 
 
 def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, seeds: Sequence[int] = (),
-                         counter: int = 0, with_tiles: bool = True,
-                         wires: Optional[Sequence[torch.Tensor]] = None) -> List[StackedPacket]:
+                         counter: int = 0, with_tiles: bool = True, wires=None) -> Optional[List[StackedPacket]]:
     """The stacked encode of many clients' flat deltas (all of one size) in one launch (flc_stacked_encode_batch):
-    packet c equals ``stacked_encode(xs[c], k, levels, seeds[c], counter)`` bit for bit.  ``wires``: one packed wire
-    record per client to write into (the packets are then views of them)."""
+    packet c equals ``stacked_encode(xs[c], k, levels, seeds[c], counter)`` bit for bit.  ``wires``: the packed wire
+    records to write into — a ``[clients, >= stride]`` uint8 tensor (then nothing is returned: the records are the
+    output) or a list of one record per client (the packets returned are views of them)."""
     import ctypes
 
-    xs = [_dev_f32(x).reshape(-1) for x in xs]
-    if not xs:
-        return []
-    n, dev = xs[0].numel(), xs[0].device
-    if any(x.numel() != n or x.device != dev for x in xs):
-        raise ValueError("a batched encode takes clients of one size on one device")
     C = len(xs)
+    if C == 0:
+        return []
+    x0 = xs[0]
+    n, dev = x0.numel(), x0.device
+    for x in xs:
+        if not (isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.device == dev and x.numel() == n
+                and x.is_contiguous() and x.data_ptr() % 16 == 0):
+            break
+    else:
+        x = None
+    if x is not None:  # (the slow path: checks with messages, copies of misaligned inputs)
+        xs = [_dev_f32(x).reshape(-1) for x in xs]
+        if any(x.numel() != n or x.device != dev for x in xs):
+            raise ValueError("a batched encode takes clients of one size on one device")
     seeds = list(seeds) if len(seeds) else [0] * C
     if len(seeds) != C:
         raise ValueError("one seed per client")
-    if wires is not None:
-        if len(wires) != C:
-            raise ValueError("one wire record per client")
-        pks = [wire_packet(r, n, k, levels) for r in wires]
+    P = ctypes.c_void_p * C
+    stride, off = stacked_wire_layout(n, k)
+    pks = None
+    if isinstance(wires, torch.Tensor):  # one [C, >= stride] record block: pointers by arithmetic
+        if (wires.dtype != torch.uint8 or wires.dim() != 2 or wires.shape[0] != C or wires.shape[1] < stride
+                or not wires.is_contiguous() or wires.device != dev or wires.data_ptr() % 16 or wires.shape[1] % 16):
+            raise ValueError(f"records must be a contiguous [{C}, >= {stride}] uint8 block (16-B rows) on {dev}")
+        rs = wires.shape[1]
+        bases = [wires.data_ptr() + c * rs for c in range(C)]
+        ptr = {f: P(*[b + off[f] for b in bases]) for f in ("idx", "codes", "norm", "tiles")}
     else:
-        pks = [StackedPacket(torch.empty(k, dtype=torch.int32, device=dev),
-                             torch.empty(max(k, 16), dtype=torch.uint8, device=dev),
-                             torch.empty(1, dtype=torch.float32, device=dev), n, levels,
-                             _tiles(n, dev) if with_tiles else None) for _ in range(C)]
-    arr = lambda vals: (ctypes.c_void_p * C)(*vals)  # noqa: E731
-    ws = workspace(dev, _lib.size("flc_stacked_encode_batch_workspace_size", n, k, C), "topk_batch")
-    call("flc_stacked_encode_batch", ctypes.cast(arr([x.data_ptr() for x in xs]), ctypes.c_void_p), C, n, k, levels,
-         ctypes.cast((ctypes.c_uint64 * C)(*[int(s) for s in seeds]), ctypes.c_void_p), counter,
-         ctypes.cast(arr([p.idx.data_ptr() for p in pks]), ctypes.c_void_p),
-         ctypes.cast(arr([p.codes.data_ptr() for p in pks]), ctypes.c_void_p),
-         ctypes.cast(arr([p.norm.data_ptr() for p in pks]), ctypes.c_void_p),
-         ctypes.cast(arr([p.tiles.data_ptr() for p in pks]), ctypes.c_void_p) if pks[0].tiles is not None else None,
-         _p(ws), ws.numel(), _stream(dev))
+        if wires is not None:
+            if len(wires) != C:
+                raise ValueError("one wire record per client")
+            pks = [wire_packet(r, n, k, levels) for r in wires]
+            ptr = {"idx": P(*[p.idx.data_ptr() for p in pks]), "codes": P(*[p.codes.data_ptr() for p in pks]),
+                   "norm": P(*[p.norm.data_ptr() for p in pks]), "tiles": P(*[p.tiles.data_ptr() for p in pks])}
+        else:  # one block per field, the packets its rows (views made in one unbind each)
+            ntl = (n + TILE - 1) // TILE + 1
+            kc = max(k, 16)
+            idx = torch.empty(C, k, dtype=torch.int32, device=dev)
+            codes = torch.empty(C, kc, dtype=torch.uint8, device=dev)
+            norm = torch.empty(C, 1, dtype=torch.float32, device=dev)
+            tiles = torch.empty(C, ntl, dtype=torch.int32, device=dev) if with_tiles else None
+            rows = zip(idx.unbind(0), codes.unbind(0), norm.unbind(0),
+                       tiles.unbind(0) if with_tiles else [None] * C)
+            pks = [StackedPacket(i_, c_, n_, n, levels, t_) for i_, c_, n_, t_ in rows]
+            b = {f: t.data_ptr() for f, t in (("idx", idx), ("codes", codes), ("norm", norm))}
+            ptr = {"idx": P(*[b["idx"] + 4 * k * c for c in range(C)]),
+                   "codes": P(*[b["codes"] + kc * c for c in range(C)]),
+                   "norm": P(*[b["norm"] + 4 * c for c in range(C)]),
+                   "tiles": P(*[tiles.data_ptr() + 4 * ntl * c for c in range(C)]) if with_tiles else None}
+    ws = workspace(dev, _ws_size("flc_stacked_encode_batch_workspace_size", n, k, C), "topk_batch")
+    vp = lambda a: None if a is None else ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+    call("flc_stacked_encode_batch", vp(P(*[x.data_ptr() for x in xs])), C, n, k, levels,
+         vp((ctypes.c_uint64 * C)(*[int(s_) for s_ in seeds])), counter, vp(ptr["idx"]), vp(ptr["codes"]),
+         vp(ptr["norm"]), vp(ptr["tiles"]), _p(ws), ws.numel(), _stream(dev))
     _after_encode(dev)
     return pks
 

@@ -152,9 +152,11 @@ struct SampleSetup {
   int take_all;
 };
 
-SampleSetup sample_setup(int64_t n, int64_t k) {
+// s_max: the sample size cap (kSample; a batched call of small clients takes fewer keys per client, because its
+// sample gathers cost one HBM line per key for every client while the floor / ceiling runs per client in parallel)
+SampleSetup sample_setup(int64_t n, int64_t k, int s_max = kSample) {
   SampleSetup s;
-  s.S = (int)(n < kSample ? n : kSample);
+  s.S = (int)(n < s_max ? n : s_max);
   const double m = (double)s.S * (double)k / (double)n;
   s.rank_lo = (long long)ceil(m + 4.0 * sqrt(m) + 16.0);
   const double rh = floor(m - 4.0 * sqrt(m) - 16.0);
@@ -170,9 +172,9 @@ SampleSetup sample_setup(int64_t n, int64_t k) {
 // area is empty up to 1 GiB inputs (M = 1 Mi: ~13 K candidates per block) and lets 2-8 GiB inputs keep their
 // candidates instead of re-reading x.
 constexpr int64_t kMaxOvf = 1ll << 17;
-SampleSetup sample_setup(int64_t n, int64_t k);
-unsigned ovf_capacity(int64_t n, int64_t k, int64_t M) {
-  const SampleSetup ss = sample_setup(n, k);
+SampleSetup sample_setup(int64_t n, int64_t k, int s_max);
+unsigned ovf_capacity(int64_t n, int64_t k, int64_t M, int s_max = kSample) {
+  const SampleSetup ss = sample_setup(n, k, s_max);
   const double frac = ss.take_all ? 1.0 : std::min(1.0, (double)ss.rank_lo / (double)ss.S);
   int64_t want = (int64_t)std::ceil(2.0 * frac * (double)M) + 4096 - kCap;
   want = std::min<int64_t>(std::min<int64_t>(want, kMaxOvf), M);
@@ -180,9 +182,10 @@ unsigned ovf_capacity(int64_t n, int64_t k, int64_t M) {
 }
 
 // staging + overflow bytes of one select over n elements with `cus` blocks at most
-size_t enc_var_bytes(int64_t n, int64_t k, int cus, EncGeom* geo, unsigned* ovf, size_t* off_ovf) {
+size_t enc_var_bytes(int64_t n, int64_t k, int cus, EncGeom* geo, unsigned* ovf, size_t* off_ovf,
+                     int s_max = kSample) {
   const EncGeom g = enc_geometry(n, cus);
-  const unsigned o = ovf_capacity(n, k, g.M);
+  const unsigned o = ovf_capacity(n, k, g.M, s_max);
   const size_t oo = al256((size_t)g.G * kCap * 8);
   if (geo) *geo = g;
   if (ovf) *ovf = o;
@@ -996,6 +999,14 @@ struct BatchEntry {
   float* norm;
   unsigned* tiles;
 };
+
+// batched: every client's header state, flags and histograms ([0, kOffBlk) of each kOffStage header) zeroed in one
+// launch at the start of a call (grid: blocks per header x headers)
+__global__ __launch_bounds__(256) void zero_headers_kernel(char* base, int n_words16) {
+  uint4* p = reinterpret_cast<uint4*>(base + (size_t)blockIdx.y * kOffStage);
+  for (int i = (int)blockIdx.x * 256 + (int)threadIdx.x; i < n_words16; i += (int)gridDim.x * 256)
+    p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
 
 // batched: `per` blocks sample each client into its own header
 __global__ __launch_bounds__(256) void topk_sample_batch_kernel(const BatchEntry* __restrict__ tab, int64_t n, int S,
@@ -2034,10 +2045,18 @@ struct BatchGeom {
   size_t table_off, need;
 };
 
+// keys per client of a batched call's sample: n / 128 rounded down to a power of two, within [4096, kSample]
+// (a 1 M-element client samples 8 K keys; 25 M and more the full 32 K)
+int batch_sample_cap(int64_t n) {
+  int s = 4096;
+  while (s < kSample && (int64_t)s * 2 * 128 <= n) s *= 2;
+  return s;
+}
+
 BatchGeom batch_geometry(int64_t n, int64_t k, int n_clients, int cus) {
   BatchGeom b;
   b.chunk = std::max(1, std::min(n_clients, cus));
-  b.vstride = enc_var_bytes(n, k, std::max(1, cus / b.chunk), &b.g, &b.ovf, &b.off_ovf);
+  b.vstride = enc_var_bytes(n, k, std::max(1, cus / b.chunk), &b.g, &b.ovf, &b.off_ovf, batch_sample_cap(n));
   b.table_off = (size_t)b.chunk * (kOffStage + b.vstride);
   b.need = b.table_off + al256((size_t)std::max(n_clients, 1) * sizeof(BatchEntry));
   return b;
@@ -2053,9 +2072,11 @@ int launch_topk_batch(const std::vector<BatchEntry>& ents, int64_t n, int64_t k,
   char* base = static_cast<char*>(ws);
   BatchEntry* tab = reinterpret_cast<BatchEntry*>(base + bg.table_off);
   FLC_CHECK_HIP(hipMemcpyAsync(tab, ents.data(), ents.size() * sizeof(BatchEntry), hipMemcpyHostToDevice, st));
-  // each call starts its headers from zero (state, flags, histograms): no history is carried between calls, so the
-  // header / staging split may move with the client count
-  FLC_CHECK_HIP(hipMemset2DAsync(base, kOffStage, 0, kOffBlk, (size_t)bg.chunk, st));
+  // each call starts its headers from zero (state, flags, histograms; one launch): no history is carried between
+  // calls, so the header / staging split may move with the client count
+  static_assert(kOffBlk % 16 == 0 && kOffStage % 16 == 0, "16-B zeroing of the headers");
+  FLC_LAUNCH("zero_headers", zero_headers_kernel, dim3(8, (unsigned)bg.chunk), dim3(256), 0, st, base,
+             (int)(kOffBlk / 16));
   EncWs w;
   w.base = base;
   w.var = base + (size_t)bg.chunk * kOffStage;
@@ -2066,7 +2087,7 @@ int launch_topk_batch(const std::vector<BatchEntry>& ents, int64_t n, int64_t k,
   w.nb = bg.g.G;
   w.vstride = bg.vstride;
   w.errp = reinterpret_cast<unsigned long long*>(base + kOffSt + offsetof(EncState, err));
-  const SampleSetup ss = sample_setup(n, k);
+  const SampleSetup ss = sample_setup(n, k, batch_sample_cap(n));
   const double step = 1.0 / (double)levels;
   SelectGate& gt = gate();
   std::lock_guard<std::mutex> lk(gt.mu);

@@ -138,7 +138,7 @@ class StackedWireCodec:
         from . import codec
 
         codec.stacked_encode_batch(deltas, self.k, self.levels, seeds=[self.seed + c for c in clients],
-                                   counter=self.counter, wires=[records[j] for j in range(len(deltas))])
+                                   counter=self.counter, wires=records[:len(deltas)])
 
     def fold(self, records: torch.Tensor, slots: Sequence[int], weights: Sequence[float],
              out: torch.Tensor) -> None:
