@@ -1975,6 +1975,35 @@ int device_cus(int dev) {
   return g.cus[dev];
 }
 
+// before a select launch (gt.mu held): not under capture, the first call on a second stream drains the device once,
+// and from then on the launch waits for the previous select's event
+int gate_enter(SelectGate& gt, int dev, hipStream_t st, bool* gated) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  FLC_CHECK_HIP(hipStreamIsCapturing(st, &cs));
+  *gated = cs == hipStreamCaptureStatusNone;
+  if (*gated) {
+    if (!gt.used[dev]) {
+      gt.used[dev] = true;
+      gt.first[dev] = st;
+    } else if (!gt.multi[dev] && st != gt.first[dev]) {
+      FLC_CHECK_HIP(hipDeviceSynchronize());
+      if (!gt.last[dev]) FLC_CHECK_HIP(hipEventCreateWithFlags(&gt.last[dev], hipEventDisableTiming));
+      gt.multi[dev] = true;
+    }
+    if (gt.multi[dev] && gt.recorded[dev]) FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
+  }
+  return FLC_OK;
+}
+
+// after it: record the chaining event once several streams are in use
+int gate_exit(SelectGate& gt, int dev, hipStream_t st, bool gated) {
+  if (gated && gt.multi[dev]) {
+    FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
+    gt.recorded[dev] = true;
+  }
+  return FLC_OK;
+}
+
 int current_cus(int* dev_out) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
@@ -2002,20 +2031,8 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
                ss.rank_hi, ss.take_all);
   SelectGate& gt = gate();
   std::lock_guard<std::mutex> lk(gt.mu);
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  FLC_CHECK_HIP(hipStreamIsCapturing(st, &cs));
-  const bool gated = cs == hipStreamCaptureStatusNone;
-  if (gated) {
-    if (!gt.used[dev]) {
-      gt.used[dev] = true;
-      gt.first[dev] = st;
-    } else if (!gt.multi[dev] && st != gt.first[dev]) {
-      FLC_CHECK_HIP(hipDeviceSynchronize());
-      if (!gt.last[dev]) FLC_CHECK_HIP(hipEventCreateWithFlags(&gt.last[dev], hipEventDisableTiming));
-      gt.multi[dev] = true;
-    }
-    if (gt.multi[dev] && gt.recorded[dev]) FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
-  }
+  bool gated = false;
+  if (int rc = gate_enter(gt, dev, st, &gated)) return rc;
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   if (split)
     FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", (topk_select_kernel<STACKED, false, Src>), dim3((unsigned)g.G),
@@ -2025,11 +2042,7 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
     FLC_LAUNCH(STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true, Src>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
                tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
-  if (gated && gt.multi[dev]) {
-    FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
-    gt.recorded[dev] = true;
-  }
-  return FLC_OK;
+  return gate_exit(gt, dev, st, gated);
 }
 
 // Batched stacked encode: the clients in chunks of at most `cus` (one select of cus / chunk blocks each, all in one
@@ -2091,20 +2104,8 @@ int launch_topk_batch(const std::vector<BatchEntry>& ents, int64_t n, int64_t k,
   const double step = 1.0 / (double)levels;
   SelectGate& gt = gate();
   std::lock_guard<std::mutex> lk(gt.mu);
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  FLC_CHECK_HIP(hipStreamIsCapturing(st, &cs));
-  const bool gated = cs == hipStreamCaptureStatusNone;
-  if (gated) {
-    if (!gt.used[dev]) {
-      gt.used[dev] = true;
-      gt.first[dev] = st;
-    } else if (!gt.multi[dev] && st != gt.first[dev]) {
-      FLC_CHECK_HIP(hipDeviceSynchronize());
-      if (!gt.last[dev]) FLC_CHECK_HIP(hipEventCreateWithFlags(&gt.last[dev], hipEventDisableTiming));
-      gt.multi[dev] = true;
-    }
-    if (gt.multi[dev] && gt.recorded[dev]) FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
-  }
+  bool gated = false;
+  if (int rc = gate_enter(gt, dev, st, &gated)) return rc;
   for (int c0 = 0; c0 < C; c0 += bg.chunk) {
     const int cn = std::min(bg.chunk, C - c0);
     const BatchEntry* t = tab + c0;
@@ -2117,11 +2118,7 @@ int launch_topk_batch(const std::vector<BatchEntry>& ents, int64_t n, int64_t k,
                dim3((unsigned)(cn * bg.g.G)), dim3(kET), 0, st, FlatSrc{nullptr}, n, (long long)k, w, nullptr, nullptr,
                nullptr, nullptr, levels, step, 0ull, counter, nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, t);
   }
-  if (gated && gt.multi[dev]) {
-    FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
-    gt.recorded[dev] = true;
-  }
-  return FLC_OK;
+  return gate_exit(gt, dev, st, gated);
 }
 
 int check_topk(const float* x, int64_t n, int64_t k, const char* who) {

@@ -114,3 +114,14 @@ def test_batch_overflow_modes_and_nan():
     for c in range(3):
         _same(pks[c], codec.stacked_encode(xs[c], k, 127, seed=1 + c, counter=8), f"x-mode/NaN client {c}")
     assert codec.topk_status() == 0
+
+
+def test_batch_without_tile_pointers():
+    n, k, C = 300_001, 3_000, 4
+    xs = [_x(n, 600 + c) for c in range(C)]
+    pks = codec.stacked_encode_batch(xs, k, 127, seeds=[c for c in range(C)], counter=1, with_tiles=False)
+    for c in range(C):
+        assert pks[c].tiles is None
+        _same(pks[c], codec.stacked_encode(xs[c], k, 127, seed=c, counter=1, with_tiles=False), f"client {c}")
+        ref = codec.stacked_decode(codec.stacked_encode(xs[c], k, 127, seed=c, counter=1))
+        assert torch.equal(codec.stacked_decode(pks[c]), ref)
