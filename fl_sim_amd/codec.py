@@ -441,6 +441,53 @@ def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, 
     return pks
 
 
+def stacked_encode_delta_batch(local_params: Sequence[Sequence[torch.Tensor]], global_params: Sequence[torch.Tensor],
+                               k: int, levels: int = 127, seeds: Sequence[int] = (),
+                               counter: int = 0) -> List[StackedPacket]:
+    """The delta-fused stacked encode of a round's clients in one launch (flc_stacked_encode_delta_batch): client c's
+    delta ``cat([l - g for l, g in zip(local_params[c], global_params)])`` (the global model shared by every client),
+    packet c equal to ``stacked_encode_delta(local_params[c], global_params, k, levels, seeds[c], counter)``."""
+    import ctypes
+
+    C = len(local_params)
+    if C == 0:
+        return []
+    ok = lambda t: t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 4 == 0  # noqa: E731
+    gs = [t if ok(t) else t.contiguous().float() for t in global_params]
+    ls = [[t if ok(t) else t.contiguous().float() for t in lp] for lp in local_params]
+    m = len(gs)
+    if m == 0 or any(len(lp) != m for lp in ls):
+        raise ValueError("every client has one local tensor per global tensor, at least one")
+    dev = gs[0].device
+    for lp in ls:
+        for a, b in zip(lp, gs):
+            if a.numel() != b.numel() or a.device != dev or b.device != dev or dev.type != "cuda":
+                raise ValueError("local and global tensors must be HIP tensors of matching sizes on one device")
+    n = sum(t.numel() for t in gs)
+    seeds = list(seeds) if len(seeds) else [0] * C
+    if len(seeds) != C:
+        raise ValueError("one seed per client")
+    ntl = (n + TILE - 1) // TILE + 1
+    kc = max(k, 16)
+    idx = torch.empty(C, k, dtype=torch.int32, device=dev)
+    codes = torch.empty(C, kc, dtype=torch.uint8, device=dev)
+    norm = torch.empty(C, 1, dtype=torch.float32, device=dev)
+    tiles = torch.empty(C, ntl, dtype=torch.int32, device=dev)
+    P = ctypes.c_void_p
+    vp = lambda a: ctypes.cast(a, P)  # noqa: E731
+    ws = workspace(dev, _ws_size("flc_stacked_encode_delta_batch_workspace_size", n, k, C, m), "topk_batch")
+    call("flc_stacked_encode_delta_batch", vp((P * (C * m))(*[t.data_ptr() for lp in ls for t in lp])),
+         vp((P * m)(*[t.data_ptr() for t in gs])), vp((ctypes.c_int64 * m)(*[t.numel() for t in gs])), m, C, k,
+         levels, vp((ctypes.c_uint64 * C)(*[int(s_) for s_ in seeds])), counter,
+         vp((P * C)(*[idx.data_ptr() + 4 * k * c for c in range(C)])),
+         vp((P * C)(*[codes.data_ptr() + kc * c for c in range(C)])),
+         vp((P * C)(*[norm.data_ptr() + 4 * c for c in range(C)])),
+         vp((P * C)(*[tiles.data_ptr() + 4 * ntl * c for c in range(C)])), _p(ws), ws.numel(), _stream(dev))
+    _after_encode(dev)
+    return [StackedPacket(i_, c_, n_, n, levels, t_)
+            for i_, c_, n_, t_ in zip(idx.unbind(0), codes.unbind(0), norm.unbind(0), tiles.unbind(0))]
+
+
 def stacked_encode_delta(local_params: Sequence[torch.Tensor], global_params: Sequence[torch.Tensor], k: int,
                          levels: int = 127, seed: int = 0, counter: int = 0) -> StackedPacket:
     """The stacked encode of the client delta ``cat([l - g for l, g in zip(local, global)])`` with the delta formed in

@@ -990,9 +990,11 @@ __global__ __launch_bounds__(256) void topk_sample_kernel(Src x, int64_t n, int 
   sample_one(x, n, S, w, blockIdx.x * 256 + threadIdx.x);
 }
 
-// one client of a batched call (flc_stacked_encode_batch): its input, Philox seed and outputs
+// one client of a batched call (flc_stacked_encode_batch[_delta]): its input, Philox seed and outputs.  `x` is the
+// client's flat delta, or (delta batch) its table of local parameter pointers; the kernel's source argument is the
+// prototype (the delta batch: offsets and global pointers shared by every client)
 struct BatchEntry {
-  const float* x;
+  const void* x;
   uint64_t seed;
   int* idx;
   uint8_t* codes;
@@ -1008,12 +1010,23 @@ __global__ __launch_bounds__(256) void zero_headers_kernel(char* base, int n_wor
     p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
+// client g's element source from the prototype and its batch entry
+__device__ __forceinline__ FlatSrc batch_src(const FlatSrc&, const BatchEntry& e) {
+  return FlatSrc{static_cast<const float*>(e.x)};
+}
+__device__ __forceinline__ DeltaSrc batch_src(const DeltaSrc& proto, const BatchEntry& e) {
+  DeltaSrc d = proto;
+  d.t.lp = static_cast<const float* const*>(e.x);
+  return d;
+}
+
 // batched: `per` blocks sample each client into its own header
-__global__ __launch_bounds__(256) void topk_sample_batch_kernel(const BatchEntry* __restrict__ tab, int64_t n, int S,
-                                                                EncWs w, int per) {
+template <class Src>
+__global__ __launch_bounds__(256) void topk_sample_batch_kernel(Src proto, const BatchEntry* __restrict__ tab,
+                                                                int64_t n, int S, EncWs w, int per) {
   const int g = (int)blockIdx.x / per;
   w.base += (size_t)g * kOffStage;
-  sample_one(FlatSrc{tab[g].x}, n, S, w, ((int)blockIdx.x - g * per) * 256 + (int)threadIdx.x);
+  sample_one(batch_src(proto, tab[g]), n, S, w, ((int)blockIdx.x - g * per) * 256 + (int)threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1225,7 +1238,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     w.base += (size_t)g * kOffStage;
     w.var += (size_t)g * w.vstride;
     const BatchEntry e = tab[g];
-    x = Src{e.x};
+    x = batch_src(x, e);
     seed = e.seed;
     idx_out = e.idx;
     code_out = e.codes;
@@ -2055,7 +2068,7 @@ struct BatchGeom {
   unsigned ovf;
   size_t off_ovf;  // from the client's staging area
   size_t vstride;
-  size_t table_off, need;
+  size_t table_off, extra_off, need;
 };
 
 // keys per client of a batched call's sample: n / 128 rounded down to a power of two, within [4096, kSample]
@@ -2066,25 +2079,33 @@ int batch_sample_cap(int64_t n) {
   return s;
 }
 
-BatchGeom batch_geometry(int64_t n, int64_t k, int n_clients, int cus) {
+// extra_bytes: the delta batch's tensor tables, after the entry table (at extra_off)
+BatchGeom batch_geometry(int64_t n, int64_t k, int n_clients, int cus, size_t extra_bytes = 0) {
   BatchGeom b;
   b.chunk = std::max(1, std::min(n_clients, cus));
   b.vstride = enc_var_bytes(n, k, std::max(1, cus / b.chunk), &b.g, &b.ovf, &b.off_ovf, batch_sample_cap(n));
   b.table_off = (size_t)b.chunk * (kOffStage + b.vstride);
-  b.need = b.table_off + al256((size_t)std::max(n_clients, 1) * sizeof(BatchEntry));
+  b.extra_off = b.table_off + al256((size_t)std::max(n_clients, 1) * sizeof(BatchEntry));
+  b.need = b.extra_off + al256(extra_bytes);
   return b;
 }
 
-int launch_topk_batch(const std::vector<BatchEntry>& ents, int64_t n, int64_t k, int levels, uint64_t counter,
-                      void* ws, size_t ws_bytes, hipStream_t st, const char* who) {
+// host: the entries, then `extra` (already holding device addresses inside the workspace), in one copy
+template <class Src>
+int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, const std::vector<char>& extra, int64_t n,
+                      int64_t k, int levels, uint64_t counter, void* ws, size_t ws_bytes, hipStream_t st,
+                      const char* who) {
   int dev = 0;
   const int cus = current_cus(&dev);
   const int C = (int)ents.size();
-  const BatchGeom bg = batch_geometry(n, k, C, cus);
+  const BatchGeom bg = batch_geometry(n, k, C, cus, extra.size());
   if (!ws || bg.need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, bg.need);
   char* base = static_cast<char*>(ws);
   BatchEntry* tab = reinterpret_cast<BatchEntry*>(base + bg.table_off);
-  FLC_CHECK_HIP(hipMemcpyAsync(tab, ents.data(), ents.size() * sizeof(BatchEntry), hipMemcpyHostToDevice, st));
+  std::vector<char> host(bg.extra_off - bg.table_off + extra.size(), 0);
+  std::memcpy(host.data(), ents.data(), ents.size() * sizeof(BatchEntry));
+  if (!extra.empty()) std::memcpy(host.data() + (bg.extra_off - bg.table_off), extra.data(), extra.size());
+  FLC_CHECK_HIP(hipMemcpyAsync(tab, host.data(), host.size(), hipMemcpyHostToDevice, st));
   // each call starts its headers from zero (state, flags, histograms; one launch): no history is carried between
   // calls, so the header / staging split may move with the client count
   static_assert(kOffBlk % 16 == 0 && kOffStage % 16 == 0, "16-B zeroing of the headers");
@@ -2111,12 +2132,12 @@ int launch_topk_batch(const std::vector<BatchEntry>& ents, int64_t n, int64_t k,
     const BatchEntry* t = tab + c0;
     if (!ss.take_all) {
       const int per = (int)cdiv(ss.S, 256);
-      FLC_LAUNCH("topk_sample_batch", topk_sample_batch_kernel, dim3((unsigned)(cn * per)), dim3(256), 0, st, t, n, ss.S,
-                 w, per);
+      FLC_LAUNCH("topk_sample_batch", topk_sample_batch_kernel<Src>, dim3((unsigned)(cn * per)), dim3(256), 0, st,
+                 proto, t, n, ss.S, w, per);
     }
-    FLC_LAUNCH("stacked_encode_batch", (topk_select_kernel<true, true, FlatSrc, true>),
-               dim3((unsigned)(cn * bg.g.G)), dim3(kET), 0, st, FlatSrc{nullptr}, n, (long long)k, w, nullptr, nullptr,
-               nullptr, nullptr, levels, step, 0ull, counter, nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, t);
+    FLC_LAUNCH("stacked_encode_batch", (topk_select_kernel<true, true, Src, true>), dim3((unsigned)(cn * bg.g.G)),
+               dim3(kET), 0, st, proto, n, (long long)k, w, nullptr, nullptr, nullptr, nullptr, levels, step, 0ull,
+               counter, nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, t);
   }
   return gate_exit(gt, dev, st, gated);
 }
@@ -2237,7 +2258,65 @@ int flc_stacked_encode_batch(const float* const* xs, int n_clients, int64_t n, i
     if (!idx[c] || !codes[c] || !norm[c]) return fail(FLC_EINVAL, "%s: null output of client %d", who, c);
     ents[c] = BatchEntry{xs[c], seeds[c], idx[c], codes[c], norm[c], tiles ? tiles[c] : nullptr};
   }
-  return launch_topk_batch(ents, n, k, levels, counter, ws, ws_bytes, as_stream(stream), who);
+  return launch_topk_batch(FlatSrc{nullptr}, ents, {}, n, k, levels, counter, ws, ws_bytes, as_stream(stream), who);
+}
+
+// the delta batch's tables: off[n_tensors + 1] (int64), the global pointers, then each client's local pointers
+size_t delta_batch_extra_bytes(int n_tensors, int n_clients) {
+  return (size_t)(n_tensors + 1) * 8 + (size_t)n_tensors * 8 + (size_t)n_clients * n_tensors * 8;
+}
+
+size_t flc_stacked_encode_delta_batch_workspace_size(int64_t n, int64_t k, int n_clients, int n_tensors) {
+  n_clients = n_clients < 1 ? 1 : n_clients;
+  n_tensors = n_tensors < 1 ? 1 : n_tensors;
+  return batch_geometry(n < 1 ? 1 : n, k < 1 ? 1 : k, n_clients, current_cus(nullptr),
+                        delta_batch_extra_bytes(n_tensors, n_clients)).need;
+}
+
+int flc_stacked_encode_delta_batch(const float* const* local, const float* const* global, const int64_t* sizes,
+                                   int n_tensors, int n_clients, int64_t k, int levels, const uint64_t* seeds,
+                                   uint64_t counter, int32_t* const* idx, uint8_t* const* codes, float* const* norm,
+                                   uint32_t* const* tiles, void* ws, size_t ws_bytes, void* stream) {
+  const char* who = "flc_stacked_encode_delta_batch";
+  if (n_tensors <= 0 || n_clients <= 0 || !local || !global || !sizes || !seeds || !idx || !codes || !norm)
+    return fail(FLC_EINVAL, "%s: bad arguments", who);
+  if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "%s: levels must be in [1, 127]", who);
+  std::vector<long long> off((size_t)n_tensors + 1, 0);
+  for (int t = 0; t < n_tensors; ++t) {
+    if (sizes[t] < 0) return fail(FLC_EINVAL, "%s: bad tensor %d", who, t);
+    if (sizes[t] > 0 && (!global[t] || (reinterpret_cast<uintptr_t>(global[t]) & 3u)))
+      return fail(FLC_EINVAL, "%s: global tensor %d is null or not 4-B aligned", who, t);
+    for (int c = 0; c < n_clients; ++c) {
+      const float* l = local[(size_t)c * n_tensors + t];
+      if (sizes[t] > 0 && (!l || (reinterpret_cast<uintptr_t>(l) & 3u)))
+        return fail(FLC_EINVAL, "%s: local tensor %d of client %d is null or not 4-B aligned", who, t, c);
+    }
+    off[t + 1] = off[t] + sizes[t];
+  }
+  const int64_t n = off[n_tensors];
+  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "%s: n must be < 2^31", who);
+  if (k <= 0 || k >= n) return fail(FLC_EINVAL, "%s: need 0 < k < n (got k=%lld, n=%lld)", who, (long long)k, (long long)n);
+  for (int c = 0; c < n_clients; ++c)
+    if (!idx[c] || !codes[c] || !norm[c]) return fail(FLC_EINVAL, "%s: null output of client %d", who, c);
+  const BatchGeom bg = batch_geometry(n, k, n_clients, current_cus(nullptr),
+                                      delta_batch_extra_bytes(n_tensors, n_clients));
+  if (!ws || bg.need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, bg.need);
+  char* dx = static_cast<char*>(ws) + bg.extra_off;  // the tables' device address
+  std::vector<char> extra(delta_batch_extra_bytes(n_tensors, n_clients), 0);
+  const size_t o_gp = off.size() * 8, o_lp = o_gp + (size_t)n_tensors * 8;
+  std::memcpy(extra.data(), off.data(), off.size() * 8);
+  std::memcpy(extra.data() + o_gp, global, (size_t)n_tensors * 8);
+  std::memcpy(extra.data() + o_lp, local, (size_t)n_clients * n_tensors * 8);
+  DeltaSrc proto;
+  proto.t.off = reinterpret_cast<const long long*>(dx);
+  proto.t.gp = reinterpret_cast<const float* const*>(dx + o_gp);
+  proto.t.lp = nullptr;
+  proto.t.nseg = n_tensors;
+  std::vector<BatchEntry> ents((size_t)n_clients);
+  for (int c = 0; c < n_clients; ++c)
+    ents[c] = BatchEntry{dx + o_lp + (size_t)c * n_tensors * 8, seeds[c], idx[c], codes[c], norm[c],
+                         tiles ? tiles[c] : nullptr};
+  return launch_topk_batch(proto, ents, extra, n, k, levels, counter, ws, ws_bytes, as_stream(stream), who);
 }
 
 int flc_topk_status(void* ws, uint64_t* err_out, int reset, void* stream) {

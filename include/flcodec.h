@@ -258,6 +258,17 @@ int flc_stacked_encode_batch(const float* const* xs, int n_clients, int64_t n, i
                              const uint64_t* seeds, uint64_t counter, int32_t* const* idx, uint8_t* const* codes,
                              float* const* norm, uint32_t* const* tiles, void* ws, size_t ws_bytes, void* stream);
 
+/* the batched encoder fused with the clients' deltas (f1 for a round's clients): client c's packet is
+ * bit-identical to flc_stacked_encode_delta(local + c * n_tensors, global, sizes, ...) with seeds[c].  local is a HOST
+ * array of n_clients * n_tensors device pointers, client-major (client c's tensors at [c * n_tensors, (c+1) *
+ * n_tensors)); global (n_tensors, shared by every client: the round's global model) and sizes are HOST arrays as in
+ * flc_stacked_encode_delta; outputs, seeds and the workspace as in flc_stacked_encode_batch. */
+size_t flc_stacked_encode_delta_batch_workspace_size(int64_t n, int64_t k, int n_clients, int n_tensors);
+int flc_stacked_encode_delta_batch(const float* const* local, const float* const* global, const int64_t* sizes,
+                                   int n_tensors, int n_clients, int64_t k, int levels, const uint64_t* seeds,
+                                   uint64_t counter, int32_t* const* idx, uint8_t* const* codes, float* const* norm,
+                                   uint32_t* const* tiles, void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------ other compressors
  * identical (compressors.py:273-275): out = +x;  lazy (276-283): out = x / p (fp32 division);
  * rand-k (284-292): out = 0, out[idx[j]] = scale * x[idx[j]] (idx in any order, unique). */

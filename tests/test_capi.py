@@ -146,6 +146,28 @@ def test_stacked_encode_batch_validates_without_gpu():
     assert 0 < a < b
 
 
+def test_stacked_encode_delta_batch_validates_without_gpu():
+    from fl_sim_amd import _lib
+
+    lib = _lib.load()
+    P2, P4 = ctypes.c_void_p * 2, ctypes.c_void_p * 4
+    c = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+    sizes, seeds = (ctypes.c_int64 * 2)(100, 100), (ctypes.c_uint64 * 2)(1, 2)
+    good2, good4 = P2(16, 32), P4(16, 32, 48, 64)
+    args = lambda loc, glob, k: (c(loc), c(glob), c(sizes), 2, 2, k, 127, c(seeds), 0, c(good2), c(good2), c(good2),  # noqa: E731
+                                 None, 16, 1 << 30, None)
+    assert lib.flc_stacked_encode_delta_batch(None, None, None, 2, 2, 10, 127, None, 0, None, None, None, None, 16,
+                                              1 << 30, None) == 1
+    assert lib.flc_stacked_encode_delta_batch(*args(P4(16, 32, 50, 64), good2, 10)) == 1  # client 1's tensor 0
+    assert "local tensor 0 of client 1" in lib.flc_last_error().decode()
+    assert lib.flc_stacked_encode_delta_batch(*args(good4, P2(16, 34), 10)) == 1
+    assert "global tensor 1" in lib.flc_last_error().decode()
+    assert lib.flc_stacked_encode_delta_batch(*args(good4, good2, 200)) == 1
+    assert "0 < k < n" in lib.flc_last_error().decode()
+    assert (lib.flc_stacked_encode_delta_batch_workspace_size(200, 2, 8, 2) >
+            lib.flc_stacked_encode_batch_workspace_size(200, 2, 8))
+
+
 def test_rccl_entries_validate_without_gpu():
     """The RCCL entries (flc_comm_* / flc_rccl_*) check their arguments before RCCL is touched; the unique id is
     RCCL's 128 bytes."""

@@ -125,3 +125,28 @@ def test_batch_without_tile_pointers():
         _same(pks[c], codec.stacked_encode(xs[c], k, 127, seed=c, counter=1, with_tiles=False), f"client {c}")
         ref = codec.stacked_decode(codec.stacked_encode(xs[c], k, 127, seed=c, counter=1))
         assert torch.equal(codec.stacked_decode(pks[c]), ref)
+
+
+def test_delta_batch_equals_single_delta_encodes():
+    # a round's clients: each local model = the shared global model + its own update, the delta formed in the pass
+    g = torch.Generator(device="cuda").manual_seed(700)
+    shapes = [(16, 1, 5, 5), (16,), (32, 16, 5, 5), (32,), (2048, 123), (123,), (62, 2048), (62,)]
+    glob = [torch.randn(*s, generator=g, device="cuda") for s in shapes]
+    C = 6
+    locs = [[t + torch.randn(*t.shape, generator=g, device="cuda") * 1e-3 for t in glob] for _ in range(C)]
+    n = sum(t.numel() for t in glob)
+    k = n // 100
+    pks = codec.stacked_encode_delta_batch(locs, glob, k, 127, seeds=[10 + c for c in range(C)], counter=4)
+    for c in range(C):
+        _same(pks[c], codec.stacked_encode_delta(locs[c], glob, k, 127, seed=10 + c, counter=4), f"client {c}")
+        _same(pks[c], codec.stacked_encode(codec.delta_flatten(locs[c], glob), k, 127, seed=10 + c, counter=4),
+              f"client {c} vs flat")
+    # 4-B aligned views (not 16-B) as the tensors
+    base = torch.randn(3 * 100_003 + 1, generator=g, device="cuda")
+    glob2 = [base[1:100_004], base[100_004:200_007]]
+    lbuf = torch.randn(3, 200_010, generator=g, device="cuda")
+    locs2 = [[lbuf[c, 3:100_006], lbuf[c, 100_006:200_009]] for c in range(3)]  # 4-B aligned views
+    pk2 = codec.stacked_encode_delta_batch(locs2, glob2, 2_000, 127, seeds=[1, 2, 3], counter=2)
+    for c in range(3):
+        _same(pk2[c], codec.stacked_encode_delta(locs2[c], glob2, 2_000, 127, seed=1 + c, counter=2), f"view {c}")
+    assert codec.topk_status() == 0

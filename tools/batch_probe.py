@@ -51,3 +51,14 @@ class OneByOne:
 t_r = tm(lambda: fdist.aggregate_round_wire(xs, w, C, wc, out=out))
 t_r1 = tm(lambda: fdist.aggregate_round_wire(xs, w, C, OneByOne, out=out))
 print(f"configs[3] wire round at N = 1: batched encode {t_r:8.1f} us, one encode launch per client {t_r1:8.1f} us")
+
+# f1 batched: the delta of 10 clients' local models (cnn-sized tensors, 401,306 parameters) against one global model
+shapes = [(16, 1, 5, 5), (16,), (32, 16, 5, 5), (32,), (2048, 123), (123,), (62, 2048), (62,)]
+glob = [torch.randn(*s, generator=g, device="cuda") for s in shapes]
+locs = [[t + torch.randn(*t.shape, generator=g, device="cuda") * 1e-3 for t in glob] for _ in range(10)]
+n = sum(t.numel() for t in glob)
+k = n // 100
+t_b = tm(lambda: codec.stacked_encode_delta_batch(locs, glob, k, 127, seeds=list(range(10)), counter=1))
+t_1 = tm(lambda: [codec.stacked_encode_delta(lp, glob, k, 127, seed=c, counter=1) for c, lp in enumerate(locs)])
+print(f"delta-fused, 10 clients x {n:,d}: batched {t_b:8.1f} us   one launch per client {t_1:8.1f} us   "
+      f"x{t_1 / t_b:.2f}")
