@@ -552,6 +552,32 @@ def main():
             "plain_encode_us": (extra.get("kernels_us") or {}).get("stacked_encode"),
         }
         del L5, G5, o5
+        # a round's many small clients on one GPU (fl-sim's usual case): the stacked encode of 100 clients x 1 M and
+        # the delta-fused encode of 10 clients x cnn_femmist-sized tensors, one batched launch against one per client
+        gb = torch.Generator(device=dev).manual_seed(77 + rank)
+        xs_b = [torch.randn(1_000_000, generator=gb, device=dev) * 1e-3 for _ in range(100)]
+        kb = 10_000
+        msb, _ = timed(lambda: codec.stacked_encode_batch(xs_b, kb, LEVELS, seeds=list(range(100)), counter=1),
+                       10, 3, world)
+        msb1, _ = timed(lambda: [codec.stacked_encode(x, kb, LEVELS, seed=i, counter=1) for i, x in enumerate(xs_b)],
+                        5, 1, world)
+        shp = [(16, 1, 5, 5), (16,), (32, 16, 5, 5), (32,), (2048, 123), (123,), (62, 2048), (62,)]
+        glb = [torch.randn(*s, generator=gb, device=dev) for s in shp]
+        lcs = [[t + torch.randn(*t.shape, generator=gb, device=dev) * 1e-3 for t in glb] for _ in range(10)]
+        nd = sum(t.numel() for t in glb)
+        msd, _ = timed(lambda: codec.stacked_encode_delta_batch(lcs, glb, nd // 100, LEVELS, seeds=list(range(10)),
+                                                                counter=1), 10, 3, world)
+        msd1, _ = timed(lambda: [codec.stacked_encode_delta(lp, glb, nd // 100, LEVELS, seed=i, counter=1)
+                                 for i, lp in enumerate(lcs)], 10, 3, world)
+        extra["batched_round_encodes"] = {
+            "stacked_100x1M_ms": round(max_over_ranks(msb, world), 4),
+            "stacked_100x1M_one_launch_per_client_ms": round(max_over_ranks(msb1, world), 4),
+            "delta_10x%d_ms" % nd: round(max_over_ranks(msd, world), 4),
+            "delta_10x%d_one_launch_per_client_ms" % nd: round(max_over_ranks(msd1, world), 4),
+            "note": "flc_stacked_encode_batch / flc_stacked_encode_delta_batch: every client's select on its share of "
+                    "the CUs in one launch, packets bit-identical to the per-client encodes (DESIGN.md 3.1b)",
+        }
+        del xs_b, glb, lcs
         torch.cuda.empty_cache()
         from fl_sim_amd import dist as fdist
 
