@@ -103,3 +103,30 @@ def test_gloo_world2_reduce_matches_single_process():
     assert np.all(np.abs(reduced.astype(np.float64) - single) <= tol)
     assert np.array_equal(allred[0], allred[1])
     assert np.all(np.abs(allred[0].astype(np.float64) - single) <= tol)
+
+
+def test_fold_dispatches_to_a_batched_codec_step():
+    """A codec step with a ``many`` attribute (the batched encoders' form, dist.stacked_decode_accumulate) gets the
+    rank's clients in one call, in client order, when it owns more than one; a single client goes through the step
+    itself.  The fold equals the per-client one."""
+    calls = []
+
+    def step(delta, w, acc, client):
+        calls.append(("one", client))
+        _cpu_topk_step(delta, w, acc, client)
+
+    def many(deltas, weights, acc, clients):
+        calls.append(("many", tuple(clients)))
+        for d, w, c in zip(deltas, weights, clients):
+            _cpu_topk_step(d, float(w), acc, c)
+
+    step.many = many
+    deltas = _deltas()
+    w = fdist.sample_weights(TS)
+    got = fdist.aggregate_round(deltas, w, list(range(N_CLIENTS)), step)
+    assert calls == [("many", tuple(range(N_CLIENTS)))]
+    ref_out = fdist.aggregate_round(deltas, w, list(range(N_CLIENTS)), _cpu_topk_step)
+    assert np.array_equal(got.numpy().view(np.uint32), ref_out.numpy().view(np.uint32))
+    calls.clear()
+    fdist.aggregate_round(deltas[:1], w[:1], [0], step)
+    assert calls == [("one", 0)]
