@@ -64,12 +64,25 @@ class OracleWireCodec:
             out.add_(self.decode(records[s]), alpha=float(np.float32(w)))
 
 
+class BatchedOracleWireCodec(OracleWireCodec):
+    """The same codec with the batched entry point (dist.StackedWireCodec.encode_many_into's form): a rank's clients
+    in one call, records[j] for clients[j]."""
+
+    calls = []
+
+    def encode_many_into(self, deltas, records, clients):
+        type(self).calls.append(tuple(clients))
+        assert records.shape[0] >= len(deltas)
+        for j, (d, c) in enumerate(zip(deltas, clients)):
+            self.encode_into(d, records[j], c)
+
+
 def _single(deltas, w):
     wc = OracleWireCodec(D, K)
     return fdist.aggregate_round_wire(deltas, w, N_CLIENTS, wc, device=torch.device("cpu"))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, batched=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -77,7 +90,7 @@ def _worker(rank, world, port, q):
         deltas = _deltas()
         w = fdist.sample_weights(TS)
         mine = fdist.client_shard(N_CLIENTS, world, rank)
-        wc = OracleWireCodec(D, K)
+        wc = BatchedOracleWireCodec(D, K) if batched else OracleWireCodec(D, K)
         res = fdist.aggregate_round_wire([deltas[c] for c in mine], w, N_CLIENTS, wc, device=torch.device("cpu"))
         q.put((rank, res.numpy().copy()))
         res0 = fdist.aggregate_round_wire([deltas[c] for c in mine], w, N_CLIENTS, wc, dst=0,
@@ -125,6 +138,15 @@ def test_single_process_wire_round_is_the_sequential_fold():
     assert np.array_equal(got.view(np.uint32), exp.numpy().view(np.uint32))
 
 
+def test_single_process_batched_codec_gets_all_clients_in_one_call():
+    deltas = _deltas()
+    w = fdist.sample_weights(TS)
+    BatchedOracleWireCodec.calls = []
+    got = fdist.aggregate_round_wire(deltas, w, N_CLIENTS, BatchedOracleWireCodec(D, K), device=torch.device("cpu"))
+    assert BatchedOracleWireCodec.calls == [tuple(range(N_CLIENTS))]
+    assert np.array_equal(got.numpy().view(np.uint32), _single(deltas, w).numpy().view(np.uint32))
+
+
 def test_wire_round_rejects_wrong_shard():
     deltas = _deltas()
     w = fdist.sample_weights(TS)
@@ -134,12 +156,12 @@ def test_wire_round_rejects_wrong_shard():
         fdist.aggregate_round_wire(deltas, w[:2], N_CLIENTS, OracleWireCodec(D, K), device=torch.device("cpu"))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_wire_round_is_bit_identical_to_single_process(world):
+@pytest.mark.parametrize("world,batched", [(2, False), (3, False), (2, True)])
+def test_gloo_wire_round_is_bit_identical_to_single_process(world, batched):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, batched)) for r in range(world)]
     for p in procs:
         p.start()
     items = dict(q.get(timeout=180) for _ in range(2 * world))
