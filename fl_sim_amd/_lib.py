@@ -81,6 +81,10 @@ SIGNATURES = {
         [c_void_p, c_int, c_int64, c_int64, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_size_t, c_void_p],
     ),
+    "flc_topk_encode_batch_workspace_size": (c_size_t, [c_int64, c_int64, c_int]),
+    "flc_topk_encode_batch": (
+        c_int, [c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    ),
     "flc_stacked_encode_delta_batch_workspace_size": (c_size_t, [c_int64, c_int64, c_int, c_int]),
     "flc_stacked_encode_delta_batch": (
         c_int,

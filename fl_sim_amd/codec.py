@@ -273,6 +273,34 @@ def topk_encode(x: torch.Tensor, k: int, with_tiles: bool = False):
     return (idx, val, tiles) if with_tiles else (idx, val)
 
 
+def topk_encode_batch(xs: Sequence[torch.Tensor], k: int, with_tiles: bool = False):
+    """The top-k of many clients' flat deltas (one size) in one launch (flc_topk_encode_batch): entry c equals
+    ``topk_encode(xs[c], k, with_tiles)``."""
+    import ctypes
+
+    xs = [_dev_f32(x).reshape(-1) for x in xs]
+    C = len(xs)
+    if C == 0:
+        return []
+    n, dev = xs[0].numel(), xs[0].device
+    if any(x.numel() != n or x.device != dev for x in xs):
+        raise ValueError("a batched encode takes clients of one size on one device")
+    ntl = (n + TILE - 1) // TILE + 1
+    idx = torch.empty(C, k, dtype=torch.int32, device=dev)
+    val = torch.empty(C, k, dtype=torch.float32, device=dev)
+    tiles = torch.empty(C, ntl, dtype=torch.int32, device=dev) if with_tiles else None
+    P = ctypes.c_void_p * C
+    vp = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+    ws = workspace(dev, _ws_size("flc_topk_encode_batch_workspace_size", n, k, C), "topk_batch")
+    call("flc_topk_encode_batch", vp(P(*[x.data_ptr() for x in xs])), C, n, k,
+         vp(P(*[idx.data_ptr() + 4 * k * c for c in range(C)])), vp(P(*[val.data_ptr() + 4 * k * c for c in range(C)])),
+         vp(P(*[tiles.data_ptr() + 4 * ntl * c for c in range(C)])) if with_tiles else None, _p(ws), ws.numel(),
+         _stream(dev))
+    _after_encode(dev)
+    rows = zip(idx.unbind(0), val.unbind(0), tiles.unbind(0) if with_tiles else [None] * C)
+    return [(i_, v_, t_) if with_tiles else (i_, v_) for i_, v_, t_ in rows]
+
+
 def sparse_decode(idx: torch.Tensor, val: torch.Tensor, n: int, scale: float = 1.0, out: Optional[torch.Tensor] = None,
                   weight: float = 1.0, accumulate: bool = False, tiles: Optional[torch.Tensor] = None) -> torch.Tensor:
     if out is None:

@@ -1000,6 +1000,7 @@ struct BatchEntry {
   uint8_t* codes;
   float* norm;
   unsigned* tiles;
+  float* val;  // plain top-k batch (flc_topk_encode_batch): the kept values
 };
 
 // batched: every client's header state, flags and histograms ([0, kOffBlk) of each kOffStage header) zeroed in one
@@ -1232,7 +1233,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
                                                           long long rank_hi, int take_all,
                                                           const BatchEntry* __restrict__ tab = nullptr) {
   if constexpr (BATCH) {
-    static_assert(STACKED && FUSED, "batched selects are the fused stacked encode");
+    static_assert(FUSED, "batched selects are the fused encode");
     const int g = (int)blockIdx.x / w.nb;  // (w.nb: blocks per client, set by the host)
     w.bid = (int)blockIdx.x - g * w.nb;
     w.base += (size_t)g * kOffStage;
@@ -1242,6 +1243,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     seed = e.seed;
     idx_out = e.idx;
     code_out = e.codes;
+    val_out = e.val;
     norm_out = e.norm;
     tile_out = e.tiles;
   } else {
@@ -2091,7 +2093,7 @@ BatchGeom batch_geometry(int64_t n, int64_t k, int n_clients, int cus, size_t ex
 }
 
 // host: the entries, then `extra` (already holding device addresses inside the workspace), in one copy
-template <class Src>
+template <class Src, bool STACKED = true>
 int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, const std::vector<char>& extra, int64_t n,
                       int64_t k, int levels, uint64_t counter, void* ws, size_t ws_bytes, hipStream_t st,
                       const char* who) {
@@ -2122,7 +2124,7 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
   w.vstride = bg.vstride;
   w.errp = reinterpret_cast<unsigned long long*>(base + kOffSt + offsetof(EncState, err));
   const SampleSetup ss = sample_setup(n, k, batch_sample_cap(n));
-  const double step = 1.0 / (double)levels;
+  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   SelectGate& gt = gate();
   std::lock_guard<std::mutex> lk(gt.mu);
   bool gated = false;
@@ -2135,7 +2137,8 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
       FLC_LAUNCH("topk_sample_batch", topk_sample_batch_kernel<Src>, dim3((unsigned)(cn * per)), dim3(256), 0, st,
                  proto, t, n, ss.S, w, per);
     }
-    FLC_LAUNCH("stacked_encode_batch", (topk_select_kernel<true, true, Src, true>), dim3((unsigned)(cn * bg.g.G)),
+    FLC_LAUNCH(STACKED ? "stacked_encode_batch" : "topk_encode_batch", (topk_select_kernel<STACKED, true, Src, true>),
+               dim3((unsigned)(cn * bg.g.G)),
                dim3(kET), 0, st, proto, n, (long long)k, w, nullptr, nullptr, nullptr, nullptr, levels, step, 0ull,
                counter, nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, t);
   }
@@ -2256,9 +2259,27 @@ int flc_stacked_encode_batch(const float* const* xs, int n_clients, int64_t n, i
   for (int c = 0; c < n_clients; ++c) {
     if (int rc = check_topk(xs[c], n, k, who)) return rc;
     if (!idx[c] || !codes[c] || !norm[c]) return fail(FLC_EINVAL, "%s: null output of client %d", who, c);
-    ents[c] = BatchEntry{xs[c], seeds[c], idx[c], codes[c], norm[c], tiles ? tiles[c] : nullptr};
+    ents[c] = BatchEntry{xs[c], seeds[c], idx[c], codes[c], norm[c], tiles ? tiles[c] : nullptr, nullptr};
   }
   return launch_topk_batch(FlatSrc{nullptr}, ents, {}, n, k, levels, counter, ws, ws_bytes, as_stream(stream), who);
+}
+
+size_t flc_topk_encode_batch_workspace_size(int64_t n, int64_t k, int n_clients) {
+  return flc_stacked_encode_batch_workspace_size(n, k, n_clients);
+}
+
+int flc_topk_encode_batch(const float* const* xs, int n_clients, int64_t n, int64_t k, int32_t* const* idx,
+                          float* const* val, uint32_t* const* tiles, void* ws, size_t ws_bytes, void* stream) {
+  const char* who = "flc_topk_encode_batch";
+  if (n_clients <= 0 || !xs || !idx || !val) return fail(FLC_EINVAL, "%s: bad arguments", who);
+  std::vector<BatchEntry> ents((size_t)n_clients);
+  for (int c = 0; c < n_clients; ++c) {
+    if (int rc = check_topk(xs[c], n, k, who)) return rc;
+    if (!idx[c] || !val[c]) return fail(FLC_EINVAL, "%s: null output of client %d", who, c);
+    ents[c] = BatchEntry{xs[c], 0, idx[c], nullptr, nullptr, tiles ? tiles[c] : nullptr, val[c]};
+  }
+  return launch_topk_batch<FlatSrc, false>(FlatSrc{nullptr}, ents, {}, n, k, 0, 0, ws, ws_bytes, as_stream(stream),
+                                           who);
 }
 
 // the delta batch's tables: off[n_tensors + 1] (int64), the global pointers, then each client's local pointers
@@ -2315,7 +2336,7 @@ int flc_stacked_encode_delta_batch(const float* const* local, const float* const
   std::vector<BatchEntry> ents((size_t)n_clients);
   for (int c = 0; c < n_clients; ++c)
     ents[c] = BatchEntry{dx + o_lp + (size_t)c * n_tensors * 8, seeds[c], idx[c], codes[c], norm[c],
-                         tiles ? tiles[c] : nullptr};
+                         tiles ? tiles[c] : nullptr, nullptr};
   return launch_topk_batch(proto, ents, extra, n, k, levels, counter, ws, ws_bytes, as_stream(stream), who);
 }
 

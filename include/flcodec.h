@@ -258,6 +258,13 @@ int flc_stacked_encode_batch(const float* const* xs, int n_clients, int64_t n, i
                              const uint64_t* seeds, uint64_t counter, int32_t* const* idx, uint8_t* const* codes,
                              float* const* norm, uint32_t* const* tiles, void* ws, size_t ws_bytes, void* stream);
 
+/* plain top-k of many clients in one launch (compressors.py:293-296 per client): client c's (idx, val, tiles) equal
+ * flc_topk_encode_tiled(xs[c], n, k, ...); arrays and workspace as in flc_stacked_encode_batch (the two share a
+ * workspace size). */
+size_t flc_topk_encode_batch_workspace_size(int64_t n, int64_t k, int n_clients);
+int flc_topk_encode_batch(const float* const* xs, int n_clients, int64_t n, int64_t k, int32_t* const* idx,
+                          float* const* val, uint32_t* const* tiles, void* ws, size_t ws_bytes, void* stream);
+
 /* the batched encoder fused with the clients' deltas (f1 for a round's clients): client c's packet is
  * bit-identical to flc_stacked_encode_delta(local + c * n_tensors, global, sizes, ...) with seeds[c].  local is a HOST
  * array of n_clients * n_tensors device pointers, client-major (client c's tensors at [c * n_tensors, (c+1) *

@@ -168,6 +168,20 @@ def test_stacked_encode_delta_batch_validates_without_gpu():
             lib.flc_stacked_encode_batch_workspace_size(200, 2, 8))
 
 
+def test_topk_encode_batch_validates_without_gpu():
+    from fl_sim_amd import _lib
+
+    lib = _lib.load()
+    P = ctypes.c_void_p * 2
+    c = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
+    assert lib.flc_topk_encode_batch(None, 2, 100, 10, None, None, None, 16, 1 << 30, None) == 1
+    assert lib.flc_topk_encode_batch(c(P(16, 40)), 2, 100, 10, c(P(16, 32)), c(P(16, 32)), None, 16, 1 << 30, None) == 1
+    assert "aligned" in lib.flc_last_error().decode()
+    assert lib.flc_topk_encode_batch(c(P(16, 32)), 2, 100, 10, c(P(16, 32)), c(P(16, 0)), None, 16, 1 << 30, None) == 1
+    assert "null output of client 1" in lib.flc_last_error().decode()
+    assert lib.flc_topk_encode_batch_workspace_size(1000, 10, 4) == lib.flc_stacked_encode_batch_workspace_size(1000, 10, 4)
+
+
 def test_rccl_entries_validate_without_gpu():
     """The RCCL entries (flc_comm_* / flc_rccl_*) check their arguments before RCCL is touched; the unique id is
     RCCL's 128 bytes."""

@@ -150,3 +150,17 @@ def test_delta_batch_equals_single_delta_encodes():
     for c in range(3):
         _same(pk2[c], codec.stacked_encode_delta(locs2[c], glob2, 2_000, 127, seed=1 + c, counter=2), f"view {c}")
     assert codec.topk_status() == 0
+
+
+@pytest.mark.parametrize("with_tiles", [False, True])
+def test_topk_batch_equals_single_topk(with_tiles):
+    n, k, C = 1_000_003, 10_000, 5
+    kinds = ["randn", "zeros", "ties", "skew", "randn"]
+    xs = [_x(n, 800 + c, kinds[c]) for c in range(C)]
+    got = codec.topk_encode_batch(xs, k, with_tiles=with_tiles)
+    for c in range(C):
+        ref = codec.topk_encode(xs[c], k, with_tiles=with_tiles)
+        assert torch.equal(got[c][0], ref[0]) and torch.equal(got[c][1].view(torch.int32), ref[1].view(torch.int32))
+        if with_tiles:
+            assert torch.equal(got[c][2], ref[2])
+    assert codec.topk_status() == 0
