@@ -407,10 +407,17 @@ class Compressor:
 
     # ------------------------------------------------------------------ extensions
     def compressBatch(self, X: torch.Tensor) -> torch.Tensor:
-        """[clients, d] batch of deltas in one launch per kernel (dithering types), philox RNG."""
+        """[clients, d] batch of deltas in one launch per kernel (dithering types, philox RNG; top-k: the clients'
+        selects in one launch, flc_topk_encode_batch, each row then decoded)."""
         t = self.compressorType
+        if t == CompressorType.TOPK_COMPRESSOR:
+            X2 = X.reshape(X.shape[0], -1)
+            out = torch.empty_like(X2)
+            for c, (idx, val, tiles) in enumerate(codec.topk_encode_batch(list(X2.unbind(0)), int(self.K), True)):
+                codec.sparse_decode(idx, val, X2.shape[1], out=out[c], tiles=tiles)
+            return out.reshape(X.shape)
         if t not in _STD and t not in _NATD:
-            raise NotImplementedError("compressBatch: dithering compressors only")
+            raise NotImplementedError("compressBatch: dithering and top-k compressors only")
         kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
         seed, ctr = self.philox.next()
         return codec.quant_encode_auto(X, kind, self.s, self.p, seed, ctr)[1]

@@ -164,3 +164,25 @@ def test_topk_batch_equals_single_topk(with_tiles):
         if with_tiles:
             assert torch.equal(got[c][2], ref[2])
     assert codec.topk_status() == 0
+
+
+def test_compressor_compress_batch():
+    """Compressor.compressBatch: top-k rows through the batched select equal the per-row top-k + decode; the
+    dithering batch equals quant_encode_auto of the same batch with the compressor's (seed, counter)."""
+    from fl_sim_amd import Compressor
+
+    g = torch.Generator(device="cuda").manual_seed(900)
+    X = torch.randn(6, 50_000, generator=g, device="cuda") * 1e-3
+    c = Compressor(rng="philox", seed=5)
+    c.makeTopKCompressor(500, 50_000)
+    got = c.compressBatch(X)
+    for r in range(6):
+        idx, val, tiles = codec.topk_encode(X[r], 500, with_tiles=True)
+        assert torch.equal(got[r], codec.sparse_decode(idx, val, 50_000, tiles=tiles))
+    nc = Compressor("norm")
+    nc.makeIdenticalCompressor()
+    d = Compressor(rng="philox", seed=5)
+    d.makeStandardDitheringFP32(8, nc)
+    seed, ctr = d.philox.seed, d.philox.counter
+    got = d.compressBatch(X)
+    assert torch.equal(got, codec.quant_encode_auto(X, 0, d.s, d.p, seed, ctr)[1])
