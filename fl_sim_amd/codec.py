@@ -379,13 +379,8 @@ def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, co
     if out is not None:
         if out.n != n or out.idx.numel() != k or out.idx.device != x.device or (with_tiles and out.tiles is None):
             raise ValueError("`out` must be a packet of the same n and k on the input's device")
-        pk = StackedPacket(out.idx, out.codes, out.norm, n, levels, out.tiles if with_tiles else None)
-        ws = workspace(x.device, _ws_size("flc_topk_workspace_size", n, k), "topk")
-        call("flc_stacked_encode_tiled", _p(x), n, k, levels, seed, counter, None, _p(pk.idx), _p(pk.codes),
-             _p(pk.norm), _p(pk.tiles), _p(ws), ws.numel(), _stream(x.device))
-        _after_encode(x.device)
-        return pk
-    if wire is not None:
+        idx, codes, norm, tiles = out.idx, out.codes, out.norm, out.tiles if with_tiles else None
+    elif wire is not None:
         if wire.device != x.device:
             raise ValueError("the wire record must be on the input's device")
         pk = wire_packet(wire, n, k, levels)
