@@ -60,11 +60,14 @@ def stacked_decode_accumulate(k: int, levels: int = 127, seed: int = 0, counter:
 
     def many(deltas: Sequence[torch.Tensor], weights: Sequence[float], acc: torch.Tensor,
              clients: Sequence[int]) -> None:
-        """The rank's clients encoded in one batched launch, then decoded into ``acc`` in client order: the same
-        packets and the same fmaf chain as one ``step`` per client."""
-        pkts = codec.stacked_encode_batch(deltas, k, levels, seeds=[seed + c for c in clients], counter=counter)
-        for pkt, w in zip(pkts, weights):
-            codec.stacked_decode(pkt, out=acc, weight=float(w), accumulate=True)
+        """The rank's clients encoded in one batched launch into packed wire records, then all of them decoded into
+        ``acc`` in client order in one pass (flc_stacked_fold_wires): the same packets and the same fmaf chain as one
+        ``step`` per client."""
+        n = acc.numel()
+        recs = torch.empty(len(deltas), codec.stacked_wire_layout(n, k)[0], dtype=torch.uint8, device=acc.device)
+        codec.stacked_encode_batch(deltas, k, levels, seeds=[seed + c for c in clients], counter=counter, wires=recs)
+        codec.stacked_fold_wires(recs, list(range(len(deltas))), [float(w) for w in weights], n, k, levels, out=acc,
+                                 accumulate=True)
 
     step.many = many
     return step
