@@ -191,10 +191,11 @@ def _time_reps(fn, budget_s: float, max_reps: int, warm: bool = True):
 
 
 def cpu_baseline():
-    """north_star's CPU baseline: the CPU-PyTorch path of the same workload (oracle/torch_ref.py: torch.topk,
-    the dithering, a dense scatter) on this host's cores, all threads on the full 1 GiB delta and one thread
-    on a 64 MiB sample; the numpy oracle (oracle/compressors_ref.py, one core) on the 64 MiB sample is kept as
-    a separately labelled field.  Rates use the same algorithmic bytes as `value` (8 D + 10 K)."""
+    """north_star's CPU baseline: the CPU-PyTorch path of the same workload (oracle/torch_ref.py: torch.topk, the
+    dithering, a dense scatter) on this host's cores, on the full 1 GiB delta at 1 thread, at 16 threads (the box's
+    CPU share per GPU) and at all threads; ``value`` is the best of the three, the others are labelled beside it.
+    The numpy oracle (oracle/compressors_ref.py, one core) on a 64 MiB sample is a separately labelled field.  Rates
+    use the same algorithmic bytes as `value` (8 D + 10 K)."""
     from oracle import compressors_ref as ref
     from oracle import torch_ref
 
@@ -206,52 +207,81 @@ def cpu_baseline():
         affinity = all_threads
     gen = torch.Generator().manual_seed(1234)
     x_full = torch.randn(D_HEADLINE, generator=gen) * 1e-3
+    K = D_HEADLINE // 100
     n_s = 16_777_216  # 64 MiB sample, same K/D ratio
-    x_s = x_full[:n_s].clone()
-
-    torch.set_num_threads(all_threads)
-    torch_ref.stacked_step(x_s, n_s // 100, LEVELS, gen)  # warm the pool on the sample, not on 1 GiB
-    per_all, reps_all = _time_reps(lambda: torch_ref.stacked_step(x_full, D_HEADLINE // 100, LEVELS, gen), 8.0, 3,
-                                   warm=False)
-    share = min(16, all_threads)  # the GPU box's CPU share per GPU
-    torch.set_num_threads(share)
-    per_share, reps_share = _time_reps(lambda: torch_ref.stacked_step(x_s, n_s // 100, LEVELS, gen), 4.0, 3)
-    torch.set_num_threads(1)
-    per_one, reps_one = _time_reps(lambda: torch_ref.stacked_step(x_s, n_s // 100, LEVELS, gen), 4.0, 3)
+    torch_ref.stacked_step(x_full[:n_s].clone(), n_s // 100, LEVELS, gen)  # warm the pool on a sample
+    runs = {}
+    for th in sorted({1, min(16, all_threads), all_threads}):
+        torch.set_num_threads(th)
+        per, reps = _time_reps(lambda: torch_ref.stacked_step(x_full, K, LEVELS, gen), 6.0, 2, warm=False)
+        runs[th] = (per, reps)
     torch.set_num_threads(threads0)
+    best = min(runs, key=lambda t: runs[t][0])
+    per_b, reps_b = runs[best]
+    xs = x_full[:n_s].numpy().copy()
     del x_full
-
-    xs = x_s.numpy()
     per_np, reps_np = _time_reps(
         lambda: ref.stacked(xs, n_s // 100, LEVELS, lambda i: ref.philox_uniforms_at(i, 1, 0)), 4.0, 3)
     model = cpu_model()
-    return {
-        "value": round(stacked_bytes(D_HEADLINE, D_HEADLINE // 100) / per_all / 1e9, 4),
+    line = {
+        "value": round(stacked_bytes(D_HEADLINE, K) / per_b / 1e9, 4),
         "unit": "GB/s",
-        "cores": all_threads,
+        "cores": best,
         "kind": "port",
         "sample": f"CPU-PyTorch stacked top-k 1% -> 8-bit dither (oracle/torch_ref.py: torch.topk + dither + dense "
-                  f"scatter) on the full 1 GiB delta, torch.set_num_threads({all_threads}) = os.cpu_count(), "
-                  f"{reps_all} reps, {per_all * 1e3:.0f} ms/rep; {model}; {affinity} CPUs in this process's "
-                  f"affinity mask",
+                  f"scatter) on the full 1 GiB delta; best of 1 / 16 / {all_threads} threads = {best} threads, "
+                  f"{reps_b} reps, {per_b * 1e3:.0f} ms/rep; {model}; {affinity} CPUs in this process's affinity mask",
         "cpu_model": model,
         "affinity_cpus": affinity,
-        "one_thread": {
-            "value": round(stacked_bytes(n_s, n_s // 100) / per_one / 1e9, 4), "unit": "GB/s", "cores": 1,
-            "sample": f"same CPU-PyTorch path, torch.set_num_threads(1), 64 MiB sample (D={n_s}), {reps_one} reps, "
-                      f"{per_one * 1e3:.0f} ms/rep",
-        },
-        f"threads_{share}": {
-            "value": round(stacked_bytes(n_s, n_s // 100) / per_share / 1e9, 4), "unit": "GB/s", "cores": share,
-            "sample": f"same CPU-PyTorch path, torch.set_num_threads({share}), 64 MiB sample, {reps_share} reps, "
-                      f"{per_share * 1e3:.0f} ms/rep",
-        },
+        "threads": {str(t): {"value": round(stacked_bytes(D_HEADLINE, K) / runs[t][0] / 1e9, 4), "unit": "GB/s",
+                             "ms_per_step": round(runs[t][0] * 1e3, 1), "reps": runs[t][1]} for t in runs},
         "numpy_oracle_1core": {
             "value": round(stacked_bytes(n_s, n_s // 100) / per_np / 1e9, 4), "unit": "GB/s", "cores": 1,
-            "sample": f"numpy oracle (oracle/compressors_ref.py stacked, O(n) selection) on the 64 MiB sample, "
+            "sample": f"numpy oracle (oracle/compressors_ref.py stacked, O(n) selection) on a 64 MiB sample, "
                       f"{reps_np} reps, {per_np * 1e3:.0f} ms/rep",
         },
     }
+    line["configs"] = cpu_configs(all_threads)
+    return line
+
+
+CONFIG0_SHAPES = [(16, 1, 5, 5), (16,), (32, 16, 5, 5), (32,), (256, 1568), (256,), (10, 256), (10,)]  # 417,482
+
+
+def cpu_configs(threads: int) -> dict:
+    """The CPU-PyTorch path beside configs[0]-[3] (BASELINE.md's "cpu_ref, same"), on this host at `threads`
+    threads: configs[0] the reference's FedAvg server update (oracle/aggregation_ref.py: the reference's own torch
+    ops) over 10 clients of cnn_femmist_tiny's 8 tensors, configs[1] 8-bit dithering of 10 x 417,482, configs[2]
+    top-k 1 % of 25 M with the dense decode, configs[3] 8 clients x 25 M stacked codec + the add_(alpha) fold."""
+    from oracle import aggregation_ref, torch_ref
+
+    threads0 = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(7)
+    res = {}
+    try:
+        theta = [torch.randn(sh, generator=g) for sh in CONFIG0_SHAPES]
+        dl = [torch.zeros(sh) for sh in CONFIG0_SHAPES]
+        msgs = [{"train_samples": 100 * (i + 1), "delta_parameters": [torch.randn(sh, generator=g) * 1e-3
+                                                                      for sh in CONFIG0_SHAPES]} for i in range(10)]
+        per, reps = _time_reps(lambda: aggregation_ref.fedopt_update(theta, dl, None, msgs, "avg", 1.0, (0.0, 1.0),
+                                                                     1e-3), 1.0, 50)
+        res["config0_fedavg_10x417482"] = {"ms": round(per * 1e3, 3), "reps": reps}
+        X = torch.randn(10, 417_482, generator=g) * 1e-3
+        per, reps = _time_reps(lambda: torch_ref.dither_step(X, LEVELS, g), 2.0, 20)
+        res["config1_quant8_10x417482"] = {"ms": round(per * 1e3, 3), "reps": reps,
+                                           "GB_s": round(10 * 417_482 * 9 / per / 1e9, 3)}
+        x3 = torch.randn(25_000_000, generator=g) * 1e-3
+        per, reps = _time_reps(lambda: torch_ref.topk_step(x3, 250_000), 3.0, 5)
+        res["config2_topk1pct_25M"] = {"ms": round(per * 1e3, 3), "reps": reps,
+                                       "GB_s": round((8 * 25_000_000 + 16 * 250_000) / per / 1e9, 3)}
+        w8 = [100 * (i + 1) / 3600 for i in range(8)]
+        per, reps = _time_reps(lambda: torch_ref.round_fold([x3] * 8, w8, 250_000, LEVELS, g), 4.0, 2, warm=False)
+        res["config3_round_8x25M"] = {"ms": round(per * 1e3, 3), "reps": reps}
+    finally:
+        torch.set_num_threads(threads0)
+    res["threads"] = threads
+    return res
 
 
 def traffic_from_profiles():
@@ -260,6 +290,66 @@ def traffic_from_profiles():
         with open(p) as f:
             return json.load(f)
     return {}
+
+
+def aggregation_extras(dev, world: int, rank: int) -> dict:
+    """The server half of north_star: the FedAvg and FedAdam server updates
+    (FedOptServer.update, _fedopt.py:196-240) and avg_parameters (nodes.py:1134-1163) at configs[0]'s model
+    (cnn_femmist_tiny: 8 tensors, 417,482 parameters) x 10 clients, and one weighted fold of 8 clients x 25 M
+    (flc_weighted_sum, configs[3]'s server fold over dense deltas).  Algorithmic bytes: a fold reads its n sources and
+    the accumulator and writes it, (n + 2) * 4 * D; the FedOpt step reads theta and delta and writes theta (avg,
+    12 B/element) or also reads and writes v (adam, 20 B/element)."""
+    from fl_sim_amd import aggregation as fagg
+    from fl_sim_amd import codec
+    from fl_sim_amd import dist as fdist
+
+    out = {}
+    ga = torch.Generator(device=dev).manual_seed(99 + rank)
+    th0 = [torch.randn(sh, generator=ga, device=dev) for sh in CONFIG0_SHAPES]
+    dl0 = [torch.zeros(sh, device=dev) for sh in CONFIG0_SHAPES]
+    v0 = [torch.rand(sh, generator=ga, device=dev) * 1e-4 + 1e-6 for sh in CONFIG0_SHAPES]
+    msgs0 = [{"train_samples": 100 * (i + 1),
+              "delta_parameters": [torch.randn(sh, generator=ga, device=dev) * 1e-3 for sh in CONFIG0_SHAPES]}
+             for i in range(10)]
+    d0, n0 = 417_482, 10
+    legs = {
+        "fedavg_update": (lambda: fagg.fedopt_update(th0, dl0, None, msgs0, "avg", 1.0, (0.0, 1.0), 1e-3),
+                          (n0 + 2) * 4 * d0 + 12 * d0),
+        "fedadam_update": (lambda: fagg.fedopt_update(th0, dl0, v0, msgs0, "adam", 1e-2, (0.9, 0.99), 1e-3),
+                           (n0 + 2) * 4 * d0 + 20 * d0),
+        "avg_parameters": (lambda: fagg.avg_parameters(th0, msgs0, size_aware=True, key="delta_parameters"),
+                           (n0 + 2) * 4 * d0),
+    }
+    line = {"model": "cnn_femmist_tiny (8 tensors, 417,482 params) x 10 clients"}
+    for name, (fn, nbytes) in legs.items():
+        ms, _ = timed(fn, 50, 10, world)
+        ms = max_over_ranks(ms, world)
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        line[name] = {"us": round(ms * 1e3, 2), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                      "algorithmic_bytes": nbytes}
+    line["bytes_formula"] = ("fold (n + 2) * 4 * D; FedOpt step avg 12 * D, adam 20 * D; D = 417,482, n = 10; one fold "
+                             "launch per tensor (flc_weighted_sum) + one step launch per tensor (flc_fedopt_step)")
+    out["aggregation_config0_fedavg_10x417482"] = line
+    del th0, dl0, v0, msgs0
+    # 8 x 25 M: distinct sources (a repeated source would be served from the caches)
+    n8 = 25_000_000
+    srcs8 = [torch.randn(n8, generator=ga, device=dev) * 1e-3 for _ in range(8)]
+    dst8 = torch.randn(n8, generator=ga, device=dev) * 1e-3
+    w8 = fdist.sample_weights([100 * (i + 1) for i in range(8)])
+    fn8 = lambda: codec.weighted_sum(dst8, srcs8, w8, init_mode=0, beta=0.5)  # noqa: E731
+    ms8, _ = timed(fn8, 20, 5, world)
+    ms8 = max_over_ranks(ms8, world)
+    _, kms8 = timed(fn8, 5, 1, world, probe="weighted_sum")
+    b8 = (8 + 2) * 4 * n8
+    ach = b8 / (kms8 * 1e-3) / 1e9 if kms8 else None
+    out["aggregation_weighted_sum_8x25M"] = {
+        "ms_per_call": round(ms8, 4), "GB_s": round(b8 / (ms8 * 1e-3) / 1e9, 1),
+        "roofline": {"kernel": "weighted_sum", "bound": "hbm", "achieved": None if ach is None else round(ach, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None if ach is None else round(ach / HBM_PEAK_GBS, 4),
+                     "avg_us": None if kms8 is None else round(kms8 * 1e3, 1), "algorithmic_bytes": b8},
+        "bytes_formula": "(n + 2) * 4 * D: 8 sources + the accumulator read (dst * beta) + dst written",
+    }
+    return out
 
 
 def main():
@@ -329,6 +419,7 @@ def main():
             "algorithmic_bytes": kernel_bytes.get(args.probe),
         }
     extra = {}
+    parity = None  # set by the configs[3] legs (skipped with --skip-extra)
     if probe_ms:
         # every kernel of the step, each timed live (HIP events on its launch stream) over its own short run
         kernels = {}
@@ -604,17 +695,15 @@ def main():
         # the local fold (encode + weighted decode-accumulate of this rank's clients), then the reduce
         fold = fdist.stacked_decode_accumulate(k3, LEVELS, seed=0, counter=0)
 
-        def step4_codec():
-            acc.zero_()
-            if len(mine) > 1:  # the rank's clients encoded in one batched launch, as aggregate_round does
-                fold.many([X3] * len(mine), [w_all[c] for c in mine], acc, mine)
-            else:
-                for c in mine:
-                    fold(X3, float(w_all[c]), acc, c)
+        def step4_codec():  # as aggregate_round does it: the rank's clients into records, one fold from +0
+            fold.many([X3] * len(mine), [w_all[c] for c in mine], acc, mine, accumulate=False)
 
         ms4c, _ = timed(step4_codec, 10, 3, world)
         ms4c = max_over_ranks(ms4c, world)
-        codec_b = len(mine) * (stacked_bytes(d3, k3) + 4 * d3) + 4 * d3  # + the accumulate read, the zeroing
+        tiles3 = 4 * (-(-d3 // 1024) + 1)
+        # per client: the encode reads x and writes its record (5 K + tiles), the fold reads the record; the fold
+        # writes the partial sum once
+        codec_b = len(mine) * (4 * d3 + 2 * (5 * k3 + tiles3)) + 4 * d3
         line4 = {
             "ms_per_step": round(ms4, 4),
             "clients": n_cl4,
@@ -622,7 +711,8 @@ def main():
             "codec_ms": round(ms4c, 4),
             "codec_GB_s_per_gpu": round(codec_b / (ms4c * 1e-3) / 1e9, 1),
             "codec_GB_s_aggregate": round(world * codec_b / (ms4c * 1e-3) / 1e9, 1),
-            "bytes_formula": "codec: n_local * (12 * D + 10 * K) + 4 * D; reduce: 4 * D (algBw = busBw)",
+            "bytes_formula": "codec: n_local * (4 * D + 2 * (5 * K + tiles)) + 4 * D (encode into records, one fold "
+                             "from +0 over them); reduce: 4 * D (algBw = busBw)",
         }
         if world > 1:
             import torch.distributed as tdist
@@ -666,12 +756,32 @@ def main():
         line4["wire_bytes_formula"] = ("codec: n_local * (4 * D + 5 * K + tiles) written as records; all_gather: "
                                        "world * ceil(8 / world) records; fold: 4 * D written + 8 records read")
         extra["config4_codec_plus_rccl_reduce_25M"] = line4
+        # self-check: one more round both ways over the process group, compared on rank 0 with the
+        # single-device per-client chain of all 8 clients — the wire round bit for bit, the dense round within
+        # 1e-6 * sum|w d| + 1e-30
+        parity = fdist.round_parity([X3] * n_cl4, w_all, fdist.StackedWireCodec(d3, k3, LEVELS, seed=0, counter=777),
+                                    fdist.stacked_decode_accumulate(k3, LEVELS, seed=0, counter=777), dst=0,
+                                    device=dev)
         del acc
         del X3
+        torch.cuda.empty_cache()
+        extra.update(aggregation_extras(dev, world, rank))
+
+    # the top-k encoders' sticky error word on every rank (co-residency / count checks, include/flcodec.h), OR-ed
+    topk_err = 0
+    for v in codec.topk_status_all(reset=True).values():
+        topk_err |= int(v)
+    topk_err = int(max_over_ranks(float(topk_err), world))
 
     cpu = None
-    if rank == 0 and world == 1 and not args.skip_cpu:
+    if rank == 0 and not args.skip_cpu:  # after the GPU work, at every N (rank 0's host cores)
         cpu = cpu_baseline()
+        for key, ck in (("config0_fedavg_10x417482", "aggregation_config0_fedavg_10x417482"),
+                        ("config1_quant8_10x417482", "config2_quant8_10x417482"),
+                        ("config2_topk1pct_25M", "config3_topk1pct_25M"),
+                        ("config3_round_8x25M", "config4_codec_plus_rccl_reduce_25M")):
+            if ck in extra and key in cpu["configs"]:
+                extra[ck]["cpu_torch"] = dict(cpu["configs"][key], threads=cpu["configs"]["threads"])
 
     if rank == 0:
         line = {
@@ -697,13 +807,19 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
+            "topk_err": topk_err,
             "extra": extra,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
+    ok = topk_err == 0 and (rank != 0 or parity is None or parity["ok"])
     if world > 1:
         import torch.distributed as dist
 
         dist.destroy_process_group()
+    if not ok:
+        print(f"bench.py: self-check failed on rank {rank}: topk_err={topk_err}, parity={parity}", file=sys.stderr)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

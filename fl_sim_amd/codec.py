@@ -47,13 +47,15 @@ TILE = 1024  # FLC_TILE (include/flcodec.h)
 _WS_SIZE: Dict[tuple, int] = {}
 
 
-def _ws_size(name: str, *args) -> int:
-    """A workspace-size entry point's result, memoised per device (a pure function of its arguments and the
-    device's CU count): one ctypes call fewer per encode."""
-    key = (torch.cuda.current_device(), name) + args
+def _ws_size(device: torch.device, name: str, *args) -> int:
+    """A workspace-size entry point's result for ``device`` (the size functions read the current device's CU count,
+    so the query runs with ``device`` current), memoised per device: one ctypes call fewer per encode."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, name) + args
     v = _WS_SIZE.get(key)
     if v is None:
-        v = _WS_SIZE[key] = _lib.size(name, *args)
+        with torch.cuda.device(idx):
+            v = _WS_SIZE[key] = _lib.size(name, *args)
     return v
 
 
@@ -267,7 +269,7 @@ def topk_encode(x: torch.Tensor, k: int, with_tiles: bool = False):
     idx = torch.empty(k, dtype=torch.int32, device=x.device)
     val = torch.empty(k, dtype=torch.float32, device=x.device)
     tiles = _tiles(n, x.device) if with_tiles else None
-    ws = workspace(x.device, _lib.size("flc_topk_workspace_size", n, k), "topk")
+    ws = workspace(x.device, _ws_size(x.device, "flc_topk_workspace_size", n, k), "topk")
     call("flc_topk_encode_tiled", _p(x), n, k, _p(idx), _p(val), _p(tiles), _p(ws), ws.numel(), _stream(x.device))
     _after_encode(x.device)
     return (idx, val, tiles) if with_tiles else (idx, val)
@@ -291,7 +293,7 @@ def topk_encode_batch(xs: Sequence[torch.Tensor], k: int, with_tiles: bool = Fal
     tiles = torch.empty(C, ntl, dtype=torch.int32, device=dev) if with_tiles else None
     P = ctypes.c_void_p * C
     vp = lambda a: ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
-    ws = workspace(dev, _ws_size("flc_topk_encode_batch_workspace_size", n, k, C), "topk_batch")
+    ws = workspace(dev, _ws_size(dev, "flc_topk_encode_batch_workspace_size", n, k, C), "topk_batch")
     call("flc_topk_encode_batch", vp(P(*[x.data_ptr() for x in xs])), C, n, k,
          vp(P(*[idx.data_ptr() + 4 * k * c for c in range(C)])), vp(P(*[val.data_ptr() + 4 * k * c for c in range(C)])),
          vp(P(*[tiles.data_ptr() + 4 * ntl * c for c in range(C)])) if with_tiles else None, _p(ws), ws.numel(),
@@ -390,7 +392,7 @@ def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, co
         codes = torch.empty(max(k, 16), dtype=torch.uint8, device=x.device)
         norm = torch.empty(1, dtype=torch.float32, device=x.device)
         tiles = _tiles(n, x.device) if with_tiles else None
-    ws = workspace(x.device, _ws_size("flc_topk_workspace_size", n, k), "topk")
+    ws = workspace(x.device, _ws_size(x.device, "flc_topk_workspace_size", n, k), "topk")
     call("flc_stacked_encode_tiled", _p(x), n, k, levels, seed, counter, None, _p(idx), _p(codes), _p(norm),
          _p(tiles), _p(ws), ws.numel(), _stream(x.device))
     _after_encode(x.device)
@@ -455,7 +457,7 @@ def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, 
                    "codes": P(*[b["codes"] + kc * c for c in range(C)]),
                    "norm": P(*[b["norm"] + 4 * c for c in range(C)]),
                    "tiles": P(*[tiles.data_ptr() + 4 * ntl * c for c in range(C)]) if with_tiles else None}
-    ws = workspace(dev, _ws_size("flc_stacked_encode_batch_workspace_size", n, k, C), "topk_batch")
+    ws = workspace(dev, _ws_size(dev, "flc_stacked_encode_batch_workspace_size", n, k, C), "topk_batch")
     vp = lambda a: None if a is None else ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
     call("flc_stacked_encode_batch", vp(P(*[x.data_ptr() for x in xs])), C, n, k, levels,
          vp((ctypes.c_uint64 * C)(*[int(s_) for s_ in seeds])), counter, vp(ptr["idx"]), vp(ptr["codes"]),
@@ -498,7 +500,7 @@ def stacked_encode_delta_batch(local_params: Sequence[Sequence[torch.Tensor]], g
     tiles = torch.empty(C, ntl, dtype=torch.int32, device=dev)
     P = ctypes.c_void_p
     vp = lambda a: ctypes.cast(a, P)  # noqa: E731
-    ws = workspace(dev, _ws_size("flc_stacked_encode_delta_batch_workspace_size", n, k, C, m), "topk_batch")
+    ws = workspace(dev, _ws_size(dev, "flc_stacked_encode_delta_batch_workspace_size", n, k, C, m), "topk_batch")
     call("flc_stacked_encode_delta_batch", vp((P * (C * m))(*[t.data_ptr() for lp in ls for t in lp])),
          vp((P * m)(*[t.data_ptr() for t in gs])), vp((ctypes.c_int64 * m)(*[t.numel() for t in gs])), m, C, k,
          levels, vp((ctypes.c_uint64 * C)(*[int(s_) for s_ in seeds])), counter,
@@ -537,7 +539,7 @@ def stacked_encode_delta(local_params: Sequence[torch.Tensor], global_params: Se
     codes = torch.empty(max(k, 16), dtype=torch.uint8, device=dev)
     norm = torch.empty(1, dtype=torch.float32, device=dev)
     tiles = _tiles(n, dev)
-    ws = workspace(dev, _lib.size("flc_stacked_encode_delta_workspace_size", n, k, m), "topk")
+    ws = workspace(dev, _ws_size(dev, "flc_stacked_encode_delta_workspace_size", n, k, m), "topk")
     call("flc_stacked_encode_delta", ctypes.cast(lp, ctypes.c_void_p), ctypes.cast(gp, ctypes.c_void_p),
          ctypes.cast(sz, ctypes.c_void_p), m, k, levels, seed, counter, _p(idx), _p(codes), _p(norm), _p(tiles), _p(ws),
          ws.numel(), _stream(dev))

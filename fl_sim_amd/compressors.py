@@ -17,6 +17,15 @@ RNG (``rng=`` constructor argument):
     index order), so outputs are bit-identical to the reference under the same seed;
   * ``"philox"``: counter-based Philox4x32-10 on the device, keyed by ``seed``; no host round trip.
 
+Dithering norm (``norm=`` constructor argument; compressors.py:332, 372 ``np.linalg.norm(x, p)``):
+  * ``"auto"`` (default): for a host input in compat mode with p != inf, the reference's own norm —
+    ``np.float32(np.linalg.norm(x, p))``, the fp32 BLAS dot numpy runs on this host — is computed on the host
+    and handed to the kernels, so the output is bit-identical to the reference at any size; otherwise (device
+    inputs, philox mode, p = inf) the device norm;
+  * ``"device"``: always the device norm (p = inf: max |x|, exact; p = 2: an fp64 sum of squares rounded once,
+    within 1 ulp of the exact norm, which a float32 BLAS dot is not at large D);
+  * ``"reference"``: always the host ``np.linalg.norm`` (a device input is copied to the host for it).
+
 Extensions over the reference (documented in DESIGN.md): ``Compressor(extended_levels=True)`` lets
 standard dithering take up to 127 levels (by default level counts > 10 fail the reference's
 ``np.arange`` assertion, as they do there), ``encode``/``decode`` expose the packed wire, and
@@ -82,9 +91,13 @@ def natural_levels(levels: int) -> np.ndarray:
 class Compressor:
     """MI355X-native drop-in for the reference ``Compressor`` (compressors.py:35-419)."""
 
-    def __init__(self, compressorName: str = "", rng: str = "compat", seed: int = 0, extended_levels: bool = False):
+    def __init__(self, compressorName: str = "", rng: str = "compat", seed: int = 0, extended_levels: bool = False,
+                 norm: str = "auto"):
         if rng not in ("compat", "philox"):
             raise ValueError("rng must be 'compat' or 'philox'")
+        if norm not in ("auto", "device", "reference"):
+            raise ValueError("norm must be 'auto', 'device' or 'reference'")
+        self.norm_mode = norm
         # extension: standard dithering with 11..127 levels (8-bit codes); off by default, where such level
         # counts fail the reference's assertion exactly as they do there
         self.extended_levels = bool(extended_levels)
@@ -274,14 +287,18 @@ class Compressor:
     def compressVector(self, x):
         """Encode + decode ``x`` (1-D); returns the dense decoded vector like the reference."""
         if isinstance(x, torch.Tensor) and x.device.type == "cuda":
-            return self._compress_device(x)
+            host_norm = None
+            if self._wants_host_norm(device_input=True):
+                host_norm = self._reference_norm(x.detach().cpu().numpy().reshape(-1))
+            return self._compress_device(x, host_norm)
         # host input: the reference's own signature (numpy); H2D -> kernels -> D2H
         is_tensor = isinstance(x, torch.Tensor)
         arr = x.detach().cpu().numpy() if is_tensor else np.asarray(x)
         if arr.dtype != np.float32:
             raise TypeError(f"the MI355X codec path is fp32; got {arr.dtype}")
+        host_norm = self._reference_norm(arr.reshape(-1)) if self._wants_host_norm(device_input=False) else None
         dev = torch.device("cuda", torch.cuda.current_device())
-        out = self._compress_device(torch.from_numpy(np.ascontiguousarray(arr)).to(dev, non_blocking=False))
+        out = self._compress_device(torch.from_numpy(np.ascontiguousarray(arr)).to(dev, non_blocking=False), host_norm)
         out_host = out.cpu()
         return out_host if is_tensor else out_host.numpy().reshape(arr.shape)
 
@@ -295,6 +312,18 @@ class Compressor:
         return self.fullName
 
     # ----------------------------------------------------------------------------------------------
+    def _wants_host_norm(self, device_input: bool) -> bool:
+        if self.compressorType not in _STD and self.compressorType not in _NATD:
+            return False
+        if self.norm_mode == "reference":
+            return True
+        return (self.norm_mode == "auto" and not device_input and self.rng_mode == "compat"
+                and not math.isinf(self.p))
+
+    def _reference_norm(self, arr: np.ndarray) -> np.float32:
+        # compressors.py:332 / 372, evaluated as the reference evaluates it (numpy on this host)
+        return np.float32(np.linalg.norm(arr, self.p))
+
     def _uniforms(self, count: int, device) -> torch.Tensor:
         u = _rng.python_random_doubles(count)
         return torch.from_numpy(u).to(device)
@@ -305,7 +334,7 @@ class Compressor:
         self.really_need_to_send_components += self.last_need_to_send_advance
         self.total_input_components += self.last_input_advance
 
-    def _compress_device(self, x: torch.Tensor) -> torch.Tensor:
+    def _compress_device(self, x: torch.Tensor, host_norm: Optional[np.float32] = None) -> torch.Tensor:
         if x.dim() != 1:
             raise ValueError("compressVector expects a 1-D vector (d = max(x.shape) in the reference)")
         d = x.numel()
@@ -374,7 +403,10 @@ class Compressor:
                 raise ValueError(f"the device dithering codec takes 1..127 levels (8-bit codes); s = {self.s}")
             kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
             x2 = x.reshape(1, d)
-            norms = codec.quant_norm(x2, self.p)
+            if host_norm is not None:  # the reference's np.linalg.norm (see the module docstring)
+                norms = torch.tensor([host_norm], dtype=torch.float32).to(x.device, non_blocking=True)
+            else:
+                norms = codec.quant_norm(x2, self.p)
             seed, ctr = self.philox.next()
             compat_u = None
             if self.rng_mode == "compat":

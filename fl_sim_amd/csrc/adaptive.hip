@@ -13,21 +13,28 @@
 //   cdf = p.cumsum()            fp64, strictly sequential: c_i = fl(c_{i-1} + p_i);
 //   cdf /= cdf[-1];  u = random_sample();  ind = cdf.searchsorted(u, side='right').
 //
-// Every rounding above is reproduced.  The one sequential dependency, the fp64 running sum, is made
-// parallel without giving up exactness by speculation with a translation argument: inside one binade
-// [2^E, 2^(E+1)) fp64 values are the multiples of U = 2^(E-52), and round-to-nearest-even commutes with a
-// shift by an EVEN multiple of U.  So a chunk's sequential run started from a guess g (close to its true
-// start t, same binade) ends at exactly e + (t - g) whenever (t - g) / U is even and both runs stay in
-// that binade.  Each chunk of kChunk elements is run twice, from g and from g + U (one of the two
-// differences is even), in parallel (phase A); one thread then chains the chunks (phase B), shifting the
-// speculated ends and re-running a chunk sequentially only when a binade boundary gets in the way
-// (a few dozen chunks per call: the running sum crosses each binade once).  Then the chunk holding the
-// crossing of u is re-run to find the index.  The guesses come from an fp64 prefix of the chunk sums of
-// |x|; their accuracy only decides how often a re-run happens, never the result.
+// Every rounding above is reproduced.  The one sequential dependency, the fp64 running sum, is made parallel
+// without giving up exactness.  Inside one binade [2^E, 2^(E+1)) fp64 values are the multiples m * U of
+// U = 2^(E-52), and round-to-nearest-even commutes with a shift by an EVEN multiple of U.  Each chunk of kChunk
+// elements is run twice from a guess g of its start (phase A: from g and from g + U, in parallel over chunks).
+// When both runs and the true run stay in binade E, the chunk maps the integer m of its true start to
+//     m + inc[m & 1]      (the parity picks the run whose distance to the true start is even)
+// exactly.  Such maps compose (a pair of increments per input parity), so:
+//   * a segmented scan composes the maps of consecutive chunks of one binade inside blocks of kPieceBlk chunks
+//     ("pieces"); a chunk whose runs leave their binade, or come within kEta of its edges, is a piece of its own
+//     that is re-run sequentially (about one per binade the running sum crosses: ~20 per call);
+//   * one wave walks the pieces in order (O(1) per composed piece, kChunk dependent adds per re-run chunk), checking
+//     that every composed piece starts and ends in its binade — which makes every chunk map in it exact;
+//   * every chunk's exact start then follows in parallel from its piece's start and its exclusive prefix map, and
+//     the chunk holding searchsorted(u) is found in the same pass and re-run to find the index.
+// If a check fails (never expected: the margins are ~100x the guesses' error) the exact chunk-by-chunk chain runs
+// instead, so the result never depends on the speculation.  The guesses come from the pairwise partial sums of |x|;
+// their accuracy only decides how many chunks are re-run.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "flc_device.hpp"
 #include "flc_runtime.hpp"
@@ -37,25 +44,49 @@ namespace {
 
 constexpr int kBuf = 8192;    // numpy's reduction buffer (np.getbufsize() default)
 constexpr int kLeaf = 128;    // numpy PW_BLOCKSIZE
-constexpr int kChunk = 2048;  // elements per speculated cdf chunk (4 per reduction buffer)
+constexpr int kChunk = 256;   // elements per speculated cdf chunk (two pairwise leaves)
 constexpr int kQ = kBuf / kChunk;
 constexpr int kPad = kBuf + kBuf / kLeaf;  // LDS copy of one buffer, one pad word per leaf
-constexpr int kRec = 1024;                 // chunk records staged in LDS per step of phase B
+constexpr int kPieceBlk = 1024;            // chunks per block of the piece scan
+constexpr int kRecMax = 128;               // pieces per scan block (more: the sequential chain)
+constexpr int kWalkBatch = 1024;           // piece records staged in LDS per step of the walk
+constexpr int kMaxScanBlocks = 8192;       // ceil(2^31 / kChunk / kPieceBlk)
+constexpr double kEta = 1.0 / 65536.0;     // relative margin to a binade edge for a speculated chunk
+constexpr int kRecLegacy = 1024;           // chunk records staged in LDS per step of the sequential chain
 
 // status word (device int32) written by ar_check
 constexpr int kStNan = 1, kStSum = 2;
 constexpr double kAtol = 3.4526698300124393e-04;  // sqrt(finfo(float32).eps)
 
+// A piece: chunks [first, last] of one scan block.  e >= 1: chunks of binade e whose maps compose to (inc0, inc1);
+// e < 0: one chunk re-run from its exact start (inc0 / inc1 then hold its guess and the end of the run from it).
+struct Rec {
+  long long inc0, inc1;
+  int first, last, e, pad;
+};
+
 struct ArWs {
-  float* buf_sum;   // [nbuf] pairwise sum of |x| per reduction buffer
-  double* q_abs;    // [nq]  approximate sum of |x| per cdf chunk (guesses only)
-  double* guess;    // [nq]  speculated start of each chunk's running sum
-  double* end_a;    // [nq]  end of the run started at guess
-  double* end_b;    // [nq]  end of the run started at guess + U
-  double* p_sum;    // [nq]  fp64 sum of p per chunk (the "sum to 1" check)
-  double* start;    // [nq + 1] exact running sum before each chunk; start[nq] = cdf[-1]
-  float* total;     // [1]   S
-  int32_t* status;  // [1]
+  float* buf_sum;    // [nbuf] pairwise sum of |x| per reduction buffer
+  double* bpre;      // [nbuf] fp64 prefix of buf_sum (guesses only)
+  double* q_abs;     // [nbuf * kQ] approximate sum of |x| per chunk (guesses only)
+  double* guess;     // [nq] speculated start of each chunk's running sum
+  double* end_a;     // [nq] end of the run started at guess
+  double* end_b;     // [nq] end of the run started at guess + U
+  long long* fn;     // [2 nq] the chunk's map: increment for an even / odd start
+  int* fe;           // [nq] the chunk's binade when its map is usable, else -1
+  long long* pre;    // [2 nq] exclusive prefix of the maps inside the chunk's piece
+  int* prec;         // [nq] the chunk's piece (index inside its scan block)
+  Rec* rec;          // [nblk * kRecMax]
+  int* rec_cnt;      // [nblk]
+  int* rec_off;      // [nblk] global index of each scan block's first piece
+  double* rec_t;     // [nblk * kRecMax] exact start of each piece (global piece index)
+  double* rec_end;   // [nblk * kRecMax] exact end of each piece
+  double* start;     // [nq + 1] exact running sum before each chunk; start[nq] = cdf[-1]
+  double* p_part;    // [ceil(nq / 256)] partial fp64 sums of p (the "sum to 1" check)
+  float* total;      // [1] S
+  int32_t* status;   // [1]
+  int32_t* fail;     // [1] 1: the speculation did not verify, the sequential chain ran
+  long long* lo;     // [1] chunk holding searchsorted(u)
 };
 
 __device__ __forceinline__ int binade(double v) {  // exponent field: one grid spacing per value
@@ -64,8 +95,13 @@ __device__ __forceinline__ int binade(double v) {  // exponent field: one grid s
 __device__ __forceinline__ double spacing(int e) {  // grid spacing of binade e (e = 0: subnormals)
   return e == 0 ? 4.9406564584124654e-324 : ldexp(1.0, e - 1075);
 }
+// the map of a chunk (or a composition of them) applied to the integer m of an exact start of binade e
+__device__ __forceinline__ long long apply_map(long long m, long long i0, long long i1) { return m + ((m & 1) ? i1 : i0); }
+__device__ __forceinline__ long long to_grid(double t, int e) { return (long long)ldexp(t, 1075 - e); }
+__device__ __forceinline__ double from_grid(long long m, int e) { return ldexp((double)m, e - 1075); }
+__device__ __forceinline__ bool in_binade(long long m) { return m >= (1ll << 52) && m < (1ll << 53); }
 
-// ---- numpy's pairwise_sum on fp32 (loops_utils.h.src), general n <= kBuf, one thread ------------------
+// ---- numpy's pairwise_sum on fp32 (loops_utils.h.src) ------------------------------------------------
 __device__ float pw_leaf(const float* a, int n) {
   if (n < 8) {
     float r = 0.0f;
@@ -85,16 +121,17 @@ __device__ float pw_leaf(const float* a, int n) {
   return res;
 }
 
+// the tree above the leaves of an n-element pairwise sum, leaves taken in order from lf[*next]
 template <int DEPTH>
-__device__ __attribute__((noinline)) float pw_sum(const float* a, int n) {
-  if (n <= kLeaf) return pw_leaf(a, n);
+__device__ __attribute__((noinline)) float pw_tree(int n, const float* lf, int* next) {
+  if (n <= kLeaf) return lf[(*next)++];
   if constexpr (DEPTH == 0) {
     return __builtin_nanf("");  // unreachable for n <= kBuf (depth <= 7)
   } else {
     int n2 = n / 2;
     n2 -= n2 % 8;
-    const float l = pw_sum<DEPTH - 1>(a, n2);
-    const float r = pw_sum<DEPTH - 1>(a + n2, n - n2);
+    const float l = pw_tree<DEPTH - 1>(n2, lf, next);
+    const float r = pw_tree<DEPTH - 1>(n - n2, lf, next);
     return l + r;
   }
 }
@@ -134,103 +171,182 @@ __global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const float* __restr
   for (int m = 1; m < kWave; m <<= 1) {
     s += __shfl_xor(s, m);
     if (m == kChunk / kLeaf / 2 && (l & (kChunk / kLeaf - 1)) == 0)
-      ws.q_abs[b * kQ + l / (kChunk / kLeaf)] = (double)s;  // 16-leaf subtree = one cdf chunk
+      ws.q_abs[b * kQ + l / (kChunk / kLeaf)] = (double)s;  // a two-leaf subtree = one cdf chunk
   }
   if (l == 0) ws.buf_sum[b] = s;
 }
 
-// ---- K1b: the last, partial buffer (irregular tree), one thread ------------------------------------
-__global__ __launch_bounds__(64) void ar_tail_sum_kernel(const float* __restrict__ x, int64_t n, ArWs ws) {
+// ---- K1b: the last, partial buffer (an irregular tree): leaves in parallel, the tree on one thread --------
+__global__ __launch_bounds__(128) void ar_tail_sum_kernel(const float* __restrict__ x, int64_t n, ArWs ws) {
   __shared__ float sh[kBuf];
+  __shared__ int lf_start[128], lf_len[128];
+  __shared__ float lf_sum[128];
+  __shared__ int s_nleaf;
+  const int tid = threadIdx.x;
   const int64_t b = n / kBuf;
   const int len = (int)(n - b * kBuf);
-  for (int i = threadIdx.x; i < len; i += 64) sh[i] = fabsf(x[b * kBuf + i]);
+  for (int i = tid; i < len; i += 128) sh[i] = fabsf(x[b * kBuf + i]);
+  if (tid == 0) {  // the leaves of pairwise_sum(len), left to right (depth-first, right half pushed first)
+    int st_s[16], st_n[16];
+    int sp = 1, nl = 0;
+    st_s[0] = 0;
+    st_n[0] = len;
+    while (sp > 0) {
+      --sp;
+      const int s0 = st_s[sp], m = st_n[sp];
+      if (m <= kLeaf) {
+        lf_start[nl] = s0;
+        lf_len[nl] = m;
+        ++nl;
+      } else {
+        int n2 = m / 2;
+        n2 -= n2 % 8;
+        st_s[sp] = s0 + n2;
+        st_n[sp] = m - n2;
+        ++sp;
+        st_s[sp] = s0;
+        st_n[sp] = n2;
+        ++sp;
+      }
+    }
+    s_nleaf = nl;
+  }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  ws.buf_sum[b] = pw_sum<8>(sh, len);
-  for (int q = 0; q * kChunk < len; ++q) {
+  if (tid < s_nleaf) lf_sum[tid] = pw_leaf(sh + lf_start[tid], lf_len[tid]);
+  // guesses: an fp64 sum of |x| per chunk of the partial buffer (any order)
+  if (tid < kQ && tid * kChunk < len) {
     double s = 0.0;
-    const int hi = std::min(len, (q + 1) * kChunk);
-    for (int i = q * kChunk; i < hi; ++i) s += (double)sh[i];
-    ws.q_abs[b * kQ + q] = s;
+    const int hi = std::min(len, (tid + 1) * kChunk);
+    for (int i = tid * kChunk; i < hi; ++i) s += (double)sh[i];
+    ws.q_abs[b * kQ + tid] = s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int next = 0;
+    ws.buf_sum[b] = pw_tree<8>(len, lf_sum, &next);
   }
 }
 
-// ---- K2: S (buffers folded in order, fp32) and the chunk guesses (fp64 prefix of |x| / S) -----------
-__global__ __launch_bounds__(1024) void ar_total_kernel(int64_t nbuf, int64_t nq, ArWs ws) {
-  __shared__ float tile[1024];
+// ---- K2: S (buffers folded in order, fp32) and the fp64 prefix of the buffer sums (guesses) --------------
+__global__ __launch_bounds__(1024) void ar_total_kernel(int64_t nbuf, ArWs ws) {
+  __shared__ __attribute__((aligned(16))) float tile[1024];
   __shared__ double scan_lds[1024 / kWave];
-  __shared__ float s_total;
   float S = 0.0f;
+  double carry = 0.0;
   for (int64_t base = 0; base < nbuf; base += 1024) {
     const int64_t i = base + threadIdx.x;
-    tile[threadIdx.x] = i < nbuf ? ws.buf_sum[i] : 0.0f;
-    __syncthreads();
+    const float v = i < nbuf ? ws.buf_sum[i] : 0.0f;
+    tile[threadIdx.x] = v;
+    double tot;
+    const double ex = block_excl_scan<double, 1024 / kWave>((double)v, scan_lds, &tot);  // (syncs: tile ready)
+    if (i < nbuf) ws.bpre[i] = carry + ex;
+    carry += tot;
     if (threadIdx.x == 0) {
       const int cnt = (int)std::min<int64_t>(1024, nbuf - base);
-      for (int j = 0; j < cnt; ++j) S = S + tile[j];
+      int j = 0;
+      for (; j + 8 <= cnt; j += 8) {
+        const float4 a = *reinterpret_cast<const float4*>(tile + j);
+        const float4 c = *reinterpret_cast<const float4*>(tile + j + 4);
+        S = S + a.x;
+        S = S + a.y;
+        S = S + a.z;
+        S = S + a.w;
+        S = S + c.x;
+        S = S + c.y;
+        S = S + c.z;
+        S = S + c.w;
+      }
+      for (; j < cnt; ++j) S = S + tile[j];
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    s_total = S;
-    ws.total[0] = S;
-  }
-  __syncthreads();
-  const double inv = 1.0 / (double)s_total;
-  double carry = 0.0;
-  for (int64_t base = 0; base < nq; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const double v = i < nq ? ws.q_abs[i] : 0.0;
-    double tot;
-    const double ex = block_excl_scan<double, 1024 / kWave>(v, scan_lds, &tot);
-    if (i < nq) ws.guess[i] = (carry + ex) * inv;
-    carry += tot;
-    __syncthreads();
-  }
+  if (threadIdx.x == 0) ws.total[0] = S;
 }
 
-// ---- K3 (phase A): two speculative sequential runs per chunk, plus the chunk's sum of p -------------
-__global__ __launch_bounds__(256) void ar_phase_a_kernel(const float* __restrict__ x, int64_t n, int64_t nq,
-                                                         ArWs ws) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= nq) return;
+// ---- K3 (phase A): per chunk, the two speculative runs, the chunk's map and its sum of p ------------------
+// A wave owns 64 consecutive chunks and stages them through LDS in four rounds of 64 elements each (16-B loads,
+// 16 lanes per 256 B row piece); lane c then runs chunk c from its row (stride 65 words: conflict-free).
+constexpr int kStageRow = 65;
+__global__ __launch_bounds__(256) void ar_phase_a_kernel(const float* __restrict__ x, int64_t n, int64_t nq, ArWs ws) {
+  __shared__ float stage[4][kWave * kStageRow];
+  __shared__ double red[4];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * 256 + wid * kWave;  // the wave's first chunk (a multiple of 2 kQ)
+  const int64_t j = j0 + lane;
   const float S = ws.total[0];
-  const int64_t lo = j * kChunk;
-  const int len = (int)std::min<int64_t>(kChunk, n - lo);
-  const double ga = ws.guess[j];
-  const double gb = ga + spacing(binade(ga));
+  const double inv = 1.0 / (double)S;
+  // guess = the buffer's fp64 prefix + the exclusive prefix of the chunk sums inside the buffer (32 lanes each)
+  const double qa = j < nq ? ws.q_abs[j] : 0.0;
+  const double incl = wave_incl_scan(qa);
+  const double half = lane_bcast(incl, kQ - 1);
+  const double ga = j < nq ? (ws.bpre[j / kQ] + (incl - qa - (lane >= kQ ? half : 0.0))) * inv : 0.0;
+  const int E = binade(ga);
+  const double gb = ga + spacing(E);
   double ca = ga, cb = gb, ps = 0.0;
-  const float* src = x + lo;
-  if (len == kChunk) {
-    for (int i = 0; i < kChunk; i += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(src + i);
-      const double q0 = (double)(fabsf(v.x) / S), q1 = (double)(fabsf(v.y) / S);
-      const double q2 = (double)(fabsf(v.z) / S), q3 = (double)(fabsf(v.w) / S);
-      ca = ca + q0; cb = cb + q0;
-      ca = ca + q1; cb = cb + q1;
-      ca = ca + q2; cb = cb + q2;
-      ca = ca + q3; cb = cb + q3;
-      ps += (q0 + q1) + (q2 + q3);
+  float* st = stage[wid];
+  for (int r = 0; r < kChunk / 64; ++r) {
+    float4 v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int f = i * kWave + lane, row = f >> 4, c4 = f & 15;
+      const int64_t e = (j0 + row) * kChunk + r * 64 + c4 * 4;
+      if (e + 4 <= n) {
+        v[i] = *reinterpret_cast<const float4*>(x + e);
+      } else {  // past n: zeros, which leave a running sum unchanged
+        v[i] = make_float4(e < n ? x[e] : 0.f, e + 1 < n ? x[e + 1] : 0.f, e + 2 < n ? x[e + 2] : 0.f, 0.f);
+      }
     }
-  } else {
-    for (int i = 0; i < len; ++i) {
-      const double q = (double)(fabsf(src[i]) / S);
+    __builtin_amdgcn_wave_barrier();  // the previous round's rows are read (LDS ops complete in order per wave)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int f = i * kWave + lane, row = f >> 4, c4 = f & 15;
+      float* d = st + row * kStageRow + c4 * 4;
+      d[0] = v[i].x;
+      d[1] = v[i].y;
+      d[2] = v[i].z;
+      d[3] = v[i].w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float* rowp = st + lane * kStageRow;
+#pragma unroll 16
+    for (int e = 0; e < 64; ++e) {
+      const double q = (double)(fabsf(rowp[e]) / S);
       ca = ca + q;
       cb = cb + q;
       ps += q;
     }
   }
-  ws.end_a[j] = ca;
-  ws.end_b[j] = cb;
-  ws.p_sum[j] = ps;
+  if (j < nq) {
+    // usable map: both runs in binade E, clear of its edges by kEta (the true start lies within ~2^-19 of ga)
+    const bool ok = E >= 1 && binade(gb) == E && binade(ca) == E && binade(cb) == E &&
+                    ga >= ldexp(1.0 + kEta, E - 1023) && fmax(ca, cb) <= ldexp(1.0 - kEta, E - 1022);
+    long long i0 = 0, i1 = 0;
+    if (ok) {
+      const long long G = to_grid(ga, E);
+      const long long d0 = to_grid(ca - ga, E), d1 = to_grid(cb - gb, E);
+      // a start of the same parity as G is an even distance from ga: the run from ga; otherwise from ga + U
+      i0 = (G & 1) ? d1 : d0;
+      i1 = (G & 1) ? d0 : d1;
+    }
+    ws.guess[j] = ga;
+    ws.end_a[j] = ca;
+    ws.end_b[j] = cb;
+    ws.fn[2 * j] = i0;
+    ws.fn[2 * j + 1] = i1;
+    ws.fe[j] = ok ? E : -1;
+  }
+  const double s = wave_sum(j < nq ? ps : 0.0);
+  if (lane == 0) red[wid] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) ws.p_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // ---- K4: numpy's checks on p (before any uniform is drawn) -------------------------------------------
-__global__ __launch_bounds__(1024) void ar_check_kernel(int64_t nq, ArWs ws) {
+__global__ __launch_bounds__(1024) void ar_check_kernel(int64_t nparts, ArWs ws) {
   __shared__ double lds[1024 / kWave];
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < nq; i += 1024) s += ws.p_sum[i];
+  for (int64_t i = threadIdx.x; i < nparts; i += 1024) s += ws.p_part[i];
   s = block_sum<double, 1024 / kWave>(s, lds);
   if (threadIdx.x == 0) {
     int st = 0;
@@ -240,114 +356,330 @@ __global__ __launch_bounds__(1024) void ar_check_kernel(int64_t nq, ArWs ws) {
   }
 }
 
-// Sequential run of chunk j from an exact start (one thread).  The loads of 64 elements are issued
-// together ahead of their dependent adds; with `u` (> -1) the run stops at the first element whose
-// normalised running sum exceeds u and returns its index through *hit.
-constexpr int kRun = 64;
-__device__ double run_chunk(const float* __restrict__ x, int64_t n, int64_t j, double c, float S, double cD = 1.0,
-                            double u = -1.0, int64_t* hit = nullptr) {
-  const int64_t lo = j * kChunk;
-  const int64_t hi = std::min<int64_t>(n, lo + kChunk);
-  int64_t i = lo;
-  for (; i + kRun <= hi; i += kRun) {
-    float4 v[kRun / 4];
-#pragma unroll
-    for (int k = 0; k < kRun / 4; ++k) v[k] = *reinterpret_cast<const float4*>(x + i + 4 * k);
-#pragma unroll
-    for (int k = 0; k < kRun / 4; ++k) {
-      const float e[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        c = c + (double)(fabsf(e[m]) / S);
-        if (u > -1.0 && c / cD > u) {
-          *hit = i + 4 * k + m;
-          return c;
-        }
-      }
-    }
-  }
-  for (; i < hi; ++i) {
-    c = c + (double)(fabsf(x[i]) / S);
-    if (u > -1.0 && c / cD > u) {
-      *hit = i;
-      return c;
-    }
-  }
-  return c;
+// ---- K5: pieces — a segmented scan of the chunk maps inside each block of kPieceBlk chunks ---------------
+// compose(f, g) = f then g: an input of parity p moves by f[p], then by g at the new parity
+__device__ __forceinline__ void compose(long long f0, long long f1, long long g0, long long g1, long long* h0,
+                                        long long* h1) {
+  *h0 = f0 + ((f0 & 1) ? g1 : g0);
+  *h1 = f1 + ((f1 & 1) ? g0 : g1);
 }
 
-// ---- K5 (phase B + search): chain the chunks exactly, then searchsorted(u, side='right') ------------
-__global__ __launch_bounds__(1024) void ar_select_kernel(const float* __restrict__ x, int64_t n, int64_t nq, double u,
-                                                         ArWs ws, int64_t* __restrict__ index, float* __restrict__ out) {
-  __shared__ double g_s[kRec], ea_s[kRec], eb_s[kRec];
-  if (ws.status[0] != 0) return;  // the host raises numpy's ValueError; nothing is drawn or written
-  const float S = ws.total[0];
-  double t = 0.0;  // cumsum starts from 0: c_0 = 0 + p_0
-  for (int64_t base = 0; base < nq; base += kRec) {
-    const int64_t i = base + threadIdx.x;
-    if (i < nq) {
-      g_s[threadIdx.x] = ws.guess[i];
-      ea_s[threadIdx.x] = ws.end_a[i];
-      eb_s[threadIdx.x] = ws.end_b[i];
+__global__ __launch_bounds__(kPieceBlk) void ar_piece_kernel(int64_t nq, ArWs ws) {
+  __shared__ long long s0[kPieceBlk], s1[kPieceBlk];
+  __shared__ int sh[kPieceBlk], se[kPieceBlk];
+  __shared__ int scan_lds[kPieceBlk / kWave];
+  if (ws.status[0] != 0) return;
+  const int tid = threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * kPieceBlk + tid;
+  const bool valid = j < nq;
+  const int e = valid ? ws.fe[j] : -2;
+  long long a0 = valid ? ws.fn[2 * j] : 0, a1 = valid ? ws.fn[2 * j + 1] : 0;
+  se[tid] = e;
+  __syncthreads();
+  const int ep = tid > 0 ? se[tid - 1] : -3;
+  // a piece starts at the block's first chunk, at a binade change, and at / after a chunk to re-run
+  int head = (tid == 0 || e < 0 || ep < 0 || e != ep) ? 1 : 0;
+  // Hillis-Steele segmented inclusive scan: (f, h) (+) (g, k) = (k ? g : f then g, h | k)
+  int hf = head;
+  s0[tid] = a0;
+  s1[tid] = a1;
+  sh[tid] = hf;
+  __syncthreads();
+  for (int d = 1; d < kPieceBlk; d <<= 1) {
+    long long n0 = a0, n1 = a1;
+    int nh = hf;
+    if (tid >= d && !hf) {
+      compose(s0[tid - d], s1[tid - d], a0, a1, &n0, &n1);
+      nh = sh[tid - d];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      const int cnt = (int)std::min<int64_t>(kRec, nq - base);
-      for (int r = 0; r < cnt; ++r) {
-        const int64_t j = base + r;
-        ws.start[j] = t;
-        const double ga = g_s[r];
-        const double d = t - ga;
-        if (d == 0.0) {  // the speculated run IS the run
-          t = ea_s[r];
-          continue;
+    a0 = n0;
+    a1 = n1;
+    hf = hf | nh;
+    s0[tid] = a0;
+    s1[tid] = a1;
+    sh[tid] = hf;
+    __syncthreads();
+  }
+  // exclusive prefix inside the piece: the previous chunk's inclusive value, or the identity at a head
+  const long long p0 = head ? 0 : (tid > 0 ? s0[tid - 1] : 0), p1 = head ? 0 : (tid > 0 ? s1[tid - 1] : 0);
+  int nheads;
+  const int hx = block_excl_scan<int, kPieceBlk / kWave>(valid ? head : 0, scan_lds, &nheads);
+  const int r = hx + (valid ? head : 0) - 1;  // this chunk's piece
+  if (!valid) return;
+  ws.pre[2 * j] = p0;
+  ws.pre[2 * j + 1] = p1;
+  ws.prec[j] = r;
+  if (tid == 0) ws.rec_cnt[blockIdx.x] = nheads;
+  if (r >= kRecMax) return;  // (the walk sees the count and takes the sequential chain)
+  Rec* rc = ws.rec + (size_t)blockIdx.x * kRecMax + r;
+  if (head) {
+    rc->first = (int)j;
+    rc->e = e;
+  }
+  const bool last = tid == kPieceBlk - 1 || j + 1 == nq || se[tid + 1] < 0 || e < 0 || se[tid + 1] != e;
+  if (last) {
+    rc->last = (int)j;
+    if (e >= 1) {
+      rc->inc0 = a0;
+      rc->inc1 = a1;
+    } else {  // a re-run chunk: its guess and the end of the run from it (the run is exact when the start is)
+      rc->inc0 = __double_as_longlong(ws.guess[j]);
+      rc->inc1 = __double_as_longlong(ws.end_a[j]);
+    }
+  }
+}
+
+// Exact sequential run of chunk u from its exact start t by one wave (every lane ends with the same t).  The
+// chunk's elements are v (4 per lane, lane-major); with cD > 0 each lane also returns, per element it holds, the
+// normalised cdf test c / cD > u as a bit of *hits.
+__device__ double wave_run(const float4 v, double t, float S, double cD = 0.0, double u = 0.0,
+                           unsigned* hits = nullptr) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const double q0 = (double)(fabsf(v.x) / S), q1 = (double)(fabsf(v.y) / S);
+  const double q2 = (double)(fabsf(v.z) / S), q3 = (double)(fabsf(v.w) / S);
+  unsigned h = 0;
+#pragma unroll 4
+  for (int L = 0; L < kWave; ++L) {
+    t = t + lane_bcast(q0, L);
+    const double c0 = t;
+    t = t + lane_bcast(q1, L);
+    const double c1 = t;
+    t = t + lane_bcast(q2, L);
+    const double c2 = t;
+    t = t + lane_bcast(q3, L);
+    if (hits && lane == L)
+      h = (c0 / cD > u ? 1u : 0u) | (c1 / cD > u ? 2u : 0u) | (c2 / cD > u ? 4u : 0u) | (t / cD > u ? 8u : 0u);
+  }
+  if (hits) *hits = h;
+  return t;
+}
+
+__device__ __forceinline__ float4 load_chunk4(const float* __restrict__ x, int64_t n, int64_t u) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t e = u * kChunk + 4 * lane;
+  if (e + 4 <= n) return *reinterpret_cast<const float4*>(x + e);
+  return make_float4(e < n ? x[e] : 0.f, e + 1 < n ? x[e + 1] : 0.f, e + 2 < n ? x[e + 2] : 0.f, 0.f);
+}
+
+// ---- K6: the walk — every piece's exact start, in order, on one wave ---------------------------------------
+__global__ __launch_bounds__(1024) void ar_walk_kernel(const float* __restrict__ x, int64_t n, int64_t nq, int nblk,
+                                                       int force_seq, ArWs ws) {
+  __shared__ int off[kMaxScanBlocks];
+  __shared__ Rec batch[kWalkBatch];
+  __shared__ int scan_lds[1024 / kWave];
+  __shared__ int s_bad, s_total;
+  __shared__ double s_t;
+  if (ws.status[0] != 0) return;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    s_bad = force_seq;
+    s_t = 0.0;  // cdf starts from 0: c_0 = 0 + p_0
+  }
+  __syncthreads();
+  // the pieces' global numbering (a scan of the per-block counts)
+  int carry = 0;
+  for (int base = 0; base < nblk; base += 1024) {
+    const int b = base + tid;
+    const int c = b < nblk ? ws.rec_cnt[b] : 0;
+    if (c > kRecMax) s_bad = 1;
+    int tot;
+    const int ex = block_excl_scan<int, 1024 / kWave>(c, scan_lds, &tot);
+    if (b < nblk) {
+      off[b] = carry + ex;
+      ws.rec_off[b] = carry + ex;
+    }
+    carry += tot;
+  }
+  if (tid == 0) s_total = carry;
+  __syncthreads();
+  const int total = s_total;
+  const float S = ws.total[0];
+  for (int g0 = 0; g0 < total && !s_bad; g0 += kWalkBatch) {
+    const int g = g0 + tid;
+    if (g < total) {  // the block holding piece g: the last b with off[b] <= g
+      int lo = 0, hi = nblk - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= g) lo = mid;
+        else hi = mid - 1;
+      }
+      batch[tid] = ws.rec[(size_t)lo * kRecMax + (g - off[lo])];
+    }
+    __syncthreads();
+    if (tid < kWave) {  // wave 0 walks the batch (every lane computes the same t)
+      const int cnt = std::min(kWalkBatch, total - g0);
+      double t = s_t;
+      bool bad = false;
+      // the next re-run chunk's elements are loaded one re-run ahead
+      int nxt = 0;
+      while (nxt < cnt && batch[nxt].e >= 1) ++nxt;
+      float4 v = nxt < cnt ? load_chunk4(x, n, batch[nxt].first) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < cnt && !bad; ++r) {
+        const Rec rc = batch[r];
+        if (tid == 0) ws.rec_t[g0 + r] = t;
+        if (rc.e >= 1) {
+          if (binade(t) != rc.e) {
+            bad = true;
+            break;
+          }
+          const long long m = apply_map(to_grid(t, rc.e), rc.inc0, rc.inc1);
+          if (!in_binade(m)) {
+            bad = true;
+            break;
+          }
+          t = from_grid(m, rc.e);
+        } else {
+          const float4 cur = v;
+          int nn = r + 1;
+          while (nn < cnt && batch[nn].e >= 1) ++nn;
+          if (nn < cnt) v = load_chunk4(x, n, batch[nn].first);
+          if (t == __longlong_as_double(rc.inc0)) t = __longlong_as_double(rc.inc1);  // started at the guess
+          else t = wave_run(cur, t, S);
         }
-        const int e = binade(ga);
-        bool ok = e > 64 && binade(t) == e;  // then d is exact and a multiple of U (and d / U fits)
-        double cand = 0.0;
-        if (ok) {
-          const double k = d * ldexp(1.0, 1075 - e);  // d / U, an exact integer
-          const bool even = (((long long)k) & 1LL) == 0;
-          const double g = even ? ga : ga + spacing(e);
-          const double end = even ? ea_s[r] : eb_s[r];
-          cand = end + (t - g);
-          ok = binade(g) == e && binade(end) == e && binade(cand) == e;
-        }
-        t = ok ? cand : run_chunk(x, n, j, t, S);
+        if (tid == 0) ws.rec_end[g0 + r] = t;
+      }
+      if (tid == 0) {
+        s_t = t;
+        if (bad) s_bad = 1;
       }
     }
     __syncthreads();
   }
-  if (threadIdx.x != 0) return;
-  ws.start[nq] = t;
-  const double cD = t;
-  // first chunk whose last normalised cdf value exceeds u (the normalised cdf is non-decreasing)
-  int64_t lo = 0, hi = nq - 1;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) / 2;
-    const double end = mid + 1 < nq ? ws.start[mid + 1] : cD;
-    if (end / cD > u) hi = mid;
-    else lo = mid + 1;
+  if (tid == 0) {
+    ws.start[nq] = s_t;
+    ws.fail[0] = s_bad;
   }
-  int64_t ind = std::min<int64_t>(n, (lo + 1) * kChunk) - 1;  // cdf[-1] / cdf[-1] == 1 > u always qualifies
-  (void)run_chunk(x, n, lo, ws.start[lo], S, cD, u, &ind);
-  index[0] = ind;
-  out[ind] = x[ind];
+}
+
+// ---- K7: every chunk's exact start from its piece, and the chunk holding searchsorted(u, side='right') ------
+__global__ __launch_bounds__(256) void ar_fill_kernel(int64_t nq, double u, ArWs ws) {
+  if (ws.status[0] != 0 || ws.fail[0] != 0) return;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= nq) return;
+  const double cD = ws.start[nq];
+  const int g = ws.rec_off[j / kPieceBlk] + ws.prec[j];
+  const double tp = ws.rec_t[g];
+  const int e = ws.fe[j];
+  double t, end;
+  if (e >= 1) {
+    const long long m = apply_map(to_grid(tp, e), ws.pre[2 * j], ws.pre[2 * j + 1]);
+    t = from_grid(m, e);
+    end = from_grid(apply_map(m, ws.fn[2 * j], ws.fn[2 * j + 1]), e);
+  } else {
+    t = tp;
+    end = ws.rec_end[g];
+  }
+  ws.start[j] = t;
+  // the normalised cdf is non-decreasing: exactly one chunk has its start <= u < its end (cdf[-1] / cdf[-1] = 1)
+  if (t / cD <= u && end / cD > u) ws.lo[0] = j;
+}
+
+// ---- K8: the index — chunk lo re-run from its exact start; or, if the speculation failed, the exact
+// chunk-by-chunk chain (phase B of the sequential design) and a binary search first ----------------------------
+__global__ __launch_bounds__(1024) void ar_final_kernel(const float* __restrict__ x, int64_t n, int64_t nq, double u,
+                                                        ArWs ws, int64_t* __restrict__ index, float* __restrict__ out) {
+  __shared__ double g_s[kRecLegacy], ea_s[kRecLegacy], eb_s[kRecLegacy];
+  __shared__ long long s_lo;
+  if (ws.status[0] != 0) return;  // the host raises numpy's ValueError; nothing is drawn or written
+  const int tid = threadIdx.x;
+  const float S = ws.total[0];
+  if (ws.fail[0] != 0) {
+    double t = 0.0;
+    for (int64_t base = 0; base < nq; base += kRecLegacy) {
+      const int64_t i = base + tid;
+      if (i < nq) {
+        g_s[tid] = ws.guess[i];
+        ea_s[tid] = ws.end_a[i];
+        eb_s[tid] = ws.end_b[i];
+      }
+      __syncthreads();
+      if (tid < kWave) {
+        const int cnt = (int)std::min<int64_t>(kRecLegacy, nq - base);
+        for (int r = 0; r < cnt; ++r) {
+          const int64_t jj = base + r;
+          if (tid == 0) ws.start[jj] = t;
+          const double ga = g_s[r];
+          const double d = t - ga;
+          if (d == 0.0) {  // the speculated run IS the run
+            t = ea_s[r];
+            continue;
+          }
+          const int e = binade(ga);
+          bool ok = e >= 1 && binade(t) == e;  // then d is exact and a multiple of U
+          double cand = 0.0;
+          if (ok) {
+            const long long k = to_grid(d, e);
+            const bool even = (k & 1) == 0;
+            const double g = even ? ga : ga + spacing(e);
+            const double end = even ? ea_s[r] : eb_s[r];
+            cand = end + (t - g);
+            ok = binade(g) == e && binade(end) == e && binade(cand) == e;
+          }
+          t = ok ? cand : wave_run(load_chunk4(x, n, jj), t, S);
+        }
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      ws.start[nq] = t;
+      const double cD = t;
+      int64_t lo = 0, hi = nq - 1;  // first chunk whose last normalised cdf value exceeds u
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        const double end = mid + 1 < nq ? ws.start[mid + 1] : cD;
+        if (end / cD > u) hi = mid;
+        else lo = mid + 1;
+      }
+      s_lo = lo;
+    }
+    __syncthreads();
+  } else if (tid == 0) {
+    s_lo = ws.lo[0];
+  }
+  __syncthreads();
+  if (tid >= kWave) return;
+  const int64_t lo = s_lo;
+  const double cD = ws.start[nq];
+  unsigned hits = 0;
+  (void)wave_run(load_chunk4(x, n, lo), ws.start[lo], S, cD, u, &hits);
+  // the first element of the chunk whose normalised cdf exceeds u (the chunk's end does: some element qualifies;
+  // elements past n add 0 and never come first)
+  const unsigned long long any = __ballot(hits != 0);
+  const int L = __builtin_ctzll(any);
+  const unsigned hl = (unsigned)__builtin_amdgcn_readlane((int)hits, L);
+  const int64_t ind = std::min<int64_t>(n - 1, lo * kChunk + 4 * L + __builtin_ctz(hl));
+  if (tid == 0) {
+    index[0] = ind;
+    out[ind] = x[ind];
+  }
 }
 
 ArWs carve(void* base, int64_t n, size_t* bytes) {
-  const int64_t nbuf = cdiv(n, kBuf), nq = cdiv(n, kChunk);
+  const int64_t nbuf = cdiv(n, kBuf), nq = cdiv(n, kChunk), nblk = cdiv(nq, kPieceBlk), npa = cdiv(nq, 256);
   Carver c(base, base ? ~size_t(0) : 0);
   ArWs w;
   w.buf_sum = c.take<float>(nbuf);
+  w.bpre = c.take<double>(nbuf);
   w.q_abs = c.take<double>(nbuf * kQ);
   w.guess = c.take<double>(nq);
   w.end_a = c.take<double>(nq);
   w.end_b = c.take<double>(nq);
-  w.p_sum = c.take<double>(nq);
+  w.fn = c.take<long long>(2 * nq);
+  w.fe = c.take<int>(nq);
+  w.pre = c.take<long long>(2 * nq);
+  w.prec = c.take<int>(nq);
+  w.rec = c.take<Rec>(nblk * kRecMax);
+  w.rec_cnt = c.take<int>(nblk);
+  w.rec_off = c.take<int>(nblk);
+  w.rec_t = c.take<double>(nblk * kRecMax);
+  w.rec_end = c.take<double>(nblk * kRecMax);
   w.start = c.take<double>(nq + 1);
+  w.p_part = c.take<double>(npa);
   w.total = c.take<float>(1);
   w.status = c.take<int32_t>(1);
+  w.fail = c.take<int32_t>(1);
+  w.lo = c.take<long long>(1);
   if (bytes) *bytes = c.off;
   return w;
 }
@@ -372,13 +704,13 @@ int flc_adaptive_prepare(const float* x, int64_t n, int32_t* status, void* ws, s
   if (!aligned16(x)) return fail(FLC_EINVAL, "flc_adaptive_prepare: x must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
   ArWs w = carve(ws, n, nullptr);
-  const int64_t nfull = n / kBuf, nbuf = cdiv(n, kBuf), nq = cdiv(n, kChunk);
+  const int64_t nfull = n / kBuf, nbuf = cdiv(n, kBuf), nq = cdiv(n, kChunk), npa = cdiv(nq, 256);
   if (nfull > 0)
     FLC_LAUNCH("adaptive_buffer_sum", ar_buffer_sum_kernel, dim3((unsigned)nfull), dim3(256), 0, st, x, nfull, w);
-  if (nbuf > nfull) FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel, dim3(1), dim3(64), 0, st, x, n, w);
-  FLC_LAUNCH("adaptive_total", ar_total_kernel, dim3(1), dim3(1024), 0, st, nbuf, nq, w);
-  FLC_LAUNCH("adaptive_phase_a", ar_phase_a_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, x, n, nq, w);
-  FLC_LAUNCH("adaptive_check", ar_check_kernel, dim3(1), dim3(1024), 0, st, nq, w);
+  if (nbuf > nfull) FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel, dim3(1), dim3(128), 0, st, x, n, w);
+  FLC_LAUNCH("adaptive_total", ar_total_kernel, dim3(1), dim3(1024), 0, st, nbuf, w);
+  FLC_LAUNCH("adaptive_phase_a", ar_phase_a_kernel, dim3((unsigned)npa), dim3(256), 0, st, x, n, nq, w);
+  FLC_LAUNCH("adaptive_check", ar_check_kernel, dim3(1), dim3(1024), 0, st, npa, w);
   if (status) FLC_CHECK_HIP(hipMemcpyAsync(status, w.status, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   return FLC_OK;
 }
@@ -391,8 +723,15 @@ int flc_adaptive_select(const float* x, int64_t n, double u, int64_t* index, flo
   hipStream_t st = as_stream(stream);
   ArWs w = carve(ws, n, nullptr);
   const int64_t nq = cdiv(n, kChunk);
+  const int nblk = (int)cdiv(nq, kPieceBlk);
+  // FLC_ADAPTIVE_SEQUENTIAL=1: skip the speculation's result and run the exact chunk-by-chunk chain (tests)
+  const char* fs = getenv("FLC_ADAPTIVE_SEQUENTIAL");
+  const int force_seq = (fs && atoi(fs) != 0) ? 1 : 0;
   FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)n * sizeof(float), st));
-  FLC_LAUNCH("adaptive_select", ar_select_kernel, dim3(1), dim3(1024), 0, st, x, n, nq, u, w, index, out);
+  FLC_LAUNCH("adaptive_piece", ar_piece_kernel, dim3((unsigned)nblk), dim3(kPieceBlk), 0, st, nq, w);
+  FLC_LAUNCH("adaptive_walk", ar_walk_kernel, dim3(1), dim3(1024), 0, st, x, n, nq, nblk, force_seq, w);
+  FLC_LAUNCH("adaptive_fill", ar_fill_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, nq, u, w);
+  FLC_LAUNCH("adaptive_final", ar_final_kernel, dim3(1), dim3(1024), 0, st, x, n, nq, u, w, index, out);
   return FLC_OK;
 }
 

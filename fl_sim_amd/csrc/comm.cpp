@@ -7,12 +7,16 @@
 //   * flc_rccl_reduce sums the ranks' partial sums to the root (fp32; RCCL's summation order across ranks), or
 //   * flc_rccl_allgather moves every rank's packed wire records (flc_stacked_wire_layout) to every rank, which then
 //     folds all clients in client order (flc_stacked_fold_wires): bit-identical to one device at any N.
-// RCCL is loaded on first use (dlopen "librccl.so.1": inside a torch process that is torch's own RCCL, the one its
-// process groups use), so the library itself has no link-time dependency on it.
+// RCCL is looked up on first use, so the library itself has no link-time dependency on it: FLC_RCCL_LIB (an explicit
+// path) if set; else an RCCL already in the process — found by its symbols, or among the loaded objects by name
+// (inside a torch process that is torch's own RCCL, whatever its soname, the one its process groups use); else
+// dlopen("librccl.so.1").
 #include <dlfcn.h>
+#include <link.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -35,11 +39,29 @@ struct Rccl {
   decltype(&ncclCommUserRank) user_rank = nullptr;
 };
 
+// the path of a loaded object whose file name starts with "librccl" (dl_iterate_phdr callback)
+int find_loaded_rccl(struct dl_phdr_info* info, size_t, void* out) {
+  const char* name = info->dlpi_name;
+  if (!name || !*name) return 0;
+  const char* base = strrchr(name, '/');
+  base = base ? base + 1 : name;
+  if (strncmp(base, "librccl", 7) != 0) return 0;
+  *static_cast<const char**>(out) = name;
+  return 1;
+}
+
 Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);  // already in the process (torch)?
+    void* h = nullptr;
+    if (const char* path = getenv("FLC_RCCL_LIB")) h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
+    if (!h && dlsym(RTLD_DEFAULT, "ncclCommInitRank")) h = RTLD_DEFAULT;  // in the global namespace already
+    if (!h) {
+      const char* loaded = nullptr;  // loaded privately (e.g. as a dependency of torch's HIP library)
+      dl_iterate_phdr(find_loaded_rccl, &loaded);
+      if (loaded) h = dlopen(loaded, RTLD_NOW | RTLD_NOLOAD);
+    }
     if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
     if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
     if (!h) return;
@@ -95,11 +117,17 @@ int flc_comm_init(const void* id, int nranks, int rank, int device, void** comm_
   if (!id || !comm_out || nranks < 1 || rank < 0 || rank >= nranks)
     return fail(FLC_EINVAL, "flc_comm_init: bad arguments (rank %d of %d)", rank, nranks);
   if (int rc = need_rccl("flc_comm_init")) return rc;
+  // ncclCommInitRank binds the communicator to the current device: switch to `device` for the call only, and give
+  // the calling thread (which torch shares) its own current device back
+  int prev = -1;
+  FLC_CHECK_HIP(hipGetDevice(&prev));
   if (device >= 0) FLC_CHECK_HIP(hipSetDevice(device));
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
   ncclComm_t c = nullptr;
-  FLC_NCCL(rccl().init_rank(&c, nranks, uid, rank), "flc_comm_init");
+  const ncclResult_t r = rccl().init_rank(&c, nranks, uid, rank);
+  if (device >= 0 && prev >= 0 && prev != device) FLC_CHECK_HIP(hipSetDevice(prev));
+  if (r != ncclSuccess) return nccl_fail(r, "flc_comm_init");
   *comm_out = c;
   return FLC_OK;
 }

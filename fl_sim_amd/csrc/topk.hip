@@ -1004,11 +1004,18 @@ struct BatchEntry {
 };
 
 // batched: every client's header state, flags and histograms ([0, kOffBlk) of each kOffStage header) zeroed in one
-// launch at the start of a call (grid: blocks per header x headers)
+// launch at the start of a call (grid: blocks per header x headers) — except header 0's error word (EncState::err,
+// the one every client ORs into and flc_topk_status reads), which stays sticky across calls until a reset
+static_assert(offsetof(EncState, call) == 0 && offsetof(EncState, err) == 8, "the error word is bytes 8-15");
 __global__ __launch_bounds__(256) void zero_headers_kernel(char* base, int n_words16) {
   uint4* p = reinterpret_cast<uint4*>(base + (size_t)blockIdx.y * kOffStage);
-  for (int i = (int)blockIdx.x * 256 + (int)threadIdx.x; i < n_words16; i += (int)gridDim.x * 256)
+  for (int i = (int)blockIdx.x * 256 + (int)threadIdx.x; i < n_words16; i += (int)gridDim.x * 256) {
+    if (i == 0 && blockIdx.y == 0) {
+      reinterpret_cast<unsigned long long*>(p)[0] = 0ull;  // the call counter only
+      continue;
+    }
     p[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
 }
 
 // client g's element source from the prototype and its batch entry
@@ -2027,12 +2034,21 @@ int current_cus(int* dev_out) {
   return device_cus(dev);
 }
 
+// the CU count of the device a launch runs on: the stream's device (the calling thread's current device for the
+// null stream), so a batch on a device other than the current one is shaped for its own CUs
+int stream_cus(hipStream_t st, int* dev_out) {
+  int dev = -1;
+  if (st == nullptr || hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) return current_cus(dev_out);
+  if (dev_out) *dev_out = dev;
+  return device_cus(dev);
+}
+
 template <bool STACKED, class Src>
 int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, hipStream_t st, int* idx, float* val,
                 uint8_t* codes, float* norm, int levels, uint64_t seed, uint64_t counter, unsigned* tiles,
                 const char* who) {
   int dev = 0;
-  const int cus = current_cus(&dev);
+  const int cus = stream_cus(st, &dev);
   size_t need = 0;
   EncWs w = carve_enc(ws, n, k, cus, &need);
   if (!ws || need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
@@ -2098,7 +2114,7 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
                       int64_t k, int levels, uint64_t counter, void* ws, size_t ws_bytes, hipStream_t st,
                       const char* who) {
   int dev = 0;
-  const int cus = current_cus(&dev);
+  const int cus = stream_cus(st, &dev);
   const int C = (int)ents.size();
   const BatchGeom bg = batch_geometry(n, k, C, cus, extra.size());
   if (!ws || bg.need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, bg.need);

@@ -17,8 +17,12 @@
 // are loaded in one batch (a wave prefix over the clients' counts) before the ordered fold; tiles holding more than
 // 128 entries over all clients take a per-client loop.  Sparse variant (a fold from +0 with finite weights, the
 // aggregation round's case): the accumulator lives in the LDS tile and only the kept entries are fma'd, in client
-// order — exact, because such an accumulator never holds -0, so fmaf(w, +0, acc) == acc everywhere else.  Bytes: 4n written (+ 4n read when accumulating) + the
-// wires' 5 B per kept entry and tile pointers.
+// order.  fmaf(w, +0, acc) == acc for every element no entry touches, with one exception: an accumulator that is -0
+// (a negative fma result below half the smallest subnormal rounds to -0, fmaf(w, v, -0) keeps it when w * v is a
+// zero of either sign, and a chained launch carries it in) becomes +0 at the next client whose w has a clear sign bit (w * +0 = +0, and
+// +0 + -0 = +0).  So the sparse fold records, per element, the last client that wrote it (a byte in LDS) and, before
+// each entry's fma and at the end, replays the skipped clients on a -0 (skip_clients) — the dense chain bit for bit.  Bytes: 4n written (+ 4n read when
+// accumulating) + the wires' 5 B per kept entry and tile pointers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -51,12 +55,21 @@ WireLayout wire_layout(int64_t n, int64_t k, size_t* total) {
   return L;
 }
 
+__device__ __forceinline__ unsigned long long lowmask(unsigned j) { return j >= 64u ? ~0ull : ((1ull << j) - 1ull); }
+
+// the dense chain's clients [from, to) with no entry at an element, applied to its accumulator: fmaf(w, +0, a) only
+// ever changes a -0, to +0, and only for a w with a clear sign bit (`pos`: one bit per such client of the launch)
+__device__ __forceinline__ float skip_clients(float a, unsigned from, unsigned to, unsigned long long pos) {
+  return (__float_as_uint(a) == 0x80000000u && (pos & lowmask(to) & ~lowmask(from)) != 0ull) ? 0.0f : a;
+}
+
 template <bool SPARSE>
 __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t* __restrict__ wires, int64_t stride,
                                                                    WireLayout L, FoldArgs a, int nw, int levels,
                                                                    double step, int64_t n, int acc_in,
                                                                    float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) float s_tile[FLC_TILE];
+  __shared__ __attribute__((aligned(16))) uint8_t s_last[SPARSE ? FLC_TILE : 4];  // sparse: last writer + 1 (0: none)
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
   const int lane = threadIdx.x;
   const int64_t t = blockIdx.x;
@@ -79,6 +92,7 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
     acc[u] = v;
     // dense: a zero tile per client; sparse: the accumulator itself lives in the LDS tile
     tile4[lane + u * kWave] = SPARSE ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (SPARSE) reinterpret_cast<unsigned*>(s_last)[lane + u * kWave] = 0u;
   }
   // client `lane`'s record, entry range in this tile and norm (lanes >= nw: empty)
   const uint8_t* rec = nullptr;
@@ -92,6 +106,7 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
     cnt = tiles[t + 1] - lo;
     nrm = *reinterpret_cast<const float*>(rec + L.norm);
   }
+  const unsigned long long pos = __ballot(lane < nw && !std::signbit(wl));  // sign-clear weights (sparse: -0 rule)
   const unsigned incl = wave_incl_scan(cnt);
   const unsigned excl = incl - cnt;
   const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)incl, kWave - 1);
@@ -143,8 +158,13 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
       // fmaf(w, +0, acc) == acc for every element no entry touches)
       for (int c = 0; c < nw; ++c) {
         const float wc = __shfl(wl, c, kWave);
-        if (cg[0] == c) s_tile[off[0]] = fmaf(wc, val[0], s_tile[off[0]]);
-        if (cg[1] == c) s_tile[off[1]] = fmaf(wc, val[1], s_tile[off[1]]);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          if (cg[r] == c) {
+            s_tile[off[r]] = fmaf(wc, val[r], skip_clients(s_tile[off[r]], s_last[off[r]], (unsigned)c, pos));
+            s_last[off[r]] = (uint8_t)(c + 1);
+          }
+        }
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -191,7 +211,11 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
       if (SPARSE) {
         for (unsigned j = lo_c + lane; j < lo_c + n_c; j += kWave) {
           const int64_t o = (int64_t)ix[j] - t0;
-          if (o >= 0 && o < FLC_TILE) s_tile[o] = fmaf(wc, stacked_dequant(cd[j], levels, step, nr_c), s_tile[o]);
+          if (o >= 0 && o < FLC_TILE) {
+            s_tile[o] = fmaf(wc, stacked_dequant(cd[j], levels, step, nr_c),
+                             skip_clients(s_tile[o], s_last[o], (unsigned)c, pos));
+            s_last[o] = (uint8_t)(c + 1);
+          }
         }
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -220,6 +244,16 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
     if (SPARSE) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = tile4[lane + u * kWave];
+    }
+  }
+  if (SPARSE) {  // the clients after each element's last writer
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned lb = reinterpret_cast<const unsigned*>(s_last)[lane + u * kWave];
+      acc[u].x = skip_clients(acc[u].x, lb & 0xFFu, 64u, pos);
+      acc[u].y = skip_clients(acc[u].y, (lb >> 8) & 0xFFu, 64u, pos);
+      acc[u].z = skip_clients(acc[u].z, (lb >> 16) & 0xFFu, 64u, pos);
+      acc[u].w = skip_clients(acc[u].w, lb >> 24, 64u, pos);
     }
   }
 #pragma unroll
@@ -272,9 +306,9 @@ int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slo
   hipStream_t st = as_stream(stream);
   const int64_t ntiles = cdiv(n, (int64_t)FLC_TILE);
   const double step = 1.0 / (double)levels;
-  // Sparse fold: starting from +0 the accumulator never holds -0 (an fma yields -0 only from -0 + -0), so with
-  // finite weights fmaf(w, +0, acc) == acc exactly and only the kept entries change it.  Otherwise (accumulating
-  // into a given vector, or a non-finite weight) every element takes every client's fma.
+  // Sparse fold (from +0, finite weights): only the kept entries are fma'd, and a final -0 is resolved as the dense
+  // chain would (kernel header).  Otherwise (accumulating into a given vector, or a non-finite weight) every element
+  // takes every client's fma.
   bool sparse = !accumulate;
   for (int c = 0; c < n_wires; ++c) sparse = sparse && std::isfinite(weights[c]);
   for (int c0 = 0; c0 < n_wires; c0 += kMaxWires) {

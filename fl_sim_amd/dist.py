@@ -59,15 +59,20 @@ def stacked_decode_accumulate(k: int, levels: int = 127, seed: int = 0, counter:
         codec.stacked_decode(pkt, out=acc, weight=weight, accumulate=True)
 
     def many(deltas: Sequence[torch.Tensor], weights: Sequence[float], acc: torch.Tensor,
-             clients: Sequence[int]) -> None:
-        """The rank's clients encoded in one batched launch into packed wire records, then all of them decoded into
-        ``acc`` in client order in one pass (flc_stacked_fold_wires): the same packets and the same fmaf chain as one
-        ``step`` per client."""
+             clients: Sequence[int], accumulate: bool = True) -> None:
+        """The rank's clients encoded into packed wire records (several: one batched launch), then all of them decoded
+        into ``acc`` in client order in one pass (flc_stacked_fold_wires): the same packets and the same fmaf chain as
+        one ``step`` per client.  ``accumulate=False``: ``acc`` is overwritten with the fold from +0 (what zeroing it
+        first gives, without the zeroing pass and the read of ``acc``)."""
         n = acc.numel()
         recs = torch.empty(len(deltas), codec.stacked_wire_layout(n, k)[0], dtype=torch.uint8, device=acc.device)
-        codec.stacked_encode_batch(deltas, k, levels, seeds=[seed + c for c in clients], counter=counter, wires=recs)
+        if len(deltas) == 1:
+            codec.stacked_encode(deltas[0], k, levels, seed=seed + clients[0], counter=counter, wire=recs[0])
+        else:
+            codec.stacked_encode_batch(deltas, k, levels, seeds=[seed + c for c in clients], counter=counter,
+                                       wires=recs)
         codec.stacked_fold_wires(recs, list(range(len(deltas))), [float(w) for w in weights], n, k, levels, out=acc,
-                                 accumulate=True)
+                                 accumulate=accumulate)
 
     step.many = many
     return step
@@ -87,16 +92,15 @@ def aggregate_round(deltas: Sequence[torch.Tensor], weights: Sequence[float], cl
     if out is None:
         if not deltas:
             raise ValueError("need `out` when this rank owns no client")
-        out = torch.zeros_like(deltas[0])
-    else:
-        out.zero_()
+        out = torch.empty_like(deltas[0])
     for d in deltas:
         if d.shape != out.shape or d.dtype != torch.float32:
             raise ValueError("every delta must be a flat fp32 tensor shaped like `out`")
     many = getattr(step, "many", None)
-    if many is not None and len(deltas) > 1:  # a codec that encodes the rank's clients in one launch
-        many(deltas, weights, out, clients)
+    if many is not None and deltas:  # a codec that folds the rank's clients from +0 itself (records + one fold pass)
+        many(deltas, weights, out, clients, accumulate=False)
     else:
+        out.zero_()
         for d, w, c in zip(deltas, weights, clients):
             step(d, float(w), out, c)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
@@ -199,3 +203,45 @@ def aggregate_round_wire(deltas: Sequence[torch.Tensor], weights: Sequence[float
             out = torch.empty(getattr(wire, "n"), dtype=torch.float32, device=dev)
         wire.fold(recs, wire_slots(n_clients, world), weights, out)
     return out
+
+
+def round_parity(all_deltas: Sequence[torch.Tensor], weights: Sequence[float], wire: WireCodec, step: CodecStep,
+                 dst: int = 0, group=None, device: Optional[torch.device] = None) -> Optional[dict]:
+    """Self-check of one aggregation round across the process group (the bench's N > 1 evidence).
+
+    Every rank runs the packed-wire round and the dense round (codec + RCCL reduce) over its own shard of the clients
+    (``all_deltas[i]`` is client ``i``'s delta; each rank only reads its own clients' entries, ``dst`` reads them all).
+    On ``dst`` the single-device fold of ALL clients is then computed locally with the codec step alone (one encode and
+    one weighted decode-accumulate per client, in client order) and compared: the wire round must equal it bit for bit
+    (the fold kernel is built to reproduce that chain exactly), the dense round within
+    ``1e-6 * sum_i |w_i d_i| + 1e-30`` per element (RCCL's summation order across ranks; ``d_i`` the decoded client
+    delta).  Returns the comparison on ``dst`` (None elsewhere)."""
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    world = dist.get_world_size(group) if multi else 1
+    rank = dist.get_rank(group) if multi else 0
+    n_clients = len(all_deltas)
+    mine = client_shard(n_clients, world, rank)
+    dev = device if device is not None else all_deltas[0].device
+    wired = aggregate_round_wire([all_deltas[c] for c in mine], weights, n_clients, wire, dst=dst, group=group,
+                                 device=dev)
+    dense = aggregate_round([all_deltas[c] for c in mine], [weights[c] for c in mine], mine, step,
+                            out=torch.empty(all_deltas[0].numel(), dtype=torch.float32, device=dev), dst=dst,
+                            group=group)
+    if rank != dst:
+        return None
+    # the single-device reference: the per-client chain (one encode + weighted decode-accumulate per client, in client
+    # order) — the codec step itself, not the fold kernel the wire round uses; and sum_i |w_i d_i| from the same decodes
+    single = torch.zeros_like(dense)
+    bound = torch.zeros_like(dense)
+    one = torch.empty_like(dense)
+    for c in range(n_clients):
+        step(all_deltas[c], float(weights[c]), single, c)
+        one.zero_()
+        step(all_deltas[c], float(weights[c]), one, c)
+        bound.add_(one.abs())
+    bound.mul_(1e-6).add_(1e-30)
+    err = (dense - single).abs()
+    wire_exact = bool(torch.equal(wired.view(torch.int32), single.view(torch.int32)))
+    dense_ok = bool(torch.all(err <= bound).item())
+    return {"clients": n_clients, "world": world, "wire_bit_exact": wire_exact, "dense_within_bound": dense_ok,
+            "dense_max_err_over_bound": float((err / bound).max().item()), "ok": wire_exact and dense_ok}

@@ -198,14 +198,16 @@ int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slo
                            int n_wires, int64_t n, int64_t k, int levels, int accumulate, float* out, void* stream);
 
 /* ------------------------------------------------------------------ multi-GPU exchange (RCCL over xGMI)
- * For callers outside torch; one process per GPU.  RCCL is the NCCL API on ROCm, loaded
- * on first use (librccl.so.1; inside a torch process, torch's own).  The round's exchange is either
+ * For callers outside torch; one process per GPU.  RCCL is the NCCL API on ROCm, looked
+ * up on first use: $FLC_RCCL_LIB if set, else an RCCL already loaded in the process (inside a torch process, torch's
+ * own, whatever its soname), else librccl.so.1.  The round's exchange is either
  *   flc_rccl_reduce: sum of the ranks' fp32 partial sums to `root` (the dense round; the cross-rank summation order is
  *     RCCL's, so the result matches one device to 1e-6 * sum|w_i d_i|), or
  *   flc_rccl_allgather: every rank's block of packed wire records to every rank (recv = nranks * bytes_per_rank, rank
  *     order), then flc_stacked_fold_wires over all clients in client order (bit-identical to one device at any N).
  * flc_comm_unique_id on one rank, its flc_comm_id_bytes() bytes shipped to the others out of band, then
- * flc_comm_init on every rank (collective; `device` >= 0 selects the HIP device first).  Collectives are
+ * flc_comm_init on every rank (collective; `device` >= 0: the communicator's HIP device, made current for the call
+ * only — the calling thread's current device is restored).  Collectives are
  * stream-ordered and asynchronous like every other call. */
 size_t flc_comm_id_bytes(void);
 int flc_comm_unique_id(void* id_out);

@@ -132,3 +132,133 @@ def test_speculated_cumsum_is_exact(n, dist, zero_frac):
     want = cdf[np.minimum(starts + chunk, n) - 1]
     assert np.array_equal(ends, want)
     assert reruns <= 80  # about one per binade the running sum crosses
+
+
+def _compose(f, g):
+    """f then g on (increment for an even start, increment for an odd start)."""
+    h0 = f[0] + (g[1] if f[0] & 1 else g[0])
+    h1 = f[1] + (g[0] if f[1] & 1 else g[1])
+    return h0, h1
+
+
+def _apply(m, f):
+    return m + (f[1] if m & 1 else f[0])
+
+
+def parallel_cumsum_starts(p: np.ndarray, chunk: int, guess: np.ndarray, piece_blk: int = 1024,
+                           rec_max: int = 128, eta: float = 2.0 ** -16):
+    """The kernels' current scheme (adaptive.hip K3, K5-K7): per-chunk parity maps from the two speculated runs,
+    composed inside pieces of one binade per scan block, a walk over the pieces (re-running the chunks whose maps
+    are unusable) and every chunk's start from its piece's start and its exclusive prefix map.  Returns (exact
+    start of every chunk + the total, number of re-run chunks) or None where the kernels take the sequential chain."""
+    n = len(p)
+    nq = -(-n // chunk)
+    P = np.zeros(nq * chunk)
+    P[:n] = p
+    P = P.reshape(nq, chunk)
+    ga = guess.astype(np.float64)
+    E = np.array([_binade(g) for g in ga])
+    gb = np.array([g + _spacing(int(e)) for g, e in zip(ga, E)])
+    ea, eb = ga.copy(), gb.copy()
+    for s in range(chunk):
+        ea = ea + P[:, s]
+        eb = eb + P[:, s]
+    fe, fn = [], []
+    for j in range(nq):
+        e = int(E[j])
+        ok = (e >= 1 and _binade(gb[j]) == e and _binade(ea[j]) == e and _binade(eb[j]) == e
+              and ga[j] >= math.ldexp(1.0 + eta, e - 1023) and max(ea[j], eb[j]) <= math.ldexp(1.0 - eta, e - 1022))
+        if ok:
+            G = int(math.ldexp(ga[j], 1075 - e))
+            d0, d1 = int(math.ldexp(ea[j] - ga[j], 1075 - e)), int(math.ldexp(eb[j] - gb[j], 1075 - e))
+            fn.append((d1, d0) if G & 1 else (d0, d1))
+        else:
+            fn.append((0, 0))
+        fe.append(e if ok else -1)
+    # pieces (K5) and their prefix maps
+    pieces, pre, piece_of = [], [None] * nq, [0] * nq
+    for b0 in range(0, nq, piece_blk):
+        nb = 0
+        for j in range(b0, min(nq, b0 + piece_blk)):
+            head = j == b0 or fe[j] < 0 or fe[j - 1] < 0 or fe[j] != fe[j - 1]
+            if head:
+                pieces.append([j, fe[j], (0, 0)])
+                nb += 1
+            pre[j] = pieces[-1][2]
+            pieces[-1][2] = _compose(pieces[-1][2], fn[j])
+            piece_of[j] = len(pieces) - 1
+        if nb > rec_max:
+            return None
+    # the walk (K6)
+    t, reruns, tstart = 0.0, 0, []
+    for first, e, f in pieces:
+        tstart.append(t)
+        if e >= 1:
+            if _binade(t) != e:
+                return None
+            m = _apply(int(math.ldexp(t, 1075 - e)), f)
+            if not (1 << 52) <= m < (1 << 53):
+                return None
+            t = math.ldexp(float(m), e - 1075)
+        elif t == ga[first]:
+            t = ea[first]
+        else:
+            reruns += 1
+            for q in P[first]:
+                t = t + q
+    # the fill (K7)
+    starts = []
+    for j in range(nq):
+        tp = tstart[piece_of[j]]
+        starts.append(math.ldexp(float(_apply(int(math.ldexp(tp, 1075 - fe[j])), pre[j])), fe[j] - 1075)
+                      if fe[j] >= 1 else tp)
+    return np.array(starts + [t]), reruns
+
+
+@pytest.mark.parametrize("n,dist,zero_frac", [(1 << 18, "normal", 0.0), (1_000_003, "normal", 0.05),
+                                              (1 << 20, "cauchy", 0.2), (300_001, "lognormal", 0.5),
+                                              (200_000, "spiky", 0.0), (300_000, "sparse", 0.0)])
+def test_parallel_cumsum_is_exact(n, dist, zero_frac):
+    g = np.random.default_rng(n + 1)
+    if dist == "normal":
+        x = g.standard_normal(n)
+    elif dist == "cauchy":
+        x = g.standard_cauchy(n)
+    elif dist == "lognormal":
+        x = g.lognormal(0, 8, n)
+    elif dist == "spiky":
+        x = g.standard_normal(n) * 1e-6
+        x[g.integers(0, n, 20)] = 1e3
+    else:
+        x = np.zeros(n)
+        x[g.integers(0, n, 50)] = g.standard_normal(50)
+    x = x.astype(F32)
+    x[g.random(n) < zero_frac] = 0
+    ax = np.abs(x)
+    S = ax.sum()
+    p = (ax / S).astype(np.float64)
+    chunk = 256
+    starts = np.arange(0, n, chunk)
+    q = np.add.reduceat(ax.astype(np.float64), starts)
+    guess = np.concatenate([[0.0], np.cumsum(q)[:-1]]) / float(S)
+    res = parallel_cumsum_starts(p, chunk, guess)
+    assert res is not None  # the speculation verifies on all of these
+    got, reruns = res
+    cdf = np.cumsum(p)
+    want = np.concatenate([[0.0], cdf[starts[1:] - 1], [cdf[-1]]])
+    assert np.array_equal(got, want)
+    assert reruns <= 80
+
+
+def test_parallel_cumsum_many_binades_takes_the_sequential_chain():
+    """Exponentially growing magnitudes cross a binade in nearly every chunk: more pieces than a scan block keeps,
+    so the kernels run the exact sequential chain instead (the model returns None there)."""
+    n = 100_000
+    x = np.exp2(np.arange(n) / 1000.0).astype(F32)  # doubles every ~4 chunks
+    ax = np.abs(x)
+    p = (ax / ax.sum()).astype(np.float64)
+    starts = np.arange(0, n, 256)
+    q = np.add.reduceat(ax.astype(np.float64), starts)
+    guess = np.concatenate([[0.0], np.cumsum(q)[:-1]]) / float(ax.sum())
+    res = parallel_cumsum_starts(p, 256, guess, piece_blk=64, rec_max=8)
+    assert res is None

@@ -107,26 +107,28 @@ def test_gloo_world2_reduce_matches_single_process():
 
 def test_fold_dispatches_to_a_batched_codec_step():
     """A codec step with a ``many`` attribute (the batched encoders' form, dist.stacked_decode_accumulate) gets the
-    rank's clients in one call, in client order, when it owns more than one; a single client goes through the step
-    itself.  The fold equals the per-client one."""
+    rank's clients in one call, in client order, and folds them from +0 itself (``accumulate=False``: no zeroing pass
+    and no read of the accumulator) — for a single client too.  The fold equals the per-client one."""
     calls = []
 
     def step(delta, w, acc, client):
         calls.append(("one", client))
         _cpu_topk_step(delta, w, acc, client)
 
-    def many(deltas, weights, acc, clients):
-        calls.append(("many", tuple(clients)))
+    def many(deltas, weights, acc, clients, accumulate=True):
+        calls.append(("many", tuple(clients), accumulate))
+        if not accumulate:
+            acc.zero_()
         for d, w, c in zip(deltas, weights, clients):
             _cpu_topk_step(d, float(w), acc, c)
 
     step.many = many
     deltas = _deltas()
     w = fdist.sample_weights(TS)
-    got = fdist.aggregate_round(deltas, w, list(range(N_CLIENTS)), step)
-    assert calls == [("many", tuple(range(N_CLIENTS)))]
+    got = fdist.aggregate_round(deltas, w, list(range(N_CLIENTS)), step, out=torch.full((D,), 7.0))
+    assert calls == [("many", tuple(range(N_CLIENTS)), False)]
     ref_out = fdist.aggregate_round(deltas, w, list(range(N_CLIENTS)), _cpu_topk_step)
     assert np.array_equal(got.numpy().view(np.uint32), ref_out.numpy().view(np.uint32))
     calls.clear()
     fdist.aggregate_round(deltas[:1], w[:1], [0], step)
-    assert calls == [("one", 0)]
+    assert calls == [("many", (0,), False)]

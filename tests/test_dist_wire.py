@@ -173,3 +173,52 @@ def test_gloo_wire_round_is_bit_identical_to_single_process(world, batched):
         assert np.array_equal(items[r].view(np.uint32), single.view(np.uint32))
     assert np.array_equal(items[100].view(np.uint32), single.view(np.uint32))
     assert all(items[100 + r] is None for r in range(1, world))
+
+
+def _oracle_dense_step(wc):
+    def step(delta, w, acc, client):  # encode, decode, fold with add_(alpha): the dense round's codec step on CPU
+        rec = torch.zeros(wc.stride, dtype=torch.uint8)
+        wc.encode_into(delta, rec, client)
+        acc.add_(wc.decode(rec), alpha=float(np.float32(w)))
+
+    return step
+
+
+class _BrokenWireCodec(OracleWireCodec):
+    """A broken fold (the last client left out) — round_parity must flag it."""
+
+    def fold(self, records, slots, weights, out):
+        super().fold(records, list(slots)[:-1], list(weights)[:-1], out)
+
+
+def _parity_worker(rank, world, port, q, broken):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        wc = (_BrokenWireCodec if broken else OracleWireCodec)(D, K)
+        res = fdist.round_parity(_deltas(), fdist.sample_weights(TS), wc, _oracle_dense_step(OracleWireCodec(D, K)),
+                                 dst=0, device=torch.device("cpu"))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,broken", [(2, False), (3, False), (2, True)])
+def test_gloo_round_parity_self_check(world, broken):
+    """bench.py's N > 1 self-check (dist.round_parity) rehearsed on CPU: the wire round is bit-identical to the local
+    single-device per-client chain, the dense round (gloo reduce) within 1e-6 * sum|w d| + 1e-30; a broken fold is caught."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_parity_worker, args=(r, world, port, q, broken)) for r in range(world)]
+    for p in procs:
+        p.start()
+    items = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(items[r] is None for r in range(1, world))
+    res = items[0]
+    assert res["clients"] == N_CLIENTS and res["world"] == world and res["dense_within_bound"]
+    assert res["wire_bit_exact"] is (not broken) and res["ok"] is (not broken)

@@ -145,3 +145,21 @@ def test_adaptive_philox_mode_is_deterministic():
         c.makeAdaptiveRandomCompressor(len(x))
         outs.append(c.compressVector(torch.from_numpy(x).to(DEV)).cpu().numpy())
     assert np.array_equal(outs[0], outs[1]) and np.count_nonzero(outs[0]) == 1
+
+
+def test_adaptive_sequential_chain_vs_oracle(monkeypatch):
+    """The exact chunk-by-chunk chain the select falls back to when the speculation does not verify, forced."""
+    monkeypatch.setenv("FLC_ADAPTIVE_SEQUENTIAL", "1")
+    g = np.random.default_rng(11)
+    x = (g.standard_normal(1_000_003) * 1e-3).astype(np.float32)
+    x[g.random(len(x)) < 0.05] = 0
+    _check(x, U_EDGES + list(g.random(4)))
+
+
+def test_adaptive_binade_every_few_chunks_vs_oracle():
+    """Magnitudes doubling every 1000 elements: the running sum crosses a binade every ~4 chunks, more re-run pieces
+    than a scan block keeps, so the select takes the sequential chain — still exact."""
+    n = 100_000
+    x = np.exp2(np.arange(n) / 1000.0).astype(np.float32)
+    x[::3] *= -1
+    _check(x, U_EDGES + [0.9, 0.99, 0.999])

@@ -186,3 +186,19 @@ def test_compressor_compress_batch():
     seed, ctr = d.philox.seed, d.philox.counter
     got = d.compressBatch(X)
     assert torch.equal(got, codec.quant_encode_auto(X, 0, d.s, d.p, seed, ctr)[1])
+
+
+def test_batch_error_word_is_sticky_across_calls():
+    """flc_topk_status reports every call since the last reset: a batched call zeroes its headers at the start, but
+    not header 0's error word, so an error bit left by an earlier call survives the next batched encode."""
+    n, k = 70_001, 700
+    xs = [_x(n, 300 + i) for i in range(3)]
+    codec.stacked_encode_batch(xs, k, 127, seeds=[1, 2, 3], counter=1)
+    assert codec.topk_status(reset=True) == 0
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ws = codec._WS[(dev.index, codec._stream(dev), "topk_batch")]
+    ws[8] = 4  # EncState::err (bytes 8-15 of header 0): an exchange time-out of an "earlier call"
+    codec.stacked_encode_batch(xs, k, 127, seeds=[1, 2, 3], counter=2)
+    assert codec.topk_status(reset=True) == 4  # still reported after the second call
+    codec.stacked_encode_batch(xs, k, 127, seeds=[1, 2, 3], counter=3)
+    assert codec.topk_status(reset=True) == 0  # and cleared by the reset

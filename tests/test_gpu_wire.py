@@ -124,3 +124,26 @@ def test_fold_wires_flat_buffer_equals_2d():
     a = codec.stacked_fold_wires(recs, [2, 1, 0], [0.5, 0.25, 0.125], n, k)
     b = codec.stacked_fold_wires(recs.reshape(-1), [2, 1, 0], [0.5, 0.25, 0.125], n, k)
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+def test_fold_wires_signed_zeros_at_underflow():
+    """Near-underflow products: a negative fma result below half the smallest subnormal rounds to -0, which the dense
+    chain turns into +0 at the next client with no entry there and a sign-clear weight.  The sparse fold (from +0,
+    finite weights) must reproduce that, within one launch and across chained launches (> 64 clients)."""
+    n, k = 100_003, 5_000
+    a, b, c, d = (_x(n, 120 + i) * 1e-27 for i in range(4))  # kept values ~1.6e-30 .. 4.5e-30 (the largest, > 0)
+    xs = [a, b, c, b, c, a, a, d]
+    # w * v: 1e-15 -> a nonzero subnormal; +-1e-17 -> +-0.  Elements kept only by b or c end +0 in the chain (the
+    # client with w = +1e-17 and no entry there clears their -0) where a sparse fold without that rule keeps -0;
+    # elements kept only by d end -0
+    weights8 = [1e-15, -1e-17, 1e-17, -1e-17, -2e-17, -1e-17, 1e-17, -1e-17]
+    recs = _records(xs, k, seeds=list(range(len(xs))))
+    for m in (8, 70):
+        slots = [i % 8 for i in range(m)]
+        weights = [weights8[i % 8] for i in range(m)]
+        exp = _fold_ref(recs, slots, weights, n, k, torch.zeros(n, device="cuda"))
+        got = codec.stacked_fold_wires(recs, slots, weights, n, k)
+        eb = _bits(exp)
+        if m == 8:
+            assert (eb == 0x80000000).any()  # the chain does end in -0 somewhere: both cases are exercised
+        assert np.array_equal(_bits(got), eb)
