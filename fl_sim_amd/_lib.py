@@ -124,6 +124,7 @@ SIGNATURES = {
     "flc_rccl_reduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "flc_rccl_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_rccl_allgather": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "flc_quant_status": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "flc_adaptive_workspace_size": (c_size_t, [c_int64]),
     "flc_adaptive_prepare": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_adaptive_select": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -215,6 +215,8 @@ def natural_decode(codes: torch.Tensor, n: int, out: Optional[torch.Tensor] = No
 TOPK_CHECK = os.environ.get("FLC_TOPK_CHECK", "0") not in ("", "0")
 TOPK_ERRORS = {1: "digit not found", 2: "count mismatch", 4: "exchange spin timeout"}
 _TOPK_KINDS = ("topk", "topk_batch")  # single-client and batched encoder workspaces (never shared)
+# every workspace kind whose kernels run a grid exchange, and the entry point reading its sticky error word
+_STATUS_FN = {"topk": "flc_topk_status", "topk_batch": "flc_topk_status", "quant": "flc_quant_status"}
 
 
 def topk_status(device: Optional[torch.device] = None, reset: bool = True) -> int:
@@ -234,16 +236,17 @@ def topk_status(device: Optional[torch.device] = None, reset: bool = True) -> in
 
 
 def topk_status_all(reset: bool = True) -> Dict[Tuple[int, int], int]:
-    """{(device, stream): error word} of every cached top-k workspace.  Synchronises each device first and
-    reads on its current stream (the stream a workspace was used on may be gone)."""
+    """{(device, stream): error word} of every cached workspace whose kernels run a grid exchange (the top-k
+    encoders, the one-launch quantizer).  Synchronises each device first and reads on its current stream (the stream
+    a workspace was used on may be gone)."""
     res: Dict[Tuple[int, int], int] = {}
     for (dev, stream, kind), ws in list(_WS.items()):
-        if kind not in _TOPK_KINDS:
+        if kind not in _STATUS_FN:
             continue
         d = torch.device("cuda", dev)
         torch.cuda.synchronize(d)
         out = torch.empty(1, dtype=torch.int64, device=d)
-        call("flc_topk_status", _p(ws), _p(out), int(reset), _stream(d))
+        call(_STATUS_FN[kind], _p(ws), _p(out), int(reset), _stream(d))
         res[(dev, stream)] = res.get((dev, stream), 0) | int(out.item())
     return res
 

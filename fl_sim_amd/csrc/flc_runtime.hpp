@@ -21,6 +21,29 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// ---- persistent launches (runtime.cpp) --------------------------------------------------------------------------
+// The top-k encoders and the fused quantizer run one block per CU and hand data between blocks inside the launch, so
+// every block must be resident at once: one such launch per device at a time.  While every call comes on one stream,
+// stream order is the guarantee and nothing is added (an event record after the launch costs the next kernel ~4 us
+// of dispatch gap).  The first call on a second stream drains the device once (the earlier stream may be gone by
+// now, so nothing is recorded on it), and from then on persistent launches are chained with an event recorded after
+// each one (stream-ordered, no host blocking).  Not under stream capture (a captured graph replays in its own order).
+int device_cus(int dev);                         // compute units of a device (cached)
+int current_cus(int* dev_out);                   // ... of the calling thread's current device
+int stream_cus(hipStream_t st, int* dev_out);    // ... of the stream's device (the current one for the null stream)
+
+class Coresident {  // scoped: construct before the persistent launch(es) on `st`, finish() after them
+ public:
+  Coresident(hipStream_t st, int dev);
+  ~Coresident();
+  int status() const { return rc_; }
+  int finish();  // records the chaining event when several streams are in use; returns FLC_OK or the error
+ private:
+  hipStream_t st_;
+  int dev_, rc_ = 0;
+  bool gated_ = false, locked_ = false;
+};
+
 // workspace carving: every region 256-byte aligned
 struct Carver {
   char* base;

@@ -20,6 +20,8 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 
 #include "flc_device.hpp"
 #include "flc_runtime.hpp"
@@ -36,17 +38,23 @@ constexpr int kNormChunk = 4096;            // elements per norm block (16 per t
 constexpr int kRowSlots = 16;              // per-block LDS nnz slots
 
 struct QuantWs {
+  unsigned long long* err;       // [1] sticky error word: 4 = a fused launch's exchange timed out (flc_quant_status)
+  unsigned* flags;               // [1024] fused launch: each block's arrival epoch
   unsigned long long* partials;  // [rows * kNormMaxParts]
   int* chunk_counts;             // [nblocks]  (compat)
   long long* chunk_offsets;      // [nblocks]  (compat)
+  unsigned long long* rowmax;    // [rows] fused launch: (epoch << 32 | max |x| bits) per row
 };
 
 QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* need) {
   Carver c(ws, bytes);
   QuantWs w;
+  w.err = c.take<unsigned long long>(1);
+  w.flags = c.take<unsigned>(1024);
   w.partials = c.take<unsigned long long>((size_t)rows * kNormMaxParts);
   w.chunk_counts = c.take<int>((size_t)nblocks);
   w.chunk_offsets = c.take<long long>((size_t)nblocks);
+  w.rowmax = c.take<unsigned long long>((size_t)rows);
   *need = c.off;
   return w;
 }
@@ -379,9 +387,89 @@ __global__ __launch_bounds__(kThreads) void quant_encode_kernel(
   }
 }
 
-// Philox mode, one group of 8 elements per thread.  The common case — a full group inside one row — takes one
-// row lookup (one 64-bit division per thread) and one norm load; groups straddling a row boundary or the end
-// take the per-element path.  DEC also writes the decoded values (flc_quant_encode_decode).
+// One group of 8 elements (flat index e0, `valid` of them real) in Philox mode: the common case — a full group inside
+// one row — takes one norm lookup and, for standard dithering, a branch-light fp32 level decision; groups straddling a
+// row boundary or the end take the per-element path.  norm_of(r): row r's norm; nnz_add(r, count) when counting.
+// DEC also writes the decoded values (flc_quant_encode_decode).
+template <int KIND, int BITS, bool DEC, class NormOf, class NnzAdd>
+__device__ __forceinline__ void philox_group_encode(const float (&v)[kGroup], int64_t e0, int valid, int64_t d, int s,
+                                                    double step, uint64_t seed, uint64_t counter,
+                                                    uint8_t* __restrict__ codes, float* __restrict__ out, bool count,
+                                                    NormOf norm_of, NnzAdd nnz_add) {
+  const U4 a = philox_group((uint64_t)e0 >> 2, seed, counter);
+  const U4 b = philox_group(((uint64_t)e0 >> 2) + 1, seed, counter);
+  const uint32_t wd[kGroup] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const int64_t r0 = e0 / d;
+  const int64_t r_end = (r0 + 1) * d;
+  uint64_t packed = 0;
+  float o[kGroup];
+  const bool whole = valid == kGroup && e0 + kGroup <= r_end;
+  const float nr0 = whole ? norm_of(r0) : 0.0f;
+  if (KIND == 0 && whole && norm_regular(nr0)) {
+    // standard dithering, branch-light: an fp32 decision for all 8 elements, then the exact fp64 rule for the rare
+    // elements its margins do not decide (whole-wave branch).  No division: t' = |x| * fp32(s / norm) is within
+    // 2^-23 t <= 1.6e-5 of s|x|/norm, and the reference's t = fp32(|x| / norm) * s within 7.6e-6 of it, so
+    // |t' - t| < 2.4e-5 and the same holds for p = ceil(t) - t (the subtraction is exact); u in fp32 straight
+    // from the Philox word is within 6e-8 of u.  Margins 1e-4 (bracket) and 5e-5 (u vs p) cover that.
+    const float rs = (float)s / nr0;
+    uint32_t lvl[kGroup];
+    uint32_t slow = 0;
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const float t = fabsf(v[j]) * rs;
+      const float jf = ceilf(t);
+      const float pf = jf - t;
+      const float uf = (float)wd[j] * 2.3283064365386963e-10f;
+      const bool ok = (pf > 1e-4f) & (t - (jf - 1.0f) > 1e-4f) & (fabsf(uf - pf) > 5e-5f);
+      lvl[j] = (uint32_t)(int)jf - (uf < pf ? 1u : 0u);
+      slow |= (uint32_t)(!ok && v[j] != 0.0f) << j;
+    }
+    if (slow) {
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j)
+        if ((slow >> j) & 1u) lvl[j] = (uint32_t)dither_level<0>(fabsf(v[j]) / nr0, s, step, u01(wd[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const uint32_t c = v[j] == 0.0f ? 0u : (((__float_as_uint(v[j]) >> 31) << (BITS - 1)) | lvl[j]);
+      packed |= (uint64_t)c << (j * BITS);
+      if (DEC) o[j] = dequant<KIND, BITS>(c, nr0, s, step);
+    }
+  } else if (whole) {
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const uint32_t c = quant_code<KIND, BITS>(v[j], nr0, s, step, u01(wd[j]));
+      packed |= (uint64_t)c << (j * BITS);
+      if (DEC) o[j] = dequant<KIND, BITS>(c, nr0, s, step);
+    }
+  } else {
+    for (int j = 0; j < valid; ++j) {
+      const int64_t r = (e0 + j) / d;
+      const float nr = norm_of(r);
+      const uint32_t c = quant_code<KIND, BITS>(v[j], nr, s, step, u01(wd[j]));
+      packed |= (uint64_t)c << (j * BITS);
+      if (DEC) o[j] = dequant<KIND, BITS>(c, nr, s, step);
+      if (count && v[j] != 0.0f) nnz_add(r, 1);
+    }
+  }
+  if (count && whole) {
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) cnt += v[j] != 0.0f;
+    if (cnt) nnz_add(r0, cnt);
+  }
+  store_codes<BITS>(codes, e0, valid, packed);
+  if (DEC) {
+    if (valid == kGroup) {
+      *reinterpret_cast<float4*>(out + e0) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(out + e0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+      for (int j = 0; j < valid; ++j) out[e0 + j] = o[j];
+    }
+  }
+}
+
+// Philox mode, one group of 8 elements per thread (every wave's loads in flight at once: a small batch fills the chip).
 // FOLD (FLC_NORM_INF / FLC_NORM_L2 + 1; 0 = norms given): the block folds the norm partials of its rows itself
 // (d >= the block's span, so at most two rows) and the block holding a row's first element writes norms[row].
 template <int KIND, int BITS, bool DEC, int FOLD>
@@ -414,100 +502,144 @@ __global__ __launch_bounds__(kThreads) void quant_encode_philox_kernel(
     const int valid = n - e0 < kGroup ? (int)(n - e0) : kGroup;
     float v[kGroup];
     load_group(x, e0, valid, v);
-    const U4 a = philox_group((uint64_t)e0 >> 2, seed, counter);
-    const U4 b = philox_group(((uint64_t)e0 >> 2) + 1, seed, counter);
-    const uint32_t wd[kGroup] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    const int64_t r0 = e0 / d;
-    const int64_t r_end = (r0 + 1) * d;
-    uint64_t packed = 0;
-    float o[kGroup];
-    const float nr0 = (valid == kGroup && e0 + kGroup <= r_end) ? (FOLD ? s_norm[r0 - row_base] : norms[r0]) : 0.0f;
-    if (KIND == 0 && valid == kGroup && e0 + kGroup <= r_end && norm_regular(nr0)) {
-      // standard dithering, branch-light: an fp32 decision for all 8 elements, then the exact fp64 rule for the rare
-      // elements its margins do not decide (whole-wave branch).  No division: t' = |x| * fp32(s / norm) is within
-      // 2^-23 t <= 1.6e-5 of s|x|/norm, and the reference's t = fp32(|x| / norm) * s within 7.6e-6 of it, so
-      // |t' - t| < 2.4e-5 and the same holds for p = ceil(t) - t (the subtraction is exact); u in fp32 straight
-      // from the Philox word is within 6e-8 of u.  Margins 1e-4 (bracket) and 5e-5 (u vs p) cover that.
-      const float rs = (float)s / nr0;
-      uint32_t lvl[kGroup];
-      uint32_t slow = 0;
-#pragma unroll
-      for (int j = 0; j < kGroup; ++j) {
-        const float t = fabsf(v[j]) * rs;
-        const float jf = ceilf(t);
-        const float pf = jf - t;
-        const float uf = (float)wd[j] * 2.3283064365386963e-10f;
-        const bool ok = (pf > 1e-4f) & (t - (jf - 1.0f) > 1e-4f) & (fabsf(uf - pf) > 5e-5f);
-        lvl[j] = (uint32_t)(int)jf - (uf < pf ? 1u : 0u);
-        slow |= (uint32_t)(!ok && v[j] != 0.0f) << j;
-      }
-      if (slow) {
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j)
-          if ((slow >> j) & 1u) lvl[j] = (uint32_t)dither_level<0>(fabsf(v[j]) / nr0, s, step, u01(wd[j]));
-      }
-#pragma unroll
-      for (int j = 0; j < kGroup; ++j) {
-        const uint32_t c = v[j] == 0.0f ? 0u : (((__float_as_uint(v[j]) >> 31) << (BITS - 1)) | lvl[j]);
-        packed |= (uint64_t)c << (j * BITS);
-        if (DEC) o[j] = dequant<KIND, BITS>(c, nr0, s, step);
-      }
-      if (nnz) {
-        int cnt = 0;
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j) cnt += v[j] != 0.0f;
-        const int rl = (int)(r0 - row_base);
-        if (cnt) {
-          if (rl < kRowSlots) atomicAdd(&s_nnz[rl], (unsigned long long)cnt);
-          else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r0]), (unsigned long long)cnt);
-        }
-      }
-    } else if (valid == kGroup && e0 + kGroup <= r_end) {
-      const float nr = nr0;
-#pragma unroll
-      for (int j = 0; j < kGroup; ++j) {
-        const uint32_t c = quant_code<KIND, BITS>(v[j], nr, s, step, u01(wd[j]));
-        packed |= (uint64_t)c << (j * BITS);
-        if (DEC) o[j] = dequant<KIND, BITS>(c, nr, s, step);
-      }
-      if (nnz) {
-        int cnt = 0;
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j) cnt += v[j] != 0.0f;
-        const int rl = (int)(r0 - row_base);
-        if (cnt) {
-          if (rl < kRowSlots) atomicAdd(&s_nnz[rl], (unsigned long long)cnt);
-          else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r0]), (unsigned long long)cnt);
-        }
-      }
-    } else {
-      for (int j = 0; j < valid; ++j) {
-        const int64_t r = (e0 + j) / d;
-        const float nr = FOLD ? s_norm[r - row_base] : norms[r];
-        const uint32_t c = quant_code<KIND, BITS>(v[j], nr, s, step, u01(wd[j]));
-        packed |= (uint64_t)c << (j * BITS);
-        if (DEC) o[j] = dequant<KIND, BITS>(c, nr, s, step);
-        if (nnz && v[j] != 0.0f) {
+    philox_group_encode<KIND, BITS, DEC>(
+        v, e0, valid, d, s, step, seed, counter, codes, out, nnz != nullptr,
+        [&](int64_t r) { return FOLD ? s_norm[r - row_base] : norms[r]; },
+        [&](int64_t r, int cnt) {
           const int rl = (int)(r - row_base);
-          if (rl < kRowSlots) atomicAdd(&s_nnz[rl], 1ull);
-          else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r]), 1ull);
-        }
-      }
-    }
-    store_codes<BITS>(codes, e0, valid, packed);
-    if (DEC) {
-      if (valid == kGroup) {
-        *reinterpret_cast<float4*>(out + e0) = make_float4(o[0], o[1], o[2], o[3]);
-        *reinterpret_cast<float4*>(out + e0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
-      } else {
-        for (int j = 0; j < valid; ++j) out[e0 + j] = o[j];
-      }
-    }
+          if (rl < kRowSlots) atomicAdd(&s_nnz[rl], (unsigned long long)cnt);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r]), (unsigned long long)cnt);
+        });
   }
   if (nnz) {
     __syncthreads();
     if (threadIdx.x < kRowSlots && s_nnz[threadIdx.x] != 0)
       atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[row_base + threadIdx.x]), s_nnz[threadIdx.x]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// configs[1] in one launch (flc_quant_encode_auto with p = inf, Philox): one 1024-thread block per CU, block b owning
+// the flat span [b SPAN, (b + 1) SPAN) of the batch (SPAN = 8192 GPT elements, d >= SPAN: at most two rows per block).
+// Each thread loads its GPT groups of 8 (coalesced: group j of thread t at (j * 1024 + t) * 8) and keeps them in
+// registers; the block's max |x| per row goes to the workspace with one 64-bit atomicMax of (epoch << 32 | bits) —
+// the epoch makes last call's values smaller than any of this one's, so nothing is zeroed; then a grid exchange
+// (every block raises its flag to the epoch, one wave polls all flags); then every block reads its rows' norms and
+// encodes (+ decodes) from the registers.  x is read once, the codes and the decoded batch written once: 9 B/element
+// in one launch, bit-identical to the two-launch form (max is exact in any order; same Philox words, same rule).
+// ------------------------------------------------------------------------------------------------
+constexpr int kFT = 1024;
+constexpr int kMaxFused = 1024;  // blocks (flags)
+
+__device__ __forceinline__ void fused_exchange(const QuantWs& ws, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(ws.flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid < kWave) {
+    const int G = (int)gridDim.x;
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < kMaxFused / kWave; ++i) {
+        const int b = tid + i * kWave;
+        if (i * kWave < G) {  // (uniform)
+          const unsigned f = __hip_atomic_load(ws.flags + (b < G ? b : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= b >= G || (int)(f - epoch) >= 0;
+        }
+      }
+      if (__ballot(!ok) == 0ull) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {  // ~1 s: a block never arrived (lost co-residency); flag it and let the launch drain
+        if (tid == 0) __hip_atomic_fetch_or(ws.err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+template <int KIND, int BITS, bool DEC, int GPT>
+__global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restrict__ x, int64_t n, int64_t d, int s,
+                                                          double step, float* __restrict__ norms, uint64_t seed,
+                                                          uint64_t counter, uint8_t* __restrict__ codes,
+                                                          long long* __restrict__ nnz, float* __restrict__ out,
+                                                          QuantWs ws, unsigned epoch) {
+  constexpr int64_t SPAN = (int64_t)kFT * kGroup * GPT;
+  __shared__ uint32_t s_m[2][kFT / kWave];
+  __shared__ float s_norm[2];
+  __shared__ unsigned long long s_nnz[2];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
+  const int64_t base = (int64_t)blockIdx.x * SPAN;
+  const int64_t r0 = base / d, rb = (r0 + 1) * d, rows = (n + d - 1) / d;
+  float v[GPT][kGroup];
+  uint32_t m0 = 0, m1 = 0;
+#pragma unroll
+  for (int g = 0; g < GPT; ++g) {
+    const int64_t e0 = base + ((int64_t)g * kFT + tid) * kGroup;
+    const int valid = e0 >= n ? 0 : (n - e0 < kGroup ? (int)(n - e0) : kGroup);
+    if (valid == kGroup) {
+      load_group(x, e0, kGroup, v[g]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) v[g][j] = j < valid ? x[e0 + j] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const uint32_t a = __float_as_uint(v[g][j]) & 0x7fffffffu;  // |v| bits; NaN > inf > finite
+      if (e0 + j < rb) m0 = a > m0 ? a : m0;
+      else m1 = a > m1 ? a : m1;
+    }
+  }
+  m0 = wave_max_u32(m0);
+  m1 = wave_max_u32(m1);
+  if (lane == 0) {
+    s_m[0][wid] = m0;
+    s_m[1][wid] = m1;
+  }
+  if (tid < 2) s_nnz[tid] = 0ull;
+  __syncthreads();
+  if (tid < 2) {
+    const int64_t r = r0 + tid;
+    const int64_t lo = tid == 0 ? base : rb, hi = base + SPAN < n ? base + SPAN : n;
+    if (r < rows && lo < hi) {  // this block holds elements of row r
+      uint32_t m = 0;
+      for (int w = 0; w < kFT / kWave; ++w) m = s_m[tid][w] > m ? s_m[tid][w] : m;
+      __hip_atomic_fetch_max(ws.rowmax + r, ((unsigned long long)epoch << 32) | m, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  fused_exchange(ws, epoch);
+  if (tid < 2) {
+    const int64_t r = r0 + tid;
+    if (r < rows) {
+      const float nr = __uint_as_float(
+          (uint32_t)__hip_atomic_load(ws.rowmax + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      s_norm[tid] = nr;
+      if (r * d >= base && r * d < base + SPAN) norms[r] = nr;  // the block holding the row's first element
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < GPT; ++g) {
+    const int64_t e0 = base + ((int64_t)g * kFT + tid) * kGroup;
+    if (e0 < n) {
+      const int valid = n - e0 < kGroup ? (int)(n - e0) : kGroup;
+      philox_group_encode<KIND, BITS, DEC>(
+          v[g], e0, valid, d, s, step, seed, counter, codes, out, nnz != nullptr,
+          [&](int64_t r) { return s_norm[r - r0]; },
+          [&](int64_t r, int cnt) { atomicAdd(&s_nnz[r - r0], (unsigned long long)cnt); });
+    }
+  }
+  if (nnz) {
+    __syncthreads();
+    if (tid < 2 && s_nnz[tid] != 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&nnz[r0 + tid]), s_nnz[tid]);
   }
 }
 
@@ -603,6 +735,14 @@ using namespace flc;
 
 extern "C" {
 
+int flc_quant_status(void* ws, uint64_t* err_out, int reset, void* stream) {
+  if (!ws || !err_out) return fail(FLC_EINVAL, "flc_quant_status: null workspace or output");
+  hipStream_t st = as_stream(stream);
+  FLC_CHECK_HIP(hipMemcpyAsync(err_out, ws, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));  // QuantWs::err
+  if (reset) FLC_CHECK_HIP(hipMemsetAsync(ws, 0, sizeof(uint64_t), st));
+  return FLC_OK;
+}
+
 size_t flc_quant_workspace_size(int64_t rows, int64_t d) {
   size_t need = 0;
   const int64_t nblocks = cdiv(rows * d, (int64_t)kGroup * kGroupsPerBlock);
@@ -685,6 +825,30 @@ int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p,
   const int64_t nb1 = cdiv(n, (int64_t)kGroup * kThreads);
   long long* nz = reinterpret_cast<long long*>(nnz);
   const char* name = DEC ? "quant_encode_decode" : "quant_encode";
+  if (norm_p == FLC_NORM_INF && !getenv("FLC_QUANT_TWO_LAUNCH")) {
+    // one launch when the batch fits one 1024-thread block per CU with at most two rows per block (configs[1])
+    int dev = 0;
+    const int cus = std::min(stream_cus(st, &dev), kMaxFused);
+    const int gpt = (d >= 2 * kFT * kGroup && n <= (int64_t)cus * 2 * kFT * kGroup)   ? 2
+                    : (d >= 4 * kFT * kGroup && n <= (int64_t)cus * 4 * kFT * kGroup) ? 4
+                                                                                        : 0;
+    if (gpt) {
+      static std::atomic<unsigned> epochs{0};
+      unsigned ep = ++epochs;
+      if (ep == 0) ep = ++epochs;  // (the flags of a fresh workspace are 0)
+      const unsigned grid = (unsigned)cdiv(n, (int64_t)gpt * kFT * kGroup);
+      const char* fname = DEC ? "quant_fused_encode_decode" : "quant_fused_encode";
+      Coresident co(st, dev);
+      if (co.status()) return co.status();
+      if (gpt == 2)
+        FLC_LAUNCH(fname, (quant_fused_kernel<KIND, BITS, DEC, 2>), dim3(grid), dim3(kFT), 0, st, x, n, d, levels, step,
+                   norms, seed, counter, codes, nz, out, w, ep);
+      else
+        FLC_LAUNCH(fname, (quant_fused_kernel<KIND, BITS, DEC, 4>), dim3(grid), dim3(kFT), 0, st, x, n, d, levels, step,
+                   norms, seed, counter, codes, nz, out, w, ep);
+      return co.finish();
+    }
+  }
   if (norm_p == FLC_NORM_INF) {
     FLC_LAUNCH("quant_norm", quant_norm_kernel<FLC_NORM_INF>, dim3((unsigned)parts, (unsigned)rows), dim3(kThreads), 0,
                st, x, d, (int)parts, chunk, vec_ok, w);

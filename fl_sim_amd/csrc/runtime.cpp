@@ -71,6 +71,101 @@ void probe_after(const char* name, hipStream_t s) {
   if (!p.pending.empty()) (void)hipEventRecord(p.pending.back().second, s);
 }
 
+// ---- persistent launches: one at a time per device (flc_runtime.hpp) ----------------------------------------------
+namespace {
+struct Gate {
+  std::mutex mu;
+  hipEvent_t last[64] = {};
+  hipStream_t first[64] = {};
+  bool used[64] = {};
+  bool multi[64] = {};
+  bool recorded[64] = {};
+  int cus[64] = {};
+};
+Gate& gate() {
+  static Gate g;
+  return g;
+}
+std::mutex& cus_mu() {
+  static std::mutex m;
+  return m;
+}
+}  // namespace
+
+int device_cus(int dev) {
+  Gate& g = gate();
+  std::lock_guard<std::mutex> lk(cus_mu());
+  if (g.cus[dev] == 0) {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0) cu = 256;
+    g.cus[dev] = cu;
+  }
+  return g.cus[dev];
+}
+
+int current_cus(int* dev_out) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (dev_out) *dev_out = dev;
+  return device_cus(dev);
+}
+
+int stream_cus(hipStream_t st, int* dev_out) {
+  int dev = -1;
+  if (st == nullptr || hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) return current_cus(dev_out);
+  if (dev_out) *dev_out = dev;
+  return device_cus(dev);
+}
+
+Coresident::Coresident(hipStream_t st, int dev) : st_(st), dev_(dev < 0 || dev >= 64 ? 0 : dev) {
+  Gate& gt = gate();
+  gt.mu.lock();
+  locked_ = true;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing(st_, &cs);
+  if (e != hipSuccess) {
+    rc_ = hip_fail(e, "hipStreamIsCapturing");
+    return;
+  }
+  gated_ = cs == hipStreamCaptureStatusNone;
+  if (!gated_) return;
+  if (!gt.used[dev_]) {
+    gt.used[dev_] = true;
+    gt.first[dev_] = st_;
+  } else if (!gt.multi[dev_] && st_ != gt.first[dev_]) {
+    if ((e = hipDeviceSynchronize()) != hipSuccess) {
+      rc_ = hip_fail(e, "hipDeviceSynchronize");
+      return;
+    }
+    if (!gt.last[dev_] && (e = hipEventCreateWithFlags(&gt.last[dev_], hipEventDisableTiming)) != hipSuccess) {
+      rc_ = hip_fail(e, "hipEventCreateWithFlags");
+      return;
+    }
+    gt.multi[dev_] = true;
+  }
+  if (gt.multi[dev_] && gt.recorded[dev_] && (e = hipStreamWaitEvent(st_, gt.last[dev_], 0)) != hipSuccess)
+    rc_ = hip_fail(e, "hipStreamWaitEvent");
+}
+
+int Coresident::finish() {
+  Gate& gt = gate();
+  if (rc_ == 0 && gated_ && gt.multi[dev_]) {
+    hipError_t e = hipEventRecord(gt.last[dev_], st_);
+    if (e != hipSuccess) rc_ = hip_fail(e, "hipEventRecord");
+    else gt.recorded[dev_] = true;
+  }
+  if (locked_) {
+    locked_ = false;
+    gt.mu.unlock();
+  }
+  return rc_;
+}
+
+Coresident::~Coresident() {
+  if (locked_) gate().mu.unlock();
+}
+
 }  // namespace flc
 
 extern "C" {

@@ -1967,82 +1967,6 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-// one select launch per device at a time, so two never compete for co-residency.  While every call
-// comes on one stream, stream order is the guarantee and nothing is added (an event record after the
-// select costs the next kernel ~4 us of dispatch gap).  The first call on a second stream drains the
-// device once (the earlier stream may be gone by now, so nothing is recorded on it), and from then on
-// selects are chained with an event recorded after each one (stream-ordered, no host blocking).
-struct SelectGate {
-  std::mutex mu;
-  hipEvent_t last[64] = {};
-  hipStream_t first[64] = {};
-  bool used[64] = {};
-  bool multi[64] = {};
-  bool recorded[64] = {};
-  int cus[64] = {};
-};
-SelectGate& gate() {
-  static SelectGate g;
-  return g;
-}
-
-int device_cus(int dev) {
-  SelectGate& g = gate();
-  std::lock_guard<std::mutex> lk(g.mu);
-  if (g.cus[dev] == 0) {
-    int cu = 0;
-    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0) cu = 256;
-    g.cus[dev] = cu;
-  }
-  return g.cus[dev];
-}
-
-// before a select launch (gt.mu held): not under capture, the first call on a second stream drains the device once,
-// and from then on the launch waits for the previous select's event
-int gate_enter(SelectGate& gt, int dev, hipStream_t st, bool* gated) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  FLC_CHECK_HIP(hipStreamIsCapturing(st, &cs));
-  *gated = cs == hipStreamCaptureStatusNone;
-  if (*gated) {
-    if (!gt.used[dev]) {
-      gt.used[dev] = true;
-      gt.first[dev] = st;
-    } else if (!gt.multi[dev] && st != gt.first[dev]) {
-      FLC_CHECK_HIP(hipDeviceSynchronize());
-      if (!gt.last[dev]) FLC_CHECK_HIP(hipEventCreateWithFlags(&gt.last[dev], hipEventDisableTiming));
-      gt.multi[dev] = true;
-    }
-    if (gt.multi[dev] && gt.recorded[dev]) FLC_CHECK_HIP(hipStreamWaitEvent(st, gt.last[dev], 0));
-  }
-  return FLC_OK;
-}
-
-// after it: record the chaining event once several streams are in use
-int gate_exit(SelectGate& gt, int dev, hipStream_t st, bool gated) {
-  if (gated && gt.multi[dev]) {
-    FLC_CHECK_HIP(hipEventRecord(gt.last[dev], st));
-    gt.recorded[dev] = true;
-  }
-  return FLC_OK;
-}
-
-int current_cus(int* dev_out) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  if (dev < 0 || dev >= 64) dev = 0;
-  if (dev_out) *dev_out = dev;
-  return device_cus(dev);
-}
-
-// the CU count of the device a launch runs on: the stream's device (the calling thread's current device for the
-// null stream), so a batch on a device other than the current one is shaped for its own CUs
-int stream_cus(hipStream_t st, int* dev_out) {
-  int dev = -1;
-  if (st == nullptr || hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) return current_cus(dev_out);
-  if (dev_out) *dev_out = dev;
-  return device_cus(dev);
-}
-
 template <bool STACKED, class Src>
 int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, hipStream_t st, int* idx, float* val,
                 uint8_t* codes, float* norm, int levels, uint64_t seed, uint64_t counter, unsigned* tiles,
@@ -2060,10 +1984,8 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
   if (split)
     FLC_LAUNCH("topk_filter", topk_filter_kernel<Src>, dim3((unsigned)g.G), dim3(kET), 0, st, x, n, w, ss.S, ss.rank_lo,
                ss.rank_hi, ss.take_all);
-  SelectGate& gt = gate();
-  std::lock_guard<std::mutex> lk(gt.mu);
-  bool gated = false;
-  if (int rc = gate_enter(gt, dev, st, &gated)) return rc;
+  Coresident co(st, dev);
+  if (co.status()) return co.status();
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   if (split)
     FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", (topk_select_kernel<STACKED, false, Src>), dim3((unsigned)g.G),
@@ -2073,7 +1995,7 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
     FLC_LAUNCH(STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true, Src>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
                tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
-  return gate_exit(gt, dev, st, gated);
+  return co.finish();
 }
 
 // Batched stacked encode: the clients in chunks of at most `cus` (one select of cus / chunk blocks each, all in one
@@ -2141,10 +2063,8 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
   w.errp = reinterpret_cast<unsigned long long*>(base + kOffSt + offsetof(EncState, err));
   const SampleSetup ss = sample_setup(n, k, batch_sample_cap(n));
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
-  SelectGate& gt = gate();
-  std::lock_guard<std::mutex> lk(gt.mu);
-  bool gated = false;
-  if (int rc = gate_enter(gt, dev, st, &gated)) return rc;
+  Coresident co(st, dev);
+  if (co.status()) return co.status();
   for (int c0 = 0; c0 < C; c0 += bg.chunk) {
     const int cn = std::min(bg.chunk, C - c0);
     const BatchEntry* t = tab + c0;
@@ -2158,7 +2078,7 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
                dim3(kET), 0, st, proto, n, (long long)k, w, nullptr, nullptr, nullptr, nullptr, levels, step, 0ull,
                counter, nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, t);
   }
-  return gate_exit(gt, dev, st, gated);
+  return co.finish();
 }
 
 int check_topk(const float* x, int64_t n, int64_t k, const char* who) {

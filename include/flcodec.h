@@ -101,11 +101,16 @@ int flc_quant_encode_decode(const float* x, int64_t rows, int64_t d, int kind, i
                             const float* norms, uint64_t seed, uint64_t counter, const double* compat_u,
                             uint8_t* codes, int64_t* nnz, float* out, void* ws, size_t ws_bytes, void* stream);
 /* philox mode, norm included: the per-row norm (as flc_quant_norm computes it, written to norms), the encode and,
- * with out != NULL, the fused decode — two launches when d >= 2048 (the encode folds the norm partials itself),
- * three otherwise. */
+ * with out != NULL, the fused decode.  p = inf with d >= 16384 and a batch of at most #CU x 32768 elements (configs[1]:
+ * 10 x 417,482) runs in ONE persistent launch (one 1024-thread block per CU, a grid exchange of the per-row maxima;
+ * the co-residency contract of the top-k encoders, flc_topk_status below: check flc_quant_status); otherwise two
+ * launches when d >= 2048 (the encode folds the norm partials itself), three below.  The result is the same. */
 int flc_quant_encode_auto(const float* x, int64_t rows, int64_t d, int kind, int levels, int bits, int norm_p,
                           uint64_t seed, uint64_t counter, uint8_t* codes, float* norms, int64_t* nnz, float* out,
                           void* ws, size_t ws_bytes, void* stream);
+/* the quantizer workspace's sticky error word (4: a one-launch encode's grid exchange timed out, i.e. its blocks were
+ * not all resident — the outputs of that call are invalid); copied to *err_out (device uint64), zeroed with reset */
+int flc_quant_status(void* ws, uint64_t* err_out, int reset, void* stream);
 /* compat mode: how many uniforms the reference draws for this batch — one per element with x != 0
  * whose y = |x| / norm is not NaN (compressors.py:339-354); norms == NULL counts x != 0 (the natural
  * compressor, compressors.py:307-316).  *count is a device int64. */

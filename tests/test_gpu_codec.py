@@ -193,9 +193,12 @@ def test_quant_encode_decode_equals_encode_then_decode(kind, levels, rows, d, co
 
 @pytest.mark.parametrize("p", [math.inf, 2])
 @pytest.mark.parametrize("kind,levels", [(0, 127), (1, 8), (0, 3)])
-@pytest.mark.parametrize("rows,d", [(10, 417482), (3, 1001), (2, 2048), (5, 4099), (1, 13)])
+@pytest.mark.parametrize("rows,d", [(10, 417482), (3, 1001), (2, 2048), (5, 4099), (1, 13), (3, 2_000_003),
+                                    (1, 16384), (300, 20_000), (7, 16_387)])
 def test_quant_encode_auto_equals_the_separate_calls(p, kind, levels, rows, d):
-    """flc_quant_encode_auto (norm folded inside the encode for d >= 2048) = quant_norm + encode + decode."""
+    """flc_quant_encode_auto = quant_norm + encode + decode.  p = inf at configs[1]'s shape (10 x 417,482), 3 x 2 M,
+    1 x 16384 and 7 x 16387 takes the one-launch path (grid exchange of the row maxima; 2 or 4 groups per thread),
+    300 x 20,000 and the rest the two-launch path (the norm partials folded inside the encode for d >= 2048)."""
     codec = _codec()
     g = np.random.default_rng(rows * 7 + d)
     x = (g.standard_normal((rows, d)) * 1e-3).astype(np.float32)
@@ -210,6 +213,25 @@ def test_quant_encode_auto_equals_the_separate_calls(p, kind, levels, rows, d):
         assert torch.equal(pkt.codes, pkt2.codes) and torch.equal(pkt.nnz, pkt2.nnz)
         if dec:
             assert gc.same_bits(out2.cpu().numpy(), ref_out.cpu().numpy())
+    pkt3, out3 = codec.quant_encode_auto(xd, kind, levels, p, 9, 4)  # repeated calls: no state carried over
+    assert torch.equal(pkt.codes, pkt3.codes) and gc.same_bits(out3.cpu().numpy(), ref_out.cpu().numpy())
+
+
+def test_quant_one_launch_nan_and_zero_rows():
+    """The one-launch path on rows with NaN / inf / all zeros: the norms and codes of the two-launch path."""
+    codec = _codec()
+    g = np.random.default_rng(3)
+    x = (g.standard_normal((4, 417_482)) * 1e-3).astype(np.float32)
+    x[1, 77] = np.nan
+    x[2, :] = 0
+    x[3, 5] = np.inf
+    xd = torch.from_numpy(x).to(DEV)
+    norms = codec.quant_norm(xd, math.inf)
+    pkt = codec.quant_encode(xd, 0, 127, norms, 3, 1, None, want_nnz=True)
+    pkt2, out2 = codec.quant_encode_auto(xd, 0, 127, math.inf, 3, 1, want_nnz=True)
+    assert gc.same_bits(pkt2.norms.cpu().numpy(), norms.cpu().numpy())
+    assert torch.equal(pkt.codes, pkt2.codes) and torch.equal(pkt.nnz, pkt2.nnz)
+    assert gc.same_bits(out2.cpu().numpy(), codec.quant_decode(pkt).cpu().numpy())
 
 
 @pytest.mark.parametrize("D,K", [(4096, 41), (1_000_003, 10_000), (25_000_000, 250_000), (100, 100), (7, 3)])
