@@ -241,7 +241,7 @@ def cpu_baseline():
                       f"{reps_np} reps, {per_np * 1e3:.0f} ms/rep",
         },
     }
-    line["configs"] = cpu_configs(all_threads)
+    line["configs"] = cpu_configs(min(16, all_threads))
     return line
 
 
@@ -250,7 +250,8 @@ CONFIG0_SHAPES = [(16, 1, 5, 5), (16,), (32, 16, 5, 5), (32,), (256, 1568), (256
 
 def cpu_configs(threads: int) -> dict:
     """The CPU-PyTorch path beside configs[0]-[3] (BASELINE.md's "cpu_ref, same"), on this host at `threads`
-    threads: configs[0] the reference's FedAvg server update (oracle/aggregation_ref.py: the reference's own torch
+    threads (the box's CPU share per GPU: every op of these small shapes is far slower with all 256 threads of the
+    box's cgroup share of 16 cores oversubscribed — 2.6 s for one FedAvg update): configs[0] the reference's FedAvg server update (oracle/aggregation_ref.py: the reference's own torch
     ops) over 10 clients of cnn_femmist_tiny's 8 tensors, configs[1] 8-bit dithering of 10 x 417,482, configs[2]
     top-k 1 % of 25 M with the dense decode, configs[3] 8 clients x 25 M stacked codec + the add_(alpha) fold."""
     from oracle import aggregation_ref, torch_ref
@@ -295,10 +296,10 @@ def traffic_from_profiles():
 def aggregation_extras(dev, world: int, rank: int) -> dict:
     """The server half of north_star: the FedAvg and FedAdam server updates
     (FedOptServer.update, _fedopt.py:196-240) and avg_parameters (nodes.py:1134-1163) at configs[0]'s model
-    (cnn_femmist_tiny: 8 tensors, 417,482 parameters) x 10 clients, and one weighted fold of 8 clients x 25 M
-    (flc_weighted_sum, configs[3]'s server fold over dense deltas).  Algorithmic bytes: a fold reads its n sources and
-    the accumulator and writes it, (n + 2) * 4 * D; the FedOpt step reads theta and delta and writes theta (avg,
-    12 B/element) or also reads and writes v (adam, 20 B/element)."""
+    (cnn_femmist_tiny: 8 tensors, 417,482 parameters) x 10 clients — each one flc_model_fold launch for the whole model
+    — and one weighted fold of 8 clients x 25 M (flc_weighted_sum, configs[3]'s server fold over dense deltas).
+    Algorithmic bytes: a fold reads its n sources and the accumulator and writes it, (n + 2) * 4 * D; the FedOpt
+    update additionally reads and writes theta (avg: (n + 4) * 4 * D) and v (adam: (n + 6) * 4 * D)."""
     from fl_sim_amd import aggregation as fagg
     from fl_sim_amd import codec
     from fl_sim_amd import dist as fdist
@@ -314,9 +315,9 @@ def aggregation_extras(dev, world: int, rank: int) -> dict:
     d0, n0 = 417_482, 10
     legs = {
         "fedavg_update": (lambda: fagg.fedopt_update(th0, dl0, None, msgs0, "avg", 1.0, (0.0, 1.0), 1e-3),
-                          (n0 + 2) * 4 * d0 + 12 * d0),
+                          (n0 + 4) * 4 * d0),
         "fedadam_update": (lambda: fagg.fedopt_update(th0, dl0, v0, msgs0, "adam", 1e-2, (0.9, 0.99), 1e-3),
-                           (n0 + 2) * 4 * d0 + 20 * d0),
+                           (n0 + 6) * 4 * d0),
         "avg_parameters": (lambda: fagg.avg_parameters(th0, msgs0, size_aware=True, key="delta_parameters"),
                            (n0 + 2) * 4 * d0),
     }
@@ -327,8 +328,9 @@ def aggregation_extras(dev, world: int, rank: int) -> dict:
         gbs = nbytes / (ms * 1e-3) / 1e9
         line[name] = {"us": round(ms * 1e3, 2), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                       "algorithmic_bytes": nbytes}
-    line["bytes_formula"] = ("fold (n + 2) * 4 * D; FedOpt step avg 12 * D, adam 20 * D; D = 417,482, n = 10; one fold "
-                             "launch per tensor (flc_weighted_sum) + one step launch per tensor (flc_fedopt_step)")
+    line["bytes_formula"] = ("avg_parameters (n + 2) * 4 * D; FedAvg update (n + 4) * 4 * D, FedAdam (n + 6) * 4 * D; "
+                             "D = 417,482, n = 10; the whole model in one flc_model_fold launch (the delta fold and "
+                             "the optimizer step fused)")
     out["aggregation_config0_fedavg_10x417482"] = line
     del th0, dl0, v0, msgs0
     # 8 x 25 M: distinct sources (a repeated source would be served from the caches)

@@ -134,6 +134,8 @@ SIGNATURES = {
     "flc_randk_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "flc_weighted_sum": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_float, c_void_p, c_void_p]),
     "flc_fedopt_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
+    "flc_model_fold": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
+                               c_int, c_double, c_double, c_double, c_void_p]),
     "flc_delta_flatten": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "flc_feddr_combine": (
         c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_int, c_float, c_void_p]

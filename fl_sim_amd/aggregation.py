@@ -13,10 +13,11 @@ subclasses unchanged (``class MyServer(AggregationMixin, FedAvgServer)``):
                                                   (and the reference's client-id bookkeeping)
 * ``feddr_update``        — _feddr.py:166-190    ``y`` relaxation, ``x̃`` fold, ``θ = prox(c_x x̃ + c_y y)``
 
-Each tensor is folded in ONE launch (``flc_weighted_sum``): one read per message, one write, the
-fmaf chain in message order — bit-identical to the reference's sequential ``add_`` loop, which torch
-evaluates as one fp32 fma per element per message.  Scalars are formed in Python double exactly as
-the reference forms them and rounded to fp32 at the boundary, as torch does.
+A whole model is folded in ONE launch (``flc_model_fold``, up to 16 messages; FedOpt's optimizer step fused into
+the same pass), else each tensor in one launch (``flc_weighted_sum``): one read per message, one write, the fmaf chain
+in message order — bit-identical to the reference's sequential ``add_`` loop, which torch evaluates as one fp32 fma
+per element per message.  Scalars are formed in Python double exactly as the reference forms them and rounded to fp32
+at the boundary, as torch does.
 """
 
 from __future__ import annotations
@@ -38,9 +39,33 @@ def _on(t: torch.Tensor, device: torch.device) -> torch.Tensor:
     return t if t.device == device else t.to(device)
 
 
+def _model_device(tensors: Sequence[torch.Tensor]) -> Optional[torch.device]:
+    """The one HIP device all of a model's tensors live on (contiguous fp32), or None (then per-tensor launches)."""
+    devs = {t.device for t in tensors}
+    if len(devs) != 1:
+        return None
+    dev = next(iter(devs))
+    ok = dev.type == "cuda" and all(t.dtype == torch.float32 and t.is_contiguous() for t in tensors)
+    return dev if ok else None
+
+
+def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
+          init_mode: int, beta: float = 0.0, **step) -> bool:
+    """The whole model in one flc_model_fold launch when it qualifies (one device, <= 16 messages); False otherwise."""
+    dev = _model_device(list(dsts) + list(step.get("theta") or []) + list(step.get("v") or []))
+    if dev is None or not dsts or len(msg_tensors) > codec.MODEL_FOLD_MAX_SRC:
+        return False
+    srcs = [[_on(t, dev) for t in mt] for mt in msg_tensors]
+    codec.model_fold(dsts, srcs, weights, init_mode, beta, **step)
+    return True
+
+
 def add_parameters(server_params: Iterable[torch.Tensor], params: Iterable[torch.Tensor], ratio: float) -> None:
     """nodes.py:1116-1132."""
-    for sp, p in zip(_params(server_params), params):
+    sps, ps = _params(server_params), list(params)
+    if _fold(sps, [ps], [ratio], 2):
+        return
+    for sp, p in zip(sps, ps):
         codec.weighted_sum(sp, [_on(p, sp.device)], [ratio], init_mode=2)
 
 
@@ -54,6 +79,8 @@ def avg_parameters(server_params: Sequence[torch.Tensor], messages: Sequence[Map
     ratios = [
         (m["train_samples"] / total_samples if size_aware else 1 / len(messages)) * (1 - inertia) for m in messages
     ]
+    if _fold(_params(server_params), [m[key] for m in messages], ratios, 0, inertia):
+        return
     for j, sp in enumerate(_params(server_params)):
         srcs = [_on(m[key][j], sp.device) for m in messages]
         codec.weighted_sum(sp, srcs, ratios, init_mode=0, beta=inertia)
@@ -66,6 +93,16 @@ def update_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Ma
     assert all(["gradients" in m for m in messages]), "some clients have not sent gradients yet"
     total_samples = sum([m["train_samples"] for m in messages])
     weights = [m["train_samples"] / total_samples for m in messages]
+    g0s = messages[0]["gradients"]
+    devs = {mp.device if mp.device.type == "cuda" else g.device for mp, g in zip(model_params, g0s)}
+    if len(devs) == 1 and next(iter(devs)).type == "cuda":
+        dev = next(iter(devs))
+        gs = [torch.empty(g.shape, dtype=torch.float32, device=dev) for g in g0s]
+        if _fold(gs, [m["gradients"] for m in messages], weights, 1):
+            for mp, g in zip(model_params, gs):
+                if isinstance(mp, torch.Tensor) and mp.requires_grad:
+                    mp.grad = g
+            return gs
     grads = []
     for j, mp in enumerate(model_params):
         g0 = messages[0]["gradients"][j]
@@ -86,6 +123,11 @@ def fedopt_update(model_params: Sequence[torch.Tensor], delta_parameters: Sequen
     if opt not in ("avg", "adagrad", "yogi", "adam"):
         raise ValueError(f"Unknown optimizer: {optimizer}")
     alpha = (1 - betas[0]) / len(messages) if len(messages) else 0.0
+    ps = _params(model_params)
+    vps = None if (v_parameters is None or opt == "avg") else list(v_parameters)
+    if _fold(list(delta_parameters), [m["delta_parameters"] for m in messages], [alpha] * len(messages), 0, betas[0],
+             theta=ps, v=vps, opt=opt if vps is not None else "avg", lr=lr, beta2=betas[1], tau=tau):
+        return  # the delta average and the optimizer step of every tensor in one launch
     for j, dp in enumerate(delta_parameters):
         srcs = [_on(m["delta_parameters"][j], dp.device) for m in messages]
         codec.weighted_sum(dp, srcs, [alpha] * len(srcs), init_mode=0, beta=betas[0])
@@ -103,6 +145,11 @@ def scaffold_update(model_params: Sequence[torch.Tensor], control_variates: Sequ
         raise ZeroDivisionError("division by zero")  # ratio_p = lr / len(messages) in the reference
     ratio_p = lr / len(messages)
     ratio_c = 1 / num_clients
+    ps, cvs = _params(model_params), list(control_variates)
+    if _model_device(ps + cvs) is not None and ps and cvs and len(messages) <= codec.MODEL_FOLD_MAX_SRC:
+        _fold(ps, [m["parameters_delta"] for m in messages], [ratio_p] * len(messages), 2)
+        _fold(cvs, [m["control_variates_delta"] for m in messages], [ratio_c] * len(messages), 2)
+        return
     for j, sp in enumerate(_params(model_params)):
         codec.weighted_sum(sp, [_on(m["parameters_delta"][j], sp.device) for m in messages], [ratio_p] * len(messages),
                            init_mode=2)

@@ -683,6 +683,38 @@ def weighted_sum(dst: torch.Tensor, srcs: Sequence[torch.Tensor], weights: Seque
     return dst
 
 
+MODEL_FOLD_MAX_SRC = 16
+
+
+def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
+               init_mode: int, beta: float = 0.0, theta: Optional[Sequence[torch.Tensor]] = None,
+               v: Optional[Sequence[torch.Tensor]] = None, opt: str = "avg", lr: float = 1.0, beta2: float = 0.0,
+               tau: float = 0.0) -> None:
+    """A whole model in one launch (flc_model_fold): per tensor t, ``weighted_sum(dsts[t], [s[t] for s in srcs],
+    weights, init_mode, beta)`` and, with ``theta``, ``fedopt_step(theta[t], dsts[t], v[t], opt, lr, beta2, tau)``.
+    ``srcs[m]`` is message m's list of tensors (all on the dsts' device); at most 16 messages."""
+    import ctypes
+
+    nt, ns = len(dsts), len(srcs)
+    if ns > MODEL_FOLD_MAX_SRC:
+        raise ValueError(f"model_fold takes at most {MODEL_FOLD_MAX_SRC} messages")
+    P = ctypes.c_void_p
+    for t in list(dsts) + list(theta or []) + list(v or []):
+        if t.device.type != "cuda" or t.dtype != torch.float32 or not t.is_contiguous():
+            raise TypeError("model tensors must be contiguous fp32 HIP tensors")
+    for msg in srcs:
+        if len(msg) != nt or any(a.numel() != b.numel() for a, b in zip(msg, dsts)):
+            raise ValueError("every message has one tensor per model tensor, of matching sizes")
+    flat = [_dev_f32(msg[t], "src") for msg in srcs for t in range(nt)]
+    vp = lambda a: ctypes.cast(a, P)  # noqa: E731
+    call("flc_model_fold", vp((P * max(nt, 1))(*[t.data_ptr() for t in dsts])),
+         vp((P * max(len(flat), 1))(*[t.data_ptr() for t in flat])), vp((ctypes.c_float * max(ns, 1))(*weights)), ns,
+         vp((ctypes.c_int64 * max(nt, 1))(*[t.numel() for t in dsts])), nt, int(init_mode), float(beta),
+         None if theta is None else vp((P * max(nt, 1))(*[t.data_ptr() for t in theta])),
+         None if v is None else vp((P * max(nt, 1))(*[t.data_ptr() for t in v])), _lib.FLC_OPT[opt], float(lr),
+         float(beta2), float(tau), _stream(dsts[0].device if nt else torch.device("cuda")))
+
+
 def fedopt_step(theta: torch.Tensor, delta: torch.Tensor, v: Optional[torch.Tensor], opt: str, lr: float,
                 beta2: float, tau: float) -> None:
     call("flc_fedopt_step", _p(theta), _p(delta), _p(v), theta.numel(), _lib.FLC_OPT[opt], float(lr), float(beta2),

@@ -121,19 +121,28 @@ __device__ float pw_leaf(const float* a, int n) {
   return res;
 }
 
-// the tree above the leaves of an n-element pairwise sum, leaves taken in order from lf[*next]
-template <int DEPTH>
-__device__ __attribute__((noinline)) float pw_tree(int n, const float* lf, int* next) {
-  if (n <= kLeaf) return lf[(*next)++];
-  if constexpr (DEPTH == 0) {
-    return __builtin_nanf("");  // unreachable for n <= kBuf (depth <= 7)
-  } else {
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    const float l = pw_tree<DEPTH - 1>(n2, lf, next);
-    const float r = pw_tree<DEPTH - 1>(n - n2, lf, next);
-    return l + r;
+// The partial last buffer's pairwise tree (its shape depends on its length only) as a program built on the host:
+// the leaves in order, then the internal nodes in post-order, each the sum of two earlier values (value code c: leaf
+// c for c < 128, node c - 128 otherwise).  <= 128 leaves and <= 127 nodes for a buffer of <= 8192 elements.
+struct TailProg {
+  int nleaf, nop;
+  short lf_start[128], lf_len[128];
+  unsigned char op_a[128], op_b[128];
+};
+
+int tail_prog_build(TailProg& p, int s0, int m) {  // (host) returns the value code of pairwise_sum(a + s0, m)
+  if (m <= kLeaf) {
+    p.lf_start[p.nleaf] = (short)s0;
+    p.lf_len[p.nleaf] = (short)m;
+    return p.nleaf++;
   }
+  int n2 = m / 2;
+  n2 -= n2 % 8;
+  const int a = tail_prog_build(p, s0, n2);
+  const int b = tail_prog_build(p, s0 + n2, m - n2);
+  p.op_a[p.nop] = (unsigned char)a;
+  p.op_b[p.nop] = (unsigned char)b;
+  return 128 + p.nop++;
 }
 
 // ---- K1: full reduction buffers (n2 splits of 8192 are a perfect tree of 64 leaves of 128) ----------
@@ -176,43 +185,18 @@ __global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const float* __restr
   if (l == 0) ws.buf_sum[b] = s;
 }
 
-// ---- K1b: the last, partial buffer (an irregular tree): leaves in parallel, the tree on one thread --------
-__global__ __launch_bounds__(128) void ar_tail_sum_kernel(const float* __restrict__ x, int64_t n, ArWs ws) {
+// ---- K1b: the last, partial buffer (an irregular tree): leaves in parallel, the tree's <= 127 additions on one
+// thread from the host-built program --------------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void ar_tail_sum_kernel(const float* __restrict__ x, int64_t n, TailProg prog,
+                                                          ArWs ws) {
   __shared__ float sh[kBuf];
-  __shared__ int lf_start[128], lf_len[128];
-  __shared__ float lf_sum[128];
-  __shared__ int s_nleaf;
+  __shared__ float lf_sum[128], op_sum[128];
   const int tid = threadIdx.x;
   const int64_t b = n / kBuf;
   const int len = (int)(n - b * kBuf);
   for (int i = tid; i < len; i += 128) sh[i] = fabsf(x[b * kBuf + i]);
-  if (tid == 0) {  // the leaves of pairwise_sum(len), left to right (depth-first, right half pushed first)
-    int st_s[16], st_n[16];
-    int sp = 1, nl = 0;
-    st_s[0] = 0;
-    st_n[0] = len;
-    while (sp > 0) {
-      --sp;
-      const int s0 = st_s[sp], m = st_n[sp];
-      if (m <= kLeaf) {
-        lf_start[nl] = s0;
-        lf_len[nl] = m;
-        ++nl;
-      } else {
-        int n2 = m / 2;
-        n2 -= n2 % 8;
-        st_s[sp] = s0 + n2;
-        st_n[sp] = m - n2;
-        ++sp;
-        st_s[sp] = s0;
-        st_n[sp] = n2;
-        ++sp;
-      }
-    }
-    s_nleaf = nl;
-  }
   __syncthreads();
-  if (tid < s_nleaf) lf_sum[tid] = pw_leaf(sh + lf_start[tid], lf_len[tid]);
+  if (tid < prog.nleaf) lf_sum[tid] = pw_leaf(sh + prog.lf_start[tid], prog.lf_len[tid]);
   // guesses: an fp64 sum of |x| per chunk of the partial buffer (any order)
   if (tid < kQ && tid * kChunk < len) {
     double s = 0.0;
@@ -222,8 +206,11 @@ __global__ __launch_bounds__(128) void ar_tail_sum_kernel(const float* __restric
   }
   __syncthreads();
   if (tid == 0) {
-    int next = 0;
-    ws.buf_sum[b] = pw_tree<8>(len, lf_sum, &next);
+    for (int o = 0; o < prog.nop; ++o) {
+      const int a = prog.op_a[o], c = prog.op_b[o];
+      op_sum[o] = (a < 128 ? lf_sum[a] : op_sum[a - 128]) + (c < 128 ? lf_sum[c] : op_sum[c - 128]);
+    }
+    ws.buf_sum[b] = prog.nop ? op_sum[prog.nop - 1] : lf_sum[0];
   }
 }
 
@@ -707,7 +694,11 @@ int flc_adaptive_prepare(const float* x, int64_t n, int32_t* status, void* ws, s
   const int64_t nfull = n / kBuf, nbuf = cdiv(n, kBuf), nq = cdiv(n, kChunk), npa = cdiv(nq, 256);
   if (nfull > 0)
     FLC_LAUNCH("adaptive_buffer_sum", ar_buffer_sum_kernel, dim3((unsigned)nfull), dim3(256), 0, st, x, nfull, w);
-  if (nbuf > nfull) FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel, dim3(1), dim3(128), 0, st, x, n, w);
+  if (nbuf > nfull) {
+    TailProg prog{};
+    (void)tail_prog_build(prog, 0, (int)(n - nfull * kBuf));
+    FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel, dim3(1), dim3(128), 0, st, x, n, prog, w);
+  }
   FLC_LAUNCH("adaptive_total", ar_total_kernel, dim3(1), dim3(1024), 0, st, nbuf, w);
   FLC_LAUNCH("adaptive_phase_a", ar_phase_a_kernel, dim3((unsigned)npa), dim3(256), 0, st, x, n, nq, w);
   FLC_LAUNCH("adaptive_check", ar_check_kernel, dim3(1), dim3(1024), 0, st, npa, w);

@@ -44,10 +44,18 @@ __global__ __launch_bounds__(kThreads) void weighted_sum_kernel(SrcPack s, int64
         a = reinterpret_cast<const float4*>(dst)[i];
         if (INIT == 0) a = make_float4(a.x * beta, a.y * beta, a.z * beta, a.w * beta);
       }
-      for (int m = 0; m < s.n; ++m) {
-        const float4 v = reinterpret_cast<const float4*>(s.p[m])[i];
-        const float w = s.w[m];
-        a = make_float4(fmaf(w, v.x, a.x), fmaf(w, v.y, a.y), fmaf(w, v.z, a.z), fmaf(w, v.w, a.w));
+      // every source's float4 loaded first (unrolled, guarded): one batch of loads in flight per thread instead of
+      // one load -> fmaf round trip per message; then the fmaf chain in message order
+      float4 v[kMaxSrc];
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m)
+        if (m < s.n) v[m] = ld_stream(s.p[m] + 4 * i);
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m) {
+        if (m < s.n) {
+          const float w = s.w[m];
+          a = make_float4(fmaf(w, v[m].x, a.x), fmaf(w, v[m].y, a.y), fmaf(w, v[m].z, a.z), fmaf(w, v[m].w, a.w));
+        }
       }
       reinterpret_cast<float4*>(dst)[i] = a;
     }
@@ -122,6 +130,112 @@ __global__ __launch_bounds__(kThreads) void feddr_combine_kernel(float* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// a whole model in one launch (flc_model_fold): a model's parameters are many small tensors (cnn_femmist_tiny: 8 of
+// 10 .. 401,408 elements), and one fold launch + one step launch per tensor is launch-bound (~14 us each from Python).
+// Block b serves one 4096-element chunk of one tensor (the tensor found from the pack's block offsets, as
+// delta_flatten does); per element the fold of weighted_sum (same init, same fmaf chain in message order) and, with
+// OPT >= 0, the step of fedopt_step on the folded value — the same roundings as the two kernels, in one pass.
+// ------------------------------------------------------------------------------------------------
+constexpr int kModelT = 16;              // tensors per launch (kernel-argument budget: ~2.7 KB)
+constexpr int kModelChunk = kThreads * 16;  // elements per block
+
+struct ModelPack {
+  float* dst[kModelT];
+  float* theta[kModelT];
+  float* v[kModelT];
+  const float* src[kMaxSrc][kModelT];
+  int64_t n[kModelT];
+  int blk0[kModelT + 1];
+  float w[kMaxSrc];
+  unsigned vec;  // bit t: tensor t's operands are 16-B aligned
+  int nt, ns;
+};
+
+template <int OPT>
+__device__ __forceinline__ void opt_step(float& th, float d, float* vp, float lr, float beta2, float omb, float nomb,
+                                         float tau) {
+  if (OPT == FLC_OPT_AVG) {
+    th = fmaf(lr, d, th);
+    return;
+  }
+  const float d2 = d * d;
+  float vi = *vp;
+  if (OPT == FLC_OPT_ADAGRAD) {
+    vi = vi + d2;
+  } else if (OPT == FLC_OPT_YOGI) {
+    const float diff = vi - d2;
+    const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : (diff == 0.f ? 0.f : diff));
+    vi = vi + (nomb * d2) * sg;
+  } else {
+    vi = fmaf(omb, d2, vi * beta2);
+  }
+  *vp = vi;
+  th = th + (lr * d) / (sqrtf(vi) + tau);
+}
+
+template <int INIT, int OPT>  // OPT < 0: the fold only
+__global__ __launch_bounds__(kThreads) void model_fold_kernel(ModelPack p, float beta, float lr, float beta2, float omb,
+                                                              float nomb, float tau) {
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < p.nt && p.blk0[t + 1] <= b) ++t;  // uniform: <= kModelT steps
+  float* __restrict__ dst = p.dst[t];
+  const int64_t n = p.n[t];
+  const int64_t c0 = (int64_t)(b - p.blk0[t]) * kModelChunk;
+  const int64_t c1 = c0 + kModelChunk < n ? c0 + kModelChunk : n;
+  if ((p.vec >> t) & 1u) {
+    for (int64_t i = c0 + 4 * (int64_t)threadIdx.x; i < c1; i += 4 * kThreads) {
+      if (i + 4 > c1) {  // the tensor's n % 4 tail
+        for (int64_t e = i; e < c1; ++e) {
+          float a = INIT == 1 ? 0.0f : (INIT == 0 ? dst[e] * beta : dst[e]);
+          for (int m = 0; m < p.ns; ++m) a = fmaf(p.w[m], p.src[m][t][e], a);
+          dst[e] = a;
+          if (OPT >= 0) opt_step<OPT < 0 ? 0 : OPT>(p.theta[t][e], a, OPT > 0 ? p.v[t] + e : nullptr, lr, beta2, omb,
+                                                  nomb, tau);
+        }
+        break;
+      }
+      float4 sv[kMaxSrc];
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m)
+        if (m < p.ns) sv[m] = *reinterpret_cast<const float4*>(p.src[m][t] + i);
+      float4 a;
+      if (INIT == 1) {
+        a = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        a = *reinterpret_cast<const float4*>(dst + i);
+        if (INIT == 0) a = make_float4(a.x * beta, a.y * beta, a.z * beta, a.w * beta);
+      }
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m) {
+        if (m < p.ns) {
+          const float w = p.w[m];
+          a = make_float4(fmaf(w, sv[m].x, a.x), fmaf(w, sv[m].y, a.y), fmaf(w, sv[m].z, a.z), fmaf(w, sv[m].w, a.w));
+        }
+      }
+      *reinterpret_cast<float4*>(dst + i) = a;
+      if (OPT >= 0) {
+        float4 th = *reinterpret_cast<const float4*>(p.theta[t] + i);
+        float* vp = OPT > 0 ? p.v[t] + i : nullptr;
+        opt_step<OPT < 0 ? 0 : OPT>(th.x, a.x, vp, lr, beta2, omb, nomb, tau);
+        opt_step<OPT < 0 ? 0 : OPT>(th.y, a.y, OPT > 0 ? vp + 1 : nullptr, lr, beta2, omb, nomb, tau);
+        opt_step<OPT < 0 ? 0 : OPT>(th.z, a.z, OPT > 0 ? vp + 2 : nullptr, lr, beta2, omb, nomb, tau);
+        opt_step<OPT < 0 ? 0 : OPT>(th.w, a.w, OPT > 0 ? vp + 3 : nullptr, lr, beta2, omb, nomb, tau);
+        *reinterpret_cast<float4*>(p.theta[t] + i) = th;
+      }
+    }
+    return;
+  }
+  for (int64_t e = c0 + threadIdx.x; e < c1; e += kThreads) {
+    float a = INIT == 1 ? 0.0f : (INIT == 0 ? dst[e] * beta : dst[e]);
+    for (int m = 0; m < p.ns; ++m) a = fmaf(p.w[m], p.src[m][t][e], a);
+    dst[e] = a;
+    if (OPT >= 0) opt_step<OPT < 0 ? 0 : OPT>(p.theta[t][e], a, OPT > 0 ? p.v[t] + e : nullptr, lr, beta2, omb, nomb,
+                                            tau);
+  }
+}
+
 unsigned grid_for(int64_t work) {
   const int64_t g = cdiv(work, kThreads);
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 256 * 16));
@@ -168,6 +282,66 @@ int flc_weighted_sum(const float* const* srcs, const float* weights, int n_src, 
     done += p.n;
     mode = 2;  // later chunks continue the same fmaf chain
   } while (done < n_src);
+  return FLC_OK;
+}
+
+int flc_model_fold(float* const* dst, const float* const* srcs, const float* weights, int n_src, const int64_t* sizes,
+                   int n_tensors, int init_mode, float beta, float* const* theta, float* const* v, int opt, double lr,
+                   double beta2, double tau, void* stream) {
+  if (n_tensors < 0 || (n_tensors > 0 && (!dst || !sizes)) || n_src < 0 || n_src > kMaxSrc ||
+      (n_src > 0 && (!srcs || !weights)))
+    return fail(FLC_EINVAL, "flc_model_fold: bad arguments (at most %d sources)", kMaxSrc);
+  if (init_mode < 0 || init_mode > 2) return fail(FLC_EINVAL, "flc_model_fold: init_mode must be 0, 1 or 2");
+  const bool step = theta != nullptr;
+  if (step && opt != FLC_OPT_AVG && opt != FLC_OPT_ADAGRAD && opt != FLC_OPT_YOGI && opt != FLC_OPT_ADAM)
+    return fail(FLC_EINVAL, "flc_model_fold: unknown optimiser %d", opt);
+  if (step && opt != FLC_OPT_AVG && !v) return fail(FLC_EINVAL, "flc_model_fold: v required for adaptive optimisers");
+  hipStream_t st = as_stream(stream);
+  const float omb = (float)(1.0 - beta2), nomb = (float)(-(1.0 - beta2));
+  const float lrf = (float)lr, b2f = (float)beta2, tauf = (float)tau;
+  for (int t0 = 0; t0 < n_tensors; t0 += kModelT) {
+    ModelPack p{};
+    p.ns = n_src;
+    for (int m = 0; m < n_src; ++m) p.w[m] = weights[m];
+    int blocks = 0;
+    for (int t = t0; t < std::min(n_tensors, t0 + kModelT); ++t) {
+      if (sizes[t] < 0) return fail(FLC_EINVAL, "flc_model_fold: negative size for tensor %d", t);
+      if (sizes[t] == 0) continue;
+      if (!dst[t] || (step && !theta[t]) || (step && opt != FLC_OPT_AVG && !v[t]))
+        return fail(FLC_EINVAL, "flc_model_fold: null pointer for tensor %d", t);
+      const int i = p.nt++;
+      p.dst[i] = dst[t];
+      p.theta[i] = step ? theta[t] : nullptr;
+      p.v[i] = (step && v) ? v[t] : nullptr;
+      p.n[i] = sizes[t];
+      bool vec = aligned16(dst[t]) && (!step || aligned16(theta[t])) && (!p.v[i] || aligned16(p.v[i]));
+      for (int m = 0; m < n_src; ++m) {
+        const float* sp = srcs[(size_t)m * n_tensors + t];
+        if (!sp) return fail(FLC_EINVAL, "flc_model_fold: null source %d of tensor %d", m, t);
+        p.src[m][i] = sp;
+        vec = vec && aligned16(sp);
+      }
+      if (vec) p.vec |= 1u << i;
+      p.blk0[i] = blocks;
+      const int64_t nb = cdiv(sizes[t], kModelChunk);
+      if (blocks + nb > 0x7fffffff) return fail(FLC_EINVAL, "flc_model_fold: too many elements");
+      blocks += (int)nb;
+    }
+    p.blk0[p.nt] = blocks;
+    if (blocks == 0) continue;
+#define FLC_MF(I, O) FLC_LAUNCH("model_fold", (model_fold_kernel<I, O>), dim3(blocks), dim3(kThreads), 0, st, p, beta, lrf, b2f, omb, nomb, tauf)
+#define FLC_MF_OPT(I)                                          \
+    if (!step) FLC_MF(I, -1);                                   \
+    else if (opt == FLC_OPT_AVG) FLC_MF(I, FLC_OPT_AVG);        \
+    else if (opt == FLC_OPT_ADAGRAD) FLC_MF(I, FLC_OPT_ADAGRAD); \
+    else if (opt == FLC_OPT_YOGI) FLC_MF(I, FLC_OPT_YOGI);      \
+    else FLC_MF(I, FLC_OPT_ADAM)
+    if (init_mode == 0) { FLC_MF_OPT(0); }
+    else if (init_mode == 1) { FLC_MF_OPT(1); }
+    else { FLC_MF_OPT(2); }
+#undef FLC_MF_OPT
+#undef FLC_MF
+  }
   return FLC_OK;
 }
 

@@ -43,7 +43,7 @@ struct QuantWs {
   unsigned long long* partials;  // [rows * kNormMaxParts]
   int* chunk_counts;             // [nblocks]  (compat)
   long long* chunk_offsets;      // [nblocks]  (compat)
-  unsigned long long* rowmax;    // [rows] fused launch: (epoch << 32 | max |x| bits) per row
+  unsigned* blkmax;              // [2 * kMaxFused] fused launch: each block's max |x| bits of its (<= 2) rows
 };
 
 QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* need) {
@@ -54,7 +54,7 @@ QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* nee
   w.partials = c.take<unsigned long long>((size_t)rows * kNormMaxParts);
   w.chunk_counts = c.take<int>((size_t)nblocks);
   w.chunk_offsets = c.take<long long>((size_t)nblocks);
-  w.rowmax = c.take<unsigned long long>((size_t)rows);
+  w.blkmax = c.take<unsigned>(2 * 1024);
   *need = c.off;
   return w;
 }
@@ -522,23 +522,24 @@ __global__ __launch_bounds__(kThreads) void quant_encode_philox_kernel(
 // configs[1] in one launch (flc_quant_encode_auto with p = inf, Philox): one 1024-thread block per CU, block b owning
 // the flat span [b SPAN, (b + 1) SPAN) of the batch (SPAN = 8192 GPT elements, d >= SPAN: at most two rows per block).
 // Each thread loads its GPT groups of 8 (coalesced: group j of thread t at (j * 1024 + t) * 8) and keeps them in
-// registers; the block's max |x| per row goes to the workspace with one 64-bit atomicMax of (epoch << 32 | bits) —
-// the epoch makes last call's values smaller than any of this one's, so nothing is zeroed; then a grid exchange
-// (every block raises its flag to the epoch, one wave polls all flags); then every block reads its rows' norms and
-// encodes (+ decodes) from the registers.  x is read once, the codes and the decoded batch written once: 9 B/element
+// registers; the block's max |x| of each of its rows goes to its own two workspace slots; then a grid exchange (every
+// block raises its flag to the call's epoch, one wave polls all flags); then every block folds its rows' maxima over
+// the blocks that hold them (a contiguous range, one batch of coherent loads) and encodes (+ decodes) from the
+// registers.  x is read once, the codes and the decoded batch written once: 9 B/element
 // in one launch, bit-identical to the two-launch form (max is exact in any order; same Philox words, same rule).
 // ------------------------------------------------------------------------------------------------
 constexpr int kFT = 1024;
 constexpr int kMaxFused = 1024;  // blocks (flags)
 
+// The payload (each block's two maxima) is stored with agent-scope atomic stores (write-through to the coherent
+// level) and drained with s_waitcnt vmcnt(0) before the flag is raised; readers load it the same way — no release /
+// acquire fence, which on gfx950 writes back / invalidates the whole L2 (measured 6-8 us over 510 blocks, quant.hip's
+// dropped ticket fold).  The exchange of topk.hip, for one kernel with its own flag region.
 __device__ __forceinline__ void fused_exchange(const QuantWs& ws, unsigned epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int tid = threadIdx.x;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_store(ws.flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (tid == 0) __hip_atomic_store(ws.flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid < kWave) {
     const int G = (int)gridDim.x;
     unsigned spins = 0;
@@ -559,7 +560,6 @@ __device__ __forceinline__ void fused_exchange(const QuantWs& ws, unsigned epoch
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
 }
@@ -604,24 +604,31 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
   }
   if (tid < 2) s_nnz[tid] = 0ull;
   __syncthreads();
-  if (tid < 2) {
-    const int64_t r = r0 + tid;
-    const int64_t lo = tid == 0 ? base : rb, hi = base + SPAN < n ? base + SPAN : n;
-    if (r < rows && lo < hi) {  // this block holds elements of row r
-      uint32_t m = 0;
-      for (int w = 0; w < kFT / kWave; ++w) m = s_m[tid][w] > m ? s_m[tid][w] : m;
-      __hip_atomic_fetch_max(ws.rowmax + r, ((unsigned long long)epoch << 32) | m, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    }
+  if (tid < 2) {  // slot 0: row r0, slot 1: row r0 + 1 (0 when the block holds none of it)
+    uint32_t m = 0;
+    for (int w = 0; w < kFT / kWave; ++w) m = s_m[tid][w] > m ? s_m[tid][w] : m;
+    __hip_atomic_store(ws.blkmax + 2 * blockIdx.x + tid, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   fused_exchange(ws, epoch);
-  if (tid < 2) {
-    const int64_t r = r0 + tid;
-    if (r < rows) {
-      const float nr = __uint_as_float(
-          (uint32_t)__hip_atomic_load(ws.rowmax + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      s_norm[tid] = nr;
-      if (r * d >= base && r * d < base + SPAN) norms[r] = nr;  // the block holding the row's first element
+  if (tid < kWave) {  // wave 0: each row's max over the blocks holding it
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int64_t r = r0 + rr;
+      if (r >= rows) break;  // (uniform)
+      const int64_t c0 = r * d / SPAN, c1 = ((r + 1) * d - 1) / SPAN < (int64_t)gridDim.x - 1
+                                               ? ((r + 1) * d - 1) / SPAN
+                                               : (int64_t)gridDim.x - 1;
+      uint32_t m = 0;
+      for (int64_t c = c0 + lane; c <= c1; c += kWave) {
+        const int slot = (c * SPAN) / d == r ? 0 : 1;  // row r is block c's first row or its second
+        const uint32_t v = __hip_atomic_load(ws.blkmax + 2 * c + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        m = v > m ? v : m;
+      }
+      m = wave_max_u32(m);
+      if (lane == 0) {
+        s_norm[rr] = __uint_as_float(m);
+        if (r * d >= base && r * d < base + SPAN) norms[r] = __uint_as_float(m);  // the block holding its 1st element
+      }
     }
   }
   __syncthreads();
@@ -690,6 +697,15 @@ int check_quant_args(int kind, int levels, int bits) {
 }
 
 double level_step(int levels) { return 1.0 / (double)levels; }
+
+// the one-launch encode's exchange epochs: process-wide and increasing, so a flag left by any earlier call (of any
+// shape, on any workspace) is older than this call's; never 0 (a fresh workspace's flags)
+unsigned next_epoch() {
+  static std::atomic<unsigned> epochs{0};
+  unsigned ep = ++epochs;
+  while (ep == 0) ep = ++epochs;
+  return ep;
+}
 
 template <int KIND, int BITS, bool DEC>
 int launch_encode(const float* x, int64_t n, int64_t d, int levels, const float* norms, uint64_t seed, uint64_t counter,
@@ -833,9 +849,7 @@ int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p,
                     : (d >= 4 * kFT * kGroup && n <= (int64_t)cus * 4 * kFT * kGroup) ? 4
                                                                                         : 0;
     if (gpt) {
-      static std::atomic<unsigned> epochs{0};
-      unsigned ep = ++epochs;
-      if (ep == 0) ep = ++epochs;  // (the flags of a fresh workspace are 0)
+      const unsigned ep = next_epoch();
       const unsigned grid = (unsigned)cdiv(n, (int64_t)gpt * kFT * kGroup);
       const char* fname = DEC ? "quant_fused_encode_decode" : "quant_fused_encode";
       Coresident co(st, dev);

@@ -320,7 +320,7 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
                                                                     const float* __restrict__ norm_ptr, int64_t n,
                                                                     float weight, float* __restrict__ out,
                                                                     const unsigned* __restrict__ tile_start,
-                                                                    int64_t ntiles, int64_t chunk, int64_t nt_from) {
+                                                                    int64_t ntiles, int64_t chunk) {
   constexpr int TILE = 1024;
   __shared__ __attribute__((aligned(16))) float s_tile[NT * TILE];
   const int lane = threadIdx.x;
@@ -377,8 +377,7 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
     float4 v = tile4[q];
     if (e + 4 <= n) {
       if (weight != 1.0f) v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
-      if (g >= nt_from) st_stream(out + e, v);
-      else *reinterpret_cast<float4*>(out + e) = v;
+      *reinterpret_cast<float4*>(out + e) = v;
     } else {
       const float vv[4] = {v.x, v.y, v.z, v.w};
       for (int c = 0; c < 4 && e + c < n; ++c) out[e + c] = weight != 1.0f ? weight * vv[c] : vv[c];
@@ -386,13 +385,6 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
   }
 }
 
-// the workgroups from which the decode's stores are non-temporal: the last FLC_DECODE_NT_TAIL per-mille of the
-// output (calibration; 0 = none)
-int64_t decode_nt_from(int64_t groups) {
-  static const int pm = getenv("FLC_DECODE_NT_TAIL") ? atoi(getenv("FLC_DECODE_NT_TAIL")) : 0;
-  if (pm <= 0) return groups;
-  return groups - groups * (int64_t)std::min(pm, 1000) / 1000;
-}
 
 // Grid-stride pipelined decode: G resident blocks, block b assembles tiles b, b + G, b + 2G, ... of
 // TILE = 1024 V outputs.  The whole grid's stores of one iteration cover ONE contiguous window (the write
@@ -674,8 +666,7 @@ int launch_decode_tiles(const int32_t* idx, const float* val, const uint8_t* cod
                codes, scale, levels, step, norm, n, weight, out, tile_start, 0);
   else
     FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, 2>), dim3((unsigned)cdiv(ntiles, 2)), dim3(kWave), 0, st, idx,
-               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, decode_chunk(),
-               decode_nt_from(cdiv(ntiles, 2)));
+               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, decode_chunk());
   return FLC_OK;
 }
 
@@ -695,8 +686,7 @@ int launch_decode_wave2(const int32_t* idx, const float* val, const uint8_t* cod
              (long long)ntiles, tile_start);
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, NT>), dim3((unsigned)cdiv(ntiles, NT)), dim3(kWave), 0, st, idx,
-             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, decode_chunk(),
-             decode_nt_from(cdiv(ntiles, NT)));
+             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, decode_chunk());
   return FLC_OK;
 }
 

@@ -313,6 +313,15 @@ int flc_delta_flatten(const float* const* local, const float* const* global, con
  * srcs and weights are HOST arrays of device pointers / fp32 weights (n_src >= 0). */
 int flc_weighted_sum(const float* const* srcs, const float* weights, int n_src, int64_t n, int init_mode,
                      float beta, float* dst, void* stream);
+/* a whole model in ONE launch (a model is many small tensors; two launches per tensor are launch-bound): for each
+ * tensor t, dst[t] = init(dst[t]) then fmaf(weights[m], srcs[m * n_tensors + t], .) for m in message order — exactly
+ * flc_weighted_sum per tensor — and, with theta != NULL, flc_fedopt_step on (theta[t], dst[t], v[t]) with the folded
+ * dst[t] as the delta: FedOptServer.update in one pass (_fedopt.py:196-265).  Host arrays of device pointers;
+ * n_src <= 16 (a longer message list: flc_weighted_sum, which chains); 16 tensors per launch, more in further launches
+ * (tensor order).  v may be NULL for opt = avg. */
+int flc_model_fold(float* const* dst, const float* const* srcs, const float* weights, int n_src, const int64_t* sizes,
+                   int n_tensors, int init_mode, float beta, float* const* theta, float* const* v, int opt, double lr,
+                   double beta2, double tau, void* stream);
 /* the rest of FedOptServer.update after the delta average (_fedopt.py:212-265):
  *   avg:     theta = fmaf(lr, delta, theta)
  *   adagrad: v = v + delta^2;                               theta += lr * delta / (sqrt(v) + tau)

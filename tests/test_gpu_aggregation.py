@@ -269,3 +269,59 @@ def test_feddr_linf_raises_like_reference():
     with pytest.raises(NotImplementedError):
         aggregation.feddr_update(_dev(params), _dev(ys), _dev(xts), _msgs_dev(msgs, "x_hat_delta"), 0.9, 0.05, 10,
                                  "linf")
+
+
+def _views(shapes, g, scale=1.0, misalign=False):
+    """Tensors of the given shapes; with misalign, views one element into a larger buffer (4-B aligned only)."""
+    out = []
+    for sh in shapes:
+        n = int(np.prod(sh))
+        base = torch.randn(n + 1, generator=g, device="cuda") * scale
+        out.append(base[1:].view(sh) if misalign else base[:n].clone().view(sh))
+    return out
+
+
+@pytest.mark.parametrize("opt", ["avg", "adagrad", "yogi", "adam"])
+@pytest.mark.parametrize("n_msgs", [0, 1, 10, 16])
+@pytest.mark.parametrize("misalign", [False, True])
+def test_model_fold_equals_per_tensor_calls(opt, n_msgs, misalign):
+    """flc_model_fold (one launch for the whole model, FedOpt's step fused) equals flc_weighted_sum + flc_fedopt_step
+    per tensor bit for bit: 20 tensors (two launches), tails of n % 4, misaligned views (the scalar path)."""
+    from fl_sim_amd import codec
+
+    shapes = [(16, 1, 5, 5), (16,), (32, 16, 5, 5), (32,), (256, 1568), (256,), (10, 256), (10,), (3,), (1,),
+              (7, 9), (4097,), (5,), (12, 12), (2, 3, 5), (1000,), (1,), (8,), (9,), (300, 7)]
+    g = torch.Generator(device="cuda").manual_seed(n_msgs * 7 + misalign)
+    theta = _views(shapes, g, 1.0, misalign)
+    delta = _views(shapes, g, 1e-3, misalign)
+    v = [t.abs() * 1e-2 + 1e-6 for t in _views(shapes, g, 1.0, misalign)]
+    msgs = [_views(shapes, g, 1e-3, misalign) for _ in range(n_msgs)]
+    w = [float(np.float32(0.1 * (i + 1))) for i in range(n_msgs)]
+    th2, d2, v2 = [t.clone() for t in theta], [t.clone() for t in delta], [t.clone() for t in v]
+    vv = None if opt == "avg" else v
+    codec.model_fold(delta, msgs, w, 0, 0.9, theta=theta, v=vv, opt=opt, lr=0.01, beta2=0.99, tau=1e-3)
+    for j in range(len(shapes)):
+        codec.weighted_sum(d2[j], [m[j] for m in msgs], w, init_mode=0, beta=0.9)
+        codec.fedopt_step(th2[j], d2[j], None if opt == "avg" else v2[j], opt, 0.01, 0.99, 1e-3)
+    for a, b in zip(theta + delta + (v if opt != "avg" else []), th2 + d2 + (v2 if opt != "avg" else [])):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    # the fold alone (init modes 1 and 2)
+    for mode in (1, 2):
+        a = [t.clone() for t in delta]
+        b = [t.clone() for t in delta]
+        codec.model_fold(a, msgs, w, mode)
+        for j in range(len(shapes)):
+            codec.weighted_sum(b[j], [m[j] for m in msgs], w, init_mode=mode)
+        assert all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(a, b))
+
+
+def test_model_fold_rejects_bad_arguments():
+    from fl_sim_amd import codec
+
+    t = [torch.zeros(5, device="cuda")]
+    with pytest.raises(ValueError):
+        codec.model_fold(t, [t] * 17, [1.0] * 17, 0)  # more than 16 messages
+    with pytest.raises(ValueError):
+        codec.model_fold(t, [[torch.zeros(6, device="cuda")]], [1.0], 0)  # size mismatch
+    with pytest.raises(RuntimeError):
+        codec.model_fold(t, [t], [1.0], 0, theta=t, v=None, opt="adam")  # adam needs v

@@ -28,8 +28,14 @@ def step3(c):
     codec.sparse_decode(idx, val, d3, out=o3, tiles=tiles)
 
 
+def step2t(c):  # the two-launch form of quant_encode_auto (norm partials, then the encode folding them)
+    os.environ["FLC_QUANT_TWO_LAUNCH"] = "1"
+    codec.quant_encode_auto(X, 0, 127, seed=0, counter=c)
+    del os.environ["FLC_QUANT_TWO_LAUNCH"]
+
+
 for name, fn, reps in (("config2_quant8_10x417482", step2, 200), ("config2_fused", step2f, 200),
-                       ("config3_topk1pct_25M", step3, 100)):
+                       ("config2_fused_two_launch", step2t, 200), ("config3_topk1pct_25M", step3, 100)):
     for i in range(20):
         fn(i)
     torch.cuda.synchronize()
