@@ -39,14 +39,19 @@ def _on(t: torch.Tensor, device: torch.device) -> torch.Tensor:
     return t if t.device == device else t.to(device)
 
 
-def _model_device(tensors: Sequence[torch.Tensor]) -> Optional[torch.device]:
-    """The one HIP device all of a model's tensors live on (contiguous fp32), or None (then per-tensor launches)."""
-    devs = {t.device for t in tensors}
-    if len(devs) != 1:
-        return None
-    dev = next(iter(devs))
-    ok = dev.type == "cuda" and all(t.dtype == torch.float32 and t.is_contiguous() for t in tensors)
-    return dev if ok else None
+def _model_device(tensors: Sequence[torch.Tensor]) -> Optional[int]:
+    """The index of the one HIP device all of a model's tensors live on (contiguous fp32), or None (then per-tensor
+    launches)."""
+    dev = None
+    for t in tensors:
+        if not (t.is_cuda and t.dtype is torch.float32 and t.is_contiguous()):
+            return None
+        d = t.get_device()
+        if dev is None:
+            dev = d
+        elif d != dev:
+            return None
+    return dev
 
 
 def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
@@ -55,7 +60,8 @@ def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence[Sequence[torch.Ten
     dev = _model_device(list(dsts) + list(step.get("theta") or []) + list(step.get("v") or []))
     if dev is None or not dsts or len(msg_tensors) > codec.MODEL_FOLD_MAX_SRC:
         return False
-    srcs = [[_on(t, dev) for t in mt] for mt in msg_tensors]
+    srcs = [[t if (t.is_cuda and t.get_device() == dev) else t.detach().to(f"cuda:{dev}") for t in mt]
+            for mt in msg_tensors]
     codec.model_fold(dsts, srcs, weights, init_mode, beta, **step)
     return True
 

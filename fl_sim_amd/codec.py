@@ -692,27 +692,43 @@ def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tenso
                tau: float = 0.0) -> None:
     """A whole model in one launch (flc_model_fold): per tensor t, ``weighted_sum(dsts[t], [s[t] for s in srcs],
     weights, init_mode, beta)`` and, with ``theta``, ``fedopt_step(theta[t], dsts[t], v[t], opt, lr, beta2, tau)``.
-    ``srcs[m]`` is message m's list of tensors (all on the dsts' device); at most 16 messages."""
+    ``srcs[m]`` is message m's list of tensors (all on the dsts' device); at most 16 messages.  The checks are one
+    lean pass per tensor: a model update is ~100 tensors, and per-tensor Python costs more than the kernel."""
     import ctypes
 
     nt, ns = len(dsts), len(srcs)
     if ns > MODEL_FOLD_MAX_SRC:
         raise ValueError(f"model_fold takes at most {MODEL_FOLD_MAX_SRC} messages")
-    P = ctypes.c_void_p
-    for t in list(dsts) + list(theta or []) + list(v or []):
-        if t.device.type != "cuda" or t.dtype != torch.float32 or not t.is_contiguous():
-            raise TypeError("model tensors must be contiguous fp32 HIP tensors")
+    if nt == 0:
+        return
+    f32 = torch.float32
+    dev = dsts[0].get_device()
+
+    def ptrs(ts, what):
+        out = []
+        for t in ts:
+            if not (t.is_cuda and t.dtype is f32 and t.is_contiguous() and t.get_device() == dev):
+                raise TypeError(f"{what} tensors must be contiguous fp32 HIP tensors on one device")
+            out.append(t.data_ptr())
+        return out
+
+    sizes = [t.numel() for t in dsts]
+    dp = ptrs(dsts, "model")
+    sp = []
     for msg in srcs:
-        if len(msg) != nt or any(a.numel() != b.numel() for a, b in zip(msg, dsts)):
-            raise ValueError("every message has one tensor per model tensor, of matching sizes")
-    flat = [_dev_f32(msg[t], "src") for msg in srcs for t in range(nt)]
+        if len(msg) != nt:
+            raise ValueError("every message has one tensor per model tensor")
+        for a, n in zip(msg, sizes):
+            if a.numel() != n:
+                raise ValueError("message tensors must match the model tensors' sizes")
+        sp.extend(ptrs(msg, "message"))
+    P = ctypes.c_void_p
     vp = lambda a: ctypes.cast(a, P)  # noqa: E731
-    call("flc_model_fold", vp((P * max(nt, 1))(*[t.data_ptr() for t in dsts])),
-         vp((P * max(len(flat), 1))(*[t.data_ptr() for t in flat])), vp((ctypes.c_float * max(ns, 1))(*weights)), ns,
-         vp((ctypes.c_int64 * max(nt, 1))(*[t.numel() for t in dsts])), nt, int(init_mode), float(beta),
-         None if theta is None else vp((P * max(nt, 1))(*[t.data_ptr() for t in theta])),
-         None if v is None else vp((P * max(nt, 1))(*[t.data_ptr() for t in v])), _lib.FLC_OPT[opt], float(lr),
-         float(beta2), float(tau), _stream(dsts[0].device if nt else torch.device("cuda")))
+    call("flc_model_fold", vp((P * nt)(*dp)), vp((P * max(len(sp), 1))(*sp)),
+         vp((ctypes.c_float * max(ns, 1))(*weights)), ns, vp((ctypes.c_int64 * nt)(*sizes)), nt, int(init_mode),
+         float(beta), None if theta is None else vp((P * nt)(*ptrs(theta, "model"))),
+         None if v is None else vp((P * nt)(*ptrs(v, "model"))), _lib.FLC_OPT[opt], float(lr), float(beta2),
+         float(tau), torch.cuda.current_stream(dev).cuda_stream)
 
 
 def fedopt_step(theta: torch.Tensor, delta: torch.Tensor, v: Optional[torch.Tensor], opt: str, lr: float,

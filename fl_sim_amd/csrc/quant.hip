@@ -391,14 +391,19 @@ __global__ __launch_bounds__(kThreads) void quant_encode_kernel(
 // one row — takes one norm lookup and, for standard dithering, a branch-light fp32 level decision; groups straddling a
 // row boundary or the end take the per-element path.  norm_of(r): row r's norm; nnz_add(r, count) when counting.
 // DEC also writes the decoded values (flc_quant_encode_decode).
-template <int KIND, int BITS, bool DEC, class NormOf, class NnzAdd>
-__device__ __forceinline__ void philox_group_encode(const float (&v)[kGroup], int64_t e0, int valid, int64_t d, int s,
-                                                    double step, uint64_t seed, uint64_t counter,
-                                                    uint8_t* __restrict__ codes, float* __restrict__ out, bool count,
-                                                    NormOf norm_of, NnzAdd nnz_add) {
+// the group's 8 Philox words (element e: word e & 3 of counter group e >> 2)
+__device__ __forceinline__ void group_words(int64_t e0, uint64_t seed, uint64_t counter, uint32_t (&wd)[kGroup]) {
   const U4 a = philox_group((uint64_t)e0 >> 2, seed, counter);
   const U4 b = philox_group(((uint64_t)e0 >> 2) + 1, seed, counter);
-  const uint32_t wd[kGroup] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  wd[0] = a.x; wd[1] = a.y; wd[2] = a.z; wd[3] = a.w;
+  wd[4] = b.x; wd[5] = b.y; wd[6] = b.z; wd[7] = b.w;
+}
+
+template <int KIND, int BITS, bool DEC, class NormOf, class NnzAdd>
+__device__ __forceinline__ void philox_group_encode(const float (&v)[kGroup], const uint32_t (&wd)[kGroup], int64_t e0,
+                                                    int valid, int64_t d, int s, double step,
+                                                    uint8_t* __restrict__ codes, float* __restrict__ out, bool count,
+                                                    NormOf norm_of, NnzAdd nnz_add) {
   const int64_t r0 = e0 / d;
   const int64_t r_end = (r0 + 1) * d;
   uint64_t packed = 0;
@@ -502,8 +507,10 @@ __global__ __launch_bounds__(kThreads) void quant_encode_philox_kernel(
     const int valid = n - e0 < kGroup ? (int)(n - e0) : kGroup;
     float v[kGroup];
     load_group(x, e0, valid, v);
+    uint32_t wd[kGroup];
+    group_words(e0, seed, counter, wd);
     philox_group_encode<KIND, BITS, DEC>(
-        v, e0, valid, d, s, step, seed, counter, codes, out, nnz != nullptr,
+        v, wd, e0, valid, d, s, step, codes, out, nnz != nullptr,
         [&](int64_t r) { return FOLD ? s_norm[r - row_base] : norms[r]; },
         [&](int64_t r, int cnt) {
           const int rl = (int)(r - row_base);
@@ -602,6 +609,14 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
     s_m[0][wid] = m0;
     s_m[1][wid] = m1;
   }
+  // the Philox words do not depend on the norm: computed here, before the exchange, so the VALU work of the encode
+  // overlaps the wait for the slowest block instead of following it (GPT = 2; at 4 they would not fit the registers)
+  constexpr bool kPre = GPT <= 2;
+  uint32_t wd[kPre ? GPT : 1][kGroup];
+  if constexpr (kPre) {
+#pragma unroll
+    for (int g = 0; g < GPT; ++g) group_words(base + ((int64_t)g * kFT + tid) * kGroup, seed, counter, wd[g]);
+  }
   if (tid < 2) s_nnz[tid] = 0ull;
   __syncthreads();
   if (tid < 2) {  // slot 0: row r0, slot 1: row r0 + 1 (0 when the block holds none of it)
@@ -637,8 +652,9 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
     const int64_t e0 = base + ((int64_t)g * kFT + tid) * kGroup;
     if (e0 < n) {
       const int valid = n - e0 < kGroup ? (int)(n - e0) : kGroup;
+      if constexpr (!kPre) group_words(e0, seed, counter, wd[0]);
       philox_group_encode<KIND, BITS, DEC>(
-          v[g], e0, valid, d, s, step, seed, counter, codes, out, nnz != nullptr,
+          v[g], wd[kPre ? g : 0], e0, valid, d, s, step, codes, out, nnz != nullptr,
           [&](int64_t r) { return s_norm[r - r0]; },
           [&](int64_t r, int cnt) { atomicAdd(&s_nnz[r - r0], (unsigned long long)cnt); });
     }
