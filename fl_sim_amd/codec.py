@@ -9,6 +9,7 @@ drives it directly for the device-resident measurement.
 
 from __future__ import annotations
 
+import collections.abc as _abc
 import math
 import os
 from dataclasses import dataclass
@@ -337,6 +338,44 @@ class StackedPacket:
         return 5 * self.idx.numel() + 4 + (4 * self.tiles.numel() if self.tiles is not None else 0)
 
 
+class PacketBatch(_abc.Sequence):
+    """The packets of a batched encode (one row per client of four [clients, ...] blocks), made on demand: packet c
+    is ``StackedPacket(idx[c], codes[c], norm[c], n, levels, tiles[c])``.  A round of many small clients would
+    otherwise spend more host time building views than the GPU spends encoding (4 views x 100 clients)."""
+
+    def __init__(self, idx, codes, norm, tiles, n: int, levels: int):
+        self.idx, self.codes, self.norm, self.tiles, self.n, self.levels = idx, codes, norm, tiles, n, levels
+
+    def __len__(self) -> int:
+        return self.idx.shape[0]
+
+    def __getitem__(self, c):
+        if isinstance(c, slice):
+            return [self[i] for i in range(*c.indices(len(self)))]
+        if c < 0:
+            c += len(self)
+        if not 0 <= c < len(self):
+            raise IndexError(c)
+        return StackedPacket(self.idx[c], self.codes[c], self.norm[c], self.n, self.levels,
+                             None if self.tiles is None else self.tiles[c])
+
+
+def _batch_ptrs(xs: Sequence[torch.Tensor], n: int, dev: torch.device) -> Optional[List[int]]:
+    """The clients' data pointers when every one is a contiguous, 16-B aligned fp32 tensor of n elements on `dev`
+    (one lean pass: the batch may hold hundreds of clients); None otherwise."""
+    f32, di = torch.float32, dev.index
+    out = []
+    for x in xs:
+        if not (isinstance(x, torch.Tensor) and x.dtype is f32 and x.numel() == n and x.is_contiguous()
+                and x.get_device() == di):
+            return None
+        p = x.data_ptr()
+        if p & 15:
+            return None
+        out.append(p)
+    return out
+
+
 _WIRE_LAYOUT = {}
 
 
@@ -403,7 +442,7 @@ def stacked_encode(x: torch.Tensor, k: int, levels: int = 127, seed: int = 0, co
 
 
 def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, seeds: Sequence[int] = (),
-                         counter: int = 0, with_tiles: bool = True, wires=None) -> Optional[List[StackedPacket]]:
+                         counter: int = 0, with_tiles: bool = True, wires=None) -> Optional[Sequence[StackedPacket]]:
     """The stacked encode of many clients' flat deltas (all of one size) in one launch (flc_stacked_encode_batch):
     packet c equals ``stacked_encode(xs[c], k, levels, seeds[c], counter)`` bit for bit.  ``wires``: the packed wire
     records to write into — a ``[clients, >= stride]`` uint8 tensor (then nothing is returned: the records are the
@@ -415,16 +454,12 @@ def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, 
         return []
     x0 = xs[0]
     n, dev = x0.numel(), x0.device
-    for x in xs:
-        if not (isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.device == dev and x.numel() == n
-                and x.is_contiguous() and x.data_ptr() % 16 == 0):
-            break
-    else:
-        x = None
-    if x is not None:  # (the slow path: checks with messages, copies of misaligned inputs)
+    xp = _batch_ptrs(xs, n, dev) if dev.type == "cuda" else None
+    if xp is None:  # (the slow path: checks with messages, copies of misaligned inputs)
         xs = [_dev_f32(x).reshape(-1) for x in xs]
         if any(x.numel() != n or x.device != dev for x in xs):
             raise ValueError("a batched encode takes clients of one size on one device")
+        xp = [x.data_ptr() for x in xs]
     seeds = list(seeds) if len(seeds) else [0] * C
     if len(seeds) != C:
         raise ValueError("one seed per client")
@@ -452,9 +487,7 @@ def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, 
             codes = torch.empty(C, kc, dtype=torch.uint8, device=dev)
             norm = torch.empty(C, 1, dtype=torch.float32, device=dev)
             tiles = torch.empty(C, ntl, dtype=torch.int32, device=dev) if with_tiles else None
-            rows = zip(idx.unbind(0), codes.unbind(0), norm.unbind(0),
-                       tiles.unbind(0) if with_tiles else [None] * C)
-            pks = [StackedPacket(i_, c_, n_, n, levels, t_) for i_, c_, n_, t_ in rows]
+            pks = PacketBatch(idx, codes, norm, tiles, n, levels)
             b = {f: t.data_ptr() for f, t in (("idx", idx), ("codes", codes), ("norm", norm))}
             ptr = {"idx": P(*[b["idx"] + 4 * k * c for c in range(C)]),
                    "codes": P(*[b["codes"] + kc * c for c in range(C)]),
@@ -462,7 +495,7 @@ def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, 
                    "tiles": P(*[tiles.data_ptr() + 4 * ntl * c for c in range(C)]) if with_tiles else None}
     ws = workspace(dev, _ws_size(dev, "flc_stacked_encode_batch_workspace_size", n, k, C), "topk_batch")
     vp = lambda a: None if a is None else ctypes.cast(a, ctypes.c_void_p)  # noqa: E731
-    call("flc_stacked_encode_batch", vp(P(*[x.data_ptr() for x in xs])), C, n, k, levels,
+    call("flc_stacked_encode_batch", vp(P(*xp)), C, n, k, levels,
          vp((ctypes.c_uint64 * C)(*[int(s_) for s_ in seeds])), counter, vp(ptr["idx"]), vp(ptr["codes"]),
          vp(ptr["norm"]), vp(ptr["tiles"]), _p(ws), ws.numel(), _stream(dev))
     _after_encode(dev)
@@ -471,7 +504,7 @@ def stacked_encode_batch(xs: Sequence[torch.Tensor], k: int, levels: int = 127, 
 
 def stacked_encode_delta_batch(local_params: Sequence[Sequence[torch.Tensor]], global_params: Sequence[torch.Tensor],
                                k: int, levels: int = 127, seeds: Sequence[int] = (),
-                               counter: int = 0) -> List[StackedPacket]:
+                               counter: int = 0) -> "PacketBatch":
     """The delta-fused stacked encode of a round's clients in one launch (flc_stacked_encode_delta_batch): client c's
     delta ``cat([l - g for l, g in zip(local_params[c], global_params)])`` (the global model shared by every client),
     packet c equal to ``stacked_encode_delta(local_params[c], global_params, k, levels, seeds[c], counter)``."""
@@ -512,8 +545,7 @@ def stacked_encode_delta_batch(local_params: Sequence[Sequence[torch.Tensor]], g
          vp((P * C)(*[norm.data_ptr() + 4 * c for c in range(C)])),
          vp((P * C)(*[tiles.data_ptr() + 4 * ntl * c for c in range(C)])), _p(ws), ws.numel(), _stream(dev))
     _after_encode(dev)
-    return [StackedPacket(i_, c_, n_, n, levels, t_)
-            for i_, c_, n_, t_ in zip(idx.unbind(0), codes.unbind(0), norm.unbind(0), tiles.unbind(0))]
+    return PacketBatch(idx, codes, norm, tiles, n, levels)
 
 
 def stacked_encode_delta(local_params: Sequence[torch.Tensor], global_params: Sequence[torch.Tensor], k: int,

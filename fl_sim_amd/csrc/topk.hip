@@ -598,8 +598,13 @@ struct DeltaSrc {
       const float* g = c.g + (wb - c.lo) + 4 * lane;
 #pragma unroll
       for (int q = 0; q < SF; ++q) {
+#if FLC_DELTA_A16  // calibration only (assumes 16-B aligned operands): the pass with dwordx4 loads
+        const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(l + 256 * q));
+        const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g + 256 * q));
+#else
         const f32x4u a = __builtin_nontemporal_load(reinterpret_cast<const f32x4u*>(l + 256 * q));
         const f32x4u b = __builtin_nontemporal_load(reinterpret_cast<const f32x4u*>(g + 256 * q));
+#endif
         st.l[q] = make_float4(a.x, a.y, a.z, a.w);
         st.g[q] = make_float4(b.x, b.y, b.z, b.w);
       }
