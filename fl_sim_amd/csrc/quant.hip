@@ -403,7 +403,7 @@ template <int KIND, int BITS, bool DEC, class NormOf, class NnzAdd>
 __device__ __forceinline__ void philox_group_encode(const float (&v)[kGroup], const uint32_t (&wd)[kGroup], int64_t e0,
                                                     int valid, int64_t d, int s, double step,
                                                     uint8_t* __restrict__ codes, float* __restrict__ out, bool count,
-                                                    NormOf norm_of, NnzAdd nnz_add) {
+                                                    NormOf norm_of, NnzAdd nnz_add, bool nt = false) {
   const int64_t r0 = e0 / d;
   const int64_t r_end = (r0 + 1) * d;
   uint64_t packed = 0;
@@ -463,9 +463,18 @@ __device__ __forceinline__ void philox_group_encode(const float (&v)[kGroup], co
     for (int j = 0; j < kGroup; ++j) cnt += v[j] != 0.0f;
     if (cnt) nnz_add(r0, cnt);
   }
-  store_codes<BITS>(codes, e0, valid, packed);
+  if (nt && BITS == 8 && valid == kGroup) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 t = {(uint32_t)packed, (uint32_t)(packed >> 32)};
+    __builtin_nontemporal_store(t, reinterpret_cast<u32x2*>(codes + e0));
+  } else {
+    store_codes<BITS>(codes, e0, valid, packed);
+  }
   if (DEC) {
-    if (valid == kGroup) {
+    if (valid == kGroup && nt) {
+      st_stream(out + e0, make_float4(o[0], o[1], o[2], o[3]));
+      st_stream(out + e0 + 4, make_float4(o[4], o[5], o[6], o[7]));
+    } else if (valid == kGroup) {
       *reinterpret_cast<float4*>(out + e0) = make_float4(o[0], o[1], o[2], o[3]);
       *reinterpret_cast<float4*>(out + e0 + 4) = make_float4(o[4], o[5], o[6], o[7]);
     } else {
@@ -576,7 +585,7 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
                                                           double step, float* __restrict__ norms, uint64_t seed,
                                                           uint64_t counter, uint8_t* __restrict__ codes,
                                                           long long* __restrict__ nnz, float* __restrict__ out,
-                                                          QuantWs ws, unsigned epoch) {
+                                                          QuantWs ws, unsigned epoch, int cal) {
   constexpr int64_t SPAN = (int64_t)kFT * kGroup * GPT;
   __shared__ uint32_t s_m[2][kFT / kWave];
   __shared__ float s_norm[2];
@@ -624,7 +633,8 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
     for (int w = 0; w < kFT / kWave; ++w) m = s_m[tid][w] > m ? s_m[tid][w] : m;
     __hip_atomic_store(ws.blkmax + 2 * blockIdx.x + tid, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  fused_exchange(ws, epoch);
+  if (!(cal & 2)) fused_exchange(ws, epoch);
+  else __syncthreads();
   if (tid < kWave) {  // wave 0: each row's max over the blocks holding it
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
@@ -652,11 +662,21 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
     const int64_t e0 = base + ((int64_t)g * kFT + tid) * kGroup;
     if (e0 < n) {
       const int valid = n - e0 < kGroup ? (int)(n - e0) : kGroup;
+      if (cal & 4) {  // calibration: the memory traffic alone (x copied to out, zero codes)
+        if (valid == kGroup) {
+          store_codes<BITS>(codes, e0, valid, 0ull);
+          if (DEC) {
+            *reinterpret_cast<float4*>(out + e0) = make_float4(v[g][0], v[g][1], v[g][2], v[g][3]);
+            *reinterpret_cast<float4*>(out + e0 + 4) = make_float4(v[g][4], v[g][5], v[g][6], v[g][7]);
+          }
+        }
+        continue;
+      }
       if constexpr (!kPre) group_words(e0, seed, counter, wd[0]);
       philox_group_encode<KIND, BITS, DEC>(
           v[g], wd[kPre ? g : 0], e0, valid, d, s, step, codes, out, nnz != nullptr,
           [&](int64_t r) { return s_norm[r - r0]; },
-          [&](int64_t r, int cnt) { atomicAdd(&s_nnz[r - r0], (unsigned long long)cnt); });
+          [&](int64_t r, int cnt) { atomicAdd(&s_nnz[r - r0], (unsigned long long)cnt); }, cal & 1);
     }
   }
   if (nnz) {
@@ -868,14 +888,15 @@ int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p,
       const unsigned ep = next_epoch();
       const unsigned grid = (unsigned)cdiv(n, (int64_t)gpt * kFT * kGroup);
       const char* fname = DEC ? "quant_fused_encode_decode" : "quant_fused_encode";
+      const int cal = getenv("FLC_QUANT_CAL") ? atoi(getenv("FLC_QUANT_CAL")) : 0;  // calibration switches
       Coresident co(st, dev);
       if (co.status()) return co.status();
       if (gpt == 2)
         FLC_LAUNCH(fname, (quant_fused_kernel<KIND, BITS, DEC, 2>), dim3(grid), dim3(kFT), 0, st, x, n, d, levels, step,
-                   norms, seed, counter, codes, nz, out, w, ep);
+                   norms, seed, counter, codes, nz, out, w, ep, cal);
       else
         FLC_LAUNCH(fname, (quant_fused_kernel<KIND, BITS, DEC, 4>), dim3(grid), dim3(kFT), 0, st, x, n, d, levels, step,
-                   norms, seed, counter, codes, nz, out, w, ep);
+                   norms, seed, counter, codes, nz, out, w, ep, cal);
       return co.finish();
     }
   }

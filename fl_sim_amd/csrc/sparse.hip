@@ -385,7 +385,6 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
   }
 }
 
-
 // Grid-stride pipelined decode: G resident blocks, block b assembles tiles b, b + G, b + 2G, ... of
 // TILE = 1024 V outputs.  The whole grid's stores of one iteration cover ONE contiguous window (the write
 // order HBM3E takes at full rate, tools/bwprobe4.hip), and each block's dependent load chain

@@ -992,7 +992,14 @@ __device__ __forceinline__ void sample_one(const Src& x, int64_t n, int S, const
 
 template <class Src>
 __global__ __launch_bounds__(256) void topk_sample_kernel(Src x, int64_t n, int S, EncWs w) {
+#ifdef FLC_SELECT_STAMPS  // diagnostic timeline: each sample block's start and end (blkt rows 512 + b)
+  if (threadIdx.x == 0 && blockIdx.x < 256) w.blkt()[(512 + blockIdx.x) * 4] = __builtin_amdgcn_s_memrealtime();
+#endif
   sample_one(x, n, S, w, blockIdx.x * 256 + threadIdx.x);
+#ifdef FLC_SELECT_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x < 256) w.blkt()[(512 + blockIdx.x) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // one client of a batched call (flc_stacked_encode_batch[_delta]): its input, Philox seed and outputs.  `x` is the
@@ -1274,6 +1281,9 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   __shared__ unsigned long long s_ex[3];
   __shared__ SelState s_cur, s_prev;
   __shared__ unsigned long long s_sum[kENW * 6];
+#ifdef FLC_SELECT_STAMPS  // diagnostic timeline: each block's first instruction (blkt rows 256 + b)
+  if (threadIdx.x == 0 && blockIdx.x < 256) w.blkt()[(256 + blockIdx.x) * 4] = __builtin_amdgcn_s_memrealtime();
+#endif
   STAMP_INIT();
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   const int64_t b0 = (int64_t)w.bid * w.M;

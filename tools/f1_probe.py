@@ -8,7 +8,24 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from fl_sim_amd import codec  # noqa: E402
+from fl_sim_amd import codec, _lib  # noqa: E402
+import ctypes  # noqa: E402
+
+
+def probe(name, fn, reps=20):
+    """average duration of the named kernel over reps calls (live HIP-event probe)"""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    _lib.call("flc_probe_set", name.encode())
+    _lib.call("flc_probe_read", None, None)
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    t, c = ctypes.c_double(), ctypes.c_int64()
+    _lib.call("flc_probe_read", ctypes.byref(t), ctypes.byref(c))
+    _lib.call("flc_probe_set", None)
+    return t.value / max(c.value, 1) * 1e3
 
 
 def tm(fn, reps=20):
@@ -44,5 +61,12 @@ for label, sizes in (("aligned", [1 << 22] * 64), ("bench_sizes", [(1 << 22) + (
         t_fused = tm(lambda: codec.stacked_encode_delta(loc, glo, k, 127, seed=1, counter=2))
         print(f"{label:12s} {layout:12s} plain {t_plain:7.1f} us  fused {t_fused:7.1f} us  ratio {t_fused / t_plain:.3f}",
               flush=True)
+        if os.environ.get("F1_KERNELS"):
+            pk = {kn: probe(kn, lambda: codec.stacked_encode(flat, k, 127, seed=1, counter=2))
+                  for kn in ("topk_sample", "stacked_encode")}
+            fk = {kn: probe(kn, lambda: codec.stacked_encode_delta(loc, glo, k, 127, seed=1, counter=2))
+                  for kn in ("topk_sample", "stacked_encode")}
+            print("   kernels plain", {a: round(b, 1) for a, b in pk.items()}, "fused", {a: round(b, 1) for a, b in fk.items()},
+                  flush=True)
         del loc, glo, flat
         torch.cuda.empty_cache()

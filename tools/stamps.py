@@ -20,9 +20,17 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
 seed = int(os.environ.get("SEED", "1"))  # bench.py's headline delta: SEED=1234
 x = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed)) * 1e-3
+if os.environ.get("DELTA"):  # f1: the delta-fused encode over 64 tensors (local = x piece + global, global random)
+    gen = torch.Generator(device="cuda").manual_seed(seed + 1)
+    sizes = [n // 64] * 63 + [n - 63 * (n // 64)]
+    glo = [torch.randn(s, device="cuda", generator=gen) for s in sizes]
+    loc = [gl + xp for gl, xp in zip(glo, torch.split(x, sizes))]
+    encode = lambda it: codec.stacked_encode_delta(loc, glo, k, 127, seed=1, counter=it)
+else:
+    encode = lambda it: codec.stacked_encode(x, k, 127, 1, it)
 names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "decide", "write+tiles"]
 for it in range(int(os.environ.get("ITERS", "12"))):
-    codec.stacked_encode(x, k, 127, 1, it)
+    encode(it)
     torch.cuda.synchronize()
     ws = [t for key, t in codec._WS.items() if key[2] == "topk"][0]
     st = ws[STAMP_OFF:STAMP_OFF + 16 * 8].cpu().numpy().view(np.uint64).astype(np.int64)
