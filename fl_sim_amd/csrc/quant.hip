@@ -888,7 +888,11 @@ int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p,
       const unsigned ep = next_epoch();
       const unsigned grid = (unsigned)cdiv(n, (int64_t)gpt * kFT * kGroup);
       const char* fname = DEC ? "quant_fused_encode_decode" : "quant_fused_encode";
-      const int cal = getenv("FLC_QUANT_CAL") ? atoi(getenv("FLC_QUANT_CAL")) : 0;  // calibration switches
+#ifdef FLC_CALIB  // calibration builds (tools/quant_cal_probe.py): 1 non-temporal stores, 2 no exchange, 4 traffic only
+      const int cal = getenv("FLC_QUANT_CAL") ? atoi(getenv("FLC_QUANT_CAL")) : 0;
+#else
+      constexpr int cal = 0;
+#endif
       Coresident co(st, dev);
       if (co.status()) return co.status();
       if (gpt == 2)

@@ -1995,7 +1995,11 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
   const SampleSetup ss = sample_setup(n, k);
   if (!ss.take_all)
     FLC_LAUNCH("topk_sample", topk_sample_kernel<Src>, dim3((unsigned)cdiv(ss.S, 256)), dim3(256), 0, st, x, n, ss.S, w);
-  static const bool split = getenv("FLC_TOPK_SPLIT") && atoi(getenv("FLC_TOPK_SPLIT")) != 0;  // calibration
+#if defined(FLC_CALIB) || defined(FLC_SELECT_STAMPS)  // calibration builds: FLC_TOPK_SPLIT=1 times the two-kernel path
+  static const bool split = getenv("FLC_TOPK_SPLIT") && atoi(getenv("FLC_TOPK_SPLIT")) != 0;
+#else
+  constexpr bool split = false;
+#endif
   if (split)
     FLC_LAUNCH("topk_filter", topk_filter_kernel<Src>, dim3((unsigned)g.G), dim3(kET), 0, st, x, n, w, ss.S, ss.rank_lo,
                ss.rank_hi, ss.take_all);

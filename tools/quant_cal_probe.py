@@ -1,6 +1,7 @@
 """configs[1]'s one-launch quantizer under its calibration switches (FLC_QUANT_CAL bits: 1 non-temporal stores,
 2 no grid exchange, 4 the memory traffic alone): kernel time by the live HIP-event probe and the step's wall time,
-variants interleaved in one process.  Switch 1 is checked bit for bit against the default."""
+variants interleaved in one process.  Switch 1 is checked bit for bit against the default.  The switches exist only
+in a calibration build: tools/build_variant.sh calib -DFLC_CALIB, then FLC_LIB=diag/lib_calib.so."""
 import ctypes, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
