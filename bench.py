@@ -571,9 +571,9 @@ def main():
             "bytes_formula": "(8 + 8/4) * D per client (norm, encode, decode reading the wire: 3 launches)",
             "fused_us_per_step": round(ms2f * 1e3, 2),
             "fused_GB_s": round(b2 * d2 * 9 / (ms2f * 1e-3) / 1e9, 1),
-            "fused_bytes_formula": "(4 + 1 + 4) * D per client (flc_quant_encode_auto: norm partials, then the encode "
-                                   "folding the norm and writing the codes and the decoded values from registers: 2 "
-                                   "launches, the wire is not read back)",
+            "fused_bytes_formula": "(4 + 1 + 4) * D per client (flc_quant_encode_auto: ONE persistent launch - x read "
+                                   "into registers, a grid exchange of the per-row maxima, the codes and the decoded "
+                                   "values written from the registers; the wire is not read back)",
         }
         del X
         # configs[2]: top-k 1% of a 25M delta (encode + dense decode)
