@@ -236,9 +236,11 @@ __global__ __launch_bounds__(kThreads) void model_fold_kernel(ModelPack p, float
   }
 }
 
+// up to 64 blocks of 256 threads per CU of a 256-CU device, grid-stride beyond (tools/wsum_probe.hip, 8 x 25 M:
+// 16 K blocks 160-162 us against 169-170 us for 4 K, 163 us for one float4 per thread; profiles/r03/r03p_wsum2.txt)
 unsigned grid_for(int64_t work) {
   const int64_t g = cdiv(work, kThreads);
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 256 * 16));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 256 * 64));
 }
 
 }  // namespace
