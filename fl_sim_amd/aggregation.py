@@ -60,6 +60,14 @@ def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence[Sequence[torch.Ten
     dev = _model_device(list(dsts) + list(step.get("theta") or []) + list(step.get("v") or []))
     if dev is None or not dsts or len(msg_tensors) > codec.MODEL_FOLD_MAX_SRC:
         return False
+    if codec._model_fold_op() is not None:
+        # the op checks every tensor in C++ before launching anything: with the messages already on the model's
+        # device (the usual case) that is the whole host cost; otherwise it raises TypeError and they are moved below
+        try:
+            codec.model_fold(dsts, msg_tensors, weights, init_mode, beta, **step)
+            return True
+        except TypeError:
+            pass
     srcs = [[t if (t.is_cuda and t.get_device() == dev) else t.detach().to(f"cuda:{dev}") for t in mt]
             for mt in msg_tensors]
     codec.model_fold(dsts, srcs, weights, init_mode, beta, **step)

@@ -718,6 +718,25 @@ def weighted_sum(dst: torch.Tensor, srcs: Sequence[torch.Tensor], weights: Seque
 MODEL_FOLD_MAX_SRC = 16
 
 
+_MODEL_FOLD_OP: list = []
+
+
+def _model_fold_op():
+    """torch.ops.flcodec.model_fold_ when libflcodec_torch.so is built (the same C-ABI call, its per-tensor checks in
+    C++), else None (the ctypes path below)."""
+    if not _MODEL_FOLD_OP:
+        op = None
+        try:
+            from . import load_torch_ops
+
+            load_torch_ops()
+            op = torch.ops.flcodec.model_fold_
+        except (ImportError, OSError, RuntimeError, AttributeError):
+            op = None
+        _MODEL_FOLD_OP.append(op)
+    return _MODEL_FOLD_OP[0]
+
+
 def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
                init_mode: int, beta: float = 0.0, theta: Optional[Sequence[torch.Tensor]] = None,
                v: Optional[Sequence[torch.Tensor]] = None, opt: str = "avg", lr: float = 1.0, beta2: float = 0.0,
@@ -732,6 +751,14 @@ def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tenso
     if ns > MODEL_FOLD_MAX_SRC:
         raise ValueError(f"model_fold takes at most {MODEL_FOLD_MAX_SRC} messages")
     if nt == 0:
+        return
+    op = _model_fold_op()
+    if op is not None:  # the checks and the pointer tables in C++ (torch_ops.cpp): one dispatcher call
+        if any(len(msg) != nt for msg in srcs):
+            raise ValueError("every message has one tensor per model tensor")
+        op(list(dsts), [t for msg in srcs for t in msg], [float(w) for w in weights], int(init_mode), float(beta),
+           [] if theta is None else list(theta), [] if v is None else list(v), _lib.FLC_OPT[opt], float(lr),
+           float(beta2), float(tau))
         return
     f32 = torch.float32
     dev = dsts[0].get_device()

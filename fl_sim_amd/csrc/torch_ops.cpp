@@ -356,6 +356,52 @@ at::Tensor& weighted_sum_(at::Tensor& dst, at::TensorList srcs, at::ArrayRef<dou
   return dst;
 }
 
+// a whole model in one launch (flc_model_fold): dsts[t] per model tensor, srcs[m * n_tensors + t] message-major,
+// theta / v empty or one per tensor.  Every tensor is checked here in C++ (device, dtype, contiguity, size): the host
+// cost of a model update is these checks plus one launch (a model is ~10-100 small tensors).
+void model_fold_(at::TensorList dsts, at::TensorList srcs, at::ArrayRef<double> weights, int64_t init_mode,
+                 double beta, at::TensorList theta, at::TensorList v, int64_t opt, double lr, double beta2, double tau) {
+  const size_t nt = dsts.size(), ns = weights.size();
+  TORCH_CHECK_VALUE(ns <= 16, "flcodec: model_fold takes at most 16 messages");
+  TORCH_CHECK_VALUE(srcs.size() == ns * nt, "flcodec: every message has one tensor per model tensor");
+  TORCH_CHECK_VALUE(theta.empty() || theta.size() == nt, "flcodec: theta has one tensor per model tensor");
+  TORCH_CHECK_VALUE(v.empty() || v.size() == nt, "flcodec: v has one tensor per model tensor");
+  if (nt == 0) return;
+  const c10::Device dev = dsts[0].device();
+  auto usable = [&](const at::Tensor& t) {
+    return t.is_cuda() && t.device() == dev && t.scalar_type() == at::kFloat && t.is_contiguous();
+  };
+  std::vector<float*> dp(nt), tp(theta.size()), vp(v.size());
+  std::vector<int64_t> sz(nt);
+  for (size_t t = 0; t < nt; ++t) {
+    TORCH_CHECK_TYPE(usable(dsts[t]), "flcodec: model tensors must be contiguous fp32 HIP tensors on one device");
+    dp[t] = dsts[t].data_ptr<float>();
+    sz[t] = dsts[t].numel();
+    if (!theta.empty()) {
+      TORCH_CHECK_TYPE(usable(theta[t]) && theta[t].numel() == sz[t], "flcodec: theta must match the model tensors");
+      tp[t] = theta[t].data_ptr<float>();
+    }
+    if (!v.empty()) {
+      TORCH_CHECK_TYPE(usable(v[t]) && v[t].numel() == sz[t], "flcodec: v must match the model tensors");
+      vp[t] = v[t].data_ptr<float>();
+    }
+  }
+  std::vector<const float*> sp(ns * nt);
+  for (size_t i = 0; i < sp.size(); ++i) {
+    const at::Tensor& a = srcs[i];
+    TORCH_CHECK_TYPE(usable(a), "flcodec: message tensors must be contiguous fp32 HIP tensors on the model's device");
+    TORCH_CHECK_VALUE(a.numel() == sz[i % nt], "flcodec: message tensors must match the model tensors' sizes");
+    sp[i] = a.data_ptr<float>();
+  }
+  std::vector<float> w(ns);
+  for (size_t m = 0; m < ns; ++m) w[m] = (float)weights[m];
+  c10::DeviceGuard g(dev);
+  check(flc_model_fold(dp.data(), sp.data(), w.data(), (int)ns, sz.data(), (int)nt, (int)init_mode, (float)beta,
+                       theta.empty() ? nullptr : tp.data(), v.empty() ? nullptr : vp.data(), (int)opt, lr, beta2, tau,
+                       stream_of(dsts[0])),
+        "model_fold");
+}
+
 void fedopt_step_(at::Tensor& theta, const at::Tensor& delta_, const c10::optional<at::Tensor>& v, int64_t opt,
                   double lr, double beta2, double tau) {
   TORCH_CHECK(theta.is_cuda() && theta.scalar_type() == at::kFloat && theta.is_contiguous(),
@@ -584,6 +630,8 @@ TORCH_LIBRARY(flcodec, m) {
   m.def("natural_decode(Tensor codes, float weight=1.0) -> Tensor");
   m.def("weighted_sum_(Tensor(a!) dst, Tensor[] srcs, float[] weights, int init_mode, float beta=0.0) -> Tensor(a!)");
   m.def("fedopt_step_(Tensor(a!) theta, Tensor delta, Tensor(b!)? v, int opt, float lr, float beta2, float tau) -> ()");
+  m.def("model_fold_(Tensor(a!)[] dsts, Tensor[] srcs, float[] weights, int init_mode, float beta, "
+        "Tensor(b!)[] theta, Tensor(c!)[] v, int opt=0, float lr=1.0, float beta2=0.0, float tau=0.0) -> ()");
   m.def("delta_flatten(Tensor[] theta_local, Tensor[] theta_global) -> Tensor");
   m.def("feddr_combine_(Tensor(a!) theta, Tensor(b!) y, Tensor x_til, float alpha, float cx, float cy, int prox, "
         "float prox_c) -> ()");
@@ -611,6 +659,7 @@ TORCH_LIBRARY_IMPL(flcodec, CUDA, m) {
   m.impl("natural_decode", &natural_decode);
   m.impl("weighted_sum_", &weighted_sum_);
   m.impl("fedopt_step_", &fedopt_step_);
+  m.impl("model_fold_", &model_fold_);
   m.impl("delta_flatten", &delta_flatten);
   m.impl("feddr_combine_", &feddr_combine_);
   m.impl("stacked_encode_delta", &stacked_encode_delta);

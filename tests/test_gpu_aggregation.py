@@ -281,10 +281,23 @@ def _views(shapes, g, scale=1.0, misalign=False):
     return out
 
 
+@pytest.fixture(params=["torch_op", "ctypes"])
+def fold_path(request, monkeypatch):
+    """codec.model_fold through torch.ops.flcodec.model_fold_ (the default when libflcodec_torch.so is built) and
+    through the ctypes binding: the same C-ABI call behind both"""
+    from fl_sim_amd import codec
+
+    if request.param == "ctypes":
+        monkeypatch.setattr(codec, "_MODEL_FOLD_OP", [None])
+    else:
+        assert codec._model_fold_op() is not None
+    return request.param
+
+
 @pytest.mark.parametrize("opt", ["avg", "adagrad", "yogi", "adam"])
 @pytest.mark.parametrize("n_msgs", [0, 1, 10, 16])
 @pytest.mark.parametrize("misalign", [False, True])
-def test_model_fold_equals_per_tensor_calls(opt, n_msgs, misalign):
+def test_model_fold_equals_per_tensor_calls(opt, n_msgs, misalign, fold_path):
     """flc_model_fold (one launch for the whole model, FedOpt's step fused) equals flc_weighted_sum + flc_fedopt_step
     per tensor bit for bit: 20 tensors (two launches), tails of n % 4, misaligned views (the scalar path)."""
     from fl_sim_amd import codec
@@ -315,7 +328,7 @@ def test_model_fold_equals_per_tensor_calls(opt, n_msgs, misalign):
         assert all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(a, b))
 
 
-def test_model_fold_rejects_bad_arguments():
+def test_model_fold_rejects_bad_arguments(fold_path):
     from fl_sim_amd import codec
 
     t = [torch.zeros(5, device="cuda")]
@@ -325,3 +338,17 @@ def test_model_fold_rejects_bad_arguments():
         codec.model_fold(t, [[torch.zeros(6, device="cuda")]], [1.0], 0)  # size mismatch
     with pytest.raises(RuntimeError):
         codec.model_fold(t, [t], [1.0], 0, theta=t, v=None, opt="adam")  # adam needs v
+
+
+def test_fold_with_host_messages_equals_device_messages(fold_path):
+    """Messages left in host memory (the reference's clients hold their tensors there) are moved to the model's
+    device and folded exactly like device-resident messages."""
+    from fl_sim_amd import aggregation
+
+    model = make_model(CONFIG1_SHAPES, 4)
+    host_msgs = make_msgs(CONFIG1_SHAPES, 10, 5, "parameters")
+    a = _dev([p.data for p in model.parameters()])
+    b = [t.clone() for t in a]
+    aggregation.avg_parameters(a, host_msgs, True, 0.3)
+    aggregation.avg_parameters(b, _msgs_dev(host_msgs, "parameters"), True, 0.3)
+    assert all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(a, b))

@@ -28,6 +28,8 @@ OPS = {
     "natural_decode": None,
     "weighted_sum_": None,
     "fedopt_step_": None,
+    "model_fold_": "flcodec::model_fold_(Tensor(a!)[] dsts, Tensor[] srcs, float[] weights, int init_mode, float beta, "
+                   "Tensor(b!)[] theta, Tensor(c!)[] v, int opt=0, float lr=1., float beta2=0., float tau=0.) -> ()",
     "delta_flatten": "flcodec::delta_flatten(Tensor[] theta_local, Tensor[] theta_global) -> Tensor",
     "feddr_combine_": None,
     "stacked_encode_delta": "flcodec::stacked_encode_delta(Tensor[] theta_local, Tensor[] theta_global, int k, "
@@ -88,6 +90,8 @@ def test_cpu_tensors_refused(ops):
         ops.stacked_encode(torch.zeros(64), 4)
     with pytest.raises(NotImplementedError):
         ops.weighted_sum_(torch.zeros(8), [torch.ones(8)], [0.5], 0)
+    with pytest.raises(NotImplementedError):
+        ops.model_fold_([torch.zeros(8)], [torch.ones(8)], [0.5], 0, 0.0, [], [])
 
 
 # ------------------------------------------------------------------------------------------------------ GPU parity
