@@ -132,6 +132,23 @@ SIGNATURES = {
     "flc_scale_div": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "flc_randk_keys": (c_int, [c_int64, c_uint64, c_uint64, c_void_p, c_void_p]),
     "flc_randk_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
+    "flc_copy_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "flc_scale_div_f64": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p]),
+    "flc_randk_apply_f64": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_double, c_void_p, c_void_p]),
+    "flc_f64_workspace_size": (c_size_t, [c_int64]),
+    "flc_count_consumers_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "flc_natural_f64": (
+        c_int, [c_void_p, c_int64, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    ),
+    "flc_natural_decode_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "flc_quant_norm_f64": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "flc_quant_f64": (
+        c_int,
+        [c_void_p, c_int64, c_int, c_int, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_size_t, c_void_p],
+    ),
+    "flc_quant_decode_f64": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "flc_topk_dense_f64": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_weighted_sum": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_float, c_void_p, c_void_p]),
     "flc_fedopt_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
     "flc_model_fold": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,

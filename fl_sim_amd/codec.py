@@ -835,3 +835,117 @@ def delta_flatten(local_params: Sequence[torch.Tensor], global_params: Sequence[
     call("flc_delta_flatten", ctypes.cast(lp, ctypes.c_void_p), ctypes.cast(gp, ctypes.c_void_p),
          ctypes.cast(sz, ctypes.c_void_p), len(ls), _p(out), _stream(dev))
     return out
+
+
+# ---------------------------------------------------------------------------------------- float64 inputs
+# The reference runs every compressor on whatever dtype x has (compressors.py:267-410); these are the float64 forms
+# (f64.hip): a float64 HIP vector in, a float64 HIP vector out.  Uniforms as for float32 (compat_u: one double per
+# consumer in index order, else Philox at the element's index).
+def _dev_f64(x: torch.Tensor, name: str = "x") -> torch.Tensor:
+    if not isinstance(x, torch.Tensor) or x.device.type != "cuda":
+        raise TypeError(f"{name} must be a torch tensor on a HIP device")
+    if x.dtype != torch.float64:
+        raise TypeError(f"{name} must be float64 (got {x.dtype})")
+    x = x.reshape(-1)
+    if not x.is_contiguous() or x.data_ptr() % 16 != 0:
+        x = x.contiguous().clone()
+    return x
+
+
+def _ws64(x: torch.Tensor) -> torch.Tensor:
+    return workspace(x.device, _lib.size("flc_f64_workspace_size", x.numel()), "f64")
+
+
+def copy_f64(x: torch.Tensor) -> torch.Tensor:
+    x = _dev_f64(x)
+    out = torch.empty_like(x)
+    call("flc_copy_f64", _p(x), x.numel(), _p(out), _stream(x.device))
+    return out
+
+
+def scale_div_f64(x: torch.Tensor, p: float) -> torch.Tensor:
+    x = _dev_f64(x)
+    out = torch.empty_like(x)
+    call("flc_scale_div_f64", _p(x), x.numel(), float(p), _p(out), _stream(x.device))
+    return out
+
+
+def randk_apply_f64(x: torch.Tensor, idx: torch.Tensor, scale: float) -> torch.Tensor:
+    x = _dev_f64(x)
+    idx = idx.to(device=x.device, dtype=torch.int32).contiguous()
+    out = torch.empty_like(x)
+    call("flc_randk_apply_f64", _p(x), x.numel(), _p(idx), idx.numel(), float(scale), _p(out), _stream(x.device))
+    return out
+
+
+def count_consumers_f64(x: torch.Tensor, norm: Optional[torch.Tensor]) -> torch.Tensor:
+    """Device int64 scalar: the uniforms the reference draws (natural: norm None, x != 0; dithering: with the norm)."""
+    x = _dev_f64(x)
+    out = torch.empty(1, dtype=torch.int64, device=x.device)
+    ws = _ws64(x)
+    call("flc_count_consumers_f64", _p(x), x.numel(), _p(norm), _p(out), _p(ws), ws.numel(), _stream(x.device))
+    return out
+
+
+def natural_f64(x: torch.Tensor, seed: int = 0, counter: int = 0, compat_u: Optional[torch.Tensor] = None,
+                want_codes: bool = False) -> Tuple[Optional[torch.Tensor], torch.Tensor]:
+    """Natural compression of a float64 vector: (codes or None, decoded float64 vector)."""
+    x = _dev_f64(x)
+    n = x.numel()
+    codes = torch.empty(n, dtype=torch.int16, device=x.device) if want_codes else None
+    out = torch.empty_like(x)
+    ws = _ws64(x)
+    call("flc_natural_f64", _p(x), n, seed, counter, _p(compat_u), _p(codes), _p(out), _p(ws), ws.numel(),
+         _stream(x.device))
+    return codes, out
+
+
+def natural_decode_f64(codes: torch.Tensor, n: int) -> torch.Tensor:
+    out = torch.empty(n, dtype=torch.float64, device=codes.device)
+    call("flc_natural_decode_f64", _p(codes), n, _p(out), _stream(out.device))
+    return out
+
+
+def quant_norm_f64(x: torch.Tensor, p: float = math.inf) -> torch.Tensor:
+    x = _dev_f64(x)
+    pk = _lib.FLC_NORM_INF if math.isinf(p) else (_lib.FLC_NORM_L2 if p == 2 else None)
+    if pk is None:
+        raise ValueError(f"p must be inf or 2 (got {p})")
+    norm = torch.empty(1, dtype=torch.float64, device=x.device)
+    ws = _ws64(x)
+    call("flc_quant_norm_f64", _p(x), x.numel(), pk, _p(norm), _p(ws), ws.numel(), _stream(x.device))
+    return norm
+
+
+def quant_f64(x: torch.Tensor, kind: int, levels: int, norm: torch.Tensor, seed: int = 0, counter: int = 0,
+              compat_u: Optional[torch.Tensor] = None, want_codes: bool = False, want_nnz: bool = False):
+    """Standard / natural dithering of a float64 vector with the given float64 norm (a 1-element device tensor):
+    (8-bit codes or None, decoded float64 vector, nnz or None)."""
+    x = _dev_f64(x)
+    n = x.numel()
+    if norm.dtype != torch.float64 or norm.device != x.device:
+        raise TypeError("norm must be a float64 tensor on x's device")
+    if compat_u is not None and compat_u.dtype != torch.float64:
+        raise TypeError("compat_u must be float64")
+    codes = torch.empty(n, dtype=torch.uint8, device=x.device) if want_codes else None
+    nnz = torch.empty(1, dtype=torch.int64, device=x.device) if want_nnz else None
+    out = torch.empty_like(x)
+    ws = _ws64(x)
+    call("flc_quant_f64", _p(x), n, kind, levels, _p(norm), seed, counter, _p(compat_u), _p(codes), _p(out), _p(nnz),
+         _p(ws), ws.numel(), _stream(x.device))
+    return codes, out, nnz
+
+
+def quant_decode_f64(codes: torch.Tensor, n: int, kind: int, levels: int, norm: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(n, dtype=torch.float64, device=codes.device)
+    call("flc_quant_decode_f64", _p(codes), n, kind, levels, _p(norm), _p(out), _stream(out.device))
+    return out
+
+
+def topk_dense_f64(x: torch.Tensor, k: int) -> torch.Tensor:
+    """out = x on the k largest elements (ties: the highest indices), +0 elsewhere; 0 < k < n."""
+    x = _dev_f64(x)
+    out = torch.empty_like(x)
+    ws = _ws64(x)
+    call("flc_topk_dense_f64", _p(x), x.numel(), int(k), _p(out), _p(ws), ws.numel(), _stream(x.device))
+    return out

@@ -294,8 +294,8 @@ class Compressor:
         # host input: the reference's own signature (numpy); H2D -> kernels -> D2H
         is_tensor = isinstance(x, torch.Tensor)
         arr = x.detach().cpu().numpy() if is_tensor else np.asarray(x)
-        if arr.dtype != np.float32:
-            raise TypeError(f"the MI355X codec path is fp32; got {arr.dtype}")
+        if arr.dtype != np.float32 and arr.dtype != np.float64:
+            raise TypeError(f"the MI355X codec path takes float32 or float64 vectors; got {arr.dtype}")
         host_norm = self._reference_norm(arr.reshape(-1)) if self._wants_host_norm(device_input=False) else None
         dev = torch.device("cuda", torch.cuda.current_device())
         out = self._compress_device(torch.from_numpy(np.ascontiguousarray(arr)).to(dev, non_blocking=False), host_norm)
@@ -320,9 +320,17 @@ class Compressor:
         return (self.norm_mode == "auto" and not device_input and self.rng_mode == "compat"
                 and not math.isinf(self.p))
 
-    def _reference_norm(self, arr: np.ndarray) -> np.float32:
-        # compressors.py:332 / 372, evaluated as the reference evaluates it (numpy on this host)
-        return np.float32(np.linalg.norm(arr, self.p))
+    def _reference_norm(self, arr: np.ndarray):
+        # compressors.py:332 / 372, evaluated as the reference evaluates it (numpy on this host), in x's dtype
+        return arr.dtype.type(np.linalg.norm(arr, self.p))
+
+    def _check_bracket(self, norm: float, consumers: int) -> None:
+        # a norm of 0 under nonzero elements (a p = 2 norm whose squares underflowed) leaves y = |x| / 0 = inf
+        # without a level bracket: the reference's level loop then indexes past its table (compressors.py:346-347)
+        # before it draws for that element
+        if norm == 0.0 and consumers > 0:
+            n = len(self.levelsValues)
+            raise IndexError(f"index {n} is out of bounds for axis 0 with size {n}")
 
     def _uniforms(self, count: int, device) -> torch.Tensor:
         u = _rng.python_random_doubles(count)
@@ -337,6 +345,8 @@ class Compressor:
     def _compress_device(self, x: torch.Tensor, host_norm: Optional[np.float32] = None) -> torch.Tensor:
         if x.dim() != 1:
             raise ValueError("compressVector expects a 1-D vector (d = max(x.shape) in the reference)")
+        if x.dtype == torch.float64:
+            return self._compress_device_f64(x, host_norm)
         d = x.numel()
         t = self.compressorType
         if t == CompressorType.IDENTICAL:
@@ -411,6 +421,7 @@ class Compressor:
             compat_u = None
             if self.rng_mode == "compat":
                 cnt = int(codec.count_consumers(x2, norms).item())
+                self._check_bracket(float(norms.item()), cnt)
                 compat_u = self._uniforms(cnt, x.device)
             pkt, out = codec.quant_encode_decode(x2, kind, self.s, norms, seed, ctr, compat_u, want_nnz=(t in _STD))
             out = out.reshape(d)
@@ -424,6 +435,80 @@ class Compressor:
                     per = (1.0 + np.ceil(math.log2(self.s))) / (64.0 if t == CompressorType.STANDARD_DITHERING_FP64 else 32.0)
                     # repeated += of a multiple of 1/64 is exact below 2^46: equals the reference's loop
                     send = send + nnz * per
+                self._finish(d, send)
+            else:
+                den = 64.0 if t == CompressorType.NATURAL_DITHERING_FP64 else 32.0
+                self._finish(d, d * (1.0 + np.ceil(math.log2(self.s))) / den)
+            return out
+        raise ValueError(f"unknown compressor type {t}")
+
+    def _compress_device_f64(self, x: torch.Tensor, host_norm=None) -> torch.Tensor:
+        """The float64 forms (f64.hip): the reference keeps every step in float64 when x is float64
+        (compressors.py:267-410); same RNG consumption and send statistics as the float32 path."""
+        d = x.numel()
+        t = self.compressorType
+        if t == CompressorType.IDENTICAL:
+            out = codec.copy_f64(x)
+            self._finish(d, d)
+            return out
+        if t == CompressorType.LAZY_COMPRESSOR:
+            testp = random.random() if self.rng_mode == "compat" else self._philox_scalar(x.device)
+            if testp < self.P:
+                out = codec.scale_div_f64(x, float(self.P))  # x / P in float64 (compressors.py:279)
+                self._finish(d, d)
+            else:
+                out = torch.zeros_like(x)
+                self._finish(d, 0)
+            return out
+        if t == CompressorType.RANDK_COMPRESSOR:
+            if self.D != d:
+                raise ValueError(f"RandK compressor built for D={self.D} applied to a vector of length {d}")
+            if self.rng_mode == "compat":
+                idx = torch.from_numpy(_rng.numpy_shuffle_prefix(self.D, self.K)).to(x.device)
+            else:
+                seed, ctr = self.philox.next()
+                idx = codec.randk_indices(self.D, int(self.K), seed, ctr, x.device)
+            out = codec.randk_apply_f64(x, idx, self.D / self.K)  # a Python float times an fp64 element (290)
+            self._finish(d, self.K)
+            return out
+        if t == CompressorType.TOPK_COMPRESSOR:
+            K = int(self.K)
+            out = codec.copy_f64(x) if K <= 0 or K >= d else codec.topk_dense_f64(x, K)
+            self._finish(d, self.K)
+            return out
+        if t == CompressorType.ADAPTIVE_RANDOM_COMPRESSOR:
+            raise NotImplementedError("the adaptive random compressor takes float32 vectors on the device path")
+        if t in _NATURAL:
+            seed, ctr = self.philox.next()
+            compat_u = None
+            if self.rng_mode == "compat":
+                compat_u = self._uniforms(int(codec.count_consumers_f64(x, None).item()), x.device)
+            _, out = codec.natural_f64(x, seed, ctr, compat_u)
+            self._finish(d, (12.0 / 64.0 if t == CompressorType.NATURAL_COMPRESSOR_FP64 else 9.0 / 32.0) * d)
+            return out
+        if t in _STD or t in _NATD:
+            if not 1 <= self.s <= 127:
+                raise ValueError(f"the device dithering codec takes 1..127 levels (8-bit codes); s = {self.s}")
+            kind = FLC_Q_STANDARD_DITHER if t in _STD else FLC_Q_NATURAL_DITHER
+            if host_norm is not None:
+                norm = torch.tensor([float(host_norm)], dtype=torch.float64).to(x.device, non_blocking=True)
+            else:
+                norm = codec.quant_norm_f64(x, self.p)
+            seed, ctr = self.philox.next()
+            compat_u = None
+            if self.rng_mode == "compat":
+                cnt = int(codec.count_consumers_f64(x, norm).item())
+                self._check_bracket(float(norm.item()), cnt)
+                compat_u = self._uniforms(cnt, x.device)
+            _, out, nnz = codec.quant_f64(x, kind, self.s, norm, seed, ctr, compat_u, want_nnz=(t in _STD))
+            if t in _STD:
+                pnorm = np.float64(norm.item())
+                self.vectorNormCompressor.compressVector(np.array([pnorm]))  # compressors.py:334-337
+                send = self.vectorNormCompressor.last_need_to_send_advance
+                nz = int(nnz.item())
+                if nz:
+                    per = (1.0 + np.ceil(math.log2(self.s))) / (64.0 if t == CompressorType.STANDARD_DITHERING_FP64 else 32.0)
+                    send = send + nz * per
                 self._finish(d, send)
             else:
                 den = 64.0 if t == CompressorType.NATURAL_DITHERING_FP64 else 32.0

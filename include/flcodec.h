@@ -295,6 +295,40 @@ int flc_randk_apply(const float* x, int64_t n, const int32_t* idx, int64_t k, fl
  * keys must be 16-B aligned. */
 int flc_randk_keys(int64_t n, uint64_t seed, uint64_t counter, float* keys, void* stream);
 
+/* ------------------------------------------------------------------ float64 inputs (f64.hip)
+ * The reference runs every compressor on whatever dtype x has (compressors.py:267-410): on a float64 vector
+ * ``np.zeros_like(x)``, ``x / P``, ``D / K * x[i]``, ``math.log2(abs(x[i]))``, ``np.linalg.norm(x, p)`` and the level
+ * arithmetic all stay float64.  These are the float64 forms of the entry points above (a fp64 vector in, a fp64
+ * vector out; buffers 16-B aligned).  Uniforms as for float32: compat_u = one double per consumer in index order
+ * (the reference's random.random() calls; count them with flc_count_consumers_f64), or Philox (compat_u == NULL).
+ *   flc_copy_f64 / flc_scale_div_f64 / flc_randk_apply_f64   IDENTICAL, LAZY (x / p), RANDK (scale * x[idx[j]])
+ *   flc_natural_f64        natural compression (compressors.py:302-318): codes (uint16 per element: 0 zero,
+ *                          0x7fff NaN, else sign << 15 | (e + 1075)) and / or the decoded vector; either may be NULL
+ *   flc_quant_norm_f64     p = inf: max |x|; p = 2: sqrt of an fp64 sum of squares (fixed order)
+ *   flc_quant_f64          standard / natural dithering (compressors.py:339-357, 376-393) with the given norm:
+ *                          8-bit codes (sign << 7 | level) and / or the decoded vector lv * sign * norm; nnz =
+ *                          count(x != 0) when non-NULL
+ *   flc_topk_dense_f64     out = x on the K largest (ties: the highest indices), +0 elsewhere (293-296), 0 < k < n
+ * Workspace: flc_f64_workspace_size(n) bytes (compat mode, the norm and top-k; not needed by the element-wise
+ * forms or by the Philox-mode encoders). */
+int flc_copy_f64(const double* x, int64_t n, double* out, void* stream);
+int flc_scale_div_f64(const double* x, int64_t n, double p, double* out, void* stream);
+int flc_randk_apply_f64(const double* x, int64_t n, const int32_t* idx, int64_t k, double scale, double* out,
+                        void* stream);
+size_t flc_f64_workspace_size(int64_t n);
+int flc_count_consumers_f64(const double* x, int64_t n, const double* norm, int64_t* count, void* ws, size_t ws_bytes,
+                            void* stream);
+int flc_natural_f64(const double* x, int64_t n, uint64_t seed, uint64_t counter, const double* compat_u,
+                    uint16_t* codes, double* out, void* ws, size_t ws_bytes, void* stream);
+int flc_natural_decode_f64(const uint16_t* codes, int64_t n, double* out, void* stream);
+int flc_quant_norm_f64(const double* x, int64_t n, int norm_p, double* norm, void* ws, size_t ws_bytes, void* stream);
+int flc_quant_f64(const double* x, int64_t n, int kind, int levels, const double* norm, uint64_t seed,
+                  uint64_t counter, const double* compat_u, uint8_t* codes, double* out, int64_t* nnz, void* ws,
+                  size_t ws_bytes, void* stream);
+int flc_quant_decode_f64(const uint8_t* codes, int64_t n, int kind, int levels, const double* norm, double* out,
+                         void* stream);
+int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------ client delta
  * FedOptClient.communicate (_fedopt.py:294-297): delta_t = clone(local_t) then add_(global_t, alpha=-1), i.e.
  * local_t - global_t per element, for each parameter tensor t; plus the flatten the codec's flat input needs.

@@ -103,7 +103,7 @@ def lazy(x: np.ndarray, P: float, testp: float):
 def randk(x: np.ndarray, K: int, D: int, S: np.ndarray):
     """compressors.py:284-292 with S = the first K entries of the shuffled arange(D)."""
     out = np.zeros_like(x)
-    out[S] = F32(D / K) * x[S]
+    out[S] = x.dtype.type(D / K) * x[S]  # a Python float times an element: x's dtype (fp32 rounds D / K first)
     return out, K
 
 
@@ -163,6 +163,8 @@ def topk_threshold(x: np.ndarray, K: int) -> float:
 def natural(x: np.ndarray, u_of: Callable[[np.ndarray], np.ndarray], fp64_stats: bool = False):
     """compressors.py:302-325.  ``u_of(nz_idx)`` returns the uniforms of the nonzero elements
     (compat: the next len(nz_idx) random.random() values; philox: u by element index)."""
+    if x.dtype == F64:
+        return natural64(x, u_of, fp64_stats)
     d = x.shape[0]
     out = np.zeros_like(x)
     nz = np.nonzero(x != 0.0)[0]
@@ -180,9 +182,57 @@ def natural(x: np.ndarray, u_of: Callable[[np.ndarray], np.ndarray], fp64_stats:
     return out, send, len(nz)
 
 
-def vector_norm(x: np.ndarray, p: float) -> np.float32:
-    """np.linalg.norm(x, p) as the reference calls it (compressors.py:332, 372)."""
-    return F32(np.linalg.norm(x, p))
+def natural64(x: np.ndarray, u_of: Callable[[np.ndarray], np.ndarray], fp64_stats: bool = False):
+    """compressors.py:302-325 on a float64 vector: every step in fp64, ``math.log2`` / ``math.floor`` /
+    ``math.ceil`` per element exactly as the reference evaluates them (a power of two gives down == up, pt = 0)."""
+    d = x.shape[0]
+    out = np.zeros_like(x)
+    nz = np.nonzero(x != 0.0)[0]
+    if len(nz):
+        ax = np.abs(x[nz])
+        alpha = [math.log2(a) for a in ax.tolist()]
+        down = np.array([math.floor(a) for a in alpha], dtype=np.int64)
+        up = np.array([math.ceil(a) for a in alpha], dtype=np.int64)
+        pt = (np.ldexp(1.0, up) - ax) / np.ldexp(1.0, down)
+        u = u_of(nz)
+        out[nz] = np.sign(x[nz]) * np.ldexp(1.0, np.where(u < pt, down, up))
+    send = 12.0 / 64.0 * d if fp64_stats else 9.0 / 32.0 * d
+    return out, send, len(nz)
+
+
+def vector_norm(x: np.ndarray, p: float):
+    """np.linalg.norm(x, p) as the reference calls it (compressors.py:332, 372), in x's dtype."""
+    return x.dtype.type(np.linalg.norm(x, p)) if x.dtype == F64 else F32(np.linalg.norm(x, p))
+
+
+def dither64(x: np.ndarray, levels: np.ndarray, pnorm: np.float64, u_of: Callable[[np.ndarray], np.ndarray]):
+    """compressors.py:339-357 / 376-394 on a float64 vector: y = |x| / norm, the level bracket, p and the decoded
+    value lv * sign * norm all in fp64.  A y above 1 (a p = 2 norm that underflowed to 0) has no bracket: the
+    reference's loop then indexes past the table, and so does this (IndexError)."""
+    out = np.zeros_like(x)
+    nz = np.nonzero(x != 0.0)[0]
+    lvl_idx = np.zeros(len(x), dtype=np.int64)
+    if len(nz) == 0:
+        return out, 0, nz, lvl_idx
+    xi = x[nz]
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        yi = np.abs(xi) / pnorm
+    cons = ~np.isnan(yi)
+    if np.any(yi[cons] > 1.0):
+        raise IndexError(f"index {len(levels)} is out of bounds for axis 0 with size {len(levels)}")
+    ci = nz[cons]
+    lvl = np.zeros(len(nz), dtype=F64)
+    if len(ci):
+        y = yi[cons]
+        j = np.searchsorted(levels, y, side="left")
+        s = np.maximum(j - 1, 0)
+        p = (y - levels[s + 1]) / (levels[s] - levels[s + 1])
+        li = np.where(u_of(ci) < p, s, s + 1)
+        lvl[cons] = levels[li]
+        lvl_idx[ci] = li
+    with np.errstate(invalid="ignore", over="ignore"):
+        out[nz] = (lvl * np.sign(xi)) * pnorm
+    return out, len(nz), ci, lvl_idx
 
 
 def dither(x: np.ndarray, levels: np.ndarray, pnorm: np.float32, u_of: Callable[[np.ndarray], np.ndarray]):
@@ -216,8 +266,12 @@ def dither(x: np.ndarray, levels: np.ndarray, pnorm: np.float32, u_of: Callable[
 
 def standard_dithering(x, s, p, u_of, pnorm=None, fp64_stats=False, norm_send=1):
     """compressors.py:327-365 (norm compressor = identical: it sends 1 component)."""
-    pn = vector_norm(x, p) if pnorm is None else F32(pnorm)
-    out, nnz, _, _ = dither(x, standard_levels(s), pn, u_of)
+    if x.dtype == F64:
+        pn = vector_norm(x, p) if pnorm is None else F64(pnorm)
+        out, nnz, _, _ = dither64(x, standard_levels(s), pn, u_of)
+    else:
+        pn = vector_norm(x, p) if pnorm is None else F32(pnorm)
+        out, nnz, _, _ = dither(x, standard_levels(s), pn, u_of)
     per = (1.0 + np.ceil(math.log2(s))) / (64.0 if fp64_stats else 32.0)
     send = norm_send
     for _ in range(nnz if nnz < 4096 else 0):
@@ -229,8 +283,12 @@ def standard_dithering(x, s, p, u_of, pnorm=None, fp64_stats=False, norm_send=1)
 
 def natural_dithering(x, s, p, u_of, pnorm=None, fp64_stats=False):
     """compressors.py:367-404."""
-    pn = vector_norm(x, p) if pnorm is None else F32(pnorm)
-    out, _, _, _ = dither(x, natural_levels(s), pn, u_of)
+    if x.dtype == F64:
+        pn = vector_norm(x, p) if pnorm is None else F64(pnorm)
+        out, _, _, _ = dither64(x, natural_levels(s), pn, u_of)
+    else:
+        pn = vector_norm(x, p) if pnorm is None else F32(pnorm)
+        out, _, _, _ = dither(x, natural_levels(s), pn, u_of)
     d = x.shape[0]
     send = d * (1.0 + np.ceil(math.log2(s))) / (64.0 if fp64_stats else 32.0)
     return out, send, pn

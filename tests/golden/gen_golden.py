@@ -22,7 +22,11 @@ Extra fixtures (``codec_extra.npz``, ``dropin_surface.json``): the adaptive rand
 its error cases; the drop-in surface (name, fullName, w, is_biased, level tables, the assertion of unconstructible
 level counts) of every factory.
 
-Usage:  python tests/golden/gen_golden.py [all|codec|extra|agg|variants]
+Float64 fixtures (``codec_f64.npz``, round 3): every compressor type on float64 vectors, which the reference keeps
+float64 throughout (identical, lazy, rand-k, top-k, natural, standard / natural dithering at p = inf and 2), plus
+special float64 vectors (subnormals, powers of two across the exponent range, wide magnitudes, ties, NaN for top-k).
+
+Usage:  python tests/golden/gen_golden.py [all|codec|extra|f64|agg|variants]
 """
 
 from __future__ import annotations
@@ -197,6 +201,110 @@ def gen_sparse(ref):
                 store[key + "|" + k] = np.array(v)
     np.savez_compressed(OUT / "codec_sparse.npz", **store)
     print("codec_sparse.npz:", len(store), "arrays")
+
+
+# ------------------------------------------------------------------------- float64 inputs (round 3)
+def make_input64(D: int, seed: int, zero_frac: float = 0.05, scale: float = 1e-3) -> np.ndarray:
+    """The float64 counterpart of make_input (the reference keeps float64 vectors float64 throughout)."""
+    g = np.random.default_rng(30_000 + seed * 7919 + D)
+    x = g.standard_normal(D) * scale
+    if D > 1:
+        x[g.random(D) < zero_frac] = 0.0
+    return x
+
+
+def special_inputs64() -> Dict[str, np.ndarray]:
+    f = np.float64
+    return {
+        "ties": np.array([1, 3, 3, 3, 2, 3, 0, -1, 3, 2], dtype=f),
+        "signed": np.array([-3.5, 1.5, 0.25, -0.0, 0.0, 2.0, -7.0, 1.5], dtype=f),
+        "zeros_pm": np.array([0.0, -0.0, 0.0, 1e-300, -0.0, -1e-300, 0.0], dtype=f),
+        "powers2": np.array([1.0, -2.0, 0.5, 2.0**100, -(2.0**-1000), 2.0**-1074, 2.0**1000, 3.0], dtype=f),
+        "subnormal": np.array([5e-324, -1e-310, 2.2e-308, -(2.0**-1022), 1e-320, 0.1], dtype=f),
+        "wide": np.array([1e300, -1e-300, 3.0e200, -7.5e-150, 1e-10, 123456.789, -1e100, 0.0], dtype=f),
+    }
+
+
+def gen_f64(ref):
+    """codec_f64.npz: every compressor type on float64 vectors (compressors.py:267-410 keeps them float64)."""
+    def std(L, p, fp64=True):
+        def mk(c):
+            nc = ref.Compressor("norm")
+            nc.makeIdenticalCompressor()
+            (c.makeStandardDitheringFP64 if fp64 else c.makeStandardDitheringFP32)(L, nc, p)
+
+        return mk
+
+    dense = {
+        "identical": lambda c: c.makeIdenticalCompressor(),
+        "lazy_p03": lambda c: c.makeLazyCompressor(0.3),
+        "lazy_p09": lambda c: c.makeLazyCompressor(0.9),
+        "natural32": lambda c: c.makeNaturalCompressorFP32(),
+        "natural64": lambda c: c.makeNaturalCompressorFP64(),
+        "natdither64_s3_p2": lambda c: c.makeNaturalDitheringFP64(3, 100, 2),
+        "natdither64_s8_inf": lambda c: c.makeNaturalDitheringFP64(8, 100, np.inf),
+        "natdither32_s8_inf": lambda c: c.makeNaturalDitheringFP32(8, 100, np.inf),
+        "stddither64_s4_inf": std(4, np.inf),
+        "stddither64_s8_p2": std(8, 2),
+        "stddither32_s8_inf": std(8, np.inf, fp64=False),
+    }
+    for L in (1, 3, 7, 10):
+        for p, pn in ((np.inf, "inf"), (2, "p2")):
+            dense[f"std64_L{L}_{pn}"] = std(L, p)
+    store: Dict[str, Any] = {}
+    big = 65537
+    for name, mk in dense.items():
+        sizes = (1, 7, 4096, big) if not name.startswith("std64_L") else (7, 4096)
+        for D in sizes:
+            for seed in (0, 1):
+                if D == big and seed != 0:
+                    continue
+                x = make_input64(D, seed)
+                out, rec = run_codec(ref, mk, x, seed)
+                key = f"{name}|{D}|{seed}"
+                store[key + "|sha_x"] = np.array(sha(x))
+                if D <= 4096:
+                    store[key + "|x"] = x
+                    store[key + "|out"] = out
+                store[key + "|sha_out"] = np.array(sha(out))
+                for k, v in rec.items():
+                    store[key + "|" + k] = np.array(v)
+    for sname, x in special_inputs64().items():
+        for name in ("identical", "natural64", "stddither64_s8_p2", "natdither64_s8_inf", "natdither64_s3_p2"):
+            key = f"{name}|special:{sname}|3"
+            store[key + "|x"] = x
+            try:  # a p = 2 norm that underflows to 0 under nonzero elements: the level loop raises IndexError
+                out, rec = run_codec(ref, dense[name], x, 3)
+            except IndexError as e:
+                store[key + "|error"] = np.array(f"IndexError: {e}")
+                continue
+            store[key + "|out"] = out
+            for k, v in rec.items():
+                store[key + "|" + k] = np.array(v)
+    for D, K in ((7, 3), (4096, 41), (4096, 1), (big, 655)):
+        for seed in (0, 1):
+            x = make_input64(D, seed)
+            for name, mk in (("topk", lambda c: c.makeTopKCompressor(K, D)),
+                             ("randk", lambda c: c.makeRandKCompressor(K, D))):
+                out, rec = run_codec(ref, mk, x, seed)
+                key = f"{name}|{D}|{K}|{seed}"
+                store[key + "|sha_x"] = np.array(sha(x))
+                if D <= 4096:
+                    store[key + "|x"] = x
+                    store[key + "|out"] = out
+                store[key + "|sha_out"] = np.array(sha(out))
+                for k, v in rec.items():
+                    store[key + "|" + k] = np.array(v)
+    for sname, x in {**special_inputs64(), "nan": np.array([0.5, np.nan, -1.0, 2.0, np.nan, 0.0, -0.0, 1.0])}.items():
+        for K in (1, 3, len(x) - 1):
+            out, rec = run_codec(ref, lambda c: c.makeTopKCompressor(K, len(x)), x, 5)
+            key = f"topk|special:{sname}|{K}|5"
+            store[key + "|x"] = x
+            store[key + "|out"] = out
+            for k, v in rec.items():
+                store[key + "|" + k] = np.array(v)
+    np.savez_compressed(OUT / "codec_f64.npz", **store)
+    print("codec_f64.npz:", len(store), "arrays")
 
 
 # ------------------------------------------------------------------------- extra codec fixtures (round 2)
@@ -594,6 +702,8 @@ def main():
         ref = load_reference_compressors()
         gen_extra(ref)
         gen_surface(ref)
+    if only in ("all", "f64"):
+        gen_f64(load_reference_compressors())
     if only in ("all", "agg"):
         gen_aggregation()
     if only in ("all", "variants"):

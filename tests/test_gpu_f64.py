@@ -1,0 +1,192 @@
+"""GPU parity of the float64 codec (f64.hip) against the reference's float64 fixtures and the oracle.
+
+The reference runs every compressor on whatever dtype x has (compressors.py:267-410); on a float64 vector every
+step stays float64.  Checked here:
+* compat RNG: the drop-in ``Compressor`` on float64 numpy inputs reproduces the reference's own outputs
+  (tests/golden/codec_f64.npz) bit for bit, its send statistics, the streams' positions afterwards, and its
+  IndexError when a p = 2 norm underflows to 0 under nonzero elements;
+* philox RNG: natural compression and both ditherings match the oracle fed the same Philox uniforms and the same
+  norm, bit for bit, up to 4 M elements; the device norms (p = inf exact, p = 2 within 4 ulp of the exact one);
+* top-k: the dense output equals the oracle's stable-argsort result (highest indices kept among ties) up to 4 M
+  elements, with ties, zeros, NaN and signed zeros; float64 device tensors in, float64 device tensors out.
+"""
+
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import compressors_ref as ref
+from tests import golden_cases as gc
+from tests import golden_f64 as g64
+
+pytestmark = pytest.mark.gpu
+
+F64 = g64.load()
+DENSE = {k: v for k, v in F64.items() if k.split("|")[0] not in ("topk", "randk")}
+SPARSE = {k: v for k, v in F64.items() if k.split("|")[0] in ("topk", "randk")}
+DEV = "cuda"
+
+
+def make_compressor(name, rng="compat", seed=0):
+    from fl_sim_amd import Compressor
+
+    c = Compressor(rng=rng, seed=seed)
+    if name == "identical":
+        c.makeIdenticalCompressor()
+    elif name.startswith("lazy"):
+        c.makeLazyCompressor(0.3 if name == "lazy_p03" else 0.9)
+    elif name == "natural32":
+        c.makeNaturalCompressorFP32()
+    elif name == "natural64":
+        c.makeNaturalCompressorFP64()
+    else:
+        kind, L, p, fp64 = g64.dense_params(name)
+        if kind == "std":
+            nc = Compressor("norm")
+            nc.makeIdenticalCompressor()
+            (c.makeStandardDitheringFP64 if fp64 else c.makeStandardDitheringFP32)(L, nc, p)
+        else:
+            (c.makeNaturalDitheringFP64 if fp64 else c.makeNaturalDitheringFP32)(L, 100, p)
+    return c
+
+
+@pytest.mark.parametrize("case", sorted(DENSE))
+def test_f64_dense_compressor_matches_reference_fixture(case):
+    rec = DENSE[case]
+    name, _, seed = case.split("|")
+    x = g64.case_input(case, rec)
+    c = make_compressor(name)
+    gc.seed_all(int(seed))
+    if "error" in rec:
+        with pytest.raises(IndexError) as ei:
+            c.compressVector(x)
+        assert str(rec["error"]).endswith(str(ei.value))
+        return
+    out = c.compressVector(x)
+    assert isinstance(out, np.ndarray) and out.dtype == np.float64 and out.shape == x.shape
+    assert random.random() == float(rec["next_random"])
+    assert np.random.random_sample() == float(rec["next_np"])
+    assert float(c.last_need_to_send_advance) == float(rec["send"])
+    assert g64.check_output(rec, out), case
+
+
+@pytest.mark.parametrize("case", sorted(SPARSE))
+def test_f64_sparse_compressor_matches_reference_fixture(case):
+    from fl_sim_amd import Compressor
+
+    rec = SPARSE[case]
+    parts = case.split("|")
+    name, K, seed = parts[0], int(parts[2]), int(parts[-1])
+    x = g64.case_input(case, rec)
+    c = Compressor()
+    (c.makeTopKCompressor if name == "topk" else c.makeRandKCompressor)(K, len(x))
+    gc.seed_all(seed)
+    out = c.compressVector(x)
+    assert out.dtype == np.float64
+    assert random.random() == float(rec["next_random"])
+    assert np.random.random_sample() == float(rec["next_np"])
+    assert float(c.last_need_to_send_advance) == float(rec["send"])
+    if name == "topk":
+        assert g64.topk_valid(x, out, K), case
+        exp, _ = ref.topk(x, K)  # the device's tie rule (stable argsort: the highest indices kept)
+        assert g64.same_bits(out, exp), case
+    else:
+        assert g64.check_output(rec, out), case
+
+
+def _x64(D, seed, zero_frac=0.05, scale=1e-3):
+    g = np.random.default_rng(seed)
+    x = g.standard_normal(D) * scale
+    x[g.random(D) < zero_frac] = 0.0
+    return x
+
+
+@pytest.mark.parametrize("D", [7, 8191, 65537, 4_000_000])
+def test_f64_natural_philox_matches_oracle(D):
+    from fl_sim_amd import codec
+
+    x = _x64(D, D)
+    x[: min(D, 6)] = [2.0**-1074, -(2.0**600), 1e-310, 3.0, -0.0, 0.0][: min(D, 6)]
+    xd = torch.from_numpy(x).to(DEV)
+    codes, out = codec.natural_f64(xd, seed=11, counter=5, want_codes=True)
+    exp, _, _ = ref.natural64(x, ref.philox_stream(11, 5, D))
+    assert g64.same_bits(out.cpu().numpy(), exp)
+    assert g64.same_bits(codec.natural_decode_f64(codes, D).cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("D", [5, 8192, 100_003, 4_000_000])
+@pytest.mark.parametrize("kind,L,p", [("std", 8, np.inf), ("std", 3, 2), ("nat", 8, 2), ("nat", 4, np.inf),
+                                      ("std", 127, np.inf)])
+def test_f64_dithering_philox_matches_oracle(D, kind, L, p):
+    from fl_sim_amd import codec
+    from fl_sim_amd._lib import FLC_Q_NATURAL_DITHER, FLC_Q_STANDARD_DITHER
+
+    x = _x64(D, D + L)
+    xd = torch.from_numpy(x).to(DEV)
+    norm = codec.quant_norm_f64(xd, p)
+    pn = np.float64(norm.item())
+    if np.isinf(p):
+        assert pn == np.max(np.abs(x))  # exact
+    else:
+        exact = np.sqrt(np.sum(x.astype(np.longdouble) ** 2))
+        assert abs(pn - float(exact)) <= 4 * np.spacing(pn)
+    k = FLC_Q_STANDARD_DITHER if kind == "std" else FLC_Q_NATURAL_DITHER
+    codes, out, nnz = codec.quant_f64(xd, k, L, norm, seed=3, counter=9, want_codes=True, want_nnz=True)
+    levels = ref.standard_levels(L) if kind == "std" else ref.natural_levels(L)
+    exp, nz, _, _ = ref.dither64(x, levels, pn, ref.philox_stream(3, 9, D))
+    assert g64.same_bits(out.cpu().numpy(), exp)
+    assert int(nnz.item()) == nz
+    dec = codec.quant_decode_f64(codes, D, k, L, norm).cpu().numpy()
+    assert g64.same_bits(dec, exp)
+
+
+@pytest.mark.parametrize("D,K", [(10, 3), (4096, 41), (100_003, 1000), (4_000_000, 40_000), (1_000_000, 999_999)])
+def test_f64_topk_matches_oracle(D, K):
+    from fl_sim_amd import codec
+
+    x = _x64(D, 7 * D + K)
+    exp, _ = ref.topk(x, K)
+    got = codec.topk_dense_f64(torch.from_numpy(x).to(DEV), K).cpu().numpy()
+    assert g64.same_bits(got, exp)
+
+
+def test_f64_topk_ties_zeros_nan():
+    from fl_sim_amd import codec
+
+    g = np.random.default_rng(5)
+    D = 300_001
+    x = np.where(g.random(D) < 0.6, 0.0, g.integers(-3, 4, D).astype(np.float64))
+    x[g.random(D) < 0.01] = np.nan
+    x[g.random(D) < 0.05] = -0.0
+    xd = torch.from_numpy(x).to(DEV)
+    for K in (1, 2000, 4000, 60_000, 150_000, D - 1):  # tie classes NaN, 3, 2, 1, 0 (with -0)
+        exp, _ = ref.topk(x, K)
+        got = codec.topk_dense_f64(xd, K).cpu().numpy()
+        assert g64.same_bits(got, exp), K
+
+
+def test_f64_device_tensor_in_device_tensor_out():
+    from fl_sim_amd import Compressor
+
+    x = torch.from_numpy(_x64(50_000, 1)).to(DEV)
+    for make in (lambda c: c.makeNaturalCompressorFP64(), lambda c: c.makeTopKCompressor(500, 50_000),
+                 lambda c: c.makeNaturalDitheringFP64(4, 50_000, np.inf), lambda c: c.makeIdenticalCompressor()):
+        c = Compressor(rng="philox", seed=4)
+        make(c)
+        out = c.compressVector(x)
+        assert out.device.type == "cuda" and out.dtype == torch.float64 and out.shape == x.shape
+
+
+def test_f64_lazy_and_randk_are_fp64_arithmetic():
+    from fl_sim_amd import codec
+
+    x = _x64(10_001, 3, zero_frac=0.0)
+    xd = torch.from_numpy(x).to(DEV)
+    assert g64.same_bits(codec.scale_div_f64(xd, 0.3).cpu().numpy(), x / 0.3)
+    idx = np.random.default_rng(1).permutation(len(x))[:777]
+    got = codec.randk_apply_f64(xd, torch.from_numpy(idx.astype(np.int32)), len(x) / 777).cpu().numpy()
+    exp, _ = ref.randk(x, 777, len(x), idx)
+    assert g64.same_bits(got, exp)
+    assert g64.same_bits(codec.copy_f64(xd).cpu().numpy(), x)
