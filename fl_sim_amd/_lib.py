@@ -128,6 +128,10 @@ SIGNATURES = {
     "flc_adaptive_workspace_size": (c_size_t, [c_int64]),
     "flc_adaptive_prepare": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_adaptive_select": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "flc_adaptive_prepare_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "flc_adaptive_select_f64": (
+        c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    ),
     "flc_copy": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_scale_div": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "flc_randk_keys": (c_int, [c_int64, c_uint64, c_uint64, c_void_p, c_void_p]),

@@ -635,14 +635,17 @@ ADAPTIVE_ERRORS = {1: "probabilities contain NaN", 2: "probabilities do not sum 
 def adaptive_prepare(x: torch.Tensor) -> torch.Tensor:
     """First half of the adaptive random compressor (compressors.py:297-301): S = sum|x| in numpy's order,
     p = |x| / S, and the speculated runs of the fp64 cumsum.  Returns numpy's check as a device int32:
-    0 = ok, 1 = NaN in p, 2 = p does not sum to 1 (see ADAPTIVE_ERRORS).  No uniform is consumed."""
-    x = _dev_f32(x).reshape(-1)
+    0 = ok, 1 = NaN in p, 2 = p does not sum to 1 (see ADAPTIVE_ERRORS).  No uniform is consumed.  A float64 x
+    runs the float64 form (S and p in fp64, flc_adaptive_prepare_f64)."""
+    f64 = isinstance(x, torch.Tensor) and x.dtype == torch.float64
+    x = (_dev_f64(x) if f64 else _dev_f32(x)).reshape(-1)
     n = x.numel()
     if n == 0:
         raise ValueError("'a' cannot be empty unless no samples are taken")
     status = torch.empty(1, dtype=torch.int32, device=x.device)
     ws = workspace(x.device, _lib.size("flc_adaptive_workspace_size", n), "adaptive")
-    call("flc_adaptive_prepare", _p(x), n, _p(status), _p(ws), ws.numel(), _stream(x.device))
+    call("flc_adaptive_prepare_f64" if f64 else "flc_adaptive_prepare", _p(x), n, _p(status), _p(ws), ws.numel(),
+         _stream(x.device))
     return status
 
 
@@ -651,13 +654,15 @@ def adaptive_select(x: torch.Tensor, u: float, out: Optional[torch.Tensor] = Non
     """Second half, after :func:`adaptive_prepare` on the same stream: the exact sequential cdf,
     ``searchsorted(u, side='right')`` and the dense output (zeros, out[ind] = x[ind]).
     Returns (out, index as a device int64)."""
-    x = _dev_f32(x).reshape(-1)
+    f64 = isinstance(x, torch.Tensor) and x.dtype == torch.float64
+    x = (_dev_f64(x) if f64 else _dev_f32(x)).reshape(-1)
     n = x.numel()
     if out is None:
-        out = torch.empty(n, dtype=torch.float32, device=x.device)
+        out = torch.empty(n, dtype=x.dtype, device=x.device)
     index = torch.empty(1, dtype=torch.int64, device=x.device)
     ws = workspace(x.device, _lib.size("flc_adaptive_workspace_size", n), "adaptive")
-    call("flc_adaptive_select", _p(x), n, float(u), _p(index), _p(out), _p(ws), ws.numel(), _stream(x.device))
+    call("flc_adaptive_select_f64" if f64 else "flc_adaptive_select", _p(x), n, float(u), _p(index), _p(out), _p(ws),
+         ws.numel(), _stream(x.device))
     return out, index
 
 

@@ -385,16 +385,7 @@ class Compressor:
             self._finish(d, self.K)
             return out
         if t == CompressorType.ADAPTIVE_RANDOM_COMPRESSOR:
-            # np.random.choice(np.arange(self.D), size=1, p=|x| / sum|x|)  (compressors.py:297-301)
-            if self.D != d:
-                raise ValueError("'a' and 'p' must have same size")
-            status = int(codec.adaptive_prepare(x).item())  # numpy checks p before drawing
-            if status:
-                raise ValueError(codec.ADAPTIVE_ERRORS.get(status, "invalid probabilities"))
-            u = _rng.numpy_random_sample() if self.rng_mode == "compat" else self._philox_scalar(x.device)
-            out, _ = codec.adaptive_select(x, u)
-            self._finish(d, 1)
-            return out
+            return self._adaptive(x, d)
         if t in _NATURAL:
             seed, ctr = self.philox.next()
             compat_u = None
@@ -477,7 +468,7 @@ class Compressor:
             self._finish(d, self.K)
             return out
         if t == CompressorType.ADAPTIVE_RANDOM_COMPRESSOR:
-            raise NotImplementedError("the adaptive random compressor takes float32 vectors on the device path")
+            return self._adaptive(x, d)
         if t in _NATURAL:
             seed, ctr = self.philox.next()
             compat_u = None
@@ -515,6 +506,18 @@ class Compressor:
                 self._finish(d, d * (1.0 + np.ceil(math.log2(self.s))) / den)
             return out
         raise ValueError(f"unknown compressor type {t}")
+
+    def _adaptive(self, x: torch.Tensor, d: int) -> torch.Tensor:
+        # np.random.choice(np.arange(self.D), size=1, p=|x| / sum|x|)  (compressors.py:297-301), in x's dtype
+        if self.D != d:
+            raise ValueError("'a' and 'p' must have same size")
+        status = int(codec.adaptive_prepare(x).item())  # numpy checks p before drawing
+        if status:
+            raise ValueError(codec.ADAPTIVE_ERRORS.get(status, "invalid probabilities"))
+        u = _rng.numpy_random_sample() if self.rng_mode == "compat" else self._philox_scalar(x.device)
+        out, _ = codec.adaptive_select(x, u)
+        self._finish(d, 1)
+        return out
 
     def _philox_scalar(self, device) -> float:
         # one uniform for the Lazy compressor in philox mode (host-side draw from the same key)

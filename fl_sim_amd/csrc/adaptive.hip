@@ -13,6 +13,10 @@
 //   cdf = p.cumsum()            fp64, strictly sequential: c_i = fl(c_{i-1} + p_i);
 //   cdf /= cdf[-1];  u = random_sample();  ind = cdf.searchsorted(u, side='right').
 //
+// On a float64 x (the reference keeps it float64) the same holds with S an fp64 sum of the same buffers and trees and
+// p = |x| / S an fp64 division; numpy's tolerance is then atol = sqrt(eps64) (the *_f64 entry points; every kernel
+// below is a template over the element type).
+//
 // Every rounding above is reproduced.  The one sequential dependency, the fp64 running sum, is made parallel
 // without giving up exactness.  Inside one binade [2^E, 2^(E+1)) fp64 values are the multiples m * U of
 // U = 2^(E-52), and round-to-nearest-even commutes with a shift by an EVEN multiple of U.  Each chunk of kChunk
@@ -56,7 +60,36 @@ constexpr int kRecLegacy = 1024;           // chunk records staged in LDS per st
 
 // status word (device int32) written by ar_check
 constexpr int kStNan = 1, kStSum = 2;
-constexpr double kAtol = 3.4526698300124393e-04;  // sqrt(finfo(float32).eps)
+constexpr double kAtol = 3.4526698300124393e-04;    // sqrt(finfo(float32).eps)
+constexpr double kAtol64 = 1.4901161193847656e-08;  // sqrt(finfo(float64).eps)
+
+// element type helpers: p_i = |x_i| / S in x's type (fp32: then cast to fp64), 16-B vectors of x
+__device__ __forceinline__ double q_of(float v, float S) { return (double)(fabsf(v) / S); }
+__device__ __forceinline__ double q_of(double v, double S) { return fabs(v) / S; }
+__device__ __forceinline__ float abs_of(float v) { return fabsf(v); }
+__device__ __forceinline__ double abs_of(double v) { return fabs(v); }
+template <class T>
+struct Vec16 {  // the elements of one 16-B load
+  static constexpr int N = 16 / (int)sizeof(T);
+  T e[N];
+};
+template <class T>
+__device__ __forceinline__ Vec16<T> load16(const T* __restrict__ x, int64_t e, int64_t n) {
+  Vec16<T> v;
+  if (e + Vec16<T>::N <= n) {
+    if constexpr (sizeof(T) == 4) {
+      const float4 q = *reinterpret_cast<const float4*>(x + e);
+      v.e[0] = q.x; v.e[1] = q.y; v.e[2] = q.z; v.e[3] = q.w;
+    } else {
+      const double2 q = *reinterpret_cast<const double2*>(x + e);
+      v.e[0] = q.x; v.e[1] = q.y;
+    }
+  } else {  // past n: zeros, which leave a running sum unchanged
+#pragma unroll
+    for (int i = 0; i < Vec16<T>::N; ++i) v.e[i] = e + i < n ? x[e + i] : (T)0;
+  }
+  return v;
+}
 
 // A piece: chunks [first, last] of one scan block.  e >= 1: chunks of binade e whose maps compose to (inc0, inc1);
 // e < 0: one chunk re-run from its exact start (inc0 / inc1 then hold its guess and the end of the run from it).
@@ -66,7 +99,7 @@ struct Rec {
 };
 
 struct ArWs {
-  float* buf_sum;    // [nbuf] pairwise sum of |x| per reduction buffer
+  double* buf_sum;   // [nbuf] pairwise sum of |x| per reduction buffer (in x's type, stored exactly)
   double* bpre;      // [nbuf] fp64 prefix of buf_sum (guesses only)
   double* q_abs;     // [nbuf * kQ] approximate sum of |x| per chunk (guesses only)
   double* guess;     // [nq] speculated start of each chunk's running sum
@@ -83,7 +116,7 @@ struct ArWs {
   double* rec_end;   // [nblk * kRecMax] exact end of each piece
   double* start;     // [nq + 1] exact running sum before each chunk; start[nq] = cdf[-1]
   double* p_part;    // [ceil(nq / 256)] partial fp64 sums of p (the "sum to 1" check)
-  float* total;      // [1] S
+  double* total;     // [1] S (in x's type, stored exactly)
   int32_t* status;   // [1]
   int32_t* fail;     // [1] 1: the speculation did not verify, the sequential chain ran
   long long* lo;     // [1] chunk holding searchsorted(u)
@@ -102,13 +135,14 @@ __device__ __forceinline__ double from_grid(long long m, int e) { return ldexp((
 __device__ __forceinline__ bool in_binade(long long m) { return m >= (1ll << 52) && m < (1ll << 53); }
 
 // ---- numpy's pairwise_sum on fp32 (loops_utils.h.src) ------------------------------------------------
-__device__ float pw_leaf(const float* a, int n) {
+template <class T>
+__device__ T pw_leaf(const T* a, int n) {
   if (n < 8) {
-    float r = 0.0f;
+    T r = 0;
     for (int i = 0; i < n; ++i) r += a[i];
     return r;
   }
-  float r[8];
+  T r[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = a[j];
   int i = 8;
@@ -116,7 +150,7 @@ __device__ float pw_leaf(const float* a, int n) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] += a[i + j];
   }
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
   for (; i < n; ++i) res += a[i];
   return res;
 }
@@ -146,27 +180,26 @@ int tail_prog_build(TailProg& p, int s0, int m) {  // (host) returns the value c
 }
 
 // ---- K1: full reduction buffers (n2 splits of 8192 are a perfect tree of 64 leaves of 128) ----------
-__global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const float* __restrict__ x, int64_t n_full_bufs,
-                                                            ArWs ws) {
-  __shared__ float sh[kPad];
+template <class T>
+__global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const T* __restrict__ x, int64_t n_full_bufs, ArWs ws) {
+  constexpr int VN = Vec16<T>::N;
+  __shared__ T sh[kPad];
   const int64_t b = blockIdx.x;
   if (b >= n_full_bufs) return;
-  const float* src = x + b * kBuf;
-  // 256 threads x 8 float4: coalesced, |x| written with one pad word per 128-element leaf
-  for (int v = threadIdx.x; v < kBuf / 4; v += 256) {
-    const float4 q = *reinterpret_cast<const float4*>(src + 4 * v);
-    const int i = 4 * v;
+  const T* src = x + b * kBuf;
+  // 256 threads x 16-B loads: coalesced, |x| written with one pad word per 128-element leaf
+  for (int v = threadIdx.x; v < kBuf / VN; v += 256) {
+    const Vec16<T> q = load16(src, (int64_t)VN * v, (int64_t)kBuf);
+    const int i = VN * v;
     const int o = i + (i >> 7);
-    sh[o] = fabsf(q.x);
-    sh[o + 1] = fabsf(q.y);
-    sh[o + 2] = fabsf(q.z);
-    sh[o + 3] = fabsf(q.w);
+#pragma unroll
+    for (int c = 0; c < VN; ++c) sh[o + c] = abs_of(q.e[c]);
   }
   __syncthreads();
   if (threadIdx.x >= kWave) return;
   const int l = threadIdx.x;
-  const float* a = sh + l * (kLeaf + 1);  // lane l's leaf: banks l + c, conflict-free
-  float r[8];
+  const T* a = sh + l * (kLeaf + 1);  // lane l's leaf: banks l + c, conflict-free
+  T r[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = a[j];
 #pragma unroll
@@ -174,27 +207,28 @@ __global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const float* __restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] += a[i + j];
   }
-  float s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  // the tree above the leaves is balanced: a butterfly over the lanes (fp32 + is commutative)
+  T s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  // the tree above the leaves is balanced: a butterfly over the lanes (+ is commutative)
 #pragma unroll
   for (int m = 1; m < kWave; m <<= 1) {
     s += __shfl_xor(s, m);
     if (m == kChunk / kLeaf / 2 && (l & (kChunk / kLeaf - 1)) == 0)
       ws.q_abs[b * kQ + l / (kChunk / kLeaf)] = (double)s;  // a two-leaf subtree = one cdf chunk
   }
-  if (l == 0) ws.buf_sum[b] = s;
+  if (l == 0) ws.buf_sum[b] = (double)s;
 }
 
 // ---- K1b: the last, partial buffer (an irregular tree): leaves in parallel, the tree's <= 127 additions on one
 // thread from the host-built program --------------------------------------------------------------------------------
-__global__ __launch_bounds__(128) void ar_tail_sum_kernel(const float* __restrict__ x, int64_t n, TailProg prog,
+template <class T>
+__global__ __launch_bounds__(128) void ar_tail_sum_kernel(const T* __restrict__ x, int64_t n, TailProg prog,
                                                           ArWs ws) {
-  __shared__ float sh[kBuf];
-  __shared__ float lf_sum[128], op_sum[128];
+  __shared__ T sh[kBuf];
+  __shared__ T lf_sum[128], op_sum[128];
   const int tid = threadIdx.x;
   const int64_t b = n / kBuf;
   const int len = (int)(n - b * kBuf);
-  for (int i = tid; i < len; i += 128) sh[i] = fabsf(x[b * kBuf + i]);
+  for (int i = tid; i < len; i += 128) sh[i] = abs_of(x[b * kBuf + i]);
   __syncthreads();
   if (tid < prog.nleaf) lf_sum[tid] = pw_leaf(sh + prog.lf_start[tid], prog.lf_len[tid]);
   // guesses: an fp64 sum of |x| per chunk of the partial buffer (any order)
@@ -210,19 +244,20 @@ __global__ __launch_bounds__(128) void ar_tail_sum_kernel(const float* __restric
       const int a = prog.op_a[o], c = prog.op_b[o];
       op_sum[o] = (a < 128 ? lf_sum[a] : op_sum[a - 128]) + (c < 128 ? lf_sum[c] : op_sum[c - 128]);
     }
-    ws.buf_sum[b] = prog.nop ? op_sum[prog.nop - 1] : lf_sum[0];
+    ws.buf_sum[b] = (double)(prog.nop ? op_sum[prog.nop - 1] : lf_sum[0]);
   }
 }
 
 // ---- K2: S (buffers folded in order, fp32) and the fp64 prefix of the buffer sums (guesses) --------------
+template <class T>
 __global__ __launch_bounds__(1024) void ar_total_kernel(int64_t nbuf, ArWs ws) {
-  __shared__ __attribute__((aligned(16))) float tile[1024];
+  __shared__ __attribute__((aligned(16))) T tile[1024];
   __shared__ double scan_lds[1024 / kWave];
-  float S = 0.0f;
+  T S = 0;
   double carry = 0.0;
   for (int64_t base = 0; base < nbuf; base += 1024) {
     const int64_t i = base + threadIdx.x;
-    const float v = i < nbuf ? ws.buf_sum[i] : 0.0f;
+    const T v = i < nbuf ? (T)ws.buf_sum[i] : (T)0;
     tile[threadIdx.x] = v;
     double tot;
     const double ex = block_excl_scan<double, 1024 / kWave>((double)v, scan_lds, &tot);  // (syncs: tile ready)
@@ -230,37 +265,26 @@ __global__ __launch_bounds__(1024) void ar_total_kernel(int64_t nbuf, ArWs ws) {
     carry += tot;
     if (threadIdx.x == 0) {
       const int cnt = (int)std::min<int64_t>(1024, nbuf - base);
-      int j = 0;
-      for (; j + 8 <= cnt; j += 8) {
-        const float4 a = *reinterpret_cast<const float4*>(tile + j);
-        const float4 c = *reinterpret_cast<const float4*>(tile + j + 4);
-        S = S + a.x;
-        S = S + a.y;
-        S = S + a.z;
-        S = S + a.w;
-        S = S + c.x;
-        S = S + c.y;
-        S = S + c.z;
-        S = S + c.w;
-      }
-      for (; j < cnt; ++j) S = S + tile[j];
+      for (int j = 0; j < cnt; ++j) S = S + tile[j];
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) ws.total[0] = S;
+  if (threadIdx.x == 0) ws.total[0] = (double)S;
 }
 
 // ---- K3 (phase A): per chunk, the two speculative runs, the chunk's map and its sum of p ------------------
 // A wave owns 64 consecutive chunks and stages them through LDS in four rounds of 64 elements each (16-B loads,
 // 16 lanes per 256 B row piece); lane c then runs chunk c from its row (stride 65 words: conflict-free).
-constexpr int kStageRow = 65;
-__global__ __launch_bounds__(256) void ar_phase_a_kernel(const float* __restrict__ x, int64_t n, int64_t nq, ArWs ws) {
-  __shared__ float stage[4][kWave * kStageRow];
+// (float64: rounds of 32 elements per row, so a lane's loads stay sixteen 16-B vectors)
+template <class T>
+__global__ __launch_bounds__(256) void ar_phase_a_kernel(const T* __restrict__ x, int64_t n, int64_t nq, ArWs ws) {
+  constexpr int VN = Vec16<T>::N, kRowE = 16 * VN, kRow = kRowE + 1;
+  __shared__ T stage[4][kWave * kRow];
   __shared__ double red[4];
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x >> 6;
   const int64_t j0 = (int64_t)blockIdx.x * 256 + wid * kWave;  // the wave's first chunk (a multiple of 2 kQ)
   const int64_t j = j0 + lane;
-  const float S = ws.total[0];
+  const T S = (T)ws.total[0];
   const double inv = 1.0 / (double)S;
   // guess = the buffer's fp64 prefix + the exclusive prefix of the chunk sums inside the buffer (32 lanes each)
   const double qa = j < nq ? ws.q_abs[j] : 0.0;
@@ -270,35 +294,28 @@ __global__ __launch_bounds__(256) void ar_phase_a_kernel(const float* __restrict
   const int E = binade(ga);
   const double gb = ga + spacing(E);
   double ca = ga, cb = gb, ps = 0.0;
-  float* st = stage[wid];
-  for (int r = 0; r < kChunk / 64; ++r) {
-    float4 v[16];
+  T* st = stage[wid];
+  for (int r = 0; r < kChunk / kRowE; ++r) {
+    Vec16<T> v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int f = i * kWave + lane, row = f >> 4, c4 = f & 15;
-      const int64_t e = (j0 + row) * kChunk + r * 64 + c4 * 4;
-      if (e + 4 <= n) {
-        v[i] = *reinterpret_cast<const float4*>(x + e);
-      } else {  // past n: zeros, which leave a running sum unchanged
-        v[i] = make_float4(e < n ? x[e] : 0.f, e + 1 < n ? x[e + 1] : 0.f, e + 2 < n ? x[e + 2] : 0.f, 0.f);
-      }
+      v[i] = load16(x, (j0 + row) * kChunk + r * kRowE + c4 * VN, n);
     }
     __builtin_amdgcn_wave_barrier();  // the previous round's rows are read (LDS ops complete in order per wave)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int f = i * kWave + lane, row = f >> 4, c4 = f & 15;
-      float* d = st + row * kStageRow + c4 * 4;
-      d[0] = v[i].x;
-      d[1] = v[i].y;
-      d[2] = v[i].z;
-      d[3] = v[i].w;
+      T* d = st + row * kRow + c4 * VN;
+#pragma unroll
+      for (int c = 0; c < VN; ++c) d[c] = v[i].e[c];
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const float* rowp = st + lane * kStageRow;
+    const T* rowp = st + lane * kRow;
 #pragma unroll 16
-    for (int e = 0; e < 64; ++e) {
-      const double q = (double)(fabsf(rowp[e]) / S);
+    for (int e = 0; e < kRowE; ++e) {
+      const double q = q_of(rowp[e], S);
       ca = ca + q;
       cb = cb + q;
       ps += q;
@@ -330,7 +347,7 @@ __global__ __launch_bounds__(256) void ar_phase_a_kernel(const float* __restrict
 }
 
 // ---- K4: numpy's checks on p (before any uniform is drawn) -------------------------------------------
-__global__ __launch_bounds__(1024) void ar_check_kernel(int64_t nparts, ArWs ws) {
+__global__ __launch_bounds__(1024) void ar_check_kernel(int64_t nparts, double atol, ArWs ws) {
   __shared__ double lds[1024 / kWave];
   double s = 0.0;
   for (int64_t i = threadIdx.x; i < nparts; i += 1024) s += ws.p_part[i];
@@ -338,7 +355,7 @@ __global__ __launch_bounds__(1024) void ar_check_kernel(int64_t nparts, ArWs ws)
   if (threadIdx.x == 0) {
     int st = 0;
     if (isnan(s)) st = kStNan;
-    else if (!(fabs(s - 1.0) <= kAtol)) st = kStSum;
+    else if (!(fabs(s - 1.0) <= atol)) st = kStSum;
     ws.status[0] = st;
   }
 }
@@ -420,11 +437,15 @@ __global__ __launch_bounds__(kPieceBlk) void ar_piece_kernel(int64_t nq, ArWs ws
 // Exact sequential run of chunk u from its exact start t by one wave (every lane ends with the same t).  The
 // chunk's elements are v (4 per lane, lane-major); with cD > 0 each lane also returns, per element it holds, the
 // normalised cdf test c / cD > u as a bit of *hits.
-__device__ double wave_run(const float4 v, double t, float S, double cD = 0.0, double u = 0.0,
-                           unsigned* hits = nullptr) {
+template <class T>
+struct Four {
+  T a, b, c, d;
+};
+template <class T>
+__device__ double wave_run(const Four<T> v, double t, T S, double cD = 0.0, double u = 0.0, unsigned* hits = nullptr) {
   const int lane = threadIdx.x & (kWave - 1);
-  const double q0 = (double)(fabsf(v.x) / S), q1 = (double)(fabsf(v.y) / S);
-  const double q2 = (double)(fabsf(v.z) / S), q3 = (double)(fabsf(v.w) / S);
+  const double q0 = q_of(v.a, S), q1 = q_of(v.b, S);
+  const double q2 = q_of(v.c, S), q3 = q_of(v.d, S);
   unsigned h = 0;
 #pragma unroll 4
   for (int L = 0; L < kWave; ++L) {
@@ -442,15 +463,25 @@ __device__ double wave_run(const float4 v, double t, float S, double cD = 0.0, d
   return t;
 }
 
-__device__ __forceinline__ float4 load_chunk4(const float* __restrict__ x, int64_t n, int64_t u) {
+template <class T>
+__device__ __forceinline__ Four<T> load_chunk4(const T* __restrict__ x, int64_t n, int64_t u) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t e = u * kChunk + 4 * lane;
-  if (e + 4 <= n) return *reinterpret_cast<const float4*>(x + e);
-  return make_float4(e < n ? x[e] : 0.f, e + 1 < n ? x[e + 1] : 0.f, e + 2 < n ? x[e + 2] : 0.f, 0.f);
+  if (e + 4 <= n) {
+    if constexpr (sizeof(T) == 4) {
+      const float4 q = *reinterpret_cast<const float4*>(x + e);
+      return Four<T>{q.x, q.y, q.z, q.w};
+    } else {
+      const double2 q0 = *reinterpret_cast<const double2*>(x + e), q1 = *reinterpret_cast<const double2*>(x + e + 2);
+      return Four<T>{q0.x, q0.y, q1.x, q1.y};
+    }
+  }
+  return Four<T>{e < n ? x[e] : (T)0, e + 1 < n ? x[e + 1] : (T)0, e + 2 < n ? x[e + 2] : (T)0, (T)0};
 }
 
 // ---- K6: the walk — every piece's exact start, in order, on one wave ---------------------------------------
-__global__ __launch_bounds__(1024) void ar_walk_kernel(const float* __restrict__ x, int64_t n, int64_t nq, int nblk,
+template <class T>
+__global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, int64_t n, int64_t nq, int nblk,
                                                        int force_seq, ArWs ws) {
   __shared__ int off[kMaxScanBlocks];
   __shared__ Rec batch[kWalkBatch];
@@ -481,7 +512,7 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const float* __restrict__
   if (tid == 0) s_total = carry;
   __syncthreads();
   const int total = s_total;
-  const float S = ws.total[0];
+  const T S = (T)ws.total[0];
   for (int g0 = 0; g0 < total && !s_bad; g0 += kWalkBatch) {
     const int g = g0 + tid;
     if (g < total) {  // the block holding piece g: the last b with off[b] <= g
@@ -501,7 +532,7 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const float* __restrict__
       // the next re-run chunk's elements are loaded one re-run ahead
       int nxt = 0;
       while (nxt < cnt && batch[nxt].e >= 1) ++nxt;
-      float4 v = nxt < cnt ? load_chunk4(x, n, batch[nxt].first) : make_float4(0.f, 0.f, 0.f, 0.f);
+      Four<T> v = nxt < cnt ? load_chunk4(x, n, batch[nxt].first) : Four<T>{0, 0, 0, 0};
       for (int r = 0; r < cnt && !bad; ++r) {
         const Rec rc = batch[r];
         if (tid == 0) ws.rec_t[g0 + r] = t;
@@ -517,7 +548,7 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const float* __restrict__
           }
           t = from_grid(m, rc.e);
         } else {
-          const float4 cur = v;
+          const Four<T> cur = v;
           int nn = r + 1;
           while (nn < cnt && batch[nn].e >= 1) ++nn;
           if (nn < cnt) v = load_chunk4(x, n, batch[nn].first);
@@ -564,13 +595,14 @@ __global__ __launch_bounds__(256) void ar_fill_kernel(int64_t nq, double u, ArWs
 
 // ---- K8: the index — chunk lo re-run from its exact start; or, if the speculation failed, the exact
 // chunk-by-chunk chain (phase B of the sequential design) and a binary search first ----------------------------
-__global__ __launch_bounds__(1024) void ar_final_kernel(const float* __restrict__ x, int64_t n, int64_t nq, double u,
-                                                        ArWs ws, int64_t* __restrict__ index, float* __restrict__ out) {
+template <class T>
+__global__ __launch_bounds__(1024) void ar_final_kernel(const T* __restrict__ x, int64_t n, int64_t nq, double u,
+                                                        ArWs ws, int64_t* __restrict__ index, T* __restrict__ out) {
   __shared__ double g_s[kRecLegacy], ea_s[kRecLegacy], eb_s[kRecLegacy];
   __shared__ long long s_lo;
   if (ws.status[0] != 0) return;  // the host raises numpy's ValueError; nothing is drawn or written
   const int tid = threadIdx.x;
-  const float S = ws.total[0];
+  const T S = (T)ws.total[0];
   if (ws.fail[0] != 0) {
     double t = 0.0;
     for (int64_t base = 0; base < nq; base += kRecLegacy) {
@@ -646,7 +678,7 @@ ArWs carve(void* base, int64_t n, size_t* bytes) {
   const int64_t nbuf = cdiv(n, kBuf), nq = cdiv(n, kChunk), nblk = cdiv(nq, kPieceBlk), npa = cdiv(nq, 256);
   Carver c(base, base ? ~size_t(0) : 0);
   ArWs w;
-  w.buf_sum = c.take<float>(nbuf);
+  w.buf_sum = c.take<double>(nbuf);
   w.bpre = c.take<double>(nbuf);
   w.q_abs = c.take<double>(nbuf * kQ);
   w.guess = c.take<double>(nq);
@@ -663,7 +695,7 @@ ArWs carve(void* base, int64_t n, size_t* bytes) {
   w.rec_end = c.take<double>(nblk * kRecMax);
   w.start = c.take<double>(nq + 1);
   w.p_part = c.take<double>(npa);
-  w.total = c.take<float>(1);
+  w.total = c.take<double>(1);
   w.status = c.take<int32_t>(1);
   w.fail = c.take<int32_t>(1);
   w.lo = c.take<long long>(1);
@@ -685,32 +717,38 @@ size_t flc_adaptive_workspace_size(int64_t n) {
   return b;
 }
 
-int flc_adaptive_prepare(const float* x, int64_t n, int32_t* status, void* ws, size_t ws_bytes, void* stream) {
-  if (!x || n <= 0 || n >= (int64_t(1) << 31) || !ws) return fail(FLC_EINVAL, "flc_adaptive_prepare: bad arguments");
-  if (ws_bytes < flc_adaptive_workspace_size(n)) return fail(FLC_EWORKSPACE, "flc_adaptive_prepare: workspace too small");
-  if (!aligned16(x)) return fail(FLC_EINVAL, "flc_adaptive_prepare: x must be 16-byte aligned");
+}  // extern "C"
+
+namespace {
+template <class T>
+int adaptive_prepare(const T* x, int64_t n, int32_t* status, void* ws, size_t ws_bytes, void* stream, double atol,
+                     const char* who) {
+  if (!x || n <= 0 || n >= (int64_t(1) << 31) || !ws) return fail(FLC_EINVAL, "%s: bad arguments", who);
+  if (ws_bytes < flc_adaptive_workspace_size(n)) return fail(FLC_EWORKSPACE, "%s: workspace too small", who);
+  if (!aligned16(x)) return fail(FLC_EINVAL, "%s: x must be 16-byte aligned", who);
   hipStream_t st = as_stream(stream);
   ArWs w = carve(ws, n, nullptr);
   const int64_t nfull = n / kBuf, nbuf = cdiv(n, kBuf), nq = cdiv(n, kChunk), npa = cdiv(nq, 256);
   if (nfull > 0)
-    FLC_LAUNCH("adaptive_buffer_sum", ar_buffer_sum_kernel, dim3((unsigned)nfull), dim3(256), 0, st, x, nfull, w);
+    FLC_LAUNCH("adaptive_buffer_sum", ar_buffer_sum_kernel<T>, dim3((unsigned)nfull), dim3(256), 0, st, x, nfull, w);
   if (nbuf > nfull) {
     TailProg prog{};
     (void)tail_prog_build(prog, 0, (int)(n - nfull * kBuf));
-    FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel, dim3(1), dim3(128), 0, st, x, n, prog, w);
+    FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel<T>, dim3(1), dim3(128), 0, st, x, n, prog, w);
   }
-  FLC_LAUNCH("adaptive_total", ar_total_kernel, dim3(1), dim3(1024), 0, st, nbuf, w);
-  FLC_LAUNCH("adaptive_phase_a", ar_phase_a_kernel, dim3((unsigned)npa), dim3(256), 0, st, x, n, nq, w);
-  FLC_LAUNCH("adaptive_check", ar_check_kernel, dim3(1), dim3(1024), 0, st, npa, w);
+  FLC_LAUNCH("adaptive_total", ar_total_kernel<T>, dim3(1), dim3(1024), 0, st, nbuf, w);
+  FLC_LAUNCH("adaptive_phase_a", ar_phase_a_kernel<T>, dim3((unsigned)npa), dim3(256), 0, st, x, n, nq, w);
+  FLC_LAUNCH("adaptive_check", ar_check_kernel, dim3(1), dim3(1024), 0, st, npa, atol, w);
   if (status) FLC_CHECK_HIP(hipMemcpyAsync(status, w.status, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   return FLC_OK;
 }
 
-int flc_adaptive_select(const float* x, int64_t n, double u, int64_t* index, float* out, void* ws, size_t ws_bytes,
-                        void* stream) {
+template <class T>
+int adaptive_select(const T* x, int64_t n, double u, int64_t* index, T* out, void* ws, size_t ws_bytes, void* stream,
+                    const char* who) {
   if (!x || n <= 0 || n >= (int64_t(1) << 31) || !ws || !index || !out || !(u >= 0.0 && u < 1.0))
-    return fail(FLC_EINVAL, "flc_adaptive_select: bad arguments");
-  if (ws_bytes < flc_adaptive_workspace_size(n)) return fail(FLC_EWORKSPACE, "flc_adaptive_select: workspace too small");
+    return fail(FLC_EINVAL, "%s: bad arguments", who);
+  if (ws_bytes < flc_adaptive_workspace_size(n)) return fail(FLC_EWORKSPACE, "%s: workspace too small", who);
   hipStream_t st = as_stream(stream);
   ArWs w = carve(ws, n, nullptr);
   const int64_t nq = cdiv(n, kChunk);
@@ -718,12 +756,33 @@ int flc_adaptive_select(const float* x, int64_t n, double u, int64_t* index, flo
   // FLC_ADAPTIVE_SEQUENTIAL=1: skip the speculation's result and run the exact chunk-by-chunk chain (tests)
   const char* fs = getenv("FLC_ADAPTIVE_SEQUENTIAL");
   const int force_seq = (fs && atoi(fs) != 0) ? 1 : 0;
-  FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)n * sizeof(float), st));
+  FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)n * sizeof(T), st));
   FLC_LAUNCH("adaptive_piece", ar_piece_kernel, dim3((unsigned)nblk), dim3(kPieceBlk), 0, st, nq, w);
-  FLC_LAUNCH("adaptive_walk", ar_walk_kernel, dim3(1), dim3(1024), 0, st, x, n, nq, nblk, force_seq, w);
+  FLC_LAUNCH("adaptive_walk", ar_walk_kernel<T>, dim3(1), dim3(1024), 0, st, x, n, nq, nblk, force_seq, w);
   FLC_LAUNCH("adaptive_fill", ar_fill_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, nq, u, w);
-  FLC_LAUNCH("adaptive_final", ar_final_kernel, dim3(1), dim3(1024), 0, st, x, n, nq, u, w, index, out);
+  FLC_LAUNCH("adaptive_final", ar_final_kernel<T>, dim3(1), dim3(1024), 0, st, x, n, nq, u, w, index, out);
   return FLC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int flc_adaptive_prepare(const float* x, int64_t n, int32_t* status, void* ws, size_t ws_bytes, void* stream) {
+  return adaptive_prepare(x, n, status, ws, ws_bytes, stream, kAtol, "flc_adaptive_prepare");
+}
+
+int flc_adaptive_select(const float* x, int64_t n, double u, int64_t* index, float* out, void* ws, size_t ws_bytes,
+                        void* stream) {
+  return adaptive_select(x, n, u, index, out, ws, ws_bytes, stream, "flc_adaptive_select");
+}
+
+int flc_adaptive_prepare_f64(const double* x, int64_t n, int32_t* status, void* ws, size_t ws_bytes, void* stream) {
+  return adaptive_prepare(x, n, status, ws, ws_bytes, stream, kAtol64, "flc_adaptive_prepare_f64");
+}
+
+int flc_adaptive_select_f64(const double* x, int64_t n, double u, int64_t* index, double* out, void* ws,
+                            size_t ws_bytes, void* stream) {
+  return adaptive_select(x, n, u, index, out, ws, ws_bytes, stream, "flc_adaptive_select_f64");
 }
 
 }  // extern "C"

@@ -237,6 +237,11 @@ size_t flc_adaptive_workspace_size(int64_t n);
 int flc_adaptive_prepare(const float* x, int64_t n, int32_t* status, void* ws, size_t ws_bytes, void* stream);
 int flc_adaptive_select(const float* x, int64_t n, double u, int64_t* index, float* out, void* ws, size_t ws_bytes,
                         void* stream);
+/* the same on a float64 x (the reference keeps it float64): S an fp64 sum of the same buffers and trees, p = |x| / S
+ * in fp64, the tolerance sqrt(eps64) = 1.4901161e-8; same workspace size */
+int flc_adaptive_prepare_f64(const double* x, int64_t n, int32_t* status, void* ws, size_t ws_bytes, void* stream);
+int flc_adaptive_select_f64(const double* x, int64_t n, double u, int64_t* index, double* out, void* ws,
+                            size_t ws_bytes, void* stream);
 
 /* the stacked encoder fused with the client delta (f1): x = local - global formed in the encoder's HBM pass
  * (FedOptClient.communicate, _fedopt.py:294-297: clone + add_(alpha=-1) per parameter tensor, then the flatten the

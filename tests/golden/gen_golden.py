@@ -303,6 +303,44 @@ def gen_f64(ref):
             store[key + "|out"] = out
             for k, v in rec.items():
                 store[key + "|" + k] = np.array(v)
+    # adaptive random on float64 (S and p in fp64; numpy's tolerance sqrt(eps64)): small cases in full, large ones
+    # (zeros, heavy tails) by the drawn index, and numpy's error cases
+    for D, seed, heavy in ((7, 0, False), (4096, 1, False), (65537, 2, False), (300_007, 3, True),
+                           (1_000_003, 4, False), (2_000_001, 5, True)):
+        if heavy:
+            g = np.random.default_rng(40_000 + seed * 104729 + D)
+            x = g.standard_cauchy(D) * 1e-3
+            x[g.random(D) < 0.2] = 0.0
+        else:
+            x = make_input64(D, seed)
+        out, rec = run_codec(ref, lambda c: c.makeAdaptiveRandomCompressor(D), x, seed)
+        key = f"adaptive{'_heavy' if heavy else ''}|{D}|{seed}"
+        store[key + "|sha_x"] = np.array(sha(x))
+        if D <= 4096:
+            store[key + "|x"] = x
+            store[key + "|out"] = out
+        store[key + "|sha_out"] = np.array(sha(out))
+        store[key + "|index"] = np.array(np.flatnonzero(out), dtype=np.int64)
+        for k, v in rec.items():
+            store[key + "|" + k] = np.array(v)
+    errs = {"zeros": np.zeros(5), "nan": np.array([1.0, np.nan, 2.0]), "inf": np.array([1.0, np.inf, 2.0]),
+            "overflow": np.array([1e308, 1e308, 1e308, 1.0])}
+    for name, x in errs.items():
+        c = ref.Compressor()
+        c.makeAdaptiveRandomCompressor(len(x))
+        random.seed(9)
+        np.random.seed(9)
+        try:
+            with np.errstate(all="ignore"):
+                c.compressVector(x)
+            err = ""
+        except ValueError as e:
+            err = str(e)
+        key = f"adaptive_err|special:{name}|9"
+        store[key + "|x"] = x
+        store[key + "|error"] = np.array(err)
+        store[key + "|next_np"] = np.array(np.random.random_sample())
+        store[key + "|next_random"] = np.array(random.random())
     np.savez_compressed(OUT / "codec_f64.npz", **store)
     print("codec_f64.npz:", len(store), "arrays")
 

@@ -29,7 +29,13 @@ def case_input(case: str, rec: Dict[str, np.ndarray]) -> np.ndarray:
     if "x" in rec:
         return rec["x"]
     parts = case.split("|")
-    x = make_input64(int(parts[1]), int(parts[-1]))
+    D, seed = int(parts[1]), int(parts[-1])
+    if parts[0] == "adaptive_heavy":  # Cauchy, 20 % zeros (gen_golden.gen_f64)
+        g = np.random.default_rng(40_000 + seed * 104729 + D)
+        x = g.standard_cauchy(D) * 1e-3
+        x[g.random(D) < 0.2] = 0.0
+    else:
+        x = make_input64(D, seed)
     assert gc.sha(x) == str(rec["sha_x"]), f"input recipe drifted for {case}"
     return x
 

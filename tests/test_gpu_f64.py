@@ -24,7 +24,8 @@ from tests import golden_f64 as g64
 pytestmark = pytest.mark.gpu
 
 F64 = g64.load()
-DENSE = {k: v for k, v in F64.items() if k.split("|")[0] not in ("topk", "randk")}
+ADAPTIVE = {k: v for k, v in F64.items() if k.startswith("adaptive")}
+DENSE = {k: v for k, v in F64.items() if k.split("|")[0] not in ("topk", "randk") and k not in ADAPTIVE}
 SPARSE = {k: v for k, v in F64.items() if k.split("|")[0] in ("topk", "randk")}
 DEV = "cuda"
 
@@ -94,6 +95,44 @@ def test_f64_sparse_compressor_matches_reference_fixture(case):
         assert g64.same_bits(out, exp), case
     else:
         assert g64.check_output(rec, out), case
+
+
+@pytest.mark.parametrize("case", sorted(ADAPTIVE))
+def test_f64_adaptive_compressor_matches_reference_fixture(case):
+    from fl_sim_amd import Compressor
+
+    rec = ADAPTIVE[case]
+    x = g64.case_input(case, rec)
+    c = Compressor()
+    c.makeAdaptiveRandomCompressor(len(x))
+    gc.seed_all(int(case.split("|")[-1]))
+    if "error" in rec:
+        with pytest.raises(ValueError) as ei:
+            c.compressVector(x)
+        assert str(ei.value) == str(rec["error"])
+    else:
+        out = c.compressVector(x)
+        assert out.dtype == np.float64
+        assert list(np.flatnonzero(out)) == list(rec["index"])
+        assert g64.check_output(rec, out), case
+    assert np.random.random_sample() == float(rec["next_np"])
+    assert random.random() == float(rec["next_random"])
+
+
+@pytest.mark.parametrize("D", [1, 8191, 8193, 1_000_003, 9_000_000])
+def test_f64_adaptive_matches_oracle(D):
+    from fl_sim_amd import codec
+
+    g = np.random.default_rng(D)
+    x = g.standard_cauchy(D) * 1e-3
+    x[g.random(D) < 0.1] = 0.0
+    xd = torch.from_numpy(x).to(DEV)
+    assert int(codec.adaptive_prepare(xd).item()) == 0
+    for u in (0.0, 0.37, 0.999999):
+        out, index = codec.adaptive_select(xd, u)
+        exp, _, ind = ref.adaptive_random(x, D, u)
+        assert int(index.item()) == ind, (D, u)
+        assert g64.same_bits(out.cpu().numpy(), exp)
 
 
 def _x64(D, seed, zero_frac=0.05, scale=1e-3):

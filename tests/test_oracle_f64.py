@@ -16,7 +16,8 @@ from tests import golden_cases as gc
 from tests import golden_f64 as g64
 
 F64 = g64.load()
-DENSE = {k: v for k, v in F64.items() if k.split("|")[0] not in ("topk", "randk")}
+ADAPTIVE = {k: v for k, v in F64.items() if k.startswith("adaptive")}
+DENSE = {k: v for k, v in F64.items() if k.split("|")[0] not in ("topk", "randk") and k not in ADAPTIVE}
 SPARSE = {k: v for k, v in F64.items() if k.split("|")[0] in ("topk", "randk")}
 
 
@@ -60,10 +61,30 @@ def test_f64_sparse_oracle_matches_reference(case):
     assert np.random.random_sample() == float(rec["next_np"])
 
 
+@pytest.mark.parametrize("case", sorted(ADAPTIVE))
+def test_f64_adaptive_oracle_matches_reference(case):
+    rec = ADAPTIVE[case]
+    x = g64.case_input(case, rec)
+    gc.seed_all(int(case.split("|")[-1]))
+    if "error" in rec:
+        with np.errstate(all="ignore"):
+            p = np.abs(x) / np.abs(x).sum()
+        # numpy's checks before the draw (mtrand choice): NaN, then |sum - 1| > sqrt(eps64)
+        err = "probabilities contain NaN" if np.isnan(p.sum()) else (
+            "probabilities do not sum to 1" if abs(p.sum() - 1.0) > np.sqrt(np.finfo(np.float64).eps) else "")
+        assert err == str(rec["error"])
+        return
+    out, send, ind = ref.adaptive_random(x, len(x), np.random.random_sample())
+    assert out.dtype == np.float64
+    assert [ind] == list(rec["index"])
+    assert g64.check_output(rec, out), case
+    assert random.random() == float(rec["next_random"])
+
+
 def test_f64_fixture_covers_every_compressor_type():
     names = {k.split("|")[0] for k in F64}
     for want in ("identical", "lazy_p03", "natural64", "natural32", "stddither64_s8_p2", "natdither64_s3_p2",
-                 "stddither32_s8_inf", "topk", "randk"):
+                 "stddither32_s8_inf", "topk", "randk", "adaptive", "adaptive_heavy", "adaptive_err"):
         assert want in names, want
     assert any("error" in rec for rec in F64.values()), "the underflowed-norm IndexError case"
 

@@ -12,7 +12,7 @@ from fl_sim_amd import codec  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 25_000_000
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(5)
-x = torch.randn(n, generator=g, device=dev) * 1e-3
+x = torch.randn(n, generator=g, device=dev, dtype=torch.float64 if os.environ.get("F64") else torch.float32) * 1e-3
 for _ in range(3):
     codec.adaptive_prepare(x)
     codec.adaptive_select(x, 0.37)
