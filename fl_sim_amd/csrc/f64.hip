@@ -173,9 +173,24 @@ __device__ __forceinline__ uint32_t natural64_code(double xv, double u) {
   const uint32_t sign = signbit(xv) ? 1u : 0u;
   const double a = fabs(xv);
   if (isinf(a)) return (sign << 15) | (uint32_t)(1025 + kNatBias);
-  // math.log2 / floor / ceil of the reference, in fp64 (a power of two gives down == up and pt = 0)
-  const double alpha = log2(a);
-  const int down = (int)floor(alpha), up = (int)ceil(alpha);
+  // math.log2 / floor / ceil of the reference, in fp64 (a power of two gives down == up and pt = 0).  Away from a
+  // power of two floor / ceil of the rounded log2 are the exponent f and f + 1: a = m * 2^f, m in [1, 2), and
+  // log2 a = f + log2 m lies at least ~1.44 (m - 1) above f and 0.72 (2 - m) below f + 1, far more than the half ulp of
+  // a number near f (<= (|f| + 1) * 2^-53).  Only mantissas within W = (|f| + 2) * 2^-48 of 1 or 2 (a generous
+  // margin) take the log2, whose rounding onto an integer decides them as it does in the reference.
+  int f;
+  const double m = 2.0 * frexp(a, &f);  // a = m * 2^(f - 1), m in [1, 2)
+  f -= 1;
+  const double W = (double)(abs(f) + 2) * 3.552713678800501e-15;  // 2^-48
+  int down, up;
+  if (m - 1.0 > W && 2.0 - m > W) {
+    down = f;
+    up = f + 1;
+  } else {
+    const double alpha = log2(a);
+    down = (int)floor(alpha);
+    up = (int)ceil(alpha);
+  }
   const double pt = (ldexp(1.0, up) - a) / ldexp(1.0, down);
   const int e = (u < pt) ? down : up;
   return (sign << 15) | (uint32_t)(e + kNatBias);
