@@ -139,7 +139,7 @@ SIGNATURES = {
     "flc_copy_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_scale_div_f64": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p]),
     "flc_randk_apply_f64": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_double, c_void_p, c_void_p]),
-    "flc_f64_workspace_size": (c_size_t, [c_int64]),
+    "flc_f64_workspace_size": (c_size_t, [c_int64, c_int64]),
     "flc_count_consumers_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_natural_f64": (
         c_int, [c_void_p, c_int64, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]

@@ -857,8 +857,8 @@ def _dev_f64(x: torch.Tensor, name: str = "x") -> torch.Tensor:
     return x
 
 
-def _ws64(x: torch.Tensor) -> torch.Tensor:
-    return workspace(x.device, _lib.size("flc_f64_workspace_size", x.numel()), "f64")
+def _ws64(x: torch.Tensor, k: int = 0) -> torch.Tensor:
+    return workspace(x.device, _lib.size("flc_f64_workspace_size", x.numel(), int(k)), "f64")
 
 
 def copy_f64(x: torch.Tensor) -> torch.Tensor:
@@ -951,6 +951,6 @@ def topk_dense_f64(x: torch.Tensor, k: int) -> torch.Tensor:
     """out = x on the k largest elements (ties: the highest indices), +0 elsewhere; 0 < k < n."""
     x = _dev_f64(x)
     out = torch.empty_like(x)
-    ws = _ws64(x)
+    ws = _ws64(x, k)
     call("flc_topk_dense_f64", _p(x), x.numel(), int(k), _p(out), _p(ws), ws.numel(), _stream(x.device))
     return out

@@ -422,77 +422,234 @@ __device__ __forceinline__ unsigned long long order_key64(double v) {
 }
 
 constexpr int kDigits = 8;  // 8-bit digits, most significant first
+constexpr int kSample64 = 8192;   // sample keys of the top-k floor
+constexpr int kFloorDigits = 3;   // the floor keeps the sample's r-th key to its top 24 bits (a floor below it)
 struct Sel64 {
-  unsigned long long prefix;  // the resolved digits of the K-th largest key
-  long long rem;              // its rank among the keys with that prefix (from the top, 1-based)
-  long long ties;             // keys equal to T (after the last pass)
+  // after q digit passes: the resolved high digits of the K-th largest key, its rank among the keys sharing them
+  // (from the top, 1-based), and the size of the last digit's bin (after all kDigits passes: the ties of T)
+  unsigned long long pre[kDigits + 1];
+  long long rem[kDigits + 1], cnt[kDigits + 1];
+  unsigned long long t_lo;  // candidate floor key (from the sample)
+  int mode;                 // 0: the digit passes run over the candidates, 1: over x itself
+  int ovf;                  // a chunk had more candidates than its segment holds
   unsigned hist[kDigits][256];
+  unsigned long long sample[kSample64];
 };
 
-__global__ __launch_bounds__(kT) void sel64_init_kernel(Sel64* __restrict__ st, long long k) {
-  for (int i = threadIdx.x; i < kDigits * 256; i += kT) (&st->hist[0][0])[i] = 0u;
-  if (threadIdx.x == 0) {
-    st->prefix = 0ull;
-    st->rem = k;
-    st->ties = 0;
+// LDS histogram add of one key per lane; a wave whose counted keys all fall in one bin (the common case in the high
+// digits, where the keys share their sign and exponent) adds once
+__device__ __forceinline__ void hist_add64(unsigned* h, unsigned bin, bool in) {
+  const unsigned long long m = __ballot(in);
+  if (m == 0ull) return;
+  const int first = __builtin_ctzll(m);
+  const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)bin, first);
+  if (__ballot(in && bin != b0) == 0ull) {
+    if ((int)(threadIdx.x & (kWave - 1)) == first) atomicAdd(&h[b0], (unsigned)__popcll(m));
+  } else if (in) {
+    atomicAdd(&h[bin], 1u);
   }
 }
 
-__global__ __launch_bounds__(kT) void sel64_hist_kernel(const double* __restrict__ x, int64_t n, int pass,
-                                                        Sel64* __restrict__ st) {
-  __shared__ unsigned s_h[256];
-  s_h[threadIdx.x] = 0u;
+// block-wide (NW waves): the bin of a 256-bin histogram (count of bin 255 - t in thread t < 256, 0 elsewhere)
+// holding rank `rem` from the top.  Returns, in every thread, (digit, count above it, its count).
+template <int NW>
+__device__ __forceinline__ void pick256(long long c, long long rem, long long* s_scan, long long* s_res) {
+  long long tot;
+  const long long ex = block_excl_scan<long long, NW>(c, s_scan, &tot);  // keys in the bins above this thread's
+  if (threadIdx.x < 256 && c > 0 && ex < rem && ex + c >= rem) {
+    s_res[0] = 255 - (long long)threadIdx.x;
+    s_res[1] = ex;
+    s_res[2] = c;
+  }
   __syncthreads();
-  const unsigned long long prefix = st->prefix;
-  const int sh = 56 - 8 * pass;
-  for (int64_t i = ((int64_t)blockIdx.x * kT + threadIdx.x) * 2; i < n; i += (int64_t)gridDim.x * kT * 2) {
-    double v[2];
-    if (i + 2 <= n) {
-      const double2 a = *reinterpret_cast<const double2*>(x + i);
-      v[0] = a.x;
-      v[1] = a.y;
-    } else {
-      v[0] = x[i];
-      v[1] = 0.0;
+}
+
+// state q + 1 from state q and the q-th pass's histogram (every block of a kernel computes it the same way; the
+// caller's block 0 stores it for the next kernel)
+__device__ __forceinline__ void sel64_step(const Sel64* __restrict__ st, int q, long long* s_scan, long long* s_res,
+                                           unsigned long long& pre, long long& rem, long long& cnt) {
+  const long long c = threadIdx.x < 256 ? (long long)st->hist[q][255 - threadIdx.x] : 0ll;
+  pre = st->pre[q];
+  rem = st->rem[q];
+  pick256<kNW>(c, rem, s_scan, s_res);
+  pre = (pre << 8) | (unsigned long long)s_res[0];
+  rem -= s_res[1];
+  cnt = s_res[2];
+}
+
+// block 0 resets the state; with S > 0 the blocks also take S evenly strided keys (the float32 encoder's sample
+// positions)
+__global__ __launch_bounds__(kT) void sel64_init_kernel(const double* __restrict__ x, int64_t n, int S, long long k,
+                                                        int mode, Sel64* __restrict__ st) {
+  if (blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < kDigits * 256; i += kT) (&st->hist[0][0])[i] = 0u;
+    if (threadIdx.x == 0) {
+      st->pre[0] = 0ull;
+      st->rem[0] = k;
+      st->cnt[0] = 0;
+      st->t_lo = 0ull;
+      st->mode = mode;
+      st->ovf = 0;
     }
+  }
+  const int j = blockIdx.x * kT + threadIdx.x;
+  if (j >= S) return;
+  const int64_t pos = (int64_t)(((double)j + 0.5) * (double)n / (double)S);
+  st->sample[j] = order_key64(x[pos < n ? pos : n - 1]);
+}
+
+// one block: t_lo = the r-th largest sample key truncated to its top 24 bits (three digit passes over the sample
+// held in registers), so that count(key >= t_lo) >= ~k + 4 sigma over the whole vector
+__global__ __launch_bounds__(1024) void sel64_floor_kernel(int S, long long r, Sel64* __restrict__ st) {
+  constexpr int kPer = kSample64 / 1024, kW = 1024 / kWave;
+  __shared__ unsigned s_h[256];
+  __shared__ long long s_scan[kW], s_res[3];
+  unsigned long long key[kPer];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (i + j >= n) break;
+  for (int i = 0; i < kPer; ++i) {
+    const int j = i * 1024 + threadIdx.x;
+    key[i] = j < S ? st->sample[j] : 0ull;
+  }
+  unsigned long long prefix = 0ull;
+  long long rem = r;
+  for (int pass = 0; pass < kFloorDigits; ++pass) {
+    if (threadIdx.x < 256) s_h[threadIdx.x] = 0u;
+    __syncthreads();
+    const int sh = 56 - 8 * pass;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const bool in = i * 1024 + (int)threadIdx.x < S && (pass == 0 || (key[i] >> (sh + 8)) == prefix);
+      hist_add64(s_h, (unsigned)(key[i] >> sh) & 255u, in);
+    }
+    __syncthreads();
+    pick256<kW>(threadIdx.x < 256 ? (long long)s_h[255 - threadIdx.x] : 0ll, rem, s_scan, s_res);
+    prefix = (prefix << 8) | (unsigned long long)s_res[0];
+    rem -= s_res[1];
+    __syncthreads();  // (s_res and s_h are rewritten by the next pass)
+  }
+  if (threadIdx.x == 0) st->t_lo = prefix << (64 - 8 * kFloorDigits);
+}
+
+// the candidates (key >= t_lo) of each 8192-element chunk appended to the chunk's own segment (no global atomics);
+// counts[c] = the chunk's candidate count (a count beyond the segment flags st->ovf: the passes then run over x)
+__global__ __launch_bounds__(kT) void sel64_filter_kernel(const double* __restrict__ x, int64_t n, int segcap,
+                                                          Sel64* __restrict__ st, unsigned long long* __restrict__ seg,
+                                                          int* __restrict__ counts) {
+  // (the digit passes only histogram the candidates: their order inside a segment is free, so each wave appends
+  // through one LDS counter, without block-wide barriers)
+  __shared__ unsigned s_n;
+  if (threadIdx.x == 0) s_n = 0u;
+  __syncthreads();
+  const unsigned long long t_lo = st->t_lo;
+  unsigned long long* my = seg + (size_t)blockIdx.x * segcap;
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int it = 0; it < kIt; ++it) {
+    const int64_t e0 = (int64_t)blockIdx.x * kChunk + ((int64_t)it * kT + threadIdx.x) * kE;
+    double v[kE] = {0.0, 0.0, 0.0, 0.0};
+    if (e0 < n) load4(x, e0, n, v);
+#pragma unroll
+    for (int j = 0; j < kE; ++j) {
       const unsigned long long key = order_key64(v[j]);
-      if (pass == 0 || (key >> (sh + 8)) == prefix) atomicAdd(&s_h[(unsigned)(key >> sh) & 255u], 1u);
+      const bool in = e0 + j < n && key >= t_lo;
+      const unsigned long long m = __ballot(in);
+      if (m == 0ull) continue;
+      unsigned base = 0;
+      if (lane == 0) base = atomicAdd(&s_n, (unsigned)__popcll(m));
+      base = (unsigned)__builtin_amdgcn_readlane((int)base, 0);
+      const unsigned p = base + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      if (in && p < (unsigned)segcap) my[p] = key;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    counts[blockIdx.x] = (int)s_n;
+    if (s_n > (unsigned)segcap) atomicOr(&st->ovf, 1);
+  }
+}
+
+// digit pass `pass`: the previous pass's digit resolved first (state pass from state pass - 1), then mode 0 over the
+// chunk segments (block b takes chunks b, b + grid, ...: slots i < counts[c]), mode 1 over x
+__global__ __launch_bounds__(kT) void sel64_hist_kernel(const double* __restrict__ x, int64_t n, int pass,
+                                                        Sel64* __restrict__ st, const unsigned long long* __restrict__ seg,
+                                                        const int* __restrict__ counts, int64_t nch, int segcap) {
+  __shared__ unsigned s_h[256];
+  __shared__ long long s_scan[kNW], s_res[3];
+  __shared__ int s_mode;
+  s_h[threadIdx.x] = 0u;
+  unsigned long long prefix = 0ull;
+  if (pass == 0) {
+    // the candidates serve unless a segment overflowed or the floor admitted fewer than k elements (the sample
+    // missed): every block sums the chunk counts itself (block 0 records the decision for the later passes)
+    long long c = 0;
+    if (st->mode == 0)
+      for (int64_t i = threadIdx.x; i < nch; i += kT) c += counts[i];
+    c = block_sum<long long, kNW>(c, s_scan);
+    if (threadIdx.x == 0) {
+      s_mode = (st->mode != 0 || st->ovf || c < st->rem[0]) ? 1 : 0;
+      if (blockIdx.x == 0) st->mode = s_mode;
+    }
+  } else {
+    if (threadIdx.x == 0) s_mode = st->mode;
+  }
+  if (pass > 0) {
+    long long rem, cnt;
+    sel64_step(st, pass - 1, s_scan, s_res, prefix, rem, cnt);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->pre[pass] = prefix;
+      st->rem[pass] = rem;
+      st->cnt[pass] = cnt;
+    }
+  }
+  __syncthreads();
+  const int sh = 56 - 8 * pass;
+  auto add = [&](unsigned long long key, bool valid) {
+    hist_add64(s_h, (unsigned)(key >> sh) & 255u, valid && (pass == 0 || (key >> (sh + 8)) == prefix));
+  };
+  if (s_mode == 0) {
+    for (int64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+      const int cnt = counts[c];
+      const unsigned long long* sc = seg + (size_t)c * segcap;
+      for (int i0 = 0; i0 < cnt; i0 += kT) {  // (block-uniform bounds)
+        const int i = i0 + (int)threadIdx.x;
+        add(i < cnt ? sc[i] : 0ull, i < cnt);
+      }
+    }
+  } else {
+    for (int64_t i0 = (int64_t)blockIdx.x * kT * 2; i0 < n; i0 += (int64_t)gridDim.x * kT * 2) {
+      const int64_t i = i0 + 2 * threadIdx.x;
+      double v[2] = {0.0, 0.0};
+      if (i + 2 <= n) {
+        const double2 a = *reinterpret_cast<const double2*>(x + i);
+        v[0] = a.x;
+        v[1] = a.y;
+      } else if (i < n) {
+        v[0] = x[i];
+      }
+      add(order_key64(v[0]), i < n);
+      add(order_key64(v[1]), i + 1 < n);
     }
   }
   __syncthreads();
   if (s_h[threadIdx.x]) atomicAdd(&st->hist[pass][threadIdx.x], s_h[threadIdx.x]);
 }
 
-// one block of 256: the digit holding rank `rem` from the top
-__global__ __launch_bounds__(256) void sel64_pick_kernel(int pass, Sel64* __restrict__ st) {
-  __shared__ long long s_c[256];
-  const int t = threadIdx.x;
-  s_c[t] = st->hist[pass][255 - t];  // from the top
-  __syncthreads();
-  if (t == 0) {
-    long long above = 0, rem = st->rem;
-    int d = 0;
-    for (int i = 0; i < 256; ++i) {
-      if (above + s_c[i] >= rem) {
-        d = 255 - i;
-        st->ties = s_c[i];
-        break;
-      }
-      above += s_c[i];
-    }
-    st->prefix = (st->prefix << 8) | (unsigned long long)d;
-    st->rem = rem - above;
-  }
-}
-
-// ties (keys == T) per chunk, for the highest-index rule
-__global__ __launch_bounds__(kT) void sel64_ties_kernel(const double* __restrict__ x, int64_t n, const Sel64* __restrict__ st,
+// ties (keys == T) per chunk, for the highest-index rule; nothing to count when every tie is kept (need == ties)
+__global__ __launch_bounds__(kT) void sel64_ties_kernel(const double* __restrict__ x, int64_t n, Sel64* __restrict__ st,
                                                         int* __restrict__ counts) {
   __shared__ int s_red[kNW];
-  const unsigned long long T = st->prefix;
+  __shared__ long long s_scan[kNW], s_res[3];
+  unsigned long long T;
+  long long need, ties;
+  sel64_step(st, kDigits - 1, s_scan, s_res, T, need, ties);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->pre[kDigits] = T;
+    st->rem[kDigits] = need;
+    st->cnt[kDigits] = ties;
+  }
+  if (need == ties) {
+    if (threadIdx.x == 0) counts[blockIdx.x] = 0;
+    return;
+  }
   int cnt = 0;
   for (int it = 0; it < kIt; ++it) {
     const int64_t e0 = (int64_t)blockIdx.x * kChunk + ((int64_t)it * kT + threadIdx.x) * kE;
@@ -512,9 +669,22 @@ __global__ __launch_bounds__(kT) void sel64_emit_kernel(const double* __restrict
                                                         const long long* __restrict__ offsets, int64_t nchunks,
                                                         double* __restrict__ out) {
   __shared__ long long s_scan[kNW];
-  const unsigned long long T = st->prefix;
-  const long long need = st->rem;
-  // ties after this chunk = total - ties up to the end of this chunk
+  const unsigned long long T = st->pre[kDigits];
+  const long long need = st->rem[kDigits];
+  // ties after this chunk = total - ties up to the end of this chunk (all 0 when every tie is kept: then
+  // `higher` below is negative, hence < need, for every tie)
+  if (need == st->cnt[kDigits]) {  // every tie kept (the common case): key >= T, no tie ranks
+    for (int it = 0; it < kIt; ++it) {
+      const int64_t e0 = (int64_t)blockIdx.x * kChunk + ((int64_t)it * kT + threadIdx.x) * kE;
+      if (e0 >= n) break;
+      double v[kE];
+      load4(x, e0, n, v);
+#pragma unroll
+      for (int j = 0; j < kE; ++j) v[j] = order_key64(v[j]) >= T ? v[j] : 0.0;
+      store4(out, e0, n, v);
+    }
+    return;
+  }
   long long after = offsets[nchunks] - offsets[blockIdx.x];
   for (int it = 0; it < kIt; ++it) {
     const int64_t e0 = (int64_t)blockIdx.x * kChunk + ((int64_t)it * kT + threadIdx.x) * kE;
@@ -585,25 +755,38 @@ int flc_randk_apply_f64(const double* x, int64_t n, const int32_t* idx, int64_t 
   return FLC_OK;
 }
 
-size_t flc_f64_workspace_size(int64_t n) {
-  Carver c(nullptr, 0);
-  const int64_t nch = cdiv(n < 1 ? 1 : n, kChunk);
-  (void)c.take<int>((size_t)nch);
-  (void)c.take<long long>((size_t)nch + 1);
-  (void)c.take<unsigned long long>((size_t)nch);
-  (void)c.take<Sel64>(1);
-  return c.off;
-}
+}  // extern "C"
 
 namespace {
+// the top-k filter's geometry: sample size, the floor's rank in the sample, and each chunk's candidate segment
+struct Filt64 {
+  int S;
+  long long r_lo;
+  bool on;
+  int segcap;
+};
+Filt64 filt64(int64_t n, int64_t k) {
+  Filt64 f{};
+  if (n < 65536 || k <= 0 || k >= n) return f;
+  f.S = (int)std::min<int64_t>(n, kSample64);
+  const double m = (double)f.S * (double)k / (double)n;
+  f.r_lo = (long long)ceil(m + 4.0 * sqrt(m) + 16.0);
+  if (f.r_lo >= f.S) return f;
+  const double frac = (double)f.r_lo / (double)f.S;
+  f.segcap = (int)align_up((size_t)std::min<double>(kChunk, ceil(2.0 * frac * kChunk) + 256.0), 64);
+  f.on = true;
+  return f;
+}
+
 struct Ws64 {
   int* counts;
   long long* offsets;
   unsigned long long* part;
   Sel64* sel;
+  unsigned long long* seg;  // top-k candidate segments: [chunks][segcap]
   size_t need;
 };
-Ws64 carve64(void* ws, size_t bytes, int64_t n) {
+Ws64 carve64(void* ws, size_t bytes, int64_t n, int64_t k = 0) {
   Carver c(ws, bytes);
   const int64_t nch = cdiv(n < 1 ? 1 : n, kChunk);
   Ws64 w;
@@ -611,10 +794,16 @@ Ws64 carve64(void* ws, size_t bytes, int64_t n) {
   w.offsets = c.take<long long>((size_t)nch + 1);
   w.part = c.take<unsigned long long>((size_t)nch);
   w.sel = c.take<Sel64>(1);
+  const Filt64 f = filt64(n, k);
+  w.seg = c.take<unsigned long long>(f.on ? (size_t)nch * f.segcap : 0);
   w.need = c.off;
   return w;
 }
 }  // namespace
+
+extern "C" {
+
+size_t flc_f64_workspace_size(int64_t n, int64_t k) { return carve64(nullptr, 0, n, k).need; }
 
 int flc_count_consumers_f64(const double* x, int64_t n, const double* norm, int64_t* count, void* ws, size_t ws_bytes,
                             void* stream) {
@@ -735,17 +924,29 @@ int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void*
   if (k <= 0 || k >= n) return fail(FLC_EINVAL, "flc_topk_dense_f64: need 0 < k < n (got k=%lld, n=%lld)",
                                     (long long)k, (long long)n);
   if (!aligned16(x) || !aligned16(out)) return fail(FLC_EINVAL, "flc_topk_dense_f64: 16-B aligned buffers required");
-  Ws64 w = carve64(ws, ws_bytes, n);
+  Ws64 w = carve64(ws, ws_bytes, n, k);
   if (!ws || w.need > ws_bytes) return fail(FLC_EWORKSPACE, "flc_topk_dense_f64: workspace %zu < %zu", ws_bytes, w.need);
   hipStream_t st = as_stream(stream);
   const int64_t nch = cdiv(n, kChunk);
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 2), kT), 256 * 8);
-  FLC_LAUNCH("sel64_init", sel64_init_kernel, dim3(1), dim3(kT), 0, st, w.sel, (long long)k);
-  for (int pass = 0; pass < kDigits; ++pass) {
-    FLC_LAUNCH("sel64_hist", sel64_hist_kernel, dim3(grid), dim3(kT), 0, st, x, n, pass, w.sel);
-    FLC_LAUNCH("sel64_pick", sel64_pick_kernel, dim3(1), dim3(256), 0, st, pass, w.sel);
+  const Filt64 f = filt64(n, k);
+  // the candidates: a sample's floor t_lo (count(key >= t_lo) ~ k + 4 sigma), one filtering pass into per-chunk
+  // segments; the digit passes then read the candidates (~1.3 k keys) instead of x, unless a segment overflowed or the
+  // floor admitted fewer than k elements (then they read x: the same result)
+  FLC_LAUNCH("sel64_init", sel64_init_kernel, dim3((unsigned)std::max<int64_t>(1, cdiv(f.S, kT))), dim3(kT), 0, st, x,
+             n, f.on ? f.S : 0, (long long)k, f.on ? 0 : 1, w.sel);
+  if (f.on) {
+    FLC_LAUNCH("sel64_floor", sel64_floor_kernel, dim3(1), dim3(1024), 0, st, f.S, f.r_lo, w.sel);
+    FLC_LAUNCH("sel64_filter", sel64_filter_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, f.segcap, w.sel, w.seg,
+               w.counts);
   }
-  FLC_LAUNCH("sel64_ties", sel64_ties_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, (const Sel64*)w.sel, w.counts);
+  // (the candidate passes need few blocks: each block flushes up to 256 bins with global atomics; the fallback over x
+  // streams with them too)
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 2), kT), 512);
+  // (each pass first resolves the previous pass's digit; the ties kernel resolves the last one)
+  for (int pass = 0; pass < kDigits; ++pass)
+    FLC_LAUNCH("sel64_hist", sel64_hist_kernel, dim3(grid), dim3(kT), 0, st, x, n, pass, w.sel,
+               (const unsigned long long*)w.seg, (const int*)w.counts, nch, f.on ? f.segcap : 1);
+  FLC_LAUNCH("sel64_ties", sel64_ties_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, w.sel, w.counts);
   FLC_LAUNCH("scan64", scan64_kernel, dim3(1), dim3(1024), 0, st, w.counts, w.offsets, nch);
   FLC_LAUNCH("sel64_emit", sel64_emit_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, (const Sel64*)w.sel,
              (const long long*)w.offsets, nch, out);

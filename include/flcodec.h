@@ -314,13 +314,13 @@ int flc_randk_keys(int64_t n, uint64_t seed, uint64_t counter, float* keys, void
  *                          8-bit codes (sign << 7 | level) and / or the decoded vector lv * sign * norm; nnz =
  *                          count(x != 0) when non-NULL
  *   flc_topk_dense_f64     out = x on the K largest (ties: the highest indices), +0 elsewhere (293-296), 0 < k < n
- * Workspace: flc_f64_workspace_size(n) bytes (compat mode, the norm and top-k; not needed by the element-wise
- * forms or by the Philox-mode encoders). */
+ * Workspace: flc_f64_workspace_size(n, k) bytes (compat mode, the norm and top-k with that k; not needed by the
+ * element-wise forms or by the Philox-mode encoders). */
 int flc_copy_f64(const double* x, int64_t n, double* out, void* stream);
 int flc_scale_div_f64(const double* x, int64_t n, double p, double* out, void* stream);
 int flc_randk_apply_f64(const double* x, int64_t n, const int32_t* idx, int64_t k, double scale, double* out,
                         void* stream);
-size_t flc_f64_workspace_size(int64_t n);
+size_t flc_f64_workspace_size(int64_t n, int64_t k);  /* k: flc_topk_dense_f64's k, else 0 */
 int flc_count_consumers_f64(const double* x, int64_t n, const double* norm, int64_t* count, void* ws, size_t ws_bytes,
                             void* stream);
 int flc_natural_f64(const double* x, int64_t n, uint64_t seed, uint64_t counter, const double* compat_u,

@@ -206,6 +206,25 @@ def test_f64_topk_ties_zeros_nan():
         assert g64.same_bits(got, exp), K
 
 
+def test_f64_topk_filter_fallbacks():
+    """The candidate filter's two ways back to the full passes give the same dense output: a chunk with more
+    candidates than its segment (sorted input), and a sample floor that admits fewer than k elements (every sampled
+    position 0, every other one -1)."""
+    from fl_sim_amd import codec
+
+    n = 1 << 20
+    x = np.sort(_x64(n, 4))  # the largest values all in the last chunks
+    for K in (n // 100, 12_345):
+        exp, _ = ref.topk(x, K)
+        assert g64.same_bits(codec.topk_dense_f64(torch.from_numpy(x).to(DEV), K).cpu().numpy(), exp)
+    S = 32768
+    y = np.full(n, -1.0)
+    y[((np.arange(S) + 0.5) * n / S).astype(np.int64)] = 0.0  # the sample positions
+    for K in (n // 2, S + 5, S - 5):
+        exp, _ = ref.topk(y, K)
+        assert g64.same_bits(codec.topk_dense_f64(torch.from_numpy(y).to(DEV), K).cpu().numpy(), exp)
+
+
 def test_f64_device_tensor_in_device_tensor_out():
     from fl_sim_amd import Compressor
 
@@ -229,3 +248,42 @@ def test_f64_lazy_and_randk_are_fp64_arithmetic():
     exp, _ = ref.randk(x, 777, len(x), idx)
     assert g64.same_bits(got, exp)
     assert g64.same_bits(codec.copy_f64(xd).cpu().numpy(), x)
+
+
+def test_f64_edge_shapes_and_views():
+    """n = 1, odd n, views at an 8-B (not 16-B) offset, non-contiguous and CPU float64 tensors: same results as the
+    oracle / the contiguous aligned input."""
+    from fl_sim_amd import Compressor, codec
+
+    base = torch.from_numpy(_x64(20_011, 9)).to(DEV)
+    view = base[1:]  # 8-B aligned view: copied once to an aligned buffer
+    assert view.data_ptr() % 16 == 8
+    for n in (1, 2, 3, 4097):
+        x = view[:n]
+        exp, _, _ = ref.natural64(x.cpu().numpy(), ref.philox_stream(1, 2, n))
+        _, out = codec.natural_f64(x, 1, 2)
+        assert g64.same_bits(out.cpu().numpy(), exp), n
+        assert g64.same_bits(codec.copy_f64(x).cpu().numpy(), x.cpu().numpy())
+    strided = base[::2]
+    assert not strided.is_contiguous()
+    exp, _ = ref.topk(strided.cpu().numpy(), 100)
+    assert g64.same_bits(codec.topk_dense_f64(strided, 100).cpu().numpy(), exp)
+    # a CPU float64 tensor goes host -> device -> host and comes back a CPU float64 tensor
+    c = Compressor()
+    c.makeTopKCompressor(10, 1000)
+    xc = torch.from_numpy(_x64(1000, 3))
+    out = c.compressVector(xc)
+    assert isinstance(out, torch.Tensor) and out.device.type == "cpu" and out.dtype == torch.float64
+    exp, _ = ref.topk(xc.numpy(), 10)
+    assert g64.same_bits(out.numpy(), exp)
+
+
+def test_f64_other_dtypes_refused():
+    from fl_sim_amd import Compressor
+
+    c = Compressor()
+    c.makeIdenticalCompressor()
+    with pytest.raises(TypeError):
+        c.compressVector(np.arange(10, dtype=np.float16))
+    with pytest.raises(TypeError):
+        c.compressVector(np.arange(10, dtype=np.int64))
