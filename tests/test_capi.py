@@ -199,3 +199,21 @@ def test_rccl_entries_validate_without_gpu():
     assert lib.flc_rccl_allreduce(None, None, 5, None, None) == 1
     assert lib.flc_rccl_allgather(None, None, 0, None, None) == 1
     assert lib.flc_comm_destroy(None) == 0  # destroying nothing is a no-op
+
+
+def test_f64_entries_validate_without_gpu():
+    """The float64 forms (f64.hip, adaptive.hip) reject bad arguments before touching the device, and the top-k
+    workspace grows with k's candidate segments."""
+    lib = _lib.load()
+    assert lib.flc_topk_dense_f64(16, 100, 0, 16, 16, 1 << 30, None) == 1
+    assert "0 < k < n" in lib.flc_last_error().decode()
+    assert lib.flc_topk_dense_f64(24, 100, 5, 16, 16, 1 << 30, None) == 1
+    assert "aligned" in lib.flc_last_error().decode()
+    assert lib.flc_quant_f64(16, 100, 0, 128, 16, 0, 0, None, 16, 16, None, 16, 1 << 30, None) == 1
+    assert "levels" in lib.flc_last_error().decode()
+    assert lib.flc_quant_f64(16, 100, 7, 8, 16, 0, 0, None, 16, 16, None, 16, 1 << 30, None) == 1
+    assert lib.flc_quant_norm_f64(16, 100, 3, 16, 16, 1 << 30, None) == 4  # p = 3: FLC_EUNSUPPORTED
+    assert lib.flc_natural_f64(16, 100, 0, 0, None, None, None, 16, 1 << 30, None) == 1  # neither codes nor out
+    assert lib.flc_adaptive_select_f64(16, 100, 1.5, 16, 16, 16, 1 << 30, None) == 1  # u outside [0, 1)
+    assert lib.flc_f64_workspace_size(1 << 24, 1 << 17) > lib.flc_f64_workspace_size(1 << 24, 0)
+    assert lib.flc_f64_workspace_size(1000, 10) == lib.flc_f64_workspace_size(1000, 0)  # small n: no filter
