@@ -136,6 +136,13 @@ SIGNATURES = {
     "flc_scale_div": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "flc_randk_keys": (c_int, [c_int64, c_uint64, c_uint64, c_void_p, c_void_p]),
     "flc_randk_apply": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
+    "flc_weighted_sum_f64": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_double, c_void_p, c_void_p]),
+    "flc_fedopt_step_f64": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p]
+    ),
+    "flc_feddr_combine_f64": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_double, c_double, c_double, c_int, c_double, c_void_p]
+    ),
     "flc_copy_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_scale_div_f64": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p]),
     "flc_randk_apply_f64": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_double, c_void_p, c_void_p]),

@@ -111,7 +111,7 @@ def update_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Ma
     devs = {mp.device if mp.device.type == "cuda" else g.device for mp, g in zip(model_params, g0s)}
     if len(devs) == 1 and next(iter(devs)).type == "cuda":
         dev = next(iter(devs))
-        gs = [torch.empty(g.shape, dtype=torch.float32, device=dev) for g in g0s]
+        gs = [torch.empty(g.shape, dtype=g.dtype, device=dev) for g in g0s]
         if _fold(gs, [m["gradients"] for m in messages], weights, 1):
             for mp, g in zip(model_params, gs):
                 if isinstance(mp, torch.Tensor) and mp.requires_grad:
@@ -121,7 +121,7 @@ def update_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Ma
     for j, mp in enumerate(model_params):
         g0 = messages[0]["gradients"][j]
         dev = mp.device if mp.device.type == "cuda" else g0.device
-        g = torch.empty(g0.shape, dtype=torch.float32, device=dev)
+        g = torch.empty(g0.shape, dtype=g0.dtype, device=dev)
         codec.weighted_sum(g, [_on(m["gradients"][j], dev) for m in messages], weights, init_mode=1)
         if isinstance(mp, torch.Tensor) and mp.requires_grad:
             mp.grad = g
@@ -238,7 +238,8 @@ def feddr_update(model_params: Sequence[torch.Tensor], y_params: Sequence[torch.
     if kind == "l2":
         sq = 0.0
         for sp in ps:
-            sq += float(codec.quant_norm(sp.reshape(1, -1), 2).item()) ** 2
+            nrm = codec.quant_norm_f64(sp, 2) if sp.dtype == torch.float64 else codec.quant_norm(sp.reshape(1, -1), 2)
+            sq += float(nrm.item()) ** 2
         norm = coeff * math.sqrt(sq)
         f = max(0, 1 - coeff / norm)
         for sp in ps:

@@ -706,17 +706,18 @@ def weighted_sum(dst: torch.Tensor, srcs: Sequence[torch.Tensor], weights: Seque
     """dst = {dst*beta | 0 | dst} then dst = fmaf(w_m, src_m, dst) for each message in order."""
     import ctypes
 
-    if dst.device.type != "cuda" or dst.dtype != torch.float32 or not dst.is_contiguous():
-        raise TypeError("dst must be a contiguous fp32 HIP tensor")
+    f64 = dst.dtype == torch.float64  # float64 models: the fold in fp64, the weights kept double (flc_weighted_sum_f64)
+    if dst.device.type != "cuda" or dst.dtype not in (torch.float32, torch.float64) or not dst.is_contiguous():
+        raise TypeError("dst must be a contiguous fp32 or fp64 HIP tensor")
     n = dst.numel()
-    srcs = [_dev_f32(s, "src") for s in srcs]
+    srcs = [(_dev_f64 if f64 else _dev_f32)(s, "src") for s in srcs]
     for s in srcs:
         if s.numel() != n:
             raise ValueError("every source must have dst's number of elements")
     ptrs = (ctypes.c_void_p * max(len(srcs), 1))(*[s.data_ptr() for s in srcs])
-    ws = (ctypes.c_float * max(len(srcs), 1))(*[float(w) for w in weights])
-    call("flc_weighted_sum", ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(ws, ctypes.c_void_p), len(srcs), n,
-         init_mode, float(beta), _p(dst), _stream(dst.device))
+    ws = ((ctypes.c_double if f64 else ctypes.c_float) * max(len(srcs), 1))(*[float(w) for w in weights])
+    call("flc_weighted_sum_f64" if f64 else "flc_weighted_sum", ctypes.cast(ptrs, ctypes.c_void_p),
+         ctypes.cast(ws, ctypes.c_void_p), len(srcs), n, init_mode, float(beta), _p(dst), _stream(dst.device))
     return dst
 
 
@@ -797,20 +798,29 @@ def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tenso
 
 def fedopt_step(theta: torch.Tensor, delta: torch.Tensor, v: Optional[torch.Tensor], opt: str, lr: float,
                 beta2: float, tau: float) -> None:
-    call("flc_fedopt_step", _p(theta), _p(delta), _p(v), theta.numel(), _lib.FLC_OPT[opt], float(lr), float(beta2),
-         float(tau), _stream(theta.device))
+    dt = theta.dtype
+    for t, name in ((theta, "theta"), (delta, "delta"), (v, "v")):
+        if t is None:
+            continue
+        if t.device.type != "cuda" or t.dtype != dt or dt not in (torch.float32, torch.float64) or not t.is_contiguous():
+            raise TypeError(f"{name} must be a contiguous HIP tensor of theta's dtype (fp32 or fp64)")
+        if t.numel() != theta.numel():
+            raise ValueError("theta, delta and v must have the same number of elements")
+    call("flc_fedopt_step_f64" if dt == torch.float64 else "flc_fedopt_step", _p(theta), _p(delta), _p(v),
+         theta.numel(), _lib.FLC_OPT[opt], float(lr), float(beta2), float(tau), _stream(theta.device))
 
 
 def feddr_combine(theta: torch.Tensor, y: torch.Tensor, x_til: torch.Tensor, alpha: float, cx: float, cy: float,
                   prox: int, prox_c: float) -> None:
     """y = fmaf(alpha, theta - y, y); theta = prox(cx * x_til + cy * y), in place (flc_feddr_combine)."""
+    dt = theta.dtype
     for t, name in ((theta, "theta"), (y, "y"), (x_til, "x_til")):
-        if t.device.type != "cuda" or t.dtype != torch.float32 or not t.is_contiguous():
-            raise TypeError(f"{name} must be a contiguous fp32 HIP tensor")
+        if t.device.type != "cuda" or t.dtype != dt or dt not in (torch.float32, torch.float64) or not t.is_contiguous():
+            raise TypeError(f"{name} must be a contiguous HIP tensor of theta's dtype (fp32 or fp64)")
         if t.numel() != theta.numel():
             raise ValueError("theta, y and x_til must have the same number of elements")
-    call("flc_feddr_combine", _p(theta), _p(y), _p(x_til), theta.numel(), float(alpha), float(cx), float(cy),
-         int(prox), float(prox_c), _stream(theta.device))
+    call("flc_feddr_combine_f64" if dt == torch.float64 else "flc_feddr_combine", _p(theta), _p(y), _p(x_til),
+         theta.numel(), float(alpha), float(cx), float(cy), int(prox), float(prox_c), _stream(theta.device))
 
 
 def delta_flatten(local_params: Sequence[torch.Tensor], global_params: Sequence[torch.Tensor],

@@ -131,6 +131,107 @@ __global__ __launch_bounds__(kThreads) void feddr_combine_kernel(float* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
+// float64 models and messages: the reference's torch ops keep float64 tensors float64 (add_ with alpha is one fp64
+// fma per element, the scalars stay Python doubles), so the same fold / step / FedDR pass run in fp64
+// (flc_weighted_sum_f64, flc_fedopt_step_f64, flc_feddr_combine_f64; per tensor, two doubles per 16-B load)
+// ------------------------------------------------------------------------------------------------
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+struct SrcPack64 {
+  const double* p[kMaxSrc];
+  double w[kMaxSrc];
+  int n;
+};
+
+template <int INIT, bool VEC>
+__global__ __launch_bounds__(kThreads) void weighted_sum64_kernel(SrcPack64 s, int64_t n, double beta,
+                                                                  double* __restrict__ dst) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  if (VEC) {
+    const int64_t n2 = n >> 1;
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n2; i += stride) {
+      double2 a;
+      if (INIT == 1) {
+        a = make_double2(0.0, 0.0);
+      } else {
+        a = reinterpret_cast<const double2*>(dst)[i];
+        if (INIT == 0) a = make_double2(a.x * beta, a.y * beta);
+      }
+      double2 v[kMaxSrc];
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m)
+        if (m < s.n) {
+          const f64x2 q = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(s.p[m]) + i);
+          v[m] = make_double2(q.x, q.y);
+        }
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m) {
+        if (m < s.n) {
+          const double w = s.w[m];
+          a = make_double2(fma(w, v[m].x, a.x), fma(w, v[m].y, a.y));
+        }
+      }
+      reinterpret_cast<double2*>(dst)[i] = a;
+    }
+    return;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    double a = INIT == 1 ? 0.0 : (INIT == 0 ? dst[i] * beta : dst[i]);
+    for (int m = 0; m < s.n; ++m) a = fma(s.w[m], s.p[m][i], a);
+    dst[i] = a;
+  }
+}
+
+template <int OPT>
+__global__ __launch_bounds__(kThreads) void fedopt_step64_kernel(double* __restrict__ theta,
+                                                                 const double* __restrict__ delta, double* __restrict__ v,
+                                                                 int64_t n, double lr, double beta2, double omb,
+                                                                 double nomb, double tau) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const double d = delta[i];
+    if (OPT == FLC_OPT_AVG) {
+      theta[i] = fma(lr, d, theta[i]);  // _fedopt.py:232-233
+      continue;
+    }
+    const double d2 = d * d;
+    double vi = v[i];
+    if (OPT == FLC_OPT_ADAGRAD) {
+      vi = vi + d2;  // _fedopt.py:248-250
+    } else if (OPT == FLC_OPT_YOGI) {
+      const double diff = vi - d2;  // _fedopt.py:252-258
+      const double sg = diff > 0.0 ? 1.0 : (diff < 0.0 ? -1.0 : (diff == 0.0 ? 0.0 : diff));
+      vi = vi + (nomb * d2) * sg;
+    } else {
+      vi = fma(omb, d2, vi * beta2);  // _fedopt.py:260-263
+    }
+    v[i] = vi;
+    theta[i] = theta[i] + (lr * d) / (sqrt(vi) + tau);  // _fedopt.py:235-239
+  }
+}
+
+template <int PROX>
+__global__ __launch_bounds__(kThreads) void feddr_combine64_kernel(double* __restrict__ theta, double* __restrict__ y,
+                                                                   const double* __restrict__ x_til, int64_t n,
+                                                                   double alpha, double cx, double cy, double pc) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const double yo = y[i];
+    const double yn = fma(alpha, theta[i] - yo, yo);
+    y[i] = yn;
+    double t = cx * x_til[i] + cy * yn;
+    if (PROX == FLC_PROX_L1) {
+      double m = fabs(t) - pc;
+      m = m < 0.0 ? 0.0 : m;
+      t = (double)((t > 0.0) - (t < 0.0)) * m;
+    } else if (PROX == FLC_PROX_SCALE) {
+      t = t * pc;
+    }
+    theta[i] = t;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // a whole model in one launch (flc_model_fold): a model's parameters are many small tensors (cnn_femmist_tiny: 8 of
 // 10 .. 401,408 elements), and one fold launch + one step launch per tensor is launch-bound (~14 us each from Python).
 // Block b serves one 4096-element chunk of one tensor (the tensor found from the pack's block offsets, as
@@ -366,6 +467,75 @@ int flc_fedopt_step(float* theta, const float* delta, float* v, int64_t n, int o
     default: return fail(FLC_EINVAL, "flc_fedopt_step: unknown optimiser %d", opt);
   }
 #undef FLC_FO
+  return FLC_OK;
+}
+
+int flc_weighted_sum_f64(const double* const* srcs, const double* weights, int n_src, int64_t n, int init_mode,
+                         double beta, double* dst, void* stream) {
+  if (!dst || n < 0 || n_src < 0 || (n_src > 0 && (!srcs || !weights)))
+    return fail(FLC_EINVAL, "flc_weighted_sum_f64: bad arguments");
+  if (init_mode < 0 || init_mode > 2) return fail(FLC_EINVAL, "flc_weighted_sum_f64: init_mode must be 0, 1 or 2");
+  if (n == 0) return FLC_OK;
+  hipStream_t st = as_stream(stream);
+  bool vec = (n % 2 == 0) && aligned16(dst);
+  for (int m = 0; m < n_src; ++m) {
+    if (!srcs[m]) return fail(FLC_EINVAL, "flc_weighted_sum_f64: null source %d", m);
+    vec = vec && aligned16(srcs[m]);
+  }
+  int done = 0, mode = init_mode;
+  do {
+    SrcPack64 p;
+    p.n = std::min(kMaxSrc, n_src - done);
+    for (int m = 0; m < kMaxSrc; ++m) {
+      p.p[m] = m < p.n ? srcs[done + m] : nullptr;
+      p.w[m] = m < p.n ? weights[done + m] : 0.0;
+    }
+    const unsigned grid = grid_for(vec ? n / 2 : n);
+#define FLC_WS(I, V) FLC_LAUNCH("weighted_sum_f64", (weighted_sum64_kernel<I, V>), dim3(grid), dim3(kThreads), 0, st, p, n, beta, dst)
+    if (mode == 0) { if (vec) FLC_WS(0, true); else FLC_WS(0, false); }
+    else if (mode == 1) { if (vec) FLC_WS(1, true); else FLC_WS(1, false); }
+    else { if (vec) FLC_WS(2, true); else FLC_WS(2, false); }
+#undef FLC_WS
+    done += p.n;
+    mode = 2;
+  } while (done < n_src);
+  return FLC_OK;
+}
+
+int flc_fedopt_step_f64(double* theta, const double* delta, double* v, int64_t n, int opt, double lr, double beta2,
+                        double tau, void* stream) {
+  if (!theta || !delta || n < 0) return fail(FLC_EINVAL, "flc_fedopt_step_f64: bad arguments");
+  if (opt != FLC_OPT_AVG && !v) return fail(FLC_EINVAL, "flc_fedopt_step_f64: v required for adaptive optimisers");
+  if (n == 0) return FLC_OK;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = grid_for(n);
+  const double omb = 1.0 - beta2, nomb = -(1.0 - beta2);  // Python doubles, kept double by float64 torch ops
+#define FLC_FO(O) FLC_LAUNCH("fedopt_step_f64", fedopt_step64_kernel<O>, dim3(grid), dim3(kThreads), 0, st, theta, delta, v, n, lr, beta2, omb, nomb, tau)
+  switch (opt) {
+    case FLC_OPT_AVG: FLC_FO(FLC_OPT_AVG); break;
+    case FLC_OPT_ADAGRAD: FLC_FO(FLC_OPT_ADAGRAD); break;
+    case FLC_OPT_YOGI: FLC_FO(FLC_OPT_YOGI); break;
+    case FLC_OPT_ADAM: FLC_FO(FLC_OPT_ADAM); break;
+    default: return fail(FLC_EINVAL, "flc_fedopt_step_f64: unknown optimiser %d", opt);
+  }
+#undef FLC_FO
+  return FLC_OK;
+}
+
+int flc_feddr_combine_f64(double* theta, double* y, const double* x_til, int64_t n, double alpha, double cx, double cy,
+                          int prox, double prox_c, void* stream) {
+  if (!theta || !y || !x_til || n < 0) return fail(FLC_EINVAL, "flc_feddr_combine_f64: bad arguments");
+  if (n == 0) return FLC_OK;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = grid_for(n);
+#define FLC_DR(P) FLC_LAUNCH("feddr_combine_f64", feddr_combine64_kernel<P>, dim3(grid), dim3(kThreads), 0, st, theta, y, x_til, n, alpha, cx, cy, prox_c)
+  switch (prox) {
+    case FLC_PROX_NONE: FLC_DR(FLC_PROX_NONE); break;
+    case FLC_PROX_L1: FLC_DR(FLC_PROX_L1); break;
+    case FLC_PROX_SCALE: FLC_DR(FLC_PROX_SCALE); break;
+    default: return fail(FLC_EINVAL, "flc_feddr_combine_f64: unknown prox %d", prox);
+  }
+#undef FLC_DR
   return FLC_OK;
 }
 

@@ -377,6 +377,15 @@ int flc_fedopt_step(float* theta, const float* delta, float* v, int64_t n, int o
  *   prox_c = 1/(1+2 coeff); L2Norm: NONE, then the host scales by max(0, 1 - 1/||theta||) with flc_weighted_sum). */
 int flc_feddr_combine(float* theta, float* y, const float* x_til, int64_t n, float alpha, float cx, float cy,
                       int prox, float prox_c, void* stream);
+/* the same three on float64 models and messages (the reference's torch ops keep them float64: add_ with alpha is one
+ * fp64 fma per element, the scalars stay Python doubles, sqrt is IEEE): weights, beta, lr, beta2, tau, alpha, cx, cy
+ * and prox_c are used as given */
+int flc_weighted_sum_f64(const double* const* srcs, const double* weights, int n_src, int64_t n, int init_mode,
+                         double beta, double* dst, void* stream);
+int flc_fedopt_step_f64(double* theta, const double* delta, double* v, int64_t n, int opt, double lr, double beta2,
+                        double tau, void* stream);
+int flc_feddr_combine_f64(double* theta, double* y, const double* x_til, int64_t n, double alpha, double cx, double cy,
+                          int prox, double prox_c, void* stream);
 
 /* ------------------------------------------------------------------ measurement
  * Record HIP events around every launch of the kernel named `kernel_name` (NULL disables);

@@ -26,7 +26,9 @@ Float64 fixtures (``codec_f64.npz``, round 3): every compressor type on float64 
 float64 throughout (identical, lazy, rand-k, top-k, natural, standard / natural dithering at p = inf and 2), plus
 special float64 vectors (subnormals, powers of two across the exponent range, wide magnitudes, ties, NaN for top-k).
 
-Usage:  python tests/golden/gen_golden.py [all|codec|extra|f64|agg|variants]
+Float64 aggregation fixtures (``agg_f64.npz``, round 3): the same server updates on float64 models and messages.
+
+Usage:  python tests/golden/gen_golden.py [all|codec|extra|f64|agg|agg64|variants]
 """
 
 from __future__ import annotations
@@ -495,23 +497,26 @@ def reference_methods() -> Dict[str, types.FunctionType]:
     return fns
 
 
-def make_model(shapes, seed):
+def make_model(shapes, seed, dtype=torch.float32):
     g = torch.Generator().manual_seed(seed)
     m = torch.nn.Module()
     for i, s in enumerate(shapes):
-        m.register_parameter(f"p{i}", torch.nn.Parameter(torch.randn(s, generator=g) * 0.1))
+        m.register_parameter(f"p{i}", torch.nn.Parameter(torch.randn(s, generator=g, dtype=dtype) * 0.1))
     return m
 
 
-def make_msgs(shapes, n, seed, key):
+def make_msgs(shapes, n, seed, key, dtype=torch.float32):
     g = torch.Generator().manual_seed(seed)
     return [
-        {"client_id": i, "train_samples": 100 * (i + 1), "metrics": {}, key: [torch.randn(s, generator=g) * 1e-3 for s in shapes]}
+        {"client_id": i, "train_samples": 100 * (i + 1), "metrics": {},
+         key: [torch.randn(s, generator=g, dtype=dtype) * 1e-3 for s in shapes]}
         for i in range(n)
     ]
 
 
-def gen_aggregation():
+def gen_aggregation(dtype=torch.float32, fname="agg.npz"):
+    """FedOptServer.update, avg_parameters and update_gradients of the reference on models / messages of ``dtype``
+    (agg.npz: float32; agg_f64.npz: float64, which the reference's torch ops keep float64)."""
     fns = reference_methods()
 
     class FakeServer:
@@ -534,13 +539,14 @@ def gen_aggregation():
         for opt, lr, betas, tau in (("avg", 1, (0, 1), 1), ("adam", 0.01, (0.9, 0.99), 1e-3),
                                     ("yogi", 0.01, (0.9, 0.99), 1e-3), ("adagrad", 0.05, (0.0, 0.99), 1e-3)):
             s = FakeServer()
-            s.model = make_model(shapes, 1)
+            s.model = make_model(shapes, 1, dtype)
             s.device = torch.device("cpu")
             s.config = types.SimpleNamespace(optimizer=opt, lr=lr, betas=betas, tau=tau)
             g = torch.Generator().manual_seed(2)
-            s.delta_parameters = [torch.randn(sh, generator=g) * 1e-3 for sh in shapes]
-            s.v_parameters = None if opt == "avg" else [torch.rand(sh, generator=g) * 1e-4 + 1e-6 for sh in shapes]
-            s._received_messages = make_msgs(shapes, 10, 3, "delta_parameters")
+            s.delta_parameters = [torch.randn(sh, generator=g, dtype=dtype) * 1e-3 for sh in shapes]
+            s.v_parameters = (None if opt == "avg" else
+                              [torch.rand(sh, generator=g, dtype=dtype) * 1e-4 + 1e-6 for sh in shapes])
+            s._received_messages = make_msgs(shapes, 10, 3, "delta_parameters", dtype)
             s.update()
             put(f"fedopt_{opt}_{tag}|theta", list(s.model.parameters()))
             put(f"fedopt_{opt}_{tag}|delta", s.delta_parameters)
@@ -550,20 +556,20 @@ def gen_aggregation():
         for size_aware in (False, True):
             for inertia in (0.0, 0.3):
                 s = FakeServer()
-                s.model = make_model(shapes, 4)
+                s.model = make_model(shapes, 4, dtype)
                 s.device = torch.device("cpu")
-                s._received_messages = make_msgs(shapes, 10, 5, "parameters")
+                s._received_messages = make_msgs(shapes, 10, 5, "parameters", dtype)
                 s.avg_parameters(size_aware=size_aware, inertia=inertia)
                 put(f"avgp_{int(size_aware)}_{inertia}_{tag}|theta", list(s.model.parameters()))
         # update_gradients
         s = FakeServer()
-        s.model = make_model(shapes, 6)
+        s.model = make_model(shapes, 6, dtype)
         s.device = torch.device("cpu")
-        s._received_messages = make_msgs(shapes, 10, 7, "gradients")
+        s._received_messages = make_msgs(shapes, 10, 7, "gradients", dtype)
         s.update_gradients()
         put(f"gradients_{tag}|grad", [p.grad for p in s.model.parameters()])
-    np.savez_compressed(OUT / "agg.npz", **store)
-    print("agg.npz:", len(store), "arrays")
+    np.savez_compressed(OUT / fname, **store)
+    print(f"{fname}:", len(store), "arrays")
 
 
 # --------------------------------------------------------------------- aggregation variants
@@ -744,6 +750,8 @@ def main():
         gen_f64(load_reference_compressors())
     if only in ("all", "agg"):
         gen_aggregation()
+    if only in ("all", "agg", "agg64"):
+        gen_aggregation(torch.float64, "agg_f64.npz")
     if only in ("all", "variants"):
         gen_variants()
     return 0
