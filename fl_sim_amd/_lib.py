@@ -132,6 +132,7 @@ SIGNATURES = {
     "flc_adaptive_select_f64": (
         c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     ),
+    "flc_adaptive_stats": (c_int, [c_void_p, c_size_t, c_int64, c_void_p, c_void_p]),
     "flc_copy": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_scale_div": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "flc_randk_keys": (c_int, [c_int64, c_uint64, c_uint64, c_void_p, c_void_p]),

@@ -666,6 +666,18 @@ def adaptive_select(x: torch.Tensor, u: float, out: Optional[torch.Tensor] = Non
     return out, index
 
 
+def adaptive_stats(x: torch.Tensor) -> dict:
+    """Diagnostics of the last :func:`adaptive_select` on x's workspace (host sync): special chunks, special maps
+    taken, chunks re-run sequentially, and whether the exact sequential chain ran instead."""
+    x = x.reshape(-1)
+    n = x.numel()
+    ws = workspace(x.device, _lib.size("flc_adaptive_workspace_size", n), "adaptive")
+    st = torch.empty(4, dtype=torch.int32, device=x.device)
+    call("flc_adaptive_stats", _p(ws), ws.numel(), n, _p(st), _stream(x.device))
+    s = [int(v) for v in st.cpu()]
+    return {"special": s[0], "taken": s[1], "reruns": s[2], "sequential": s[3]}
+
+
 # ------------------------------------------------------------------------------------------------- misc
 def copy(x: torch.Tensor) -> torch.Tensor:
     x = _dev_f32(x)

@@ -26,9 +26,13 @@
 // exactly.  Such maps compose (a pair of increments per input parity), so:
 //   * a segmented scan composes the maps of consecutive chunks of one binade inside blocks of kPieceBlk chunks
 //     ("pieces"); a chunk whose runs leave their binade, or come within kEta of its edges, is a piece of its own
-//     that is re-run sequentially (about one per binade the running sum crosses: ~20 per call);
-//   * one wave walks the pieces in order (O(1) per composed piece, kChunk dependent adds per re-run chunk), checking
-//     that every composed piece starts and ends in its binade — which makes every chunk map in it exact;
+//     that is special: K3b runs it from four starts G + r (the guess's grid index, r = 0..3) and records, per run,
+//     its end and the largest shift d (d = 0 mod 4) under which the run shifted by d stays the run from G + r + d —
+//     across one binade edge too, where the spacing doubles (a shift by a multiple of 4 spacings is an even multiple
+//     of the new binade's spacing);
+//   * one wave walks the pieces in order (O(1) per composed piece and per special chunk whose true start lies within
+//     its run's margin; kChunk dependent adds for a chunk re-run), checking that every composed piece starts and ends
+//     in its binade — which makes every chunk map in it exact;
 //   * every chunk's exact start then follows in parallel from its piece's start and its exclusive prefix map, and
 //     the chunk holding searchsorted(u) is found in the same pass and re-run to find the index.
 // If a check fails (never expected: the margins are ~100x the guesses' error) the exact chunk-by-chunk chain runs
@@ -57,6 +61,8 @@ constexpr int kWalkBatch = 1024;           // piece records staged in LDS per st
 constexpr int kMaxScanBlocks = 8192;       // ceil(2^31 / kChunk / kPieceBlk)
 constexpr double kEta = 1.0 / 65536.0;     // relative margin to a binade edge for a speculated chunk
 constexpr int kRecLegacy = 1024;           // chunk records staged in LDS per step of the sequential chain
+constexpr int kSpecMax = 4096;             // special chunks per call (more: re-run)
+constexpr int kSpecLds = 256;              // special chunks' maps staged in LDS per step of the walk
 
 // status word (device int32) written by ar_check
 constexpr int kStNan = 1, kStSum = 2;
@@ -93,9 +99,21 @@ __device__ __forceinline__ Vec16<T> load16(const T* __restrict__ x, int64_t e, i
 
 // A piece: chunks [first, last] of one scan block.  e >= 1: chunks of binade e whose maps compose to (inc0, inc1);
 // e < 0: one chunk re-run from its exact start (inc0 / inc1 then hold its guess and the end of the run from it).
+// e <= -2: a special chunk, its four-run map in spec[-2 - e] (the walk's LDS slot of it in `slot`).
 struct Rec {
   long long inc0, inc1;
-  int first, last, e, pad;
+  int first, last, e, slot;
+};
+
+// A special chunk (K3b): runs from the grid indices G + r of binade E.  Run r ends at grid index end[r] of binade
+// E + ((cross >> r) & 1); a true start m = G + r + d (d = 0 mod 4, |d| <= margin[r]) ends at end[r] + d (no crossing)
+// or end[r] + d / 2 (crossed).  margin[r] < 0: run r is unusable.
+struct Spec {
+  long long G;
+  long long end[4];
+  long long margin[4];
+  int E, cross;
+  long long chunk;
 };
 
 struct ArWs {
@@ -117,8 +135,11 @@ struct ArWs {
   double* start;     // [nq + 1] exact running sum before each chunk; start[nq] = cdf[-1]
   double* p_part;    // [ceil(nq / 256)] partial fp64 sums of p (the "sum to 1" check)
   double* total;     // [1] S (in x's type, stored exactly)
+  Spec* spec;        // [kSpecMax] special chunks (K3 appends, K3b fills)
+  int32_t* nspec;    // [1] special chunks appended (may exceed kSpecMax: the rest are re-run)
   int32_t* status;   // [1]
   int32_t* fail;     // [1] 1: the speculation did not verify, the sequential chain ran
+  int32_t* stats;    // [4] the walk's counts: special chunks, special maps taken, chunks re-run, sequential chain
   long long* lo;     // [1] chunk holding searchsorted(u)
 };
 
@@ -133,6 +154,23 @@ __device__ __forceinline__ long long apply_map(long long m, long long i0, long l
 __device__ __forceinline__ long long to_grid(double t, int e) { return (long long)ldexp(t, 1075 - e); }
 __device__ __forceinline__ double from_grid(long long m, int e) { return ldexp((double)m, e - 1075); }
 __device__ __forceinline__ bool in_binade(long long m) { return m >= (1ll << 52) && m < (1ll << 53); }
+// wave-uniform copies (SGPRs) of a lane-0 value
+__device__ __forceinline__ int rfl32(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {  // lane l's value (l wave-uniform)
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
+// the same two conversions as bit operations, for a normal t of binade e and m in [2^52, 2^53) (the walk's chain)
+__device__ __forceinline__ long long grid_bits(double t) {
+  return (long long)(((uint64_t)__double_as_longlong(t) & ((1ull << 52) - 1)) | (1ull << 52));
+}
+__device__ __forceinline__ double bits_grid(long long m, int e) {
+  return __longlong_as_double(((long long)e << 52) | (m & ((1ll << 52) - 1)));
+}
 
 // ---- numpy's pairwise_sum on fp32 (loops_utils.h.src) ------------------------------------------------
 template <class T>
@@ -159,10 +197,21 @@ __device__ T pw_leaf(const T* a, int n) {
 // the leaves in order, then the internal nodes in post-order, each the sum of two earlier values (value code c: leaf
 // c for c < 128, node c - 128 otherwise).  <= 128 leaves and <= 127 nodes for a buffer of <= 8192 elements.
 struct TailProg {
-  int nleaf, nop;
+  int nleaf, nop, nlvl;
   short lf_start[128], lf_len[128];
   unsigned char op_a[128], op_b[128];
+  unsigned char op_lvl[128];  // 1 + the larger of its operands' levels (leaves: 0); one level's nodes are independent
 };
+
+void tail_prog_levels(TailProg& p) {  // (host)
+  p.nlvl = 0;
+  for (int o = 0; o < p.nop; ++o) {
+    const int la = p.op_a[o] < 128 ? 0 : p.op_lvl[p.op_a[o] - 128];
+    const int lb = p.op_b[o] < 128 ? 0 : p.op_lvl[p.op_b[o] - 128];
+    p.op_lvl[o] = (unsigned char)(1 + std::max(la, lb));
+    p.nlvl = std::max(p.nlvl, (int)p.op_lvl[o]);
+  }
+}
 
 int tail_prog_build(TailProg& p, int s0, int m) {  // (host) returns the value code of pairwise_sum(a + s0, m)
   if (m <= kLeaf) {
@@ -218,58 +267,85 @@ __global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const T* __restrict_
   if (l == 0) ws.buf_sum[b] = (double)s;
 }
 
-// ---- K1b: the last, partial buffer (an irregular tree): leaves in parallel, the tree's <= 127 additions on one
-// thread from the host-built program --------------------------------------------------------------------------------
+// ---- K1b: the last, partial buffer (an irregular tree): leaves in parallel, then the tree's <= 127 additions level by
+// level (the host-built program; every addition as in the tree, so the same sum) -------------------------------------
 template <class T>
-__global__ __launch_bounds__(128) void ar_tail_sum_kernel(const T* __restrict__ x, int64_t n, TailProg prog,
-                                                          ArWs ws) {
+__global__ __launch_bounds__(1024) void ar_tail_sum_kernel(const T* __restrict__ x, int64_t n, TailProg prog,
+                                                           ArWs ws) {
+  constexpr int VN = Vec16<T>::N;
   __shared__ T sh[kBuf];
   __shared__ T lf_sum[128], op_sum[128];
   const int tid = threadIdx.x;
   const int64_t b = n / kBuf;
   const int len = (int)(n - b * kBuf);
-  for (int i = tid; i < len; i += 128) sh[i] = abs_of(x[b * kBuf + i]);
+  for (int v = tid; v * VN < len; v += 1024) {
+    const Vec16<T> q = load16(x + b * kBuf, (int64_t)v * VN, (int64_t)len);
+#pragma unroll
+    for (int c = 0; c < VN; ++c) sh[v * VN + c] = abs_of(q.e[c]);
+  }
   __syncthreads();
   if (tid < prog.nleaf) lf_sum[tid] = pw_leaf(sh + prog.lf_start[tid], prog.lf_len[tid]);
-  // guesses: an fp64 sum of |x| per chunk of the partial buffer (any order)
-  if (tid < kQ && tid * kChunk < len) {
+  // guesses: an fp64 sum of |x| per chunk of the partial buffer (any order: eight 32-element parts per chunk)
+  if (tid < kQ * 8) {
+    const int c = tid >> 3, lo = c * kChunk + (tid & 7) * 32, hi = std::min(len, lo + 32);
     double s = 0.0;
-    const int hi = std::min(len, (tid + 1) * kChunk);
-    for (int i = tid * kChunk; i < hi; ++i) s += (double)sh[i];
-    ws.q_abs[b * kQ + tid] = s;
+    for (int i = lo; i < hi; ++i) s += (double)sh[i];
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    if ((tid & 7) == 0 && c * kChunk < len) ws.q_abs[b * kQ + c] = s;
+  }
+  for (int l = 1; l <= prog.nlvl; ++l) {
+    __syncthreads();
+    if (tid < prog.nop && prog.op_lvl[tid] == l) {
+      const int a = prog.op_a[tid], c = prog.op_b[tid];
+      op_sum[tid] = (a < 128 ? lf_sum[a] : op_sum[a - 128]) + (c < 128 ? lf_sum[c] : op_sum[c - 128]);
+    }
   }
   __syncthreads();
-  if (tid == 0) {
-    for (int o = 0; o < prog.nop; ++o) {
-      const int a = prog.op_a[o], c = prog.op_b[o];
-      op_sum[o] = (a < 128 ? lf_sum[a] : op_sum[a - 128]) + (c < 128 ? lf_sum[c] : op_sum[c - 128]);
-    }
-    ws.buf_sum[b] = (double)(prog.nop ? op_sum[prog.nop - 1] : lf_sum[0]);
-  }
+  if (tid == 0) ws.buf_sum[b] = (double)(prog.nop ? op_sum[prog.nop - 1] : lf_sum[0]);
 }
 
-// ---- K2: S (buffers folded in order, fp32) and the fp64 prefix of the buffer sums (guesses) --------------
+// ---- K2: S (buffers folded in order, in x's type) and the fp64 prefix of the buffer sums (guesses) -------------
+// The fold is one dependent chain of adds: thread 0 reads the tile 16 B at a time (the reads off the chain).  Past
+// nbuf the tile holds +0, which leaves S (a sum of |x|, never -0) unchanged.
 template <class T>
 __global__ __launch_bounds__(1024) void ar_total_kernel(int64_t nbuf, ArWs ws) {
   __shared__ __attribute__((aligned(16))) T tile[1024];
   __shared__ double scan_lds[1024 / kWave];
+  const int tid = threadIdx.x;
   T S = 0;
   double carry = 0.0;
+  if (tid == 0) ws.nspec[0] = 0;  // (phase A, the next kernel but one, appends the special chunks)
   for (int64_t base = 0; base < nbuf; base += 1024) {
-    const int64_t i = base + threadIdx.x;
+    const int64_t i = base + tid;
     const T v = i < nbuf ? (T)ws.buf_sum[i] : (T)0;
-    tile[threadIdx.x] = v;
+    tile[tid] = v;
     double tot;
     const double ex = block_excl_scan<double, 1024 / kWave>((double)v, scan_lds, &tot);  // (syncs: tile ready)
     if (i < nbuf) ws.bpre[i] = carry + ex;
     carry += tot;
-    if (threadIdx.x == 0) {
-      const int cnt = (int)std::min<int64_t>(1024, nbuf - base);
-      for (int j = 0; j < cnt; ++j) S = S + tile[j];
+    if (tid == 0) {
+      constexpr int VN = Vec16<T>::N;
+      const int nv = (int)((std::min<int64_t>(1024, nbuf - base) + VN - 1) / VN);
+#pragma unroll 8
+      for (int j = 0; j < nv; ++j) {
+        if constexpr (sizeof(T) == 4) {
+          const float4 q = reinterpret_cast<const float4*>(tile)[j];
+          S = S + q.x;
+          S = S + q.y;
+          S = S + q.z;
+          S = S + q.w;
+        } else {
+          const double2 q = reinterpret_cast<const double2*>(tile)[j];
+          S = S + q.x;
+          S = S + q.y;
+        }
+      }
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) ws.total[0] = (double)S;
+  if (tid == 0) ws.total[0] = (double)S;
 }
 
 // ---- K3 (phase A): per chunk, the two speculative runs, the chunk's map and its sum of p ------------------
@@ -338,7 +414,18 @@ __global__ __launch_bounds__(256) void ar_phase_a_kernel(const T* __restrict__ x
     ws.end_b[j] = cb;
     ws.fn[2 * j] = i0;
     ws.fn[2 * j + 1] = i1;
-    ws.fe[j] = ok ? E : -1;
+    int fe = ok ? E : -1;
+    if (!ok && E >= 1 && E <= 2044 && binade(ca) <= E + 1) {  // crosses one edge, or near one: a special chunk
+      const int idx = atomicAdd(ws.nspec, 1);
+      if (idx < kSpecMax) {
+        Spec* sp = ws.spec + idx;
+        sp->G = to_grid(ga, E);
+        sp->E = E;
+        sp->chunk = j;
+        fe = -2 - idx;
+      }
+    }
+    ws.fe[j] = fe;
   }
   const double s = wave_sum(j < nq ? ps : 0.0);
   if (lane == 0) red[wid] = s;
@@ -435,31 +522,75 @@ __global__ __launch_bounds__(kPieceBlk) void ar_piece_kernel(int64_t nq, ArWs ws
 }
 
 // Exact sequential run of chunk u from its exact start t by one wave (every lane ends with the same t).  The
-// chunk's elements are v (4 per lane, lane-major); with cD > 0 each lane also returns, per element it holds, the
-// normalised cdf test c / cD > u as a bit of *hits.
+// chunk's elements are v (4 per lane, lane-major); their p values are staged in the wave's LDS scratch qs (kChunk
+// doubles) and every lane reads them in order (same address: a broadcast; the reads are off the add chain).  With
+// cD > 0 each lane also returns, per element it holds, the normalised cdf test c / cD > u as a bit of *hits.
 template <class T>
 struct Four {
   T a, b, c, d;
 };
 template <class T>
-__device__ double wave_run(const Four<T> v, double t, T S, double cD = 0.0, double u = 0.0, unsigned* hits = nullptr) {
+__device__ __forceinline__ void stage_q(const Four<T> v, T S, double* qs) {
   const int lane = threadIdx.x & (kWave - 1);
-  const double q0 = q_of(v.a, S), q1 = q_of(v.b, S);
-  const double q2 = q_of(v.c, S), q3 = q_of(v.d, S);
-  unsigned h = 0;
-#pragma unroll 4
+  __builtin_amdgcn_wave_barrier();  // (this wave's earlier reads of qs come first: LDS ops complete in order)
+  reinterpret_cast<double2*>(qs)[2 * lane] = make_double2(q_of(v.a, S), q_of(v.b, S));
+  reinterpret_cast<double2*>(qs)[2 * lane + 1] = make_double2(q_of(v.c, S), q_of(v.d, S));
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <class T>
+__device__ double wave_run(const Four<T> v, double t, T S, double* qs, double cD = 0.0, double u = 0.0,
+                           unsigned* hits = nullptr) {
+  const int lane = threadIdx.x & (kWave - 1);
+  stage_q(v, S, qs);
+  const double2* q2 = reinterpret_cast<const double2*>(qs);
+  double k0 = 0.0, k1 = 0.0, k2 = 0.0, k3 = 0.0;  // (hits) this lane's own four running sums
+#pragma unroll 8
   for (int L = 0; L < kWave; ++L) {
-    t = t + lane_bcast(q0, L);
+    const double2 a = q2[2 * L], b = q2[2 * L + 1];
+    t = t + a.x;
     const double c0 = t;
-    t = t + lane_bcast(q1, L);
+    t = t + a.y;
     const double c1 = t;
-    t = t + lane_bcast(q2, L);
+    t = t + b.x;
     const double c2 = t;
-    t = t + lane_bcast(q3, L);
-    if (hits && lane == L)
-      h = (c0 / cD > u ? 1u : 0u) | (c1 / cD > u ? 2u : 0u) | (c2 / cD > u ? 4u : 0u) | (t / cD > u ? 8u : 0u);
+    t = t + b.y;
+    if (hits && lane == L) {
+      k0 = c0;
+      k1 = c1;
+      k2 = c2;
+      k3 = t;
+    }
   }
-  if (hits) *hits = h;
+  // (the divisions after the chain, all lanes at once, not 256 of them on it)
+  if (hits) *hits = (k0 / cD > u ? 1u : 0u) | (k1 / cD > u ? 2u : 0u) | (k2 / cD > u ? 4u : 0u) | (k3 / cD > u ? 8u : 0u);
+  return t;
+}
+
+// The same run from a per-lane start t, also returning the last running sum below `edge` (or the start) and the
+// first at or above it (or inf).
+template <class T>
+__device__ double wave_run_edges(const Four<T> v, double t, T S, double* qs, double edge, double* below,
+                                 double* above) {
+  stage_q(v, S, qs);
+  const double2* q2 = reinterpret_cast<const double2*>(qs);
+  double lo = t, hi = __longlong_as_double(0x7ff0000000000000ll);
+#define FLC_AR_STEP(q)    \
+  t = t + (q);            \
+  lo = t < edge ? t : lo; \
+  hi = (t >= edge && t < hi) ? t : hi;
+#pragma unroll 8
+  for (int L = 0; L < kWave; ++L) {
+    const double2 a = q2[2 * L], b = q2[2 * L + 1];
+    FLC_AR_STEP(a.x)
+    FLC_AR_STEP(a.y)
+    FLC_AR_STEP(b.x)
+    FLC_AR_STEP(b.y)
+  }
+#undef FLC_AR_STEP
+  *below = lo;
+  *above = hi;
   return t;
 }
 
@@ -479,19 +610,89 @@ __device__ __forceinline__ Four<T> load_chunk4(const T* __restrict__ x, int64_t 
   return Four<T>{e < n ? x[e] : (T)0, e + 1 < n ? x[e + 1] : (T)0, e + 2 < n ? x[e + 2] : (T)0, (T)0};
 }
 
+// ---- K3b: the special chunks' four runs (one wave per chunk; lane r & 3 runs from G + r) -----------------------
+// Run r is the true run from G + r + d (d = 0 mod 4) when the true start is in binade E and |d| <= margin[r]:
+//   * no crossing: every sum of the run shifted by d stays below the edge 2^(E+1) while it is <= margin + 2 spacings
+//     from it, and round-to-nearest-even commutes with a shift by an even multiple of the spacing;
+//   * one crossing: the sums before it stay below the edge (lo), the first one after it stays above (hi, in spacings
+//     of E; its rounding error is at most one), and the rest stay below 2^(E+2) (top).  In binade E + 1 the shift d is
+//     an even multiple of the spacing 2 U because d = 0 mod 4.
+template <class T>
+__global__ __launch_bounds__(256) void ar_special_kernel(const T* __restrict__ x, int64_t n, ArWs ws) {
+  if (ws.status[0] != 0) return;
+  __shared__ double q_lds[256 / kWave][kChunk];
+  const int nsp = min(ws.nspec[0], kSpecMax);
+  const int lane = threadIdx.x & (kWave - 1), r = lane & 3;
+  const T S = (T)ws.total[0];
+  for (int s = blockIdx.x * (256 / kWave) + (threadIdx.x >> 6); s < nsp; s += gridDim.x * (256 / kWave)) {
+    Spec* sp = ws.spec + s;
+    const int E = sp->E;
+    const long long G = sp->G;
+    const Four<T> v = load_chunk4(x, n, sp->chunk);
+    const bool valid = G + r >= (1ll << 52) && G + r < (1ll << 53);
+    const double edge = ldexp(1.0, E - 1022);
+    double below, above;
+    const double t =
+        wave_run_edges(v, from_grid(valid ? G + r : (1ll << 52), E), S, q_lds[threadIdx.x >> 6], edge, &below, &above);
+    long long end = 0, margin = -1;
+    int cross = 0;
+    if (valid) {
+      const int eb = binade(t);
+      if (eb == E) {
+        end = to_grid(t, E);
+        margin = to_grid(edge - t, E) - 2;
+      } else if (eb == E + 1) {
+        cross = 1;
+        end = to_grid(t, E + 1);
+        const long long lo = to_grid(edge - below, E), hi = to_grid(above - edge, E), top = to_grid(2.0 * edge - t, E);
+        margin = std::min(std::min(lo, hi), top) - 2;
+      }
+    }
+    const unsigned long long cm = __ballot(cross != 0);
+    if (lane < 4) {
+      sp->end[r] = end;
+      sp->margin[r] = margin;
+    }
+    if (lane == 0) sp->cross = (int)(cm & 15ull);
+  }
+}
+
 // ---- K6: the walk — every piece's exact start, in order, on one wave ---------------------------------------
+// Blocks 1.. of the launch write the dense output's zeros meanwhile (the walk is one wave's latency chain).
 template <class T>
 __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, int64_t n, int64_t nq, int nblk,
-                                                       int force_seq, ArWs ws) {
+                                                       int force_seq, ArWs ws, T* __restrict__ out) {
   __shared__ int off[kMaxScanBlocks];
   __shared__ Rec batch[kWalkBatch];
+  __shared__ Spec spec_lds[kSpecLds];
+  __shared__ double t_lds[kWalkBatch], end_lds[kWalkBatch];  // the batch's piece starts / ends (written out after)
+  __shared__ double q_lds[kChunk];                             // wave 0's re-run scratch
   __shared__ int scan_lds[1024 / kWave];
-  __shared__ int s_bad, s_total;
+  __shared__ int s_bad, s_total, s_taken, s_reruns;
   __shared__ double s_t;
   if (ws.status[0] != 0) return;
   const int tid = threadIdx.x;
+  if (blockIdx.x > 0) {  // out = 0 (16-B stores past a head of < 16 B; the final kernel writes out[ind] later)
+    constexpr int VN = Vec16<T>::N;
+    const int64_t head = std::min<int64_t>(n, (int64_t)((16 - ((uintptr_t)out & 15)) & 15) / (int64_t)sizeof(T));
+    const int64_t nv = (n - head) / VN;
+    const int64_t stride = (int64_t)(gridDim.x - 1) * 1024;
+    uint4* o4 = reinterpret_cast<uint4*>(out + head);
+    for (int64_t i = (int64_t)(blockIdx.x - 1) * 1024 + tid; i < nv; i += stride) o4[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (blockIdx.x == 1) {
+      if (tid < head) out[tid] = (T)0;
+      if (tid < n - head - nv * VN) out[head + nv * VN + tid] = (T)0;
+    }
+    return;
+  }
+#if FLC_CALIB_AR_STAMPS  // calibration builds only: the walk's phase times (10 ns ticks) replace the stats
+  const uint64_t st0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t st1 = 0, st2 = 0, st3 = 0, st4 = 0;
+#endif
   if (tid == 0) {
     s_bad = force_seq;
+    s_taken = 0;
+    s_reruns = 0;
     s_t = 0.0;  // cdf starts from 0: c_0 = 0 + p_0
   }
   __syncthreads();
@@ -512,9 +713,13 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
   if (tid == 0) s_total = carry;
   __syncthreads();
   const int total = s_total;
+#if FLC_CALIB_AR_STAMPS
+  st1 = __builtin_amdgcn_s_memrealtime();
+#endif
   const T S = (T)ws.total[0];
   for (int g0 = 0; g0 < total && !s_bad; g0 += kWalkBatch) {
     const int g = g0 + tid;
+    Rec rc{};
     if (g < total) {  // the block holding piece g: the last b with off[b] <= g
       int lo = 0, hi = nblk - 1;
       while (lo < hi) {
@@ -522,51 +727,117 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
         if (off[mid] <= g) lo = mid;
         else hi = mid - 1;
       }
-      batch[tid] = ws.rec[(size_t)lo * kRecMax + (g - off[lo])];
+      rc = ws.rec[(size_t)lo * kRecMax + (g - off[lo])];
+    }
+    // the batch's special chunks' maps into LDS slots (beyond kSpecLds of them: read from memory on the walk)
+    const bool is_sp = g < total && rc.e <= -2;
+    int nsp;
+    const int slot = block_excl_scan<int, 1024 / kWave>(is_sp ? 1 : 0, scan_lds, &nsp);
+    if (g < total) {
+      rc.slot = (is_sp && slot < kSpecLds) ? slot : -1;
+      if (rc.slot >= 0) spec_lds[slot] = ws.spec[-2 - rc.e];
+      batch[tid] = rc;
     }
     __syncthreads();
-    if (tid < kWave) {  // wave 0 walks the batch (every lane computes the same t)
+#if FLC_CALIB_AR_STAMPS
+    if (g0 == 0) st2 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (tid < kWave) {  // wave 0 walks the batch
+      // The state is t's bit pattern, wave-uniform (readfirstlane of every record field), so the chain of a composed
+      // piece is a few scalar integer ops on it: grid index = mantissa | 2^52, binade = the exponent field.
       const int cnt = std::min(kWalkBatch, total - g0);
-      double t = s_t;
+      uint64_t tb = rfl64((uint64_t)__double_as_longlong(s_t));
       bool bad = false;
-      // the next re-run chunk's elements are loaded one re-run ahead
-      int nxt = 0;
-      while (nxt < cnt && batch[nxt].e >= 1) ++nxt;
-      Four<T> v = nxt < cnt ? load_chunk4(x, n, batch[nxt].first) : Four<T>{0, 0, 0, 0};
-      for (int r = 0; r < cnt && !bad; ++r) {
-        const Rec rc = batch[r];
-        if (tid == 0) ws.rec_t[g0 + r] = t;
-        if (rc.e >= 1) {
-          if (binade(t) != rc.e) {
-            bad = true;
-            break;
+      int taken = 0, reruns = 0;
+      // records in windows of 64: lane i holds record w0 + i (one LDS read per lane per window), the step takes its
+      // fields with readlane, and lane i keeps the step's start / end for one store per lane after the window
+      const int lane = tid;
+      constexpr uint64_t kMant = (1ull << 52) - 1, kHid = 1ull << 52;
+      for (int w0 = 0; w0 < cnt && !bad; w0 += kWave) {
+        const int wn = std::min(kWave, cnt - w0);
+        Rec mine{};
+        if (lane < wn) mine = batch[w0 + lane];
+        uint64_t my_t = 0, my_end = 0;
+        for (int i = 0; i < wn; ++i) {
+          const int e = __builtin_amdgcn_readlane(mine.e, i), first = __builtin_amdgcn_readlane(mine.first, i);
+          const int slot = __builtin_amdgcn_readlane(mine.slot, i);
+          const uint64_t inc0 = rl64((uint64_t)mine.inc0, i), inc1 = rl64((uint64_t)mine.inc1, i);
+          my_t = lane == i ? tb : my_t;
+          if (e >= 1) {  // a composed piece of binade e: its map on the grid index
+            const uint64_t m = (tb & kMant) | kHid;
+            const uint64_t m2 = m + ((m & 1) ? inc1 : inc0);
+            if ((int)(tb >> 52) != e || m2 < kHid || m2 >= 2 * kHid) {
+              bad = true;
+              break;
+            }
+            tb = ((uint64_t)e << 52) | (m2 & kMant);
+          } else {
+            bool done = false;
+            if (e <= -2) {  // a special chunk: its run's map when the true start is within its margin
+              const Spec* sp = slot >= 0 ? spec_lds + slot : ws.spec + (-2 - e);
+              const int se = rfl32(sp->E), cross = rfl32(sp->cross);
+              const long long m = (long long)((tb & kMant) | kHid);
+              const long long G = (long long)rfl64((uint64_t)sp->G);
+              const int rr = (int)((m - G) & 3);
+              const long long d = m - G - rr;
+              const long long mg = (long long)rfl64((uint64_t)sp->margin[rr]);
+              const long long end = (long long)rfl64((uint64_t)sp->end[rr]);
+              const int cr = (cross >> rr) & 1;
+              const long long m2 = end + (cr ? d / 2 : d);
+              if ((int)(tb >> 52) == se && mg >= 0 && (d < 0 ? -d : d) <= mg && in_binade(m2)) {
+                tb = ((uint64_t)(se + cr) << 52) | ((uint64_t)m2 & kMant);
+                done = true;
+                ++taken;
+              }
+            }
+            if (!done) {
+              if (tb == inc0) {
+                tb = inc1;  // started at the guess: the run from it is the run
+              } else {
+                const double t = wave_run(load_chunk4(x, n, first), __longlong_as_double((long long)tb), S, q_lds);
+                tb = rfl64((uint64_t)__double_as_longlong(t));
+                ++reruns;
+              }
+            }
           }
-          const long long m = apply_map(to_grid(t, rc.e), rc.inc0, rc.inc1);
-          if (!in_binade(m)) {
-            bad = true;
-            break;
-          }
-          t = from_grid(m, rc.e);
-        } else {
-          const Four<T> cur = v;
-          int nn = r + 1;
-          while (nn < cnt && batch[nn].e >= 1) ++nn;
-          if (nn < cnt) v = load_chunk4(x, n, batch[nn].first);
-          if (t == __longlong_as_double(rc.inc0)) t = __longlong_as_double(rc.inc1);  // started at the guess
-          else t = wave_run(cur, t, S);
+          my_end = lane == i ? tb : my_end;
         }
-        if (tid == 0) ws.rec_end[g0 + r] = t;
+        if (lane < wn) {
+          t_lds[w0 + lane] = __longlong_as_double((long long)my_t);
+          end_lds[w0 + lane] = __longlong_as_double((long long)my_end);
+        }
       }
+      const double t = __longlong_as_double((long long)tb);
       if (tid == 0) {
         s_t = t;
         if (bad) s_bad = 1;
+        s_taken += taken;
+        s_reruns += reruns;
+#if FLC_CALIB_AR_STAMPS
+        st4 = __builtin_amdgcn_s_memrealtime();
+#endif
       }
     }
     __syncthreads();
+    if (g < total) {  // (read before the next batch's barriers let wave 0 rewrite them)
+      ws.rec_t[g] = t_lds[tid];
+      ws.rec_end[g] = end_lds[tid];
+    }
   }
   if (tid == 0) {
     ws.start[nq] = s_t;
     ws.fail[0] = s_bad;
+    ws.stats[0] = ws.nspec[0];
+    ws.stats[1] = s_taken;
+    ws.stats[2] = s_reruns;
+    ws.stats[3] = s_bad;
+#if FLC_CALIB_AR_STAMPS
+    st3 = __builtin_amdgcn_s_memrealtime();
+    ws.stats[0] = (int)(st1 - st0);
+    ws.stats[1] = (int)(st2 - st0);
+    ws.stats[2] = (int)(st3 - st0);
+    ws.stats[3] = (int)(st4 - st0);
+#endif
   }
 }
 
@@ -599,6 +870,7 @@ template <class T>
 __global__ __launch_bounds__(1024) void ar_final_kernel(const T* __restrict__ x, int64_t n, int64_t nq, double u,
                                                         ArWs ws, int64_t* __restrict__ index, T* __restrict__ out) {
   __shared__ double g_s[kRecLegacy], ea_s[kRecLegacy], eb_s[kRecLegacy];
+  __shared__ double q_lds[kChunk];  // wave 0's run scratch
   __shared__ long long s_lo;
   if (ws.status[0] != 0) return;  // the host raises numpy's ValueError; nothing is drawn or written
   const int tid = threadIdx.x;
@@ -635,7 +907,7 @@ __global__ __launch_bounds__(1024) void ar_final_kernel(const T* __restrict__ x,
             cand = end + (t - g);
             ok = binade(g) == e && binade(end) == e && binade(cand) == e;
           }
-          t = ok ? cand : wave_run(load_chunk4(x, n, jj), t, S);
+          t = ok ? cand : wave_run(load_chunk4(x, n, jj), t, S, q_lds);
         }
       }
       __syncthreads();
@@ -661,7 +933,7 @@ __global__ __launch_bounds__(1024) void ar_final_kernel(const T* __restrict__ x,
   const int64_t lo = s_lo;
   const double cD = ws.start[nq];
   unsigned hits = 0;
-  (void)wave_run(load_chunk4(x, n, lo), ws.start[lo], S, cD, u, &hits);
+  (void)wave_run(load_chunk4(x, n, lo), ws.start[lo], S, q_lds, cD, u, &hits);
   // the first element of the chunk whose normalised cdf exceeds u (the chunk's end does: some element qualifies;
   // elements past n add 0 and never come first)
   const unsigned long long any = __ballot(hits != 0);
@@ -696,8 +968,11 @@ ArWs carve(void* base, int64_t n, size_t* bytes) {
   w.start = c.take<double>(nq + 1);
   w.p_part = c.take<double>(npa);
   w.total = c.take<double>(1);
+  w.spec = c.take<Spec>(kSpecMax);
+  w.nspec = c.take<int32_t>(1);
   w.status = c.take<int32_t>(1);
   w.fail = c.take<int32_t>(1);
+  w.stats = c.take<int32_t>(4);
   w.lo = c.take<long long>(1);
   if (bytes) *bytes = c.off;
   return w;
@@ -734,11 +1009,13 @@ int adaptive_prepare(const T* x, int64_t n, int32_t* status, void* ws, size_t ws
   if (nbuf > nfull) {
     TailProg prog{};
     (void)tail_prog_build(prog, 0, (int)(n - nfull * kBuf));
-    FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel<T>, dim3(1), dim3(128), 0, st, x, n, prog, w);
+    tail_prog_levels(prog);
+    FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel<T>, dim3(1), dim3(1024), 0, st, x, n, prog, w);
   }
   FLC_LAUNCH("adaptive_total", ar_total_kernel<T>, dim3(1), dim3(1024), 0, st, nbuf, w);
   FLC_LAUNCH("adaptive_phase_a", ar_phase_a_kernel<T>, dim3((unsigned)npa), dim3(256), 0, st, x, n, nq, w);
   FLC_LAUNCH("adaptive_check", ar_check_kernel, dim3(1), dim3(1024), 0, st, npa, atol, w);
+  FLC_LAUNCH("adaptive_special", ar_special_kernel<T>, dim3(64), dim3(256), 0, st, x, n, w);
   if (status) FLC_CHECK_HIP(hipMemcpyAsync(status, w.status, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   return FLC_OK;
 }
@@ -756,9 +1033,14 @@ int adaptive_select(const T* x, int64_t n, double u, int64_t* index, T* out, voi
   // FLC_ADAPTIVE_SEQUENTIAL=1: skip the speculation's result and run the exact chunk-by-chunk chain (tests)
   const char* fs = getenv("FLC_ADAPTIVE_SEQUENTIAL");
   const int force_seq = (fs && atoi(fs) != 0) ? 1 : 0;
-  FLC_CHECK_HIP(hipMemsetAsync(out, 0, (size_t)n * sizeof(T), st));
   FLC_LAUNCH("adaptive_piece", ar_piece_kernel, dim3((unsigned)nblk), dim3(kPieceBlk), 0, st, nq, w);
-  FLC_LAUNCH("adaptive_walk", ar_walk_kernel<T>, dim3(1), dim3(1024), 0, st, x, n, nq, nblk, force_seq, w);
+  // (block 0 walks; the other blocks write the output's zeros on the other CUs meanwhile)
+#if FLC_CALIB_AR_NOZERO  // calibration builds only (tools/adaptive_probe.py): no zero blocks, results invalid
+  const unsigned zb = 0;
+#else
+  const unsigned zb = (unsigned)std::min<int64_t>(255, std::max<int64_t>(1, cdiv(n * (int64_t)sizeof(T), 256 * 1024)));
+#endif
+  FLC_LAUNCH("adaptive_walk", ar_walk_kernel<T>, dim3(1 + zb), dim3(1024), 0, st, x, n, nq, nblk, force_seq, w, out);
   FLC_LAUNCH("adaptive_fill", ar_fill_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, nq, u, w);
   FLC_LAUNCH("adaptive_final", ar_final_kernel<T>, dim3(1), dim3(1024), 0, st, x, n, nq, u, w, index, out);
   return FLC_OK;
@@ -783,6 +1065,14 @@ int flc_adaptive_prepare_f64(const double* x, int64_t n, int32_t* status, void* 
 int flc_adaptive_select_f64(const double* x, int64_t n, double u, int64_t* index, double* out, void* ws,
                             size_t ws_bytes, void* stream) {
   return adaptive_select(x, n, u, index, out, ws, ws_bytes, stream, "flc_adaptive_select_f64");
+}
+
+int flc_adaptive_stats(const void* ws, size_t ws_bytes, int64_t n, int32_t* stats, void* stream) {
+  if (!ws || !stats || n <= 0 || n >= (int64_t(1) << 31)) return fail(FLC_EINVAL, "flc_adaptive_stats: bad arguments");
+  if (ws_bytes < flc_adaptive_workspace_size(n)) return fail(FLC_EWORKSPACE, "flc_adaptive_stats: workspace too small");
+  ArWs w = carve(const_cast<void*>(ws), n, nullptr);
+  FLC_CHECK_HIP(hipMemcpyAsync(stats, w.stats, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, as_stream(stream)));
+  return FLC_OK;
 }
 
 }  // extern "C"

@@ -242,6 +242,10 @@ int flc_adaptive_select(const float* x, int64_t n, double u, int64_t* index, flo
 int flc_adaptive_prepare_f64(const double* x, int64_t n, int32_t* status, void* ws, size_t ws_bytes, void* stream);
 int flc_adaptive_select_f64(const double* x, int64_t n, double u, int64_t* index, double* out, void* ws,
                             size_t ws_bytes, void* stream);
+/* the last select's walk on this workspace, as 4 device int32: special chunks (a binade crossing or near an edge),
+ * special maps taken, chunks re-run sequentially, 1 if the exact sequential chain ran instead (diagnostics: the
+ * result never depends on them) */
+int flc_adaptive_stats(const void* ws, size_t ws_bytes, int64_t n, int32_t* stats, void* stream);
 
 /* the stacked encoder fused with the client delta (f1): x = local - global formed in the encoder's HBM pass
  * (FedOptClient.communicate, _fedopt.py:294-297: clone + add_(alpha=-1) per parameter tensor, then the flatten the

@@ -145,12 +145,59 @@ def _apply(m, f):
     return m + (f[1] if m & 1 else f[0])
 
 
+def special_map(row: np.ndarray, ga: float, e: int):
+    """adaptive.hip K3b: a chunk whose speculated runs cross into binade e + 1 or come near an edge, run from the
+    guess's grid index G + r (r = 0..3).  Per run: its end (grid index of binade e + cross), whether it crossed, and the
+    largest |d| (in spacings of binade e) for which the run shifted by d (d = 0 mod 4) is the run from G + r + d."""
+    G = int(math.ldexp(ga, 1075 - e))
+    edge = math.ldexp(1.0, e - 1022)
+    out = []
+    for r in range(4):
+        t0 = math.ldexp(float(G + r), e - 1075)
+        if not (1 << 52) <= G + r < (1 << 53):
+            out.append((0, 0, -1))
+            continue
+        t, below, above = t0, t0, math.inf
+        for q in row:
+            t = t + q
+            if t < edge:
+                below = t
+            elif t < above:
+                above = t
+        eb = _binade(t)
+        if eb == e:
+            out.append((int(math.ldexp(t, 1075 - e)), 0, int(math.ldexp(edge - t, 1075 - e)) - 2))
+        elif eb == e + 1:
+            lo = int(math.ldexp(edge - below, 1075 - e))
+            hi = int(math.ldexp(above - edge, 1075 - e))
+            top = int(math.ldexp(2.0 * edge - t, 1075 - e))
+            out.append((int(math.ldexp(t, 1074 - e)), 1, min(lo, hi, top) - 2))
+        else:
+            out.append((0, 0, -1))
+    return G, out
+
+
+def special_apply(t: float, e: int, G: int, runs):
+    """The walk's step over a special chunk: the exact end, or None (re-run the chunk)."""
+    if _binade(t) != e:
+        return None
+    m = int(math.ldexp(t, 1075 - e))
+    r = (m - G) & 3
+    d = m - G - r
+    end, cross, margin = runs[r]
+    if margin < 0 or abs(d) > margin:
+        return None
+    return math.ldexp(float(end + d // 2), e + 1 - 1075) if cross else math.ldexp(float(end + d), e - 1075)
+
+
 def parallel_cumsum_starts(p: np.ndarray, chunk: int, guess: np.ndarray, piece_blk: int = 1024,
-                           rec_max: int = 128, eta: float = 2.0 ** -16):
-    """The kernels' current scheme (adaptive.hip K3, K5-K7): per-chunk parity maps from the two speculated runs,
-    composed inside pieces of one binade per scan block, a walk over the pieces (re-running the chunks whose maps
-    are unusable) and every chunk's start from its piece's start and its exclusive prefix map.  Returns (exact
-    start of every chunk + the total, number of re-run chunks) or None where the kernels take the sequential chain."""
+                           rec_max: int = 128, eta: float = 2.0 ** -16, specials: bool = True):
+    """The kernels' current scheme (adaptive.hip K3, K3b, K5-K7): per-chunk parity maps from the two speculated runs,
+    composed inside pieces of one binade per scan block; the chunks whose runs cross into the next binade or come near
+    an edge get a four-run map of their own (K3b); a walk over the pieces (re-running the chunks whose maps are
+    unusable for the true start) and every chunk's start from its piece's start and its exclusive prefix map.  Returns
+    (exact start of every chunk + the total, number of re-run chunks) or None where the kernels take the sequential
+    chain.  specials=False: the round-3 scheme before K3b (every such chunk re-run)."""
     n = len(p)
     nq = -(-n // chunk)
     P = np.zeros(nq * chunk)
@@ -163,7 +210,7 @@ def parallel_cumsum_starts(p: np.ndarray, chunk: int, guess: np.ndarray, piece_b
     for s in range(chunk):
         ea = ea + P[:, s]
         eb = eb + P[:, s]
-    fe, fn = [], []
+    fe, fn, spec = [], [], []
     for j in range(nq):
         e = int(E[j])
         ok = (e >= 1 and _binade(gb[j]) == e and _binade(ea[j]) == e and _binade(eb[j]) == e
@@ -174,7 +221,13 @@ def parallel_cumsum_starts(p: np.ndarray, chunk: int, guess: np.ndarray, piece_b
             fn.append((d1, d0) if G & 1 else (d0, d1))
         else:
             fn.append((0, 0))
-        fe.append(e if ok else -1)
+        if ok:
+            fe.append(e)
+        elif specials and 1 <= e <= 2045 and _binade(ea[j]) <= e + 1:
+            fe.append(-2 - len(spec))
+            spec.append(special_map(P[j], float(ga[j]), e))
+        else:
+            fe.append(-1)
     # pieces (K5) and their prefix maps
     pieces, pre, piece_of = [], [None] * nq, [0] * nq
     for b0 in range(0, nq, piece_blk):
@@ -202,6 +255,8 @@ def parallel_cumsum_starts(p: np.ndarray, chunk: int, guess: np.ndarray, piece_b
             t = math.ldexp(float(m), e - 1075)
         elif t == ga[first]:
             t = ea[first]
+        elif e <= -2 and (nt := special_apply(t, int(E[first]), *spec[-2 - e])) is not None:
+            t = nt
         else:
             reruns += 1
             for q in P[first]:
@@ -247,7 +302,55 @@ def test_parallel_cumsum_is_exact(n, dist, zero_frac):
     cdf = np.cumsum(p)
     want = np.concatenate([[0.0], cdf[starts[1:] - 1], [cdf[-1]]])
     assert np.array_equal(got, want)
-    assert reruns <= 80
+    assert reruns <= 3  # the special chunks' maps serve nearly every binade crossing
+    _, reruns_before = parallel_cumsum_starts(p, chunk, guess, specials=False)
+    assert reruns_before <= 80
+
+
+@pytest.mark.parametrize("noise", [1e-13, 1e-10, 1e-7])
+def test_special_maps_stay_exact_under_poor_guesses(noise):
+    """Guesses perturbed far beyond the kernels' own error: every special map that is taken must still give the exact
+    run (the margins fail over to a re-run, never to a wrong sum)."""
+    n = 400_000
+    g = np.random.default_rng(7)
+    x = g.standard_normal(n).astype(F32)
+    ax = np.abs(x)
+    S = ax.sum()
+    p = (ax / S).astype(np.float64)
+    starts = np.arange(0, n, 256)
+    q = np.add.reduceat(ax.astype(np.float64), starts)
+    guess = np.concatenate([[0.0], np.cumsum(q)[:-1]]) / float(S)
+    guess[1:] *= 1.0 + noise * g.standard_normal(len(guess) - 1)
+    res = parallel_cumsum_starts(p, 256, guess, eta=2.0 ** -30)
+    assert res is not None
+    got, _ = res
+    cdf = np.cumsum(p)
+    want = np.concatenate([[0.0], cdf[starts[1:] - 1], [cdf[-1]]])
+    assert np.array_equal(got, want)
+
+
+def test_special_map_crossing_shifts_exhaustive():
+    """One crossing chunk, every true start within +-64 spacings of the guess: the map, where it answers, equals the
+    sequential run from that start."""
+    g = np.random.default_rng(3)
+    row = np.abs(g.standard_normal(256)) * 2.0 ** -20
+    e = _binade(0.5)
+    edge = 1.0
+    ga = edge - 100.5 * 2.0 ** -20  # the run crosses 1.0 about half-way
+    ga = math.ldexp(float(int(math.ldexp(ga, 1075 - e))), e - 1075)
+    G, runs = special_map(row, ga, e)
+    assert all(c == 1 for _, c, _ in runs)
+    answered = 0
+    for dm in range(-64, 65):
+        t0 = math.ldexp(float(G + dm), e - 1075)
+        want = t0
+        for v in row:
+            want = want + v
+        got = special_apply(t0, e, G, runs)
+        if got is not None:
+            answered += 1
+            assert got == want, dm
+    assert answered == 129
 
 
 def test_parallel_cumsum_many_binades_takes_the_sequential_chain():

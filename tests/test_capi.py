@@ -215,5 +215,7 @@ def test_f64_entries_validate_without_gpu():
     assert lib.flc_quant_norm_f64(16, 100, 3, 16, 16, 1 << 30, None) == 4  # p = 3: FLC_EUNSUPPORTED
     assert lib.flc_natural_f64(16, 100, 0, 0, None, None, None, 16, 1 << 30, None) == 1  # neither codes nor out
     assert lib.flc_adaptive_select_f64(16, 100, 1.5, 16, 16, 16, 1 << 30, None) == 1  # u outside [0, 1)
+    assert lib.flc_adaptive_stats(None, 1 << 30, 100, 16, None) == 1  # no workspace
+    assert lib.flc_adaptive_stats(16, 8, 100, 16, None) == 3  # workspace too small: FLC_EWORKSPACE
     assert lib.flc_f64_workspace_size(1 << 24, 1 << 17) > lib.flc_f64_workspace_size(1 << 24, 0)
     assert lib.flc_f64_workspace_size(1000, 10) == lib.flc_f64_workspace_size(1000, 0)  # small n: no filter

@@ -163,3 +163,73 @@ def test_adaptive_binade_every_few_chunks_vs_oracle():
     x = np.exp2(np.arange(n) / 1000.0).astype(np.float32)
     x[::3] *= -1
     _check(x, U_EDGES + [0.9, 0.99, 0.999])
+    from fl_sim_amd import codec
+
+    assert codec.adaptive_stats(torch.from_numpy(x).to(DEV))["sequential"] == 1
+
+
+def _crossing_us(x: np.ndarray, limit: int = 48):
+    """Uniforms on the normalised cdf's own values where the running sum crosses a binade (the special chunks of
+    adaptive.hip K3b): the value at the crossing element, one element before it, and the end of its chunk — a cdf one
+    ulp off there moves the index."""
+    ax = np.abs(x)
+    raw = (ax / ax.sum()).astype(np.float64).cumsum()
+    cdf = raw / raw[-1]
+    e = np.frexp(raw)[1]
+    cross = np.flatnonzero(np.diff(e) != 0) + 1
+    cross = cross[raw[cross - 1] > 0]
+    pick = cross[np.linspace(0, len(cross) - 1, min(limit, len(cross))).astype(int)] if len(cross) else cross
+    us = []
+    for i in pick:
+        end = min(len(x) - 1, (i // 256 + 1) * 256 - 1)
+        us += [float(cdf[i]), float(cdf[i - 1]), float(cdf[end])]
+    return [u for u in us if 0.0 <= u < 1.0]
+
+
+def test_adaptive_many_special_chunks_vs_oracle():
+    """Magnitudes doubling every 24 chunks: a binade crossing (a special chunk, K3b) every 24 chunks — about 40 per scan
+    block, under its piece limit, so they go through the special maps, not the sequential chain.  Uniforms on the cdf's
+    values at every sampled crossing."""
+    n = 700_001
+    x = np.exp2(np.arange(n) / 6144.0 - 60.0).astype(np.float32)
+    x[1::5] *= -1
+    us = _crossing_us(x)
+    assert len(us) > 60
+    _check(x, us)
+    from fl_sim_amd import codec
+
+    st = codec.adaptive_stats(torch.from_numpy(x).to(DEV))
+    assert st["sequential"] == 0 and st["special"] >= 100 and st["taken"] >= st["special"] - 4, st
+
+
+def test_adaptive_crossing_uniforms_25M_vs_oracle():
+    n = 25_000_000
+    g = np.random.default_rng(26)
+    x = (g.standard_normal(n) * 1e-3).astype(np.float32)
+    x[g.random(n) < 0.05] = 0
+    _check(x, _crossing_us(x, limit=24))
+    from fl_sim_amd import codec
+
+    st = codec.adaptive_stats(torch.from_numpy(x).to(DEV))
+    # every binade crossing through a special map: at most a couple of chunks re-run
+    assert st["sequential"] == 0 and st["special"] >= 15 and st["reruns"] <= 2, st
+
+
+@pytest.mark.parametrize("n", [5, 8193, 1_000_003])
+def test_adaptive_select_into_unaligned_out(n):
+    """The walk's other blocks write the output's zeros: an output view at a 4-B offset is zeroed entirely (head, 16-B
+    body, tail) except out[ind] = x[ind]."""
+    from fl_sim_amd import codec
+
+    g = np.random.default_rng(n)
+    x = (g.standard_normal(n) * 1e-3).astype(np.float32)
+    xd = torch.from_numpy(x).to(DEV)
+    assert int(codec.adaptive_prepare(xd).item()) == 0
+    buf = torch.full((n + 2,), 7.0, device=DEV)
+    out = buf[1:n + 1]
+    _, idx = codec.adaptive_select(xd, 0.4, out=out)
+    _, _, exp_ind = ref.adaptive_random(x, n, 0.4)
+    assert int(idx.item()) == exp_ind
+    o = out.cpu().numpy()
+    assert o[exp_ind] == x[exp_ind] and np.count_nonzero(o) == (1 if x[exp_ind] != 0 else 0)
+    assert float(buf[0]) == 7.0 and float(buf[n + 1]) == 7.0

@@ -287,3 +287,31 @@ def test_f64_other_dtypes_refused():
         c.compressVector(np.arange(10, dtype=np.float16))
     with pytest.raises(TypeError):
         c.compressVector(np.arange(10, dtype=np.int64))
+
+
+@pytest.mark.parametrize("structured", [False, True])
+def test_f64_adaptive_many_special_chunks_vs_oracle(structured):
+    """float64: a binade crossing every 24 chunks over ~330 binades — more special chunks in one walk batch than its
+    LDS slots (the rest read from memory), still under each scan block's piece limit.  Structured: x doubling exactly
+    every 6144 elements makes the running sum land within a few spacings below each power of two, so no special map
+    can be validated and those chunks re-run (still exact); with a random factor per element they go through the maps."""
+    from tests.test_gpu_adaptive import _crossing_us
+    from fl_sim_amd import codec
+
+    n = 2_000_003
+    x = np.exp2(np.arange(n) / 6144.0 - 160.0)
+    if not structured:
+        x *= 1.0 + 0.3 * np.random.default_rng(5).random(n)
+    x[1::7] *= -1
+    us = _crossing_us(x, limit=64)
+    assert len(us) > 100
+    xd = torch.from_numpy(x).to(DEV)
+    assert int(codec.adaptive_prepare(xd).item()) == 0
+    for u in us:
+        out, index = codec.adaptive_select(xd, u)
+        _, _, ind = ref.adaptive_random(x, n, u)
+        assert int(index.item()) == ind, u
+    st = codec.adaptive_stats(xd)
+    assert st["sequential"] == 0 and st["special"] > 256, st
+    if not structured:
+        assert st["taken"] >= st["special"] - 8, st

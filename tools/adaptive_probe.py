@@ -29,3 +29,4 @@ for _ in range(10):
     _, ind = codec.adaptive_select(x, 0.37)
 torch.cuda.synchronize()
 print(f"both: {(time.perf_counter() - t0) * 1e2:.3f} ms per call, index {int(ind.item())}", flush=True)
+print("walk:", codec.adaptive_stats(x), flush=True)
