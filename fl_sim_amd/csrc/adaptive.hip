@@ -667,6 +667,8 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
   __shared__ Spec spec_lds[kSpecLds];
   __shared__ double t_lds[kWalkBatch], end_lds[kWalkBatch];  // the batch's piece starts / ends (written out after)
   __shared__ double q_lds[kChunk];                             // wave 0's re-run scratch
+  __shared__ long long run0[kWalkBatch], run1[kWalkBatch];     // the runs' segmented map scan
+  __shared__ int run_h[kWalkBatch], run_x[kWalkBatch], run_e[kWalkBatch], item_r[kWalkBatch];
   __shared__ int scan_lds[1024 / kWave];
   __shared__ int s_bad, s_total, s_taken, s_reruns;
   __shared__ double s_t;
@@ -719,8 +721,9 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
   const T S = (T)ws.total[0];
   for (int g0 = 0; g0 < total && !s_bad; g0 += kWalkBatch) {
     const int g = g0 + tid;
+    const bool valid = g < total;
     Rec rc{};
-    if (g < total) {  // the block holding piece g: the last b with off[b] <= g
+    if (valid) {  // the block holding piece g: the last b with off[b] <= g
       int lo = 0, hi = nblk - 1;
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -729,41 +732,106 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
       }
       rc = ws.rec[(size_t)lo * kRecMax + (g - off[lo])];
     }
+    // Consecutive composed pieces of one binade (split only by the scan blocks' bounds) compose further: a segmented
+    // scan of their maps over the batch ("runs"), so the walk steps once per run and once per other piece.
+    const bool mp = valid && rc.e >= 1;
+    run_e[tid] = valid ? rc.e : -100;
+    __syncthreads();
+    const int ep = tid > 0 ? run_e[tid - 1] : -100, en = tid + 1 < kWalkBatch ? run_e[tid + 1] : -100;
+    const bool head = mp && !(ep >= 1 && ep == rc.e), last = mp && !(en >= 1 && en == rc.e);
+    long long a0 = mp ? rc.inc0 : 0, a1 = mp ? rc.inc1 : 0;
+    int hf = (head || !mp) ? 1 : 0, hx = tid;  // segment flag; the run's head (its own index at a head)
+    run0[tid] = a0;
+    run1[tid] = a1;
+    run_h[tid] = hf;
+    run_x[tid] = hx;
+    __syncthreads();
+    for (int d = 1; d < kWalkBatch; d <<= 1) {
+      long long n0 = a0, n1 = a1;
+      int nh = hf, nx = hx;
+      if (tid >= d && !hf) {
+        compose(run0[tid - d], run1[tid - d], a0, a1, &n0, &n1);
+        nh = run_h[tid - d];
+        nx = run_x[tid - d];
+      }
+      __syncthreads();
+      a0 = n0;
+      a1 = n1;
+      hf = hf | nh;
+      hx = nx;
+      run0[tid] = a0;
+      run1[tid] = a1;
+      run_h[tid] = hf;
+      run_x[tid] = hx;
+      __syncthreads();
+    }
+    // exclusive map inside the run (identity at its head); the walk items: every non-map piece and each run's last
+    const long long x0 = (mp && !head) ? run0[tid - 1] : 0, x1 = (mp && !head) ? run1[tid - 1] : 0;
+    const bool item = valid && (!mp || last);
+    int nitems;
+    const int ii = block_excl_scan<int, 1024 / kWave>(item ? 1 : 0, scan_lds, &nitems);
     // the batch's special chunks' maps into LDS slots (beyond kSpecLds of them: read from memory on the walk)
-    const bool is_sp = g < total && rc.e <= -2;
+    const bool is_sp = valid && rc.e <= -2;
     int nsp;
     const int slot = block_excl_scan<int, 1024 / kWave>(is_sp ? 1 : 0, scan_lds, &nsp);
-    if (g < total) {
+    if (valid) {
       rc.slot = (is_sp && slot < kSpecLds) ? slot : -1;
       if (rc.slot >= 0) spec_lds[slot] = ws.spec[-2 - rc.e];
-      batch[tid] = rc;
+      if (mp) {  // a run's last: the run's composed map, and its head's index in `first`
+        rc.inc0 = a0;
+        rc.inc1 = a1;
+        rc.first = hx;
+      }
+      if (item) {
+        batch[ii] = rc;
+        item_r[ii] = tid;
+      }
     }
     __syncthreads();
 #if FLC_CALIB_AR_STAMPS
     if (g0 == 0) st2 = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (tid < kWave) {  // wave 0 walks the batch
-      // The state is t's bit pattern, wave-uniform (readfirstlane of every record field), so the chain of a composed
-      // piece is a few scalar integer ops on it: grid index = mantissa | 2^52, binade = the exponent field.
-      const int cnt = std::min(kWalkBatch, total - g0);
+    if (tid < kWave) {  // wave 0 walks the batch's items
+      // The state is t's bit pattern, wave-uniform (scalar registers), so a composed run's step is a few scalar
+      // integer ops on it: grid index = mantissa | 2^52, binade = the exponent field.  Items in windows of 64: lane i
+      // holds item w0 + i (one LDS read per lane per window), the step reads its fields with readlane, and lane i keeps
+      // the item's start / end for one LDS store per lane after the window.
+      const int cnt = nitems;
       uint64_t tb = rfl64((uint64_t)__double_as_longlong(s_t));
       bool bad = false;
       int taken = 0, reruns = 0;
-      // records in windows of 64: lane i holds record w0 + i (one LDS read per lane per window), the step takes its
-      // fields with readlane, and lane i keeps the step's start / end for one store per lane after the window
       const int lane = tid;
       constexpr uint64_t kMant = (1ull << 52) - 1, kHid = 1ull << 52;
       for (int w0 = 0; w0 < cnt && !bad; w0 += kWave) {
         const int wn = std::min(kWave, cnt - w0);
         Rec mine{};
-        if (lane < wn) mine = batch[w0 + lane];
+        int my_r = 0;
+        if (lane < wn) {
+          mine = batch[w0 + lane];
+          my_r = item_r[w0 + lane];
+        }
+        // a special item's map in its lane's registers too (from its LDS slot, or from memory past kSpecLds)
+        long long sG = 0, sEnd[4] = {0, 0, 0, 0}, sMg[4] = {-1, -1, -1, -1};
+        int sE = -1, sCross = 0;
+        if (lane < wn && mine.e <= -2) {
+          Spec v;
+          if (mine.slot >= 0) v = spec_lds[mine.slot];
+          else v = ws.spec[-2 - mine.e];
+          sG = v.G;
+          sE = v.E;
+          sCross = v.cross;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            sEnd[q] = v.end[q];
+            sMg[q] = v.margin[q];
+          }
+        }
         uint64_t my_t = 0, my_end = 0;
         for (int i = 0; i < wn; ++i) {
-          const int e = __builtin_amdgcn_readlane(mine.e, i), first = __builtin_amdgcn_readlane(mine.first, i);
-          const int slot = __builtin_amdgcn_readlane(mine.slot, i);
+          const int e = __builtin_amdgcn_readlane(mine.e, i);
           const uint64_t inc0 = rl64((uint64_t)mine.inc0, i), inc1 = rl64((uint64_t)mine.inc1, i);
           my_t = lane == i ? tb : my_t;
-          if (e >= 1) {  // a composed piece of binade e: its map on the grid index
+          if (e >= 1) {  // a composed run of binade e: its map on the grid index
             const uint64_t m = (tb & kMant) | kHid;
             const uint64_t m2 = m + ((m & 1) ? inc1 : inc0);
             if ((int)(tb >> 52) != e || m2 < kHid || m2 >= 2 * kHid) {
@@ -772,16 +840,17 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
             }
             tb = ((uint64_t)e << 52) | (m2 & kMant);
           } else {
+            const int first = __builtin_amdgcn_readlane(mine.first, i);
             bool done = false;
             if (e <= -2) {  // a special chunk: its run's map when the true start is within its margin
-              const Spec* sp = slot >= 0 ? spec_lds + slot : ws.spec + (-2 - e);
-              const int se = rfl32(sp->E), cross = rfl32(sp->cross);
+              const int se = __builtin_amdgcn_readlane(sE, i), cross = __builtin_amdgcn_readlane(sCross, i);
               const long long m = (long long)((tb & kMant) | kHid);
-              const long long G = (long long)rfl64((uint64_t)sp->G);
+              const long long G = (long long)rl64((uint64_t)sG, i);
               const int rr = (int)((m - G) & 3);
               const long long d = m - G - rr;
-              const long long mg = (long long)rfl64((uint64_t)sp->margin[rr]);
-              const long long end = (long long)rfl64((uint64_t)sp->end[rr]);
+              const long long mgv = rr == 0 ? sMg[0] : rr == 1 ? sMg[1] : rr == 2 ? sMg[2] : sMg[3];
+              const long long env = rr == 0 ? sEnd[0] : rr == 1 ? sEnd[1] : rr == 2 ? sEnd[2] : sEnd[3];
+              const long long mg = (long long)rl64((uint64_t)mgv, i), end = (long long)rl64((uint64_t)env, i);
               const int cr = (cross >> rr) & 1;
               const long long m2 = end + (cr ? d / 2 : d);
               if ((int)(tb >> 52) == se && mg >= 0 && (d < 0 ? -d : d) <= mg && in_binade(m2)) {
@@ -802,9 +871,9 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
           }
           my_end = lane == i ? tb : my_end;
         }
-        if (lane < wn) {
-          t_lds[w0 + lane] = __longlong_as_double((long long)my_t);
-          end_lds[w0 + lane] = __longlong_as_double((long long)my_end);
+        if (lane < wn) {  // a run's start goes to its head's slot (the write-out below needs it); ends by record
+          t_lds[mine.e >= 1 ? mine.first : my_r] = __longlong_as_double((long long)my_t);
+          end_lds[my_r] = __longlong_as_double((long long)my_end);
         }
       }
       const double t = __longlong_as_double((long long)tb);
@@ -819,10 +888,17 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
       }
     }
     __syncthreads();
-    if (g < total) {  // (read before the next batch's barriers let wave 0 rewrite them)
-      ws.rec_t[g] = t_lds[tid];
-      ws.rec_end[g] = end_lds[tid];
+    if (valid) {  // every piece's start and end (a run's pieces from its start and their maps, all in its binade)
+      double ts = t_lds[tid], te = end_lds[tid];
+      if (mp) {
+        const long long m0 = grid_bits(t_lds[hx]);
+        ts = bits_grid(apply_map(m0, x0, x1), rc.e);
+        te = bits_grid(apply_map(m0, a0, a1), rc.e);
+      }
+      ws.rec_t[g] = ts;
+      ws.rec_end[g] = te;
     }
+    __syncthreads();  // (the next batch rewrites the LDS arrays)
   }
   if (tid == 0) {
     ws.start[nq] = s_t;
