@@ -433,17 +433,18 @@ __global__ __launch_bounds__(256) void ar_phase_a_kernel(const T* __restrict__ x
   if (threadIdx.x == 0) ws.p_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// ---- K4: numpy's checks on p (before any uniform is drawn) -------------------------------------------
-__global__ __launch_bounds__(1024) void ar_check_kernel(int64_t nparts, double atol, ArWs ws) {
-  __shared__ double lds[1024 / kWave];
+// ---- K4: numpy's checks on p (before any uniform is drawn): block 0 of the special kernel's launch (K3b) -----------
+__device__ void ar_check(int64_t nparts, double atol, ArWs ws, int32_t* status_out) {
+  __shared__ double lds[256 / kWave];
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < nparts; i += 1024) s += ws.p_part[i];
-  s = block_sum<double, 1024 / kWave>(s, lds);
+  for (int64_t i = threadIdx.x; i < nparts; i += 256) s += ws.p_part[i];
+  s = block_sum<double, 256 / kWave>(s, lds);
   if (threadIdx.x == 0) {
     int st = 0;
     if (isnan(s)) st = kStNan;
     else if (!(fabs(s - 1.0) <= atol)) st = kStSum;
     ws.status[0] = st;
+    if (status_out) *status_out = st;
   }
 }
 
@@ -617,9 +618,11 @@ __device__ __forceinline__ Four<T> load_chunk4(const T* __restrict__ x, int64_t 
 //   * one crossing: the sums before it stay below the edge (lo), the first one after it stays above (hi, in spacings
 //     of E; its rounding error is at most one), and the rest stay below 2^(E+2) (top).  In binade E + 1 the shift d is
 //     an even multiple of the spacing 2 U because d = 0 mod 4.
+// (block 0 first runs the check, K4; the runs do not wait for it: with a failed check the select never reads them)
 template <class T>
-__global__ __launch_bounds__(256) void ar_special_kernel(const T* __restrict__ x, int64_t n, ArWs ws) {
-  if (ws.status[0] != 0) return;
+__global__ __launch_bounds__(256) void ar_special_kernel(const T* __restrict__ x, int64_t n, ArWs ws, int64_t nparts,
+                                                         double atol, int32_t* status_out) {
+  if (blockIdx.x == 0) ar_check(nparts, atol, ws, status_out);
   __shared__ double q_lds[256 / kWave][kChunk];
   const int nsp = min(ws.nspec[0], kSpecMax);
   const int lane = threadIdx.x & (kWave - 1), r = lane & 3;
@@ -1090,9 +1093,7 @@ int adaptive_prepare(const T* x, int64_t n, int32_t* status, void* ws, size_t ws
   }
   FLC_LAUNCH("adaptive_total", ar_total_kernel<T>, dim3(1), dim3(1024), 0, st, nbuf, w);
   FLC_LAUNCH("adaptive_phase_a", ar_phase_a_kernel<T>, dim3((unsigned)npa), dim3(256), 0, st, x, n, nq, w);
-  FLC_LAUNCH("adaptive_check", ar_check_kernel, dim3(1), dim3(1024), 0, st, npa, atol, w);
-  FLC_LAUNCH("adaptive_special", ar_special_kernel<T>, dim3(64), dim3(256), 0, st, x, n, w);
-  if (status) FLC_CHECK_HIP(hipMemcpyAsync(status, w.status, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+  FLC_LAUNCH("adaptive_special", ar_special_kernel<T>, dim3(64), dim3(256), 0, st, x, n, w, npa, atol, status);
   return FLC_OK;
 }
 
