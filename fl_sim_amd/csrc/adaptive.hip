@@ -228,13 +228,23 @@ int tail_prog_build(TailProg& p, int s0, int m) {  // (host) returns the value c
   return 128 + p.nop++;
 }
 
-// ---- K1: full reduction buffers (n2 splits of 8192 are a perfect tree of 64 leaves of 128) ----------
 template <class T>
-__global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const T* __restrict__ x, int64_t n_full_bufs, ArWs ws) {
+__device__ void ar_tail_sum(const T* __restrict__ x, int64_t n, const TailProg& prog, ArWs ws, T* sh);
+
+// ---- K1: full reduction buffers (n2 splits of 8192 are a perfect tree of 64 leaves of 128); one block more for the
+// partial last buffer (K1b) when there is one -----------------------------------------------------------------------
+template <class T>
+__global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const T* __restrict__ x, int64_t n, int64_t n_full_bufs,
+                                                            TailProg prog, ArWs ws) {
   constexpr int VN = Vec16<T>::N;
   __shared__ T sh[kPad];
-  const int64_t b = blockIdx.x;
-  if (b >= n_full_bufs) return;
+  // (the partial buffer, when there is one, takes block 0: its serial tree starts first and hides under the others)
+  const bool tail = (int64_t)gridDim.x > n_full_bufs;
+  if (tail && blockIdx.x == 0) {
+    ar_tail_sum(x, n, prog, ws, sh);
+    return;
+  }
+  const int64_t b = (int64_t)blockIdx.x - (tail ? 1 : 0);
   const T* src = x + b * kBuf;
   // 256 threads x 16-B loads: coalesced, |x| written with one pad word per 128-element leaf
   for (int v = threadIdx.x; v < kBuf / VN; v += 256) {
@@ -267,18 +277,16 @@ __global__ __launch_bounds__(256) void ar_buffer_sum_kernel(const T* __restrict_
   if (l == 0) ws.buf_sum[b] = (double)s;
 }
 
-// ---- K1b: the last, partial buffer (an irregular tree): leaves in parallel, then the tree's <= 127 additions level by
-// level (the host-built program; every addition as in the tree, so the same sum) -------------------------------------
+// ---- K1b: the last, partial buffer (an irregular tree; the last block of K1's launch): leaves in parallel, then the
+// tree's <= 127 additions level by level (the host-built program; every addition as in the tree, so the same sum) ----
 template <class T>
-__global__ __launch_bounds__(1024) void ar_tail_sum_kernel(const T* __restrict__ x, int64_t n, TailProg prog,
-                                                           ArWs ws) {
+__device__ void ar_tail_sum(const T* __restrict__ x, int64_t n, const TailProg& prog, ArWs ws, T* sh) {
   constexpr int VN = Vec16<T>::N;
-  __shared__ T sh[kBuf];
   __shared__ T lf_sum[128], op_sum[128];
   const int tid = threadIdx.x;
   const int64_t b = n / kBuf;
   const int len = (int)(n - b * kBuf);
-  for (int v = tid; v * VN < len; v += 1024) {
+  for (int v = tid; v * VN < len; v += 256) {
     const Vec16<T> q = load16(x + b * kBuf, (int64_t)v * VN, (int64_t)len);
 #pragma unroll
     for (int c = 0; c < VN; ++c) sh[v * VN + c] = abs_of(q.e[c]);
@@ -1083,14 +1091,12 @@ int adaptive_prepare(const T* x, int64_t n, int32_t* status, void* ws, size_t ws
   hipStream_t st = as_stream(stream);
   ArWs w = carve(ws, n, nullptr);
   const int64_t nfull = n / kBuf, nbuf = cdiv(n, kBuf), nq = cdiv(n, kChunk), npa = cdiv(nq, 256);
-  if (nfull > 0)
-    FLC_LAUNCH("adaptive_buffer_sum", ar_buffer_sum_kernel<T>, dim3((unsigned)nfull), dim3(256), 0, st, x, nfull, w);
+  TailProg prog{};
   if (nbuf > nfull) {
-    TailProg prog{};
     (void)tail_prog_build(prog, 0, (int)(n - nfull * kBuf));
     tail_prog_levels(prog);
-    FLC_LAUNCH("adaptive_tail_sum", ar_tail_sum_kernel<T>, dim3(1), dim3(1024), 0, st, x, n, prog, w);
   }
+  FLC_LAUNCH("adaptive_buffer_sum", ar_buffer_sum_kernel<T>, dim3((unsigned)nbuf), dim3(256), 0, st, x, n, nfull, prog, w);
   FLC_LAUNCH("adaptive_total", ar_total_kernel<T>, dim3(1), dim3(1024), 0, st, nbuf, w);
   FLC_LAUNCH("adaptive_phase_a", ar_phase_a_kernel<T>, dim3((unsigned)npa), dim3(256), 0, st, x, n, nq, w);
   FLC_LAUNCH("adaptive_special", ar_special_kernel<T>, dim3(64), dim3(256), 0, st, x, n, w, npa, atol, status);
