@@ -33,8 +33,8 @@
 //   * one wave walks the pieces in order (O(1) per composed piece and per special chunk whose true start lies within
 //     its run's margin; kChunk dependent adds for a chunk re-run), checking that every composed piece starts and ends
 //     in its binade — which makes every chunk map in it exact;
-//   * every chunk's exact start then follows in parallel from its piece's start and its exclusive prefix map, and
-//     the chunk holding searchsorted(u) is found in the same pass and re-run to find the index.
+//   * the piece holding searchsorted(u) is found among the pieces' exact starts and ends, the chunk inside it from the
+//     piece's start and each chunk's exclusive prefix map (one chunk per thread), and that chunk is re-run for the index.
 // If a check fails (never expected: the margins are ~100x the guesses' error) the exact chunk-by-chunk chain runs
 // instead, so the result never depends on the speculation.  The guesses come from the pairwise partial sums of |x|;
 // their accuracy only decides how many chunks are re-run.
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(256) void ar_special_kernel(const T* __restrict__ x
 // Blocks 1.. of the launch write the dense output's zeros meanwhile (the walk is one wave's latency chain).
 template <class T>
 __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, int64_t n, int64_t nq, int nblk,
-                                                       int force_seq, ArWs ws, T* __restrict__ out) {
+                                                       int force_seq, double u, ArWs ws, T* __restrict__ out) {
   __shared__ int off[kMaxScanBlocks];
   __shared__ Rec batch[kWalkBatch];
   __shared__ Spec spec_lds[kSpecLds];
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
   __shared__ long long run0[kWalkBatch], run1[kWalkBatch];     // the runs' segmented map scan
   __shared__ int run_h[kWalkBatch], run_x[kWalkBatch], run_e[kWalkBatch], item_r[kWalkBatch];
   __shared__ int scan_lds[1024 / kWave];
-  __shared__ int s_bad, s_total, s_taken, s_reruns;
+  __shared__ int s_bad, s_total, s_taken, s_reruns, s_piece;
   __shared__ double s_t;
   if (ws.status[0] != 0) return;
   const int tid = threadIdx.x;
@@ -911,6 +911,41 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
     }
     __syncthreads();  // (the next batch rewrites the LDS arrays)
   }
+  // The chunk holding searchsorted(u, side='right'): the piece first (the normalised cdf is non-decreasing and
+  // cdf[-1] / cdf[-1] = 1 > u, so exactly one piece has start <= u < end), then the chunk inside it, one per thread.
+  if (!s_bad) {
+    const double cD = s_t;
+    if (tid == 0) s_piece = -1;
+    __syncthreads();  // (and every batch's rec_t / rec_end, written by this block, are visible)
+    for (int g = tid; g < total; g += 1024)
+      if (ws.rec_t[g] / cD <= u && ws.rec_end[g] / cD > u) s_piece = g;
+    __syncthreads();
+    const int gp = s_piece;
+    if (gp >= 0) {
+      int lo = 0, hi = nblk - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= gp) lo = mid;
+        else hi = mid - 1;
+      }
+      const Rec rc = ws.rec[(size_t)lo * kRecMax + (gp - off[lo])];
+      const int64_t j = (int64_t)rc.first + tid;
+      if (j <= rc.last) {
+        const double tp = ws.rec_t[gp];
+        const int e = ws.fe[j];
+        double t = tp, end = ws.rec_end[gp];
+        if (e >= 1) {
+          const long long m = apply_map(to_grid(tp, e), ws.pre[2 * j], ws.pre[2 * j + 1]);
+          t = from_grid(m, e);
+          end = from_grid(apply_map(m, ws.fn[2 * j], ws.fn[2 * j + 1]), e);
+        }
+        if (t / cD <= u && end / cD > u) {
+          ws.lo[0] = j;
+          ws.start[j] = t;
+        }
+      }
+    }
+  }
   if (tid == 0) {
     ws.start[nq] = s_t;
     ws.fail[0] = s_bad;
@@ -926,29 +961,6 @@ __global__ __launch_bounds__(1024) void ar_walk_kernel(const T* __restrict__ x, 
     ws.stats[3] = (int)(st4 - st0);
 #endif
   }
-}
-
-// ---- K7: every chunk's exact start from its piece, and the chunk holding searchsorted(u, side='right') ------
-__global__ __launch_bounds__(256) void ar_fill_kernel(int64_t nq, double u, ArWs ws) {
-  if (ws.status[0] != 0 || ws.fail[0] != 0) return;
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= nq) return;
-  const double cD = ws.start[nq];
-  const int g = ws.rec_off[j / kPieceBlk] + ws.prec[j];
-  const double tp = ws.rec_t[g];
-  const int e = ws.fe[j];
-  double t, end;
-  if (e >= 1) {
-    const long long m = apply_map(to_grid(tp, e), ws.pre[2 * j], ws.pre[2 * j + 1]);
-    t = from_grid(m, e);
-    end = from_grid(apply_map(m, ws.fn[2 * j], ws.fn[2 * j + 1]), e);
-  } else {
-    t = tp;
-    end = ws.rec_end[g];
-  }
-  ws.start[j] = t;
-  // the normalised cdf is non-decreasing: exactly one chunk has its start <= u < its end (cdf[-1] / cdf[-1] = 1)
-  if (t / cD <= u && end / cD > u) ws.lo[0] = j;
 }
 
 // ---- K8: the index — chunk lo re-run from its exact start; or, if the speculation failed, the exact
@@ -1123,8 +1135,8 @@ int adaptive_select(const T* x, int64_t n, double u, int64_t* index, T* out, voi
 #else
   const unsigned zb = (unsigned)std::min<int64_t>(255, std::max<int64_t>(1, cdiv(n * (int64_t)sizeof(T), 256 * 1024)));
 #endif
-  FLC_LAUNCH("adaptive_walk", ar_walk_kernel<T>, dim3(1 + zb), dim3(1024), 0, st, x, n, nq, nblk, force_seq, w, out);
-  FLC_LAUNCH("adaptive_fill", ar_fill_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, st, nq, u, w);
+  FLC_LAUNCH("adaptive_walk", ar_walk_kernel<T>, dim3(1 + zb), dim3(1024), 0, st, x, n, nq, nblk, force_seq, u, w,
+             out);
   FLC_LAUNCH("adaptive_final", ar_final_kernel<T>, dim3(1), dim3(1024), 0, st, x, n, nq, u, w, index, out);
   return FLC_OK;
 }
