@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "grad-codec GB/s (device-resident encode+decode), flat fp32 delta, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+XGMI_GBS = 7 * 153.0  # 7 xGMI links x ~153 GB/s per GPU
 D_HEADLINE = 268_435_456
 LEVELS = 127
 
@@ -131,6 +132,21 @@ def settle_gpu(buf: torch.Tensor, seconds: float = 0.2) -> None:
     while time.perf_counter() - t0 < seconds:
         buf.zero_()
         torch.cuda.synchronize()
+
+
+def stream_copy_gbs(src: torch.Tensor, dst: torch.Tensor, world: int) -> float:
+    """The box's stream-copy rate: 2 * 4 * D bytes per device-to-device copy of src into dst (torch's copy kernel and
+    flc_copy, 10 copies each after 3 warm ones; the better of the two), max over ranks of the time."""
+    from fl_sim_amd import _lib
+
+    st = lambda: torch.cuda.current_stream(src.device).cuda_stream  # noqa: E731
+    best = None
+    for fn in (lambda: dst.copy_(src),
+               lambda: _lib.call("flc_copy", src.data_ptr(), src.numel(), dst.data_ptr(), st())):
+        ms, _ = timed(fn, 10, 3, world)
+        ms = max_over_ranks(ms, world)
+        best = ms if best is None else min(best, ms)
+    return 8 * src.numel() / (best * 1e-3) / 1e9
 
 
 def stacked_bytes(D: int, K: int) -> int:
@@ -332,6 +348,37 @@ def aggregation_extras(dev, world: int, rank: int) -> dict:
                              "D = 417,482, n = 10; the whole model in one flc_model_fold launch (the delta fold and "
                              "the optimizer step fused)")
     out["aggregation_config0_fedavg_10x417482"] = line
+    # the reference's own placement (nodes.py:606): the server model and its FedOpt state in HOST memory, the 10
+    # clients' messages on the device; FedOptUpdateMixin stages the server's tensors (adopted into one pinned buffer:
+    # one H2D and one D2H per update), folds in one launch and writes back in place; host to host, synchronised
+    import types
+
+    from fl_sim_amd.aggregation import FedOptUpdateMixin
+
+    class _HostServer(FedOptUpdateMixin):
+        pass
+
+    hl = {"model": line["model"], "placement": "server model + delta (+ v) in host memory (nodes.py:606), messages on "
+                                               "the device (clients on cuda:i mod N)"}
+    for name, opt, lr, betas in (("fedavg_update", "avg", 1.0, (0.0, 1.0)), ("fedadam_update", "adam", 1e-2, (0.9, 0.99))):
+        hs = _HostServer()
+        hs.model = torch.nn.Module()
+        gh = torch.Generator().manual_seed(5)
+        for i, sh in enumerate(CONFIG0_SHAPES):
+            hs.model.register_parameter(f"p{i}", torch.nn.Parameter(torch.randn(sh, generator=gh)))
+        hs.delta_parameters = [torch.zeros(sh) for sh in CONFIG0_SHAPES]
+        hs.v_parameters = None if opt == "avg" else [torch.rand(sh, generator=gh) * 1e-4 + 1e-6 for sh in CONFIG0_SHAPES]
+        hs.config = types.SimpleNamespace(optimizer=opt, lr=lr, betas=betas, tau=1e-3)
+        hs._received_messages = msgs0
+        ms_h, _ = timed(hs.update, 50, 10, world)
+        ms_h = max_over_ranks(ms_h, world)
+        pcie = (2 if opt == "avg" else 3) * 2 * 4 * d0  # theta, delta (, v) each way
+        hl[name] = {"us": round(ms_h * 1e3, 2), "pcie_bytes": pcie,
+                    "pcie_GB_s": round(pcie / (ms_h * 1e-3) / 1e9, 1)}
+    hl["note"] = ("host to host per update: H2D of the server state, one flc_model_fold launch (fold + optimizer step), "
+                  "D2H back into the same CPU tensors, stream synchronised; cpu_torch is the reference's CPU update "
+                  "with its messages already in host memory")
+    out["aggregation_config0_host_server"] = hl
     del th0, dl0, v0, msgs0
     # 8 x 25 M: distinct sources (a repeated source would be served from the caches)
     n8 = 25_000_000
@@ -420,6 +467,13 @@ def main():
             "avg_ms": round(probe_ms, 5),
             "algorithmic_bytes": kernel_bytes.get(args.probe),
         }
+    if roof is not None:
+        # the box's own achievable HBM rate beside the spec peak: a 1 GiB device-to-device copy (read
+        # 4 D + write 4 D), the best of torch's copy kernel and flc_copy, timed over its own short run
+        cp = stream_copy_gbs(x, out, world)
+        roof["stream_copy_GB_s"] = round(cp, 1)
+        roof["frac_of_stream_copy"] = round(roof["achieved"] / cp, 4)
+        roof["value_frac_of_stream_copy"] = round(value / world / cp, 4)
     extra = {}
     parity = None  # set by the configs[3] legs (skipped with --skip-extra)
     if probe_ms:
@@ -576,35 +630,57 @@ def main():
                                    "values written from the registers; the wire is not read back)",
         }
         del X
-        # configs[2]: top-k 1% of a 25M delta (encode + dense decode)
+        from fl_sim_amd import dist as fdist
+
+        # configs[2]: top-k 1% of a 25M delta (encode + dense decode).  Fresh inputs: the steps rotate over the 8
+        # distinct client deltas of configs[3] (800 MB, above the 256 MiB Infinity Cache), as fl-sim's clients each
+        # bring a new delta; the same-input figure (x cache-resident after the first step) is kept beside it
         d3 = 25_000_000
         k3 = d3 // 100
-        X3 = torch.randn(d3, generator=gen, device=dev) * 1e-3
+        n_cl4 = 8
+        X8 = [fdist.synthetic_client_delta(c, d3, dev) for c in range(n_cl4)]
+        X3 = X8[0]
         o3 = torch.empty(d3, dtype=torch.float32, device=dev)
+        r3 = [0]
 
-        def step3():  # the TopK compressor's path: encoder-emitted tile pointers, decode without an index pass
-            idx, val, tiles = codec.topk_encode(X3, k3, with_tiles=True)
+        def step3(rotate=True):  # the TopK compressor's path: encoder-emitted tile pointers, no index pass
+            r3[0] += 1
+            xi = X8[r3[0] % n_cl4] if rotate else X3
+            idx, val, tiles = codec.topk_encode(xi, k3, with_tiles=True)
             codec.sparse_decode(idx, val, d3, out=o3, tiles=tiles)
 
-        ms3, _ = timed(step3, 20, 5, world)
+        ms3, _ = timed(step3, 24, 8, world)
         ms3 = max_over_ranks(ms3, world)
+        ms3c, _ = timed(lambda: step3(False), 20, 5, world)
+        ms3c = max_over_ranks(ms3c, world)
         extra["config3_topk1pct_25M"] = {
             "ms_per_step": round(ms3, 4),
             "GB_s": round((8 * d3 + 16 * k3) / (ms3 * 1e-3) / 1e9, 1),
             "bytes_formula": "8 * D + 16 * K",
+            "inputs": f"{n_cl4} distinct 100 MB deltas in rotation (fresh: not cache-resident)",
+            "same_input_ms_per_step": round(ms3c, 4),
         }
         del o3
-        # a7: adaptive random (np.random.choice with p = |x| / sum|x|) on the 25M delta, device u (philox mode)
-        def step_ar():
-            codec.adaptive_prepare(X3)
-            codec.adaptive_select(X3, 0.37)
+        # a7: adaptive random (np.random.choice with p = |x| / sum|x|) on a 25M delta, device u (philox mode);
+        # rotating over the distinct deltas as above
+        ra = [0]
 
-        ms_ar, _ = timed(step_ar, 10, 3, world)
+        def step_ar(rotate=True):
+            ra[0] += 1
+            xi = X8[ra[0] % n_cl4] if rotate else X3
+            codec.adaptive_prepare(xi)
+            codec.adaptive_select(xi, 0.37)
+
+        ms_ar, _ = timed(step_ar, 16, 8, world)
         ms_ar = max_over_ranks(ms_ar, world)
+        ms_arc, _ = timed(lambda: step_ar(False), 10, 3, world)
+        ms_arc = max_over_ranks(ms_arc, world)
         extra["adaptive_random_25M"] = {
             "ms_per_call": round(ms_ar, 4),
             "GB_s": round(12 * d3 / (ms_ar * 1e-3) / 1e9, 1),
             "bytes_formula": "12 * D: two reads of x (the buffer sums, the speculated cumsum) + the dense output",
+            "inputs": f"{n_cl4} distinct 100 MB deltas in rotation",
+            "same_input_ms_per_call": round(ms_arc, 4),
             "note": "bit-exact numpy order: pairwise fp32 sum per 8192-element buffer, speculated exact fp64 cumsum "
                     "(DESIGN.md 3.5); the numpy reference takes ~0.3 s for this call",
         }
@@ -672,13 +748,11 @@ def main():
         }
         del xs_b, glb, lcs
         torch.cuda.empty_cache()
-        from fl_sim_amd import dist as fdist
 
         # configs[3]: 8 clients, client i on rank i mod N (nodes.py:706-713), w_i = ts_i / sum ts with
         # ts_i = 100 (i + 1); each rank folds its clients (stacked codec + fused weighted decode-accumulate), then
         # ONE RCCL reduce to rank 0 (none at N = 1: the fold is the whole round).  8 clients at every N: the total
         # work is fixed (strong scaling for this line; the headline is weak scaling).
-        n_cl4 = 8
         acc = torch.empty(d3, dtype=torch.float32, device=dev)
         w_all = fdist.sample_weights([100 * (i + 1) for i in range(n_cl4)])
         mine = fdist.client_shard(n_cl4, world, rank)
@@ -686,7 +760,7 @@ def main():
 
         def step4():
             c4[0] += 1
-            fdist.aggregate_round([X3] * len(mine), [w_all[c] for c in mine], mine,
+            fdist.aggregate_round([X8[c] for c in mine], [w_all[c] for c in mine], mine,
                                   fdist.stacked_decode_accumulate(k3, LEVELS, seed=0, counter=c4[0]),
                                   out=acc, dst=0)
 
@@ -698,7 +772,7 @@ def main():
         fold = fdist.stacked_decode_accumulate(k3, LEVELS, seed=0, counter=0)
 
         def step4_codec():  # as aggregate_round does it: the rank's clients into records, one fold from +0
-            fold.many([X3] * len(mine), [w_all[c] for c in mine], acc, mine, accumulate=False)
+            fold.many([X8[c] for c in mine], [w_all[c] for c in mine], acc, mine, accumulate=False)
 
         ms4c, _ = timed(step4_codec, 10, 3, world)
         ms4c = max_over_ranks(ms4c, world)
@@ -725,6 +799,8 @@ def main():
             # nccl-tests convention for reduce: busBw = algBw = bytes / time (every non-root rank's whole 4 D
             # buffer crosses a link); the timed reduces re-reduce `acc` in place (values unused)
             line4["reduce_algbw_GB_s"] = round(4 * d3 / (ms4r * 1e-3) / 1e9, 1)
+            # against the xGMI bound (7 links x ~153 GB/s per GPU)
+            line4["reduce_frac_of_xgmi"] = round(4 * d3 / (ms4r * 1e-3) / 1e9 / XGMI_GBS, 4)
         # the same round with the packed wire as the only exchange (SURVEY §8(e)'s sparse alternative): each rank
         # encodes its clients into wire records, ONE all_gather of the records, the fold of all 8 clients in
         # client order in one pass on rank 0 (bit-identical to the single-device fold at every N)
@@ -733,7 +809,7 @@ def main():
         def step4w():
             c4[0] += 1
             wc4.counter = c4[0]
-            fdist.aggregate_round_wire([X3] * len(mine), w_all, n_cl4, wc4, out=acc, dst=0, device=dev)
+            fdist.aggregate_round_wire([X8[c] for c in mine], w_all, n_cl4, wc4, out=acc, dst=0, device=dev)
 
         ms4w, _ = timed(step4w, 10, 3, world)
         ms4w = max_over_ranks(ms4w, world)
@@ -749,10 +825,27 @@ def main():
             def step4w1():
                 c4[0] += 1
                 wc4.counter = c4[0]
-                fdist.aggregate_round_wire([X3] * len(mine), w_all, n_cl4, _OneByOne, out=acc, dst=0, device=dev)
+                fdist.aggregate_round_wire([X8[c] for c in mine], w_all, n_cl4, _OneByOne, out=acc, dst=0, device=dev)
 
             ms4w1, _ = timed(step4w1, 10, 3, world)
             line4["wire_ms_per_step_one_launch_per_client"] = round(max_over_ranks(ms4w1, world), 4)
+        if world > 1:
+            # the wire exchange alone: one all_gather of every rank's block of records (nccl-tests convention:
+            # algBw = world * block / t, busBw = algBw * (world - 1) / world), against the xGMI bound
+            import torch.distributed as tdist
+
+            blk = torch.zeros(per4 * wc4.stride, dtype=torch.uint8, device=dev)
+            gat = torch.empty(world * blk.numel(), dtype=torch.uint8, device=dev)
+            msg, _ = timed(lambda: tdist.all_gather_into_tensor(gat, blk), 10, 3, world)
+            msg = max_over_ranks(msg, world)
+            alg = world * blk.numel() / (msg * 1e-3) / 1e9
+            line4["wire_allgather_ms"] = round(msg, 4)
+            line4["wire_allgather_algbw_GB_s"] = round(alg, 1)
+            line4["wire_allgather_busbw_GB_s"] = round(alg * (world - 1) / world, 1)
+            line4["wire_allgather_frac_of_xgmi"] = round(alg * (world - 1) / world / XGMI_GBS, 4)
+            del blk, gat
+        line4["xgmi_GB_s"] = XGMI_GBS
+        line4["inputs"] = f"{n_cl4} distinct client deltas (dist.synthetic_client_delta), 100 MB each"
         line4["wire_record_bytes"] = wc4.stride
         line4["wire_gather_bytes_per_rank"] = per4 * wc4.stride
         line4["wire_bytes_formula"] = ("codec: n_local * (4 * D + 5 * K + tiles) written as records; all_gather: "
@@ -761,11 +854,11 @@ def main():
         # self-check: one more round both ways over the process group, compared on rank 0 with the
         # single-device per-client chain of all 8 clients — the wire round bit for bit, the dense round within
         # 1e-6 * sum|w d| + 1e-30
-        parity = fdist.round_parity([X3] * n_cl4, w_all, fdist.StackedWireCodec(d3, k3, LEVELS, seed=0, counter=777),
+        parity = fdist.round_parity(X8, w_all, fdist.StackedWireCodec(d3, k3, LEVELS, seed=0, counter=777),
                                     fdist.stacked_decode_accumulate(k3, LEVELS, seed=0, counter=777), dst=0,
                                     device=dev)
         del acc
-        del X3
+        del X3, X8
         torch.cuda.empty_cache()
         extra.update(aggregation_extras(dev, world, rank))
 
@@ -779,6 +872,7 @@ def main():
     if rank == 0 and not args.skip_cpu:  # after the GPU work, at every N (rank 0's host cores)
         cpu = cpu_baseline()
         for key, ck in (("config0_fedavg_10x417482", "aggregation_config0_fedavg_10x417482"),
+                        ("config0_fedavg_10x417482", "aggregation_config0_host_server"),
                         ("config1_quant8_10x417482", "config2_quant8_10x417482"),
                         ("config2_topk1pct_25M", "config3_topk1pct_25M"),
                         ("config3_round_8x25M", "config4_codec_plus_rccl_reduce_25M")):

@@ -117,6 +117,7 @@ SIGNATURES = {
         [c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int64, c_int64, c_int, c_int, c_void_p, c_void_p],
     ),
     "flc_comm_id_bytes": (c_size_t, []),
+    "flc_comm_rccl_origin": (c_char_p, []),
     "flc_comm_unique_id": (c_int, [c_void_p]),
     "flc_comm_init": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "flc_comm_size": (c_int, [c_void_p, c_void_p, c_void_p]),

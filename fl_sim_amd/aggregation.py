@@ -13,6 +13,10 @@ subclasses unchanged (``class MyServer(AggregationMixin, FedAvgServer)``):
                                                   (and the reference's client-id bookkeeping)
 * ``feddr_update``        — _feddr.py:166-190    ``y`` relaxation, ``x̃`` fold, ``θ = prox(c_x x̃ + c_y y)``
 
+A server whose model lives in host memory — the reference's own placement (nodes.py:606) — is served by the same
+launches: its tensors are staged to the device and written back in place (``hoststage``; the mixins adopt the
+server's tensors into one pinned buffer so that staging is one copy each way).
+
 A whole model is folded in ONE launch (``flc_model_fold``, up to 16 messages; FedOpt's optimizer step fused into
 the same pass), else each tensor in one launch (``flc_weighted_sum``): one read per message, one write, the fmaf chain
 in message order — bit-identical to the reference's sequential ``add_`` loop, which torch evaluates as one fp32 fma
@@ -27,7 +31,7 @@ from typing import Iterable, List, Mapping, Optional, Sequence
 
 import torch
 
-from . import _lib, codec
+from . import _lib, codec, hoststage
 
 
 def _params(ps) -> List[torch.Tensor]:
@@ -56,27 +60,45 @@ def _model_device(tensors: Sequence[torch.Tensor]) -> Optional[int]:
 
 def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
           init_mode: int, beta: float = 0.0, **step) -> bool:
-    """The whole model in one flc_model_fold launch when it qualifies (one device, <= 16 messages); False otherwise."""
+    """The whole model in flc_model_fold launches when it qualifies (one device): one launch per 16 messages, the
+    chain continued from the stored partial sums (init mode 2) and the FedOpt step fused into the last launch only —
+    the same fmaf chain as one launch.  False when the model does not qualify."""
     dev = _model_device(list(dsts) + list(step.get("theta") or []) + list(step.get("v") or []))
-    if dev is None or not dsts or len(msg_tensors) > codec.MODEL_FOLD_MAX_SRC:
+    if dev is None or not dsts:
         return False
+    cap = codec.MODEL_FOLD_MAX_SRC
+    if len(msg_tensors) > cap:
+        for c0 in range(0, len(msg_tensors) - cap, cap):
+            _fold_one(dev, dsts, msg_tensors[c0:c0 + cap], weights[c0:c0 + cap], init_mode if c0 == 0 else 2, beta)
+        last = (len(msg_tensors) - 1) // cap * cap
+        _fold_one(dev, dsts, msg_tensors[last:], weights[last:], 2, beta, **step)
+        return True
+    _fold_one(dev, dsts, msg_tensors, weights, init_mode, beta, **step)
+    return True
+
+
+def _fold_one(dev: int, dsts, msg_tensors, weights, init_mode: int, beta: float, **step) -> None:
     if codec._model_fold_op() is not None:
         # the op checks every tensor in C++ before launching anything: with the messages already on the model's
         # device (the usual case) that is the whole host cost; otherwise it raises TypeError and they are moved below
         try:
             codec.model_fold(dsts, msg_tensors, weights, init_mode, beta, **step)
-            return True
+            return
         except TypeError:
             pass
     srcs = [[t if (t.is_cuda and t.get_device() == dev) else t.detach().to(f"cuda:{dev}") for t in mt]
             for mt in msg_tensors]
     codec.model_fold(dsts, srcs, weights, init_mode, beta, **step)
-    return True
 
 
 def add_parameters(server_params: Iterable[torch.Tensor], params: Iterable[torch.Tensor], ratio: float) -> None:
     """nodes.py:1116-1132."""
-    sps, ps = _params(server_params), list(params)
+    sps, ps = list(server_params), list(params)
+    if hoststage.is_host(sps):  # the reference's CPU server: staged, folded on the device, written back in place
+        with hoststage.staged([sps], [True], [True], [ps]) as ((dsps,), (dps,)):
+            add_parameters(dsps, dps, ratio)
+        return
+    sps = _params(sps)
     if _fold(sps, [ps], [ratio], 2):
         return
     for sp, p in zip(sps, ps):
@@ -89,43 +111,66 @@ def avg_parameters(server_params: Sequence[torch.Tensor], messages: Sequence[Map
     assert 0.0 <= inertia < 1.0, "`inertia` should be in [0, 1)"
     if len(messages) == 0:
         return
+    sps = list(server_params)
+    if hoststage.is_host(sps):
+        with hoststage.staged([sps], [True], [True], [m[key] for m in messages]) as ((dsps,), dmsgs):
+            avg_parameters(dsps, [{key: d, "train_samples": m["train_samples"]} for m, d in zip(messages, dmsgs)],
+                           size_aware, inertia, key)
+        return
     total_samples = sum([m["train_samples"] for m in messages])
     ratios = [
         (m["train_samples"] / total_samples if size_aware else 1 / len(messages)) * (1 - inertia) for m in messages
     ]
-    if _fold(_params(server_params), [m[key] for m in messages], ratios, 0, inertia):
+    if _fold(_params(sps), [m[key] for m in messages], ratios, 0, inertia):
         return
-    for j, sp in enumerate(_params(server_params)):
+    for j, sp in enumerate(_params(sps)):
         srcs = [_on(m[key][j], sp.device) for m in messages]
         codec.weighted_sum(sp, srcs, ratios, init_mode=0, beta=inertia)
 
 
-def update_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Mapping]) -> Optional[List[torch.Tensor]]:
-    """nodes.py:1165-1180: sets ``.grad`` of each model parameter to the sample-weighted gradient sum."""
-    if len(messages) == 0:
-        return None
-    assert all(["gradients" in m for m in messages]), "some clients have not sent gradients yet"
+def _gradients_on(dev: torch.device, messages: Sequence[Mapping]) -> List[torch.Tensor]:
+    """Σ_m (ts_m / Σts) · g_m per tensor, folded on ``dev`` into one flat buffer's views."""
     total_samples = sum([m["train_samples"] for m in messages])
     weights = [m["train_samples"] / total_samples for m in messages]
     g0s = messages[0]["gradients"]
-    devs = {mp.device if mp.device.type == "cuda" else g.device for mp, g in zip(model_params, g0s)}
-    if len(devs) == 1 and next(iter(devs)).type == "cuda":
-        dev = next(iter(devs))
-        gs = [torch.empty(g.shape, dtype=g.dtype, device=dev) for g in g0s]
-        if _fold(gs, [m["gradients"] for m in messages], weights, 1):
-            for mp, g in zip(model_params, gs):
-                if isinstance(mp, torch.Tensor) and mp.requires_grad:
-                    mp.grad = g
-            return gs
-    grads = []
-    for j, mp in enumerate(model_params):
-        g0 = messages[0]["gradients"][j]
-        dev = mp.device if mp.device.type == "cuda" else g0.device
-        g = torch.empty(g0.shape, dtype=g0.dtype, device=dev)
+    dt = g0s[0].dtype
+    flat = torch.empty(max(sum(g.numel() for g in g0s), 1), dtype=dt, device=dev)
+    gs, off = [], 0
+    for g in g0s:
+        gs.append(flat[off:off + g.numel()].view(g.shape))
+        off += g.numel()
+    if all(g.dtype == dt for g in g0s) and _fold(gs, [m["gradients"] for m in messages], weights, 1):
+        return gs
+    gs = [torch.empty(g.shape, dtype=g.dtype, device=dev) for g in g0s]
+    for j, g in enumerate(gs):
         codec.weighted_sum(g, [_on(m["gradients"][j], dev) for m in messages], weights, init_mode=1)
+    return gs
+
+
+def update_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Mapping]) -> Optional[List[torch.Tensor]]:
+    """nodes.py:1165-1180: sets ``.grad`` of each model parameter to the sample-weighted gradient sum, on the model's
+    device (a host-resident model gets host gradients, as the reference's ``.to(self.device)`` gives)."""
+    if len(messages) == 0:
+        return None
+    assert all(["gradients" in m for m in messages]), "some clients have not sent gradients yet"
+    model_params = list(model_params)
+    if hoststage.is_host(model_params):
+        dev = hoststage._device_for([m["gradients"] for m in messages])
+        with torch.cuda.device(dev):
+            dmsgs = hoststage.stage_messages([m["gradients"] for m in messages], dev, messages[0]["gradients"][0].dtype)
+            dgs = _gradients_on(dev, [{"gradients": d, "train_samples": m["train_samples"]}
+                                      for m, d in zip(messages, dmsgs)])
+            grads = [g.to("cpu") for g in dgs]
+    else:
+        g0s = messages[0]["gradients"]
+        devs = {mp.device if mp.device.type == "cuda" else g.device for mp, g in zip(model_params, g0s)}
+        if len(devs) != 1 or next(iter(devs)).type != "cuda":
+            raise TypeError("update_gradients: the model and the gradients must live on one HIP device, or the model "
+                            "in host memory")
+        grads = _gradients_on(next(iter(devs)), messages)
+    for mp, g in zip(model_params, grads):
         if isinstance(mp, torch.Tensor) and mp.requires_grad:
             mp.grad = g
-        grads.append(g)
     return grads
 
 
@@ -137,8 +182,16 @@ def fedopt_update(model_params: Sequence[torch.Tensor], delta_parameters: Sequen
     if opt not in ("avg", "adagrad", "yogi", "adam"):
         raise ValueError(f"Unknown optimizer: {optimizer}")
     alpha = (1 - betas[0]) / len(messages) if len(messages) else 0.0
-    ps = _params(model_params)
+    model_params, delta_parameters = list(model_params), list(delta_parameters)
     vps = None if (v_parameters is None or opt == "avg") else list(v_parameters)
+    if hoststage.is_host(model_params):
+        groups = [model_params, delta_parameters] + ([vps] if vps is not None else [])
+        n = len(groups)
+        with hoststage.staged(groups, [True] * n, [True] * n, [m["delta_parameters"] for m in messages]) as (dg, dm):
+            fedopt_update(dg[0], dg[1], dg[2] if vps is not None else None,
+                          [{"delta_parameters": d} for d in dm], optimizer, lr, betas, tau)
+        return
+    ps = _params(model_params)
     if _fold(list(delta_parameters), [m["delta_parameters"] for m in messages], [alpha] * len(messages), 0, betas[0],
              theta=ps, v=vps, opt=opt if vps is not None else "avg", lr=lr, beta2=betas[1], tau=tau):
         return  # the delta average and the optimizer step of every tensor in one launch
@@ -159,6 +212,15 @@ def scaffold_update(model_params: Sequence[torch.Tensor], control_variates: Sequ
         raise ZeroDivisionError("division by zero")  # ratio_p = lr / len(messages) in the reference
     ratio_p = lr / len(messages)
     ratio_c = 1 / num_clients
+    model_params, control_variates = list(model_params), list(control_variates)
+    if hoststage.is_host(model_params):
+        n = len(messages)
+        with hoststage.staged([model_params, control_variates], [True, True], [True, True],
+                              [m["parameters_delta"] for m in messages]
+                              + [m["control_variates_delta"] for m in messages]) as ((dps, dcvs), dm):
+            scaffold_update(dps, dcvs, [{"parameters_delta": a, "control_variates_delta": b}
+                                        for a, b in zip(dm[:n], dm[n:])], lr, num_clients)
+        return
     ps, cvs = _params(model_params), list(control_variates)
     if _model_device(ps + cvs) is not None and ps and cvs and len(messages) <= codec.MODEL_FOLD_MAX_SRC:
         _fold(ps, [m["parameters_delta"] for m in messages], [ratio_p] * len(messages), 2)
@@ -191,7 +253,13 @@ def ifca_update(cluster_centers: Mapping[int, dict], messages: Sequence[Mapping]
     for c, v in cluster_centers.items():
         v["client_ids"].extend(i for i in prev[c] if i not in collected)
     for c, ms in members.items():
-        for j, p in enumerate(_params(cluster_centers[c]["center_model_params"])):
+        center = list(cluster_centers[c]["center_model_params"])
+        if hoststage.is_host(center):
+            with hoststage.staged([center], [True], [True], [m["delta_parameters"] for m in ms]) as ((dc,), dm):
+                for j, p in enumerate(dc):
+                    codec.weighted_sum(p, [d[j] for d in dm], [1 / sizes[c]] * len(ms), init_mode=2)
+            continue
+        for j, p in enumerate(_params(center)):
             codec.weighted_sum(p, [_on(m["delta_parameters"][j], p.device) for m in ms], [1 / sizes[c]] * len(ms),
                                init_mode=2)
     for m in messages:
@@ -220,6 +288,13 @@ def feddr_update(model_params: Sequence[torch.Tensor], y_params: Sequence[torch.
     if kind not in _PROX_KIND:
         raise ValueError(f"Unknown regularizer type: {reg_type}")
     kind = _PROX_KIND[kind]
+    model_params, y_params, x_til_params = list(model_params), list(y_params), list(x_til_params)
+    if hoststage.is_host(model_params):
+        with hoststage.staged([model_params, y_params, x_til_params], [True] * 3, [True] * 3,
+                              [m["x_hat_delta"] for m in messages]) as ((dps, dys, dxs), dm):
+            feddr_update(dps, dys, dxs, [{"x_hat_delta": d, "train_samples": m["train_samples"]}
+                                         for m, d in zip(messages, dm)], alpha, eta, num_clients, reg_type)
+        return
     coeff = eta * num_clients / (num_clients + 1)
     total = sum([m["train_samples"] for m in messages])
     weights = [m["train_samples"] / total for m in messages]
@@ -246,16 +321,28 @@ def feddr_update(model_params: Sequence[torch.Tensor], y_params: Sequence[torch.
             codec.weighted_sum(sp, [], [], init_mode=0, beta=f)
 
 
+def _adopt(groups, messages_tensors=()) -> None:
+    """The mixins own the server's tensors: a host-resident server's groups are adopted into one pinned buffer with a
+    device mirror (hoststage.adopt), so each update stages them with one copy each way."""
+    groups = [list(g) for g in groups if g is not None]
+    if groups and hoststage.is_host(groups[0]):
+        hoststage.adopt(groups, hoststage._device_for(messages_tensors))
+
+
 class AggregationMixin:
     """Mix in before a reference ``Server`` subclass to run its aggregation on the device.
 
-    Requires the server model on a HIP device (``self.model`` parameters on ``cuda:k``).
+    The server model may live on a HIP device or in host memory (the reference's ``Server`` keeps it on the CPU,
+    nodes.py:606): host tensors are staged to the device and written back in place, bit-identical either way.
     """
 
     def add_parameters(self, params, ratio: float) -> None:  # nodes.py:1116
+        params = list(params)
+        _adopt([list(self.model.parameters())], [params])
         add_parameters(self.model.parameters(), params, ratio)
 
     def avg_parameters(self, size_aware: bool = False, inertia: float = 0.0) -> None:  # nodes.py:1134
+        _adopt([list(self.model.parameters())], [m["parameters"] for m in self._received_messages])
         avg_parameters(list(self.model.parameters()), self._received_messages, size_aware, inertia)
 
     def update_gradients(self) -> None:  # nodes.py:1165
@@ -263,9 +350,13 @@ class AggregationMixin:
 
 
 class FedOptUpdateMixin:
-    """Device ``update()`` for the reference's ``FedOptServer`` family (_fedopt.py:196-240)."""
+    """Device ``update()`` for the reference's ``FedOptServer`` family (_fedopt.py:196-240), for a server model on a
+    HIP device or in host memory."""
 
     def update(self) -> None:
+        adaptive = self.v_parameters is not None and self.config.optimizer.lower() != "avg"
+        _adopt([list(self.model.parameters()), self.delta_parameters, self.v_parameters if adaptive else None],
+               [m["delta_parameters"] for m in self._received_messages])
         fedopt_update(list(self.model.parameters()), self.delta_parameters, self.v_parameters,
                       self._received_messages, self.config.optimizer, self.config.lr, self.config.betas,
                       self.config.tau)
@@ -275,6 +366,8 @@ class SCAFFOLDUpdateMixin:
     """Device ``update()`` for the reference's ``SCAFFOLDServer`` (_scaffold.py:158-167)."""
 
     def update(self) -> None:
+        _adopt([list(self.model.parameters()), self._control_variates],
+               [m["parameters_delta"] for m in self._received_messages])
         scaffold_update(list(self.model.parameters()), self._control_variates, self._received_messages,
                         self.config.lr, len(self._clients))
 
@@ -290,6 +383,8 @@ class FedDRUpdateMixin:
     """Device ``update()`` for the reference's ``FedDRServer`` (_feddr.py:166-190)."""
 
     def update(self) -> None:
+        _adopt([list(self.model.parameters()), self._y_parameters, self._x_til_parameters],
+               [m["x_hat_delta"] for m in self._received_messages])
         feddr_update(list(self.model.parameters()), self._y_parameters, self._x_til_parameters,
                      self._received_messages, self.config.alpha, self.config.eta, self.config.num_clients,
                      self.config.reg_type)

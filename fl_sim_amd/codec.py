@@ -174,6 +174,7 @@ def quant_encode_auto(x2d: torch.Tensor, kind: int, levels: int, p: float = math
     ws = workspace(x2d.device, _lib.size("flc_quant_workspace_size", rows, d), "quant")
     call("flc_quant_encode_auto", _p(x2d), rows, d, kind, levels, bits, pk, seed, counter, _p(codes), _p(norms),
          _p(nnz), _p(out), _p(ws), ws.numel(), _stream(x2d.device))
+    _after_encode(x2d.device, ("quant",))
     return QuantPacket(codes, norms, rows, d, kind, levels, bits, nnz), out
 
 
@@ -220,20 +221,31 @@ _TOPK_KINDS = ("topk", "topk_batch")  # single-client and batched encoder worksp
 _STATUS_FN = {"topk": "flc_topk_status", "topk_batch": "flc_topk_status", "quant": "flc_quant_status"}
 
 
-def topk_status(device: Optional[torch.device] = None, reset: bool = True) -> int:
-    """The sticky error word of the top-k workspace of ``device``'s current stream (0 = every encode since
-    the last reset was exact).  Synchronises that stream."""
-    device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+def _status(device: torch.device, kinds: Sequence[str], reset: bool = True) -> int:
     err = 0
-    for kind in _TOPK_KINDS:
+    for kind in kinds:
         key = (device.index if device.index is not None else torch.cuda.current_device(), _stream(device), kind)
         ws = _WS.get(key)
         if ws is None:
             continue
         out = torch.empty(1, dtype=torch.int64, device=device)
-        call("flc_topk_status", _p(ws), _p(out), int(reset), _stream(device))
+        call(_STATUS_FN[kind], _p(ws), _p(out), int(reset), _stream(device))
         err |= int(out.item())
     return err
+
+
+def topk_status(device: Optional[torch.device] = None, reset: bool = True) -> int:
+    """The sticky error word of the top-k workspace of ``device``'s current stream (0 = every encode since
+    the last reset was exact).  Synchronises that stream."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    return _status(device, _TOPK_KINDS, reset)
+
+
+def quant_status(device: Optional[torch.device] = None, reset: bool = True) -> int:
+    """The sticky error word of the one-launch quantizer's workspace (quant_fused_kernel's grid exchange) of
+    ``device``'s current stream; 0 = every call since the last reset had all its blocks resident."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    return _status(device, ("quant",), reset)
 
 
 def topk_status_all(reset: bool = True) -> Dict[Tuple[int, int], int]:
@@ -252,12 +264,15 @@ def topk_status_all(reset: bool = True) -> Dict[Tuple[int, int], int]:
     return res
 
 
-def _after_encode(device: torch.device) -> None:
+def _after_encode(device: torch.device, kinds: Sequence[str] = _TOPK_KINDS) -> None:
+    """FLC_TOPK_CHECK: read the sticky error word of the workspaces ``kinds`` (one host synchronisation) and raise
+    if a grid-exchange launch lost co-residency; its output would be wrong."""
     if TOPK_CHECK:
-        err = topk_status(device)
+        err = _status(device, kinds)
         if err:
             bits = ", ".join(v for b, v in TOPK_ERRORS.items() if err & b)
-            raise _lib.FlcError(f"top-k encode lost co-residency or failed ({bits}); its kept set may be wrong")
+            what = "quantizer" if tuple(kinds) == ("quant",) else "top-k encode"
+            raise _lib.FlcError(f"{what} lost co-residency or failed ({bits}); its output may be wrong")
 
 
 def _tiles(n: int, device: torch.device) -> torch.Tensor:
@@ -774,6 +789,8 @@ def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tenso
     if op is not None:  # the checks and the pointer tables in C++ (torch_ops.cpp): one dispatcher call
         if any(len(msg) != nt for msg in srcs):
             raise ValueError("every message has one tensor per model tensor")
+        if len(weights) != ns:
+            raise ValueError("one weight per message")
         op(list(dsts), [t for msg in srcs for t in msg], [float(w) for w in weights], int(init_mode), float(beta),
            [] if theta is None else list(theta), [] if v is None else list(v), _lib.FLC_OPT[opt], float(lr),
            float(beta2), float(tau))
@@ -789,7 +806,12 @@ def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tenso
             out.append(t.data_ptr())
         return out
 
+    if len(weights) != ns:
+        raise ValueError("one weight per message")
     sizes = [t.numel() for t in dsts]
+    for what, ts in (("theta", theta), ("v", v)):
+        if ts is not None and (len(ts) != nt or any(t.numel() != n for t, n in zip(ts, sizes))):
+            raise ValueError(f"{what} must have one tensor per model tensor, of the model tensors' sizes")
     dp = ptrs(dsts, "model")
     sp = []
     for msg in srcs:

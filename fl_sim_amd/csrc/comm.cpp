@@ -50,32 +50,51 @@ int find_loaded_rccl(struct dl_phdr_info* info, size_t, void* out) {
   return 1;
 }
 
+// where the symbols came from (flc_comm_rccl_origin): "env", "global", "loaded", "dlopen" or "none"
+const char* g_origin = "none";
+
 Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
     void* h = nullptr;
-    if (const char* path = getenv("FLC_RCCL_LIB")) h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
-    if (!h && dlsym(RTLD_DEFAULT, "ncclCommInitRank")) h = RTLD_DEFAULT;  // in the global namespace already
-    if (!h) {
+    const char* origin = "none";
+    if (const char* path = getenv("FLC_RCCL_LIB")) {
+      h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
+      if (h) origin = "env";
+    }
+    // in the global namespace already: every symbol is then resolved there.  glibc's RTLD_DEFAULT is a null handle,
+    // so this case is tracked by its own flag, never by testing the handle
+    bool global = false;
+    if (!h && dlsym(RTLD_DEFAULT, "ncclCommInitRank")) {
+      global = true;
+      origin = "global";
+    }
+    if (!h && !global) {
       const char* loaded = nullptr;  // loaded privately (e.g. as a dependency of torch's HIP library)
       dl_iterate_phdr(find_loaded_rccl, &loaded);
       if (loaded) h = dlopen(loaded, RTLD_NOW | RTLD_NOLOAD);
+      if (h) origin = "loaded";
     }
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) return;
-    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
-    r.init_rank = reinterpret_cast<decltype(r.init_rank)>(dlsym(h, "ncclCommInitRank"));
-    r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(h, "ncclCommDestroy"));
-    r.reduce = reinterpret_cast<decltype(r.reduce)>(dlsym(h, "ncclReduce"));
-    r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
-    r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
-    r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
-    r.count = reinterpret_cast<decltype(r.count)>(dlsym(h, "ncclCommCount"));
-    r.user_rank = reinterpret_cast<decltype(r.user_rank)>(dlsym(h, "ncclCommUserRank"));
+    if (!h && !global) {
+      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+      if (h) origin = "dlopen";
+    }
+    if (!h && !global) return;
+    void* const src = global ? RTLD_DEFAULT : h;
+    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(src, "ncclGetUniqueId"));
+    r.init_rank = reinterpret_cast<decltype(r.init_rank)>(dlsym(src, "ncclCommInitRank"));
+    r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(src, "ncclCommDestroy"));
+    r.reduce = reinterpret_cast<decltype(r.reduce)>(dlsym(src, "ncclReduce"));
+    r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(src, "ncclAllReduce"));
+    r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(src, "ncclAllGather"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(src, "ncclGetErrorString"));
+    r.count = reinterpret_cast<decltype(r.count)>(dlsym(src, "ncclCommCount"));
+    r.user_rank = reinterpret_cast<decltype(r.user_rank)>(dlsym(src, "ncclCommUserRank"));
     r.ok = r.get_unique_id && r.init_rank && r.destroy && r.reduce && r.all_reduce && r.all_gather &&
            r.error_string && r.count && r.user_rank;
+    g_origin = r.ok ? origin : "none";
   });
   return r;
 }
@@ -103,6 +122,11 @@ using namespace flc;
 extern "C" {
 
 size_t flc_comm_id_bytes(void) { return sizeof(ncclUniqueId); }
+
+const char* flc_comm_rccl_origin(void) {
+  rccl();
+  return g_origin;
+}
 
 int flc_comm_unique_id(void* id_out) {
   if (!id_out) return fail(FLC_EINVAL, "flc_comm_unique_id: null output");

@@ -39,7 +39,7 @@ constexpr int kRowSlots = 16;              // per-block LDS nnz slots
 
 struct QuantWs {
   unsigned long long* err;       // [1] sticky error word: 4 = a fused launch's exchange timed out (flc_quant_status)
-  unsigned* flags;               // [1024] fused launch: each block's arrival epoch
+  unsigned long long* flags;     // [1024] fused launch: each block's arrival epoch (64-bit: never wraps)
   unsigned long long* partials;  // [rows * kNormMaxParts]
   int* chunk_counts;             // [nblocks]  (compat)
   long long* chunk_offsets;      // [nblocks]  (compat)
@@ -50,7 +50,7 @@ QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* nee
   Carver c(ws, bytes);
   QuantWs w;
   w.err = c.take<unsigned long long>(1);
-  w.flags = c.take<unsigned>(1024);
+  w.flags = c.take<unsigned long long>(1024);
   w.partials = c.take<unsigned long long>((size_t)rows * kNormMaxParts);
   w.chunk_counts = c.take<int>((size_t)nblocks);
   w.chunk_offsets = c.take<long long>((size_t)nblocks);
@@ -551,7 +551,7 @@ constexpr int kMaxFused = 1024;  // blocks (flags)
 // level) and drained with s_waitcnt vmcnt(0) before the flag is raised; readers load it the same way — no release /
 // acquire fence, which on gfx950 writes back / invalidates the whole L2 (measured 6-8 us over 510 blocks, quant.hip's
 // dropped ticket fold).  The exchange of topk.hip, for one kernel with its own flag region.
-__device__ __forceinline__ void fused_exchange(const QuantWs& ws, unsigned epoch) {
+__device__ __forceinline__ void fused_exchange(const QuantWs& ws, unsigned long long epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int tid = threadIdx.x;
@@ -565,8 +565,9 @@ __device__ __forceinline__ void fused_exchange(const QuantWs& ws, unsigned epoch
       for (int i = 0; i < kMaxFused / kWave; ++i) {
         const int b = tid + i * kWave;
         if (i * kWave < G) {  // (uniform)
-          const unsigned f = __hip_atomic_load(ws.flags + (b < G ? b : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok &= b >= G || (int)(f - epoch) >= 0;
+          const unsigned long long f =
+              __hip_atomic_load(ws.flags + (b < G ? b : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= b >= G || f >= epoch;  // a zeroed flag (0) or any earlier call's epoch is below this call's
         }
       }
       if (__ballot(!ok) == 0ull) break;
@@ -585,7 +586,7 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
                                                           double step, float* __restrict__ norms, uint64_t seed,
                                                           uint64_t counter, uint8_t* __restrict__ codes,
                                                           long long* __restrict__ nnz, float* __restrict__ out,
-                                                          QuantWs ws, unsigned epoch, int cal) {
+                                                          QuantWs ws, unsigned long long epoch, int cal) {
   constexpr int64_t SPAN = (int64_t)kFT * kGroup * GPT;
   __shared__ uint32_t s_m[2][kFT / kWave];
   __shared__ float s_norm[2];
@@ -734,13 +735,11 @@ int check_quant_args(int kind, int levels, int bits) {
 
 double level_step(int levels) { return 1.0 / (double)levels; }
 
-// the one-launch encode's exchange epochs: process-wide and increasing, so a flag left by any earlier call (of any
-// shape, on any workspace) is older than this call's; never 0 (a fresh workspace's flags)
-unsigned next_epoch() {
-  static std::atomic<unsigned> epochs{0};
-  unsigned ep = ++epochs;
-  while (ep == 0) ep = ++epochs;
-  return ep;
+// the one-launch encode's exchange epochs: process-wide and increasing (64-bit, so they never wrap), so a flag left by
+// any earlier call (of any shape, on any workspace) is below this call's; never 0 (a fresh workspace's flags)
+unsigned long long next_epoch() {
+  static std::atomic<unsigned long long> epochs{0};
+  return ++epochs;
 }
 
 template <int KIND, int BITS, bool DEC>
@@ -885,7 +884,7 @@ int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p,
                     : (d >= 4 * kFT * kGroup && n <= (int64_t)cus * 4 * kFT * kGroup) ? 4
                                                                                         : 0;
     if (gpt) {
-      const unsigned ep = next_epoch();
+      const unsigned long long ep = next_epoch();
       const unsigned grid = (unsigned)cdiv(n, (int64_t)gpt * kFT * kGroup);
       const char* fname = DEC ? "quant_fused_encode_decode" : "quant_fused_encode";
 #ifdef FLC_CALIB  // calibration builds (tools/quant_cal_probe.py): 1 non-temporal stores, 2 no exchange, 4 traffic only

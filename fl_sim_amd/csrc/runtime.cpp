@@ -134,12 +134,22 @@ Coresident::Coresident(hipStream_t st, int dev) : st_(st), dev_(dev < 0 || dev >
     gt.used[dev_] = true;
     gt.first[dev_] = st_;
   } else if (!gt.multi[dev_] && st_ != gt.first[dev_]) {
-    if ((e = hipDeviceSynchronize()) != hipSuccess) {
-      rc_ = hip_fail(e, "hipDeviceSynchronize");
+    // drain dev_ (the device of the earlier persistent launches, not necessarily the calling thread's current
+    // device) and make its gate event there: dev_ is made current for these two calls only
+    int cur = -1;
+    if ((e = hipGetDevice(&cur)) != hipSuccess) {
+      rc_ = hip_fail(e, "hipGetDevice");
       return;
     }
-    if (!gt.last[dev_] && (e = hipEventCreateWithFlags(&gt.last[dev_], hipEventDisableTiming)) != hipSuccess) {
-      rc_ = hip_fail(e, "hipEventCreateWithFlags");
+    if (cur != dev_ && (e = hipSetDevice(dev_)) != hipSuccess) {
+      rc_ = hip_fail(e, "hipSetDevice");
+      return;
+    }
+    e = hipDeviceSynchronize();
+    if (e == hipSuccess && !gt.last[dev_]) e = hipEventCreateWithFlags(&gt.last[dev_], hipEventDisableTiming);
+    const hipError_t e2 = cur != dev_ ? hipSetDevice(cur) : hipSuccess;
+    if (e != hipSuccess || e2 != hipSuccess) {
+      rc_ = hip_fail(e != hipSuccess ? e : e2, "draining the gate's device");
       return;
     }
     gt.multi[dev_] = true;

@@ -378,11 +378,13 @@ void model_fold_(at::TensorList dsts, at::TensorList srcs, at::ArrayRef<double> 
     dp[t] = dsts[t].data_ptr<float>();
     sz[t] = dsts[t].numel();
     if (!theta.empty()) {
-      TORCH_CHECK_TYPE(usable(theta[t]) && theta[t].numel() == sz[t], "flcodec: theta must match the model tensors");
+      TORCH_CHECK_TYPE(usable(theta[t]), "flcodec: theta tensors must be contiguous fp32 HIP tensors on one device");
+      TORCH_CHECK_VALUE(theta[t].numel() == sz[t], "flcodec: theta must match the model tensors' sizes");
       tp[t] = theta[t].data_ptr<float>();
     }
     if (!v.empty()) {
-      TORCH_CHECK_TYPE(usable(v[t]) && v[t].numel() == sz[t], "flcodec: v must match the model tensors");
+      TORCH_CHECK_TYPE(usable(v[t]), "flcodec: v tensors must be contiguous fp32 HIP tensors on one device");
+      TORCH_CHECK_VALUE(v[t].numel() == sz[t], "flcodec: v must match the model tensors' sizes");
       vp[t] = v[t].data_ptr<float>();
     }
   }

@@ -42,6 +42,15 @@ def client_shard(n_clients: int, world: int, rank: int) -> List[int]:
     return [i for i in range(n_clients) if i % world == rank]
 
 
+def synthetic_client_delta(client: int, n: int, device: torch.device, seed: int = 5000,
+                           scale: float = 1e-3) -> torch.Tensor:
+    """Client ``client``'s synthetic flat delta (N(0, 1) * scale, n fp32 elements) from a generator keyed by the client
+    id alone, so every rank that builds it holds the same values (the N > 1 self-check folds every client on rank 0)
+    and distinct clients hold distinct deltas (no cache-resident repeats in the bench's configs[3] legs)."""
+    g = torch.Generator(device=device).manual_seed(seed + client)
+    return torch.randn(n, generator=g, device=device) * scale
+
+
 def sample_weights(train_samples: Sequence[int]) -> List[float]:
     """w_i = ts_i / sum(ts), formed in double as nodes.py:1173-1180 forms them (rounded to fp32 by the kernels)."""
     total = sum(train_samples)

@@ -215,6 +215,10 @@ int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slo
  * only — the calling thread's current device is restored).  Collectives are
  * stream-ordered and asynchronous like every other call. */
 size_t flc_comm_id_bytes(void);
+/* Where the RCCL symbols were found on first use (loads RCCL if not yet loaded): "env" (FLC_RCCL_LIB), "global" (the
+ * process's global namespace, e.g. torch's RCCL loaded RTLD_GLOBAL), "loaded" (an already-loaded librccl* object),
+ * "dlopen" (librccl.so.1), or "none" (not found; every flc_comm_* / flc_rccl_* call then fails with FLC_ECOMM). */
+const char* flc_comm_rccl_origin(void);
 int flc_comm_unique_id(void* id_out);
 int flc_comm_init(const void* id, int nranks, int rank, int device, void** comm_out);
 int flc_comm_size(void* comm, int* nranks, int* rank);

@@ -85,11 +85,17 @@ def test_topk_status_plumbing_without_gpu(monkeypatch):
     assert lib.flc_topk_status(None, None, 1, None) == 1  # FLC_EINVAL
     assert "flc_topk_status" in lib.flc_last_error().decode()
     monkeypatch.setattr(codec, "TOPK_CHECK", True)
-    monkeypatch.setattr(codec, "topk_status", lambda device=None, reset=True: 4)
-    with pytest.raises(_lib.FlcError, match="spin timeout"):
+    seen = []
+    monkeypatch.setattr(codec, "_status", lambda device, kinds, reset=True: seen.append(tuple(kinds)) or 4)
+    with pytest.raises(_lib.FlcError, match="top-k encode.*spin timeout"):
         codec._after_encode(None)
-    monkeypatch.setattr(codec, "topk_status", lambda device=None, reset=True: 0)
+    # the one-launch quantizer's exchange is checked too (its own workspace kind)
+    with pytest.raises(_lib.FlcError, match="quantizer.*spin timeout"):
+        codec._after_encode(None, ("quant",))
+    assert seen == [codec._TOPK_KINDS, ("quant",)]
+    monkeypatch.setattr(codec, "_status", lambda device, kinds, reset=True: 0)
     codec._after_encode(None)  # clean word: no error
+    codec._after_encode(None, ("quant",))
 
 
 def test_stacked_encode_delta_validates_without_gpu():
@@ -219,3 +225,70 @@ def test_f64_entries_validate_without_gpu():
     assert lib.flc_adaptive_stats(16, 8, 100, 16, None) == 3  # workspace too small: FLC_EWORKSPACE
     assert lib.flc_f64_workspace_size(1 << 24, 1 << 17) > lib.flc_f64_workspace_size(1 << 24, 0)
     assert lib.flc_f64_workspace_size(1000, 10) == lib.flc_f64_workspace_size(1000, 0)  # small n: no filter
+
+
+_STUB_RCCL = r"""
+#include <string.h>
+typedef struct { char internal[128]; } ncclUniqueId;
+int ncclGetUniqueId(ncclUniqueId* id) { memset(id, 0x5a, sizeof(*id)); return 0; }
+int ncclCommInitRank(void** c, int n, ncclUniqueId id, int r) { return 5; }
+int ncclCommDestroy(void* c) { return 0; }
+int ncclReduce(const void* a, void* b, unsigned long n, int t, int o, int root, void* c, void* s) { return 5; }
+int ncclAllReduce(const void* a, void* b, unsigned long n, int t, int o, void* c, void* s) { return 5; }
+int ncclAllGather(const void* a, void* b, unsigned long n, int t, void* c, void* s) { return 5; }
+const char* ncclGetErrorString(int e) { return "stub rccl"; }
+int ncclCommCount(void* c, int* n) { *n = 1; return 0; }
+int ncclCommUserRank(void* c, int* r) { *r = 0; return 0; }
+"""
+
+_STUB_DRIVER = r"""
+import ctypes, sys
+ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL)  # the stub's nccl* symbols in the global namespace first
+from fl_sim_amd import _lib
+lib = _lib.load()
+uid = ctypes.create_string_buffer(128)
+assert lib.flc_comm_unique_id(ctypes.cast(uid, ctypes.c_void_p)) == 0, lib.flc_last_error()
+assert uid.raw == b"\x5a" * 128, "the id did not come from the global-namespace RCCL"
+print(lib.flc_comm_rccl_origin().decode())
+"""
+
+
+def test_rccl_found_in_global_namespace(tmp_path):
+    """RCCL symbols already in the process's global namespace (glibc's RTLD_DEFAULT is a null handle) are
+    the ones used — no second RCCL is loaded.  A stub RCCL is loaded RTLD_GLOBAL in a fresh process first."""
+    import shutil
+    import subprocess
+    import sys
+
+    gcc = shutil.which("gcc") or shutil.which("cc")
+    if gcc is None:
+        pytest.skip("no C compiler")
+    src = tmp_path / "stub_rccl.c"
+    src.write_text(_STUB_RCCL)
+    so = tmp_path / "libstubnccl.so"
+    subprocess.run([gcc, "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    env = dict(os.environ)
+    env.pop("FLC_RCCL_LIB", None)
+    env["PYTHONPATH"] = os.pathsep.join([ROOT, env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", _STUB_DRIVER, str(so)], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == "global"
+
+
+def test_model_fold_ctypes_checks_sizes(monkeypatch):
+    """the ctypes form of model_fold checks theta / v sizes and the weight count (ValueError) before any
+    pointer is taken, as the torch op does; a mismatch must never reach the kernel."""
+    import torch
+
+    from fl_sim_amd import codec
+
+    monkeypatch.setattr(codec, "_MODEL_FOLD_OP", [None])
+    d = [torch.zeros(5), torch.zeros(3)]
+    msgs = [[torch.zeros(5), torch.zeros(3)]]
+    with pytest.raises(ValueError, match="one weight per message"):
+        codec.model_fold(d, msgs, [0.5, 0.5], 0)
+    with pytest.raises(ValueError, match="theta"):
+        codec.model_fold(d, msgs, [0.5], 0, theta=[torch.zeros(5), torch.zeros(4)])
+    with pytest.raises(ValueError, match="v must"):
+        codec.model_fold(d, msgs, [0.5], 0, theta=[torch.zeros(5), torch.zeros(3)], v=[torch.zeros(5)], opt="adam")

@@ -222,3 +222,42 @@ def test_gloo_round_parity_self_check(world, broken):
     res = items[0]
     assert res["clients"] == N_CLIENTS and res["world"] == world and res["dense_within_bound"]
     assert res["wire_bit_exact"] is (not broken) and res["ok"] is (not broken)
+
+
+def _distinct_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cpu = torch.device("cpu")
+        deltas = [fdist.synthetic_client_delta(c, D, cpu) for c in range(N_CLIENTS)]
+        sums = torch.tensor([float(d.double().sum()) for d in deltas], dtype=torch.float64)
+        got = [torch.zeros_like(sums) for _ in range(world)]
+        dist.all_gather(got, sums)
+        res = fdist.round_parity(deltas, fdist.sample_weights(TS), OracleWireCodec(D, K),
+                                 _oracle_dense_step(OracleWireCodec(D, K)), dst=0, device=cpu)
+        q.put((rank, (res, [g.tolist() for g in got])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_round_parity_with_distinct_synthetic_clients():
+    """bench.py's configs[3] legs and N > 1 parity round use distinct client deltas (dist.synthetic_client_delta, a
+    generator keyed by the client id): every rank builds the same deltas, the clients differ from each other, and the
+    self-check passes on them (gloo world 2)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_distinct_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    items = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res, sums = items[0]
+    assert sums[0] == sums[1], "every rank holds the same client deltas"
+    assert len(set(sums[0])) == N_CLIENTS, "the clients' deltas are distinct"
+    assert res["ok"] and res["wire_bit_exact"] and res["clients"] == N_CLIENTS
+    assert items[1][0] is None

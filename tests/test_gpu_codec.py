@@ -105,12 +105,14 @@ def test_dense_l2_with_reference_norm_is_bit_exact(case):
     assert abs(ours - exact) <= 2 * np.spacing(exact)
 
 
+@pytest.mark.parametrize("where", ["host", "device"])
 @pytest.mark.parametrize("D", [4_000_000, 25_000_000])
 @pytest.mark.parametrize("kind", ["std", "nat"])
-def test_dense_l2_compat_large_d_matches_oracle(D, kind):
+def test_dense_l2_compat_large_d_matches_oracle(D, kind, where):
     """p = 2 at realistic D through the drop-in Compressor (compat mode, numpy input): the norm is the reference's
     own np.linalg.norm (an fp32 BLAS dot, 3e-6 .. 6e-5 away from the exact norm at these sizes), so the output
-    equals the oracle's, which calls np.linalg.norm on this same host, bit for bit."""
+    equals the oracle's, which calls np.linalg.norm on this same host, bit for bit.  ``device``: the same vector as a
+    HIP tensor, where the default norm="auto" also takes the reference's norm (round 4)."""
     from fl_sim_amd import Compressor
 
     g = np.random.default_rng(D + (kind == "nat"))
@@ -124,7 +126,10 @@ def test_dense_l2_compat_large_d_matches_oracle(D, kind):
     else:
         c.makeNaturalDitheringFP32(8, D, 2)
     random.seed(17)
-    got = c.compressVector(x)
+    got = c.compressVector(x if where == "host" else torch.from_numpy(x).to(DEV))
+    if where == "device":
+        assert got.device.type == "cuda"
+        got = got.cpu().numpy()
     after = random.random()
     random.seed(17)
     fn = ref.standard_dithering if kind == "std" else ref.natural_dithering
