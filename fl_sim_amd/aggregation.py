@@ -44,18 +44,17 @@ def _on(t: torch.Tensor, device: torch.device) -> torch.Tensor:
 
 
 def _model_device(tensors: Sequence[torch.Tensor]) -> Optional[int]:
-    """The index of the one HIP device all of a model's tensors live on (contiguous fp32), or None (then per-tensor
-    launches)."""
-    dev = None
-    for t in tensors:
-        if not (t.is_cuda and t.dtype is torch.float32 and t.is_contiguous()):
-            return None
-        d = t.get_device()
-        if dev is None:
-            dev = d
-        elif d != dev:
-            return None
-    return dev
+    """The HIP device index of a model whose first tensor is a contiguous fp32 HIP tensor, else None (then per-tensor
+    launches).  Only the first tensor is looked at here: the model-fold op checks every tensor (device, dtype,
+    contiguity, size) in C++ before it launches anything, and a model that fails those checks falls back to the
+    per-tensor path in ``_fold`` — a model update is ~10-100 tensors, and a Python check per tensor cost more than the
+    kernel."""
+    if not tensors:
+        return None
+    t = tensors[0]
+    if not (t.is_cuda and t.dtype is torch.float32):
+        return None
+    return t.get_device()
 
 
 def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
@@ -67,13 +66,20 @@ def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence[Sequence[torch.Ten
     if dev is None or not dsts:
         return False
     cap = codec.MODEL_FOLD_MAX_SRC
-    if len(msg_tensors) > cap:
-        for c0 in range(0, len(msg_tensors) - cap, cap):
-            _fold_one(dev, dsts, msg_tensors[c0:c0 + cap], weights[c0:c0 + cap], init_mode if c0 == 0 else 2, beta)
-        last = (len(msg_tensors) - 1) // cap * cap
-        _fold_one(dev, dsts, msg_tensors[last:], weights[last:], 2, beta, **step)
-        return True
-    _fold_one(dev, dsts, msg_tensors, weights, init_mode, beta, **step)
+    try:
+        if len(msg_tensors) > cap:
+            for c0 in range(0, len(msg_tensors) - cap, cap):
+                _fold_one(dev, dsts, msg_tensors[c0:c0 + cap], weights[c0:c0 + cap], init_mode if c0 == 0 else 2,
+                          beta)
+                init_mode = 2  # (the first launch has run: the chain continues from the stored partial sums)
+            last = (len(msg_tensors) - 1) // cap * cap
+            _fold_one(dev, dsts, msg_tensors[last:], weights[last:], 2, beta, **step)
+            return True
+        _fold_one(dev, dsts, msg_tensors, weights, init_mode, beta, **step)
+    except TypeError:
+        if init_mode == 2 and len(msg_tensors) > cap:
+            raise  # (a later chunk's tensors failed after the first launch ran: no clean fallback)
+        return False  # a model tensor the fold does not take (dtype, device, layout): per-tensor launches
     return True
 
 

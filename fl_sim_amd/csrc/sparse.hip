@@ -209,20 +209,29 @@ __global__ __launch_bounds__(kThreads) void randk_scatter_kernel(const float* __
   }
 }
 
-// out = x / p (lazy) or out = x (identical, p == 1 handled as a copy)
+// out = x / p (lazy) or out = x (identical, p == 1 handled as a copy): one short workgroup per 16 KB chunk (4 float4
+// per lane in flight, every load issued before the first store), the tail elements by the last workgroup.  (A
+// grid-stride form moving one float4 per lane per iteration copied 1 GiB at 5.2 TB/s.)
+constexpr int kCopyF4 = 4;
+constexpr int64_t kCopyChunk = (int64_t)kThreads * kCopyF4 * 4;  // elements per workgroup
 template <bool DIV>
-__global__ __launch_bounds__(kThreads) void elementwise_kernel(const float* __restrict__ x, int64_t n, float p,
-                                                               float* __restrict__ out) {
-  const int64_t n4 = n >> 2;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  float4* o4 = reinterpret_cast<float4*>(out);
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads) {
-    float4 v = x4[i];
-    if (DIV) v = make_float4(v.x / p, v.y / p, v.z / p, v.w / p);
-    o4[i] = v;
+__global__ __launch_bounds__(kThreads) void stream_kernel(const float* __restrict__ x, int64_t n, float p,
+                                                          float* __restrict__ out) {
+  const int64_t c0 = (int64_t)blockIdx.x * kCopyChunk;
+  const int t = threadIdx.x;
+  if (c0 + kCopyChunk <= n) {
+    float4 v[kCopyF4];
+#pragma unroll
+    for (int j = 0; j < kCopyF4; ++j) v[j] = ld_stream(x + c0 + 4 * (j * kThreads + t));
+#pragma unroll
+    for (int j = 0; j < kCopyF4; ++j) {
+      float4 a = v[j];
+      if (DIV) a = make_float4(a.x / p, a.y / p, a.z / p, a.w / p);
+      *reinterpret_cast<float4*>(out + c0 + 4 * (j * kThreads + t)) = a;
+    }
+  } else {
+    for (int64_t i = c0 + t; i < n; i += kThreads) out[i] = DIV ? x[i] / p : x[i];
   }
-  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads)
-    out[i] = DIV ? x[i] / p : x[i];
 }
 
 size_t decode_ws_bytes(int64_t n) {  // tile index for the smallest tile (1024 outputs)
@@ -359,8 +368,8 @@ int flc_copy(const float* x, int64_t n, float* out, void* stream) {
   if (n == 0) return FLC_OK;
   if (!aligned16(x) || !aligned16(out)) return fail(FLC_EINVAL, "flc_copy: 16-B aligned buffers required");
   hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 4), kThreads), 256 * 16);
-  FLC_LAUNCH("copy", elementwise_kernel<false>, dim3(grid), dim3(kThreads), 0, st, x, n, 1.0f, out);
+  if (cdiv(n, kCopyChunk) >= (1ll << 31)) return fail(FLC_EINVAL, "flc_copy: n too large");
+  FLC_LAUNCH("copy", stream_kernel<false>, dim3((unsigned)cdiv(n, kCopyChunk)), dim3(kThreads), 0, st, x, n, 1.0f, out);
   return FLC_OK;
 }
 
@@ -369,8 +378,9 @@ int flc_scale_div(const float* x, int64_t n, float p, float* out, void* stream) 
   if (n == 0) return FLC_OK;
   if (!aligned16(x) || !aligned16(out)) return fail(FLC_EINVAL, "flc_scale_div: 16-B aligned buffers required");
   hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 4), kThreads), 256 * 16);
-  FLC_LAUNCH("scale_div", elementwise_kernel<true>, dim3(grid), dim3(kThreads), 0, st, x, n, p, out);
+  if (cdiv(n, kCopyChunk) >= (1ll << 31)) return fail(FLC_EINVAL, "flc_scale_div: n too large");
+  FLC_LAUNCH("scale_div", stream_kernel<true>, dim3((unsigned)cdiv(n, kCopyChunk)), dim3(kThreads), 0, st, x, n, p,
+             out);
   return FLC_OK;
 }
 

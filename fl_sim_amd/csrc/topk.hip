@@ -97,7 +97,8 @@ constexpr size_t kOffBlkT = al256(kOffStamps + 128);   // [kMaxBlocks][4] per-bl
 constexpr size_t kOffSample = al256(kOffBlkT + (size_t)kMaxBlocks * 32);
 constexpr size_t kOffInbin = al256(kOffSample + (size_t)kSample * 4);
 constexpr size_t kOffBlkC = al256(kOffInbin + (size_t)kMaxBlocks * kInbin * 4);
-constexpr size_t kOffStage = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // + G * kCap * 8 (keys, then indices)
+constexpr size_t kOffPair = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // per block pair: its step-claim word
+constexpr size_t kOffStage = al256(kOffPair + (size_t)(kMaxBlocks / 2) * 8);  // + G * kCap * 8 (keys, then indices)
 static_assert(kOffAcc % 8 == 0, "acc words are 64-bit");
 static_assert(sizeof(EncState) <= 128, "state block");
 
@@ -113,6 +114,7 @@ struct EncWs {
   unsigned ovf;   // candidates per block kept in HBM beyond the LDS's kCap (0: none)
   int bid, nb;    // this block's index in its select, the blocks of its select (set in the kernel prologue)
   size_t vstride; // batched: bytes between two clients' staging / overflow areas
+  int pair_r;     // paired pass (see filter_phase): dynamic steps per block side, 0 = static ranges
   unsigned long long* errp;
   __device__ EncState* st() const { return reinterpret_cast<EncState*>(base + kOffSt); }
   __device__ unsigned* flags() const { return reinterpret_cast<unsigned*>(base + kOffFlags); }
@@ -124,6 +126,7 @@ struct EncWs {
   __device__ unsigned* sample() const { return reinterpret_cast<unsigned*>(base + kOffSample); }
   __device__ unsigned* inbin() const { return reinterpret_cast<unsigned*>(base + kOffInbin); }
   __device__ unsigned* blk_c() const { return reinterpret_cast<unsigned*>(base + kOffBlkC); }  // candidates / block
+  __device__ unsigned long long* pairw() const { return reinterpret_cast<unsigned long long*>(base + kOffPair); }  // (32 bits used)
   __device__ unsigned* stage_key(int b) const { return reinterpret_cast<unsigned*>(var) + (size_t)b * 2 * kCap; }
   __device__ unsigned* stage_idx(int b) const { return stage_key(b) + kCap; }
   __device__ unsigned* ovf_key(int b) const {
@@ -203,6 +206,7 @@ EncWs carve_enc(void* ws, int64_t n, int64_t k, int cus, size_t* need) {
   w.bid = 0;
   w.nb = g.G;
   w.vstride = 0;
+  w.pair_r = 0;
   w.errp = reinterpret_cast<unsigned long long*>(w.base + kOffSt + offsetof(EncState, err));
   *need = kOffStage + vb;
   return w;
@@ -581,13 +585,19 @@ struct DeltaSrc {
     const int64_t r = e - t.off[sg];
     return t.lp[sg][r] - t.gp[sg][r];
   }
+  // (every cursor field through readfirstlane: wave-uniform values the compiler would otherwise keep in VGPRs, which
+  // the paired pass's second copy of the load loop could not afford)
+  static __device__ __forceinline__ long long rfl64(long long v) {
+    return (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v) |
+           ((long long)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32);
+  }
   __device__ __forceinline__ void seek(Cursor& c, int64_t wb) const {
     if (wb >= c.lo && wb < c.hi) return;
     const int sg = __builtin_amdgcn_readfirstlane(seg_of(wb));
-    c.lo = t.off[sg];
-    c.hi = t.off[sg + 1];
-    c.l = t.lp[sg];
-    c.g = t.gp[sg];
+    c.lo = rfl64(t.off[sg]);
+    c.hi = rfl64(t.off[sg + 1]);
+    c.l = reinterpret_cast<const float*>(rfl64(reinterpret_cast<long long>(t.lp[sg])));
+    c.g = reinterpret_cast<const float*>(rfl64(reinterpret_cast<long long>(t.gp[sg])));
   }
   template <bool FULL>
   __device__ __forceinline__ void load(Cursor& c, int64_t wb, int64_t end, int lane, Step& st) const {
@@ -668,11 +678,16 @@ struct FilterCtx {
   unsigned above;         // per thread: candidates >= t_hi
   unsigned mk;            // per thread: max candidate key
   unsigned swept;         // (block-uniform) LDS candidates [0, swept) already in the band histogram
+  // paired pass, second block of a pair (it streams its range from the top down): candidate count r (its rank from
+  // the top of the block's range, r = rb - p for the step's ascending position p) lives at LDS slot kCap - 1 - r, so
+  // the block's candidates end up in index order in [kCap - C, kCap); past kCap they go to the HBM overflow at r - kCap
+  bool rev;
+  unsigned rb;            // (block-uniform) per step: 2 * base + tot - 1
 };
 
 // one LDS candidate into the band histogram / above count / max key
 __device__ __forceinline__ void band_bin(FilterCtx& c, unsigned p) {
-  const unsigned key = order_key(c.s_key[p]);
+  const unsigned key = order_key(c.s_key[c.rev ? (unsigned)kCap - 1u - p : p]);
   const unsigned long long rel = (unsigned long long)(key - c.t_lo);
   if (rel >= c.width0) ++c.above;
   else atomicAdd(&c.s_hist[(unsigned)(rel >> c.sh0)], 1u);
@@ -684,11 +699,13 @@ __device__ __forceinline__ void band_bin(FilterCtx& c, unsigned p) {
 // beyond the LDS capacity are binned here (and kept in the HBM overflow while it has room)
 // (OVF = false: the caller has checked that the whole step lands below kCap — the hot path, LDS stores only)
 template <bool OVF>
-__device__ __forceinline__ void emit(FilterCtx& c, unsigned p, unsigned e, float v) {
+__device__ __forceinline__ void emit(FilterCtx& c, unsigned q, unsigned e, float v) {
   const unsigned raw = __float_as_uint(v);
+  const unsigned p = c.rev ? c.rb - q : q;  // (count order: from the range's bottom, or its top for a reverse block)
   if (!OVF || p < (unsigned)kCap) {
-    c.s_key[p] = raw;
-    c.s_idx[p] = e;
+    const unsigned ph = c.rev ? (unsigned)kCap - 1u - p : p;
+    c.s_key[ph] = raw;
+    c.s_idx[ph] = e;
   } else {
     if (p - (unsigned)kCap < c.gcap) {
       c.g_key[p - kCap] = raw;
@@ -759,6 +776,7 @@ __device__ __forceinline__ void step_process(const Step& v, int64_t wb, int64_t 
   // stops the compiler from reusing the count pass's compares)
   float tf2 = tf;
   asm volatile("" : "+v"(tf2));
+  c.rb = 2u * base + tot - 1u;
   if (cnt != 0u) {
     if (base + tot <= (unsigned)kCap)  // (block-uniform) the step lands in LDS: no overflow code on the hot path
       step_write<FULL, Step, SF, false>(v, tf2, lim, lane, (unsigned)wb, base + pre, c);
@@ -927,7 +945,7 @@ __device__ __forceinline__ void pick_digit(const EncWs& w, SelState& cur, long l
 // range itself — every element, since no later phase keeps an element below the floor anyway
 template <class Src>
 struct CandSrc {
-  const unsigned* s_key;
+  const unsigned* s_key;  // LDS candidates in index order (a reverse block's: offset by kCap - C)
   const unsigned* s_idx;
   unsigned* g_key;  // the HBM overflow: candidates kCap.. (gmode)
   unsigned* g_idx;
@@ -935,18 +953,29 @@ struct CandSrc {
   int64_t b0;
   bool xmode;
   bool gmode;       // more candidates than LDS holds, all of them in LDS + the overflow
+  bool rev;         // gmode of a reverse block (paired pass): the overflow holds the LOWEST indices, top down
+  unsigned C;       // the block's candidates (rev gmode)
 };
 template <class Src>
 __device__ __forceinline__ void cand_get(const CandSrc<Src>& c, unsigned p, unsigned& raw, unsigned& id) {
   if (c.xmode) {
     raw = __float_as_uint(c.x.get(c.b0 + p));
     id = (unsigned)(c.b0 + p);
-  } else if (!c.gmode || p < (unsigned)kCap) {
+  } else if (!c.gmode || (!c.rev && p < (unsigned)kCap)) {
     raw = c.s_key[p];
     id = c.s_idx[p];
-  } else {  // (written by this block's waves in the filter pass, before the exchange that followed it)
+  } else if (!c.rev) {  // (written by this block's waves in the filter pass, before the exchange that followed it)
     raw = ld_mem(c.g_key + (p - kCap));
     id = ld_mem(c.g_idx + (p - kCap));
+  } else {  // reverse block, gmode: count from the top r = C - 1 - p; LDS for r < kCap, the overflow beyond
+    const unsigned r = c.C - 1u - p;
+    if (r < (unsigned)kCap) {
+      raw = c.s_key[kCap - 1u - r];
+      id = c.s_idx[kCap - 1u - r];
+    } else {
+      raw = ld_mem(c.g_key + (r - kCap));
+      id = ld_mem(c.g_idx + (r - kCap));
+    }
   }
 }
 
@@ -996,6 +1025,9 @@ __global__ __launch_bounds__(256) void topk_sample_kernel(Src x, int64_t n, int 
   if (threadIdx.x == 0 && blockIdx.x < 256) w.blkt()[(512 + blockIdx.x) * 4] = __builtin_amdgcn_s_memrealtime();
 #endif
   sample_one(x, n, S, w, blockIdx.x * 256 + threadIdx.x);
+  // the paired pass's step-claim words start every call from zero (this kernel precedes the encode in the stream)
+  if (w.pair_r > 0 && blockIdx.x == 0)
+    for (int i = (int)threadIdx.x; i < (w.nb + 1) / 2; i += 256) w.pairw()[i] = 0ull;
 #ifdef FLC_SELECT_STAMPS
   __syncthreads();
   if (threadIdx.x == 0 && blockIdx.x < 256) w.blkt()[(512 + blockIdx.x) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1056,11 +1088,13 @@ struct FilterOut {
   unsigned C_b;            // candidates of this block (<= kCap of them in s_key / s_idx)
   unsigned t_lo;           // floor key
   unsigned long long t_hi; // ceiling key (exclusive)
+  int64_t b0, b1;          // the block's element range (paired pass: decided during the pass)
+  bool rev;                // paired pass, second block: LDS candidates at the top (see FilterCtx)
 };
 
 // floor / ceiling from the sample, the HBM pass into the block's LDS candidate arrays, the round-0 band
 // histogram and counts; STAGE: also the staging copy of the candidates for a separate select kernel
-template <bool STAGE, class Src>
+template <bool STAGE, class Src, bool PAIR = false>
 __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const EncWs& w, int S,
                                                   long long rank_lo, long long rank_hi, int take_all,
                                                   unsigned* s_key, unsigned* s_idx, unsigned* s_hist,
@@ -1069,20 +1103,36 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   SampleLds& SL = *reinterpret_cast<SampleLds*>(s_key);  // the sample phase precedes every candidate write
   static_assert(sizeof(SampleLds) <= sizeof(unsigned) * kCap, "sample scratch must fit the key array");
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
-  const int64_t b0 = (int64_t)w.bid * w.M;
-  const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
+  int64_t b0 = (int64_t)w.bid * w.M;
+  int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
   constexpr int SF = Src::SF;
   constexpr int64_t kWS = SF * 256;         // elements per wave step
   constexpr int64_t kBS = kENW * kWS;       // elements per block step (M is a multiple of it)
   using Step = typename Src::Step;
   const int nsteps = (int)cdiv_dev(b1 - b0, kBS);
+  // Paired pass (w.pair_r > 0, both blocks of the pair with whole ranges): blocks 2j and 2j + 1 (neighbouring XCDs)
+  // stream the 2M elements of both ranges from the two ends towards each other — block 2j upwards from the bottom,
+  // block 2j + 1 downwards from the top — each taking its first NS / 2 - R steps statically and the 2R steps in the
+  // middle one at a time from a shared claim word.  The pair's
+  // boundary thus falls where the two meet, so a block on a slower XCD hands steps to its partner instead of making
+  // every block wait for it at the first exchange; each block's range stays contiguous and in index order, so the
+  // select and the compaction are unchanged.
+  const bool pairm = PAIR && !STAGE && w.pair_r > 0 && (int64_t)((w.bid | 1) + 1) * w.M <= n;  // (per pair)
+  const bool rev = pairm && (w.bid & 1);
+  const int64_t ps = (int64_t)(w.bid & ~1) * w.M;   // the pair's range start
+  const int NSp = (int)(2 * w.M / kBS);             // the pair's steps
+  const int64_t sA = rev ? ps + (int64_t)(NSp - 1) * kBS : b0;  // the block's first step
+  const int64_t sD = rev ? -kBS : kBS;                          // and its direction
+  const int64_t pend = pairm ? ps + 2 * w.M : b1;               // load clamp (full steps only in the paired pass)
   STAMP(0);
 
   // ---- floor / ceiling (identical in every block); the first step of the HBM pass is already in flight
   // meanwhile (issued after the sample keys, so waiting for the keys does not wait for it)
   Step va, vb;
   typename Src::Cursor cur;
-  const int64_t wb0 = b0 + (int64_t)wid * kWS;
+  // (the wave's offset through readfirstlane: wave-uniform, so every step address and the DeltaSrc cursor stay scalar)
+  const int64_t woff = (int64_t)__builtin_amdgcn_readfirstlane(wid) * kWS;
+  const int64_t wb0 = sA + woff;
   const int nfull = (int)((b1 - b0) / kBS);
   unsigned t_lo;
   unsigned long long t_hi;
@@ -1098,13 +1148,13 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
       // the first two steps stream while the floor / ceiling are picked (unconditional, clamped
       // in-range loads, so no wait is merged in): the first right away, the second in the registers the
       // keys leave free after the histogram
-      x.template load<false>(cur, wb0, b1, lane, va);
+      x.template load<false>(cur, wb0, pend, lane, va);
       unsigned B = 0;
       int shB = 0;
       const bool fast = rank_lo <= kET;  // grid-uniform
       if (fast) sample_fast_hist(keys, S, SL, s_hist, &B, &shB);
       STAMP(1);
-      x.template load<false>(cur, wb0 + kBS, b1, lane, vb);
+      x.template load<false>(cur, wb0 + sD, pend, lane, vb);
       if (fast) ok = sample_fast_pick(w.sample(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
     }
     if (!ok) sample_general(w.sample(), S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
@@ -1138,8 +1188,66 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   fc.above = 0;
   fc.mk = 0;
   fc.swept = 0;
+  fc.rev = rev;
+  fc.rb = 0;
   unsigned base = 0;
-  {
+  if (pairm) {
+    // ordinal i = the block's i-th step: i < P static, then one claimed step at a time (s_ring[i & 3]: its step index
+    // in the pair's range, or -1 once the middle is used up).  Thread 0 stores ordinal i + 3's claim result (issued
+    // at the end of ordinal i - 1, before the loads of ordinal i + 1, so waiting for it does not wait for those
+    // loads) into the ring and issues the claim of ordinal i + 4 at the end of ordinal i, before the loads of
+    // ordinal i + 2; the barrier inside the next step_process publishes the ring entry.  The claim word (32 bits:
+    // front claims in bits 0-15, back claims in 16-31) only grows, so once a claim comes back past the middle every
+    // later one does too.
+    __shared__ int s_ring[4];
+    const int P = NSp / 2 - w.pair_r, D = 2 * w.pair_r;
+    unsigned* const pw = reinterpret_cast<unsigned*>(w.pairw() + (w.bid >> 1));
+    const unsigned inc = rev ? 0x10000u : 1u;
+    unsigned claim = 0;  // thread 0: the claim in flight (the first at the end of ordinal P - 4 >= 0)
+    // Loads are never conditional (a conditional load made the compiler copy the previous step's registers into the
+    // new ones, waiting for them) and the loop has no second copy of a step's processing (which cost the registers
+    // the kernel has none of): past the block's last step a buffer reloads the step it just processed (still in the
+    // Infinity Cache; the data is dropped), and the loop ends after the other buffer's step.
+    int sa = 0, sb = 1;  // the steps (ordinal-space: 0 = the block's first) held in va / vb
+    bool vb_ok = true;
+    int done = 0;
+    for (int i = 0;; i += 2) {
+      step_process<true, Step, SF>(va, sA + (int64_t)sa * sD + woff, pend, tf, s_wc, 0, base, fc);
+      if (tid == 0) {
+        if (i + 3 >= P) {
+          const int u = (int)((claim & 0xffffu) + (claim >> 16));
+          s_ring[(i + 3) & 3] = u < D ? P + (int)(rev ? claim >> 16 : claim & 0xffffu) : -1;
+        }
+        if (i + 4 >= P) claim = __hip_atomic_fetch_add(pw, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const int n2 = i + 2 < P ? i + 2 : __builtin_amdgcn_readfirstlane(s_ring[(i + 2) & 3]);
+      x.template load<true>(cur, sA + (int64_t)(n2 >= 0 ? n2 : sa) * sD + woff, pend, lane, va);
+      if (!vb_ok) {
+        done = i + 1;
+        break;
+      }
+      step_process<true, Step, SF>(vb, sA + (int64_t)sb * sD + woff, pend, tf, s_wc, 1, base, fc);
+      if (tid == 0) {
+        if (i + 4 >= P) {
+          const int u = (int)((claim & 0xffffu) + (claim >> 16));
+          s_ring[(i + 4) & 3] = u < D ? P + (int)(rev ? claim >> 16 : claim & 0xffffu) : -1;
+        }
+        if (i + 5 >= P) claim = __hip_atomic_fetch_add(pw, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const int n3 = i + 3 < P ? i + 3 : __builtin_amdgcn_readfirstlane(s_ring[(i + 3) & 3]);
+      x.template load<true>(cur, sA + (int64_t)(n3 >= 0 ? n3 : sb) * sD + woff, pend, lane, vb);
+      if (n2 < 0) {
+        done = i + 2;
+        break;
+      }
+      sa = n2;
+      sb = n3;
+      vb_ok = n3 >= 0;
+    }
+    // the block's range: `done` steps from its end of the pair's range
+    b0 = rev ? ps + 2 * w.M - (int64_t)done * kBS : ps;
+    b1 = rev ? ps + 2 * w.M : ps + (int64_t)done * kBS;
+  } else {
     // full block steps in a two-deep software pipeline; every load in the loop body is unconditional
     // (a conditional prefetch makes the compiler copy the loaded registers on a side path, and the copy
     // waits for the load), and the partial tail step is peeled off
@@ -1217,6 +1325,9 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   o.C_b = C_b;
   o.t_lo = t_lo;
   o.t_hi = t_hi;
+  o.b0 = b0;
+  o.b1 = b1;
+  o.rev = rev;
   return o;
 }
 
@@ -1286,11 +1397,14 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
 #endif
   STAMP_INIT();
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
-  const int64_t b0 = (int64_t)w.bid * w.M;
-  const int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
+  int64_t b0 = (int64_t)w.bid * w.M;  // (the paired pass decides them in the filter phase)
+  int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
   unsigned* hist = w.hist();
   unsigned C_b;
   unsigned ep;
+  bool rev = false;
+  const unsigned* s_keyl = s_key;  // the block's LDS candidates in index order (a reverse block's sit at the top)
+  const unsigned* s_idxl = s_idx;
   // Philox words of the candidates (stacked), precomputed in exchange waits into the block's staging
   // area (unused by the fused path; the split path has copied its staged candidates to LDS by then):
   // chunk c = wave range c % kENW, its 64 candidates of iteration c / kENW; chunks [0, s_rnext) are
@@ -1308,7 +1422,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     const unsigned r0 = wr * Qn < rnd_n ? wr * Qn : rnd_n, r1 = r0 + Qn < rnd_n ? r0 + Qn : rnd_n;
     const unsigned p = r0 + it * kWave + lane;
     if (p < r1) {
-      const unsigned id = s_idx[p];
+      const unsigned id = s_idxl[p];
       rnd[p] = pick(philox_group((uint64_t)id >> 2, seed, counter), (int)(id & 3u));
     }
     return true;
@@ -1317,8 +1431,16 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     __shared__ unsigned s_wc[2][kENW];
     if (tid == 0) s_glob[2] = ld_mem64(&w.st()->call);  // (read before any exchange of this call)
     const FilterOut fo =
-        filter_phase<false>(x, n, w, S, rank_lo, rank_hi, take_all, s_key, s_idx, s_hist, s_wc, s_red, s_mx);
+        filter_phase<false, Src, !BATCH>(x, n, w, S, rank_lo, rank_hi, take_all, s_key, s_idx, s_hist, s_wc, s_red,
+                                         s_mx);
     C_b = fo.C_b;
+    b0 = fo.b0;
+    b1 = fo.b1;
+    rev = fo.rev;
+    if (rev && C_b <= (unsigned)kCap) {
+      s_keyl = s_key + (kCap - C_b);
+      s_idxl = s_idx + (kCap - C_b);
+    }
     if (tid == 0) {
       s_glob[0] = fo.t_lo;
       s_glob[1] = fo.t_hi;
@@ -1382,8 +1504,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     prev = cur;
   }
   CandSrc<Src> src;
-  src.s_key = s_key;
-  src.s_idx = s_idx;
+  src.s_key = s_keyl;
+  src.s_idx = s_idxl;
   src.x = x;
   src.b0 = b0;
   src.g_key = w.ovf_key(w.bid);
@@ -1391,6 +1513,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   const unsigned gcap = FUSED ? w.ovf : 0u;
   src.xmode = fb || C_b > (unsigned)kCap + gcap;  // block-uniform
   src.gmode = !src.xmode && C_b > (unsigned)kCap;
+  src.rev = rev;
+  src.C = C_b;
   const unsigned ncand = src.xmode ? (unsigned)(b1 - b0) : C_b;
 
   auto flush = [&](int sl, unsigned above_t, unsigned mk_t) {
@@ -1493,7 +1617,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const unsigned p = p00 + (unsigned)(j * kWave) + lane;
-          r4[j] = s_key[p < wq1 ? p : pl];
+          r4[j] = src.s_key[p < wq1 ? p : pl];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) scan_one(p00 + (unsigned)(j * kWave) + lane, r4[j]);
@@ -1993,13 +2117,20 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
   if (!ws || need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
   const EncGeom g = enc_geometry(n, cus);
   const SampleSetup ss = sample_setup(n, k);
-  if (!ss.take_all)
-    FLC_LAUNCH("topk_sample", topk_sample_kernel<Src>, dim3((unsigned)cdiv(ss.S, 256)), dim3(256), 0, st, x, n, ss.S, w);
 #if defined(FLC_CALIB) || defined(FLC_SELECT_STAMPS)  // calibration builds: FLC_TOPK_SPLIT=1 times the two-kernel path
   static const bool split = getenv("FLC_TOPK_SPLIT") && atoi(getenv("FLC_TOPK_SPLIT")) != 0;
 #else
   constexpr bool split = false;
 #endif
+  // the paired pass (filter_phase): R dynamic steps per side, about 1/16 of a pair's steps, at least 4 static steps
+  // per block (the claims run 4 steps ahead).  Off unless FLC_PAIR=1: measured slower so far
+  static const bool pair_on = getenv("FLC_PAIR") && atoi(getenv("FLC_PAIR")) == 1;
+  if (!split && !ss.take_all && pair_on) {
+    const int ns = (int)(2 * g.M / ((int64_t)kENW * Src::SF * 256));
+    w.pair_r = std::max(0, std::min(ns / 2 - 4, std::max(4, ns / 16)));
+  }
+  if (!ss.take_all)
+    FLC_LAUNCH("topk_sample", topk_sample_kernel<Src>, dim3((unsigned)cdiv(ss.S, 256)), dim3(256), 0, st, x, n, ss.S, w);
   if (split)
     FLC_LAUNCH("topk_filter", topk_filter_kernel<Src>, dim3((unsigned)g.G), dim3(kET), 0, st, x, n, w, ss.S, ss.rank_lo,
                ss.rank_hi, ss.take_all);
@@ -2079,6 +2210,7 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
   w.bid = 0;
   w.nb = bg.g.G;
   w.vstride = bg.vstride;
+  w.pair_r = 0;  // (batched selects keep static ranges: a client's few blocks)
   w.errp = reinterpret_cast<unsigned long long*>(base + kOffSt + offsetof(EncState, err));
   const SampleSetup ss = sample_setup(n, k, batch_sample_cap(n));
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;

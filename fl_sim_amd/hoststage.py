@@ -42,8 +42,9 @@ def _round_up(n: int, a: int) -> int:
 
 
 def is_host(ts: Sequence[torch.Tensor]) -> bool:
-    """True when a non-empty tensor list lives in host memory (the reference server's placement)."""
-    return len(ts) > 0 and all(isinstance(t, torch.Tensor) and t.device.type == "cpu" for t in ts)
+    """True when a non-empty tensor list lives in host memory (the reference server's placement), judged by its first
+    tensor (a model on one device; the staging copies any other tensor it meets)."""
+    return len(ts) > 0 and isinstance(ts[0], torch.Tensor) and ts[0].is_cpu
 
 
 def _layout(groups: Sequence[Sequence[torch.Tensor]]) -> Tuple[List[List[int]], List[Tuple[int, int]], int]:
@@ -117,7 +118,7 @@ def adopt(groups: Sequence[Sequence[torch.Tensor]], device: Optional[torch.devic
     own the tensor objects (the ``Server`` mixins) adopt: re-pointing a temporary ``p.data`` object would leave the
     parameter itself behind."""
     groups = [list(g) for g in groups if len(g)]
-    if not groups or not all(is_host(g) for g in groups):
+    if not groups or not all(isinstance(t, torch.Tensor) and t.is_cpu for g in groups for t in g):
         return None
     dtype = groups[0][0].dtype
     if dtype not in (torch.float32, torch.float64) or any(t.dtype != dtype for g in groups for t in g):
