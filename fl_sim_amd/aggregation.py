@@ -57,14 +57,26 @@ def _model_device(tensors: Sequence[torch.Tensor]) -> Optional[int]:
     return t.get_device()
 
 
-def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
-          init_mode: int, beta: float = 0.0, **step) -> bool:
+def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence, weights: Sequence[float], init_mode: int,
+          beta: float = 0.0, key: Optional[str] = None, **step) -> bool:
     """The whole model in flc_model_fold launches when it qualifies (one device): one launch per 16 messages, the
     chain continued from the stored partial sums (init mode 2) and the FedOpt step fused into the last launch only —
-    the same fmaf chain as one launch.  False when the model does not qualify."""
-    dev = _model_device(list(dsts) + list(step.get("theta") or []) + list(step.get("v") or []))
-    if dev is None or not dsts:
+    the same fmaf chain as one launch.  ``msg_tensors``: one tensor list per message, or (``key``) the messages
+    themselves, each holding its list under ``key``.  False when the model does not qualify."""
+    dev = _model_device(dsts)
+    if dev is None:
         return False
+    pf = codec._pyfold()
+    if pf is not None:
+        try:  # the common case in one C call: messages already on the model's device
+            pf(dsts, msg_tensors, key, weights, init_mode, beta, step.get("theta"), step.get("v"),
+               _lib.FLC_OPT[step.get("opt", "avg")], float(step.get("lr", 1.0)), float(step.get("beta2", 0.0)),
+               float(step.get("tau", 0.0)))
+            return True
+        except TypeError:
+            pass  # messages elsewhere (moved below) or a model the fold does not take (per-tensor launches)
+    if key is not None:
+        msg_tensors = [m[key] for m in msg_tensors]
     cap = codec.MODEL_FOLD_MAX_SRC
     try:
         if len(msg_tensors) > cap:
@@ -127,7 +139,7 @@ def avg_parameters(server_params: Sequence[torch.Tensor], messages: Sequence[Map
     ratios = [
         (m["train_samples"] / total_samples if size_aware else 1 / len(messages)) * (1 - inertia) for m in messages
     ]
-    if _fold(_params(sps), [m[key] for m in messages], ratios, 0, inertia):
+    if _fold(_params(sps), messages, ratios, 0, inertia, key=key):
         return
     for j, sp in enumerate(_params(sps)):
         srcs = [_on(m[key][j], sp.device) for m in messages]
@@ -145,7 +157,7 @@ def _gradients_on(dev: torch.device, messages: Sequence[Mapping]) -> List[torch.
     for g in g0s:
         gs.append(flat[off:off + g.numel()].view(g.shape))
         off += g.numel()
-    if all(g.dtype == dt for g in g0s) and _fold(gs, [m["gradients"] for m in messages], weights, 1):
+    if all(g.dtype == dt for g in g0s) and _fold(gs, messages, weights, 1, key="gradients"):
         return gs
     gs = [torch.empty(g.shape, dtype=g.dtype, device=dev) for g in g0s]
     for j, g in enumerate(gs):
@@ -198,7 +210,7 @@ def fedopt_update(model_params: Sequence[torch.Tensor], delta_parameters: Sequen
                           [{"delta_parameters": d} for d in dm], optimizer, lr, betas, tau)
         return
     ps = _params(model_params)
-    if _fold(list(delta_parameters), [m["delta_parameters"] for m in messages], [alpha] * len(messages), 0, betas[0],
+    if _fold(delta_parameters, messages, [alpha] * len(messages), 0, betas[0], key="delta_parameters",
              theta=ps, v=vps, opt=opt if vps is not None else "avg", lr=lr, beta2=betas[1], tau=tau):
         return  # the delta average and the optimizer step of every tensor in one launch
     for j, dp in enumerate(delta_parameters):
@@ -228,16 +240,14 @@ def scaffold_update(model_params: Sequence[torch.Tensor], control_variates: Sequ
                                         for a, b in zip(dm[:n], dm[n:])], lr, num_clients)
         return
     ps, cvs = _params(model_params), list(control_variates)
-    if _model_device(ps + cvs) is not None and ps and cvs and len(messages) <= codec.MODEL_FOLD_MAX_SRC:
-        _fold(ps, [m["parameters_delta"] for m in messages], [ratio_p] * len(messages), 2)
-        _fold(cvs, [m["control_variates_delta"] for m in messages], [ratio_c] * len(messages), 2)
-        return
-    for j, sp in enumerate(_params(model_params)):
-        codec.weighted_sum(sp, [_on(m["parameters_delta"][j], sp.device) for m in messages], [ratio_p] * len(messages),
-                           init_mode=2)
-    for j, cv in enumerate(control_variates):
-        codec.weighted_sum(cv, [_on(m["control_variates_delta"][j], cv.device) for m in messages],
-                           [ratio_c] * len(messages), init_mode=2)
+    if not _fold(ps, messages, [ratio_p] * len(messages), 2, key="parameters_delta"):
+        for j, sp in enumerate(ps):
+            codec.weighted_sum(sp, [_on(m["parameters_delta"][j], sp.device) for m in messages],
+                               [ratio_p] * len(messages), init_mode=2)
+    if not _fold(cvs, messages, [ratio_c] * len(messages), 2, key="control_variates_delta"):
+        for j, cv in enumerate(cvs):
+            codec.weighted_sum(cv, [_on(m["control_variates_delta"][j], cv.device) for m in messages],
+                               [ratio_c] * len(messages), init_mode=2)
 
 
 def ifca_update(cluster_centers: Mapping[int, dict], messages: Sequence[Mapping], num_clusters: int) -> None:

@@ -770,6 +770,22 @@ def _model_fold_op():
     return _MODEL_FOLD_OP[0]
 
 
+_PYFOLD: list = []
+
+
+def _pyfold():
+    """fl_sim_amd._flcfold.model_fold (csrc/pyfold.cpp: the fold on Python lists of tensors, no dispatcher boxing,
+    more than 16 messages in chained launches) when built, else None."""
+    if not _PYFOLD:
+        try:
+            from . import _flcfold
+
+            _PYFOLD.append(_flcfold.model_fold)
+        except ImportError:
+            _PYFOLD.append(None)
+    return _PYFOLD[0]
+
+
 def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
                init_mode: int, beta: float = 0.0, theta: Optional[Sequence[torch.Tensor]] = None,
                v: Optional[Sequence[torch.Tensor]] = None, opt: str = "avg", lr: float = 1.0, beta2: float = 0.0,
@@ -781,6 +797,11 @@ def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tenso
     import ctypes
 
     nt, ns = len(dsts), len(srcs)
+    pf = _pyfold()
+    if pf is not None:  # every tensor checked in C before anything is launched; > 16 messages chained
+        pf(dsts, srcs, None, weights, int(init_mode), float(beta), theta, v, _lib.FLC_OPT[opt], float(lr), float(beta2),
+           float(tau))
+        return
     if ns > MODEL_FOLD_MAX_SRC:
         raise ValueError(f"model_fold takes at most {MODEL_FOLD_MAX_SRC} messages")
     if nt == 0:

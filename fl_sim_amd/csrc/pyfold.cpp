@@ -1,0 +1,163 @@
+// pyfold.cpp — `fl_sim_amd._flcfold.model_fold`: the server's whole-model fold (flc_model_fold) called straight from
+// Python lists of tensors, for the per-round host path of FedOptServer.update / avg_parameters / add_parameters /
+// update_gradients (_fedopt.py:196-240, nodes.py:1116-1180).
+//
+// At configs[0] (cnn_femmist_tiny: 8 tensors, 10 clients) the kernel takes ~9 us, but going through the dispatcher
+// (torch.ops.flcodec.model_fold_) cost ~14 us of host time: every tensor of the 96 in the call is boxed into an IValue
+// list and unboxed again.  Here each Python tensor object is unpacked in place (THPVariable_Unpack, no refcount or
+// IValue traffic), checked (HIP device, fp32, contiguous, sizes) and its pointer written into the table the C ABI
+// takes; more than 16 messages are folded in chained launches (init mode 2 after the first launch, the optimizer
+// step fused into the last one — the same fmaf chain as one launch).  Nothing is launched before every tensor of
+// the call has passed its checks.  Errors: TypeError for a tensor the fold does not take (the caller then moves
+// messages or folds per tensor), ValueError for mismatched sizes or counts.
+#include <Python.h>
+#include <torch/csrc/autograd/python_variable.h>
+#include <c10/hip/HIPStream.h>
+
+#include <vector>
+
+#include "flcodec.h"
+
+namespace {
+
+constexpr int kMaxSrc = 16;  // messages per flc_model_fold launch
+
+PyObject* type_error(const char* msg) {
+  PyErr_SetString(PyExc_TypeError, msg);
+  return nullptr;
+}
+PyObject* value_error(const char* msg) {
+  PyErr_SetString(PyExc_ValueError, msg);
+  return nullptr;
+}
+
+// a contiguous fp32 tensor on HIP device `dev` (-1: any HIP device, returned in *dev); nullptr if not one
+const at::Tensor* usable(PyObject* o, int* dev) {
+  if (!THPVariable_Check(o)) return nullptr;
+  const at::Tensor& t = THPVariable_Unpack(o);
+  if (!t.is_cuda() || t.scalar_type() != at::kFloat || !t.is_contiguous()) return nullptr;
+  const int d = t.get_device();
+  if (*dev < 0) *dev = d;
+  else if (d != *dev) return nullptr;
+  return &t;
+}
+
+// model_fold(dsts, msgs, key, weights, init_mode, beta, theta, v, opt, lr, beta2, tau)
+//   dsts: sequence of model tensors (accumulators); msgs: sequence of messages, each a sequence of tensors or (key
+//   not None) a mapping holding one under `key`; weights: one float per message; theta / v: sequences or None
+PyObject* model_fold(PyObject*, PyObject* args) {
+  PyObject *dsts, *msgs, *key, *weights, *theta, *v;
+  int init_mode, opt;
+  double beta, lr, beta2, tau;
+  if (!PyArg_ParseTuple(args, "OOOOidOOiddd", &dsts, &msgs, &key, &weights, &init_mode, &beta, &theta, &v, &opt, &lr,
+                        &beta2, &tau))
+    return nullptr;
+  PyObject* fd = PySequence_Fast(dsts, "dsts must be a sequence of tensors");
+  if (!fd) return nullptr;
+  PyObject* fm = PySequence_Fast(msgs, "messages must be a sequence");
+  if (!fm) {
+    Py_DECREF(fd);
+    return nullptr;
+  }
+  PyObject* fw = PySequence_Fast(weights, "weights must be a sequence of floats");
+  if (!fw) {
+    Py_DECREF(fd);
+    Py_DECREF(fm);
+    return nullptr;
+  }
+  std::vector<PyObject*> keep = {fd, fm, fw};
+  auto done = [&](PyObject* r) {
+    for (PyObject* o : keep) Py_XDECREF(o);
+    return r;
+  };
+  const Py_ssize_t nt = PySequence_Fast_GET_SIZE(fd), ns = PySequence_Fast_GET_SIZE(fm);
+  if (PySequence_Fast_GET_SIZE(fw) != ns) return done(value_error("one weight per message"));
+  if (nt == 0) return done((Py_INCREF(Py_None), Py_None));
+  int dev = -1;
+  std::vector<float*> dp(nt), tp, vp;
+  std::vector<int64_t> sz(nt);
+  PyObject** di = PySequence_Fast_ITEMS(fd);
+  for (Py_ssize_t t = 0; t < nt; ++t) {
+    const at::Tensor* a = usable(di[t], &dev);
+    if (!a) return done(type_error("model tensors must be contiguous fp32 HIP tensors on one device"));
+    dp[t] = a->data_ptr<float>();
+    sz[t] = a->numel();
+  }
+  for (int which = 0; which < 2; ++which) {  // theta, v
+    PyObject* src = which == 0 ? theta : v;
+    if (src == Py_None) continue;
+    PyObject* f = PySequence_Fast(src, "theta / v must be sequences of tensors");
+    if (!f) return done(nullptr);
+    keep.push_back(f);
+    if (PySequence_Fast_GET_SIZE(f) != nt) return done(value_error("theta / v need one tensor per model tensor"));
+    std::vector<float*>& out = which == 0 ? tp : vp;
+    out.resize(nt);
+    PyObject** it = PySequence_Fast_ITEMS(f);
+    for (Py_ssize_t t = 0; t < nt; ++t) {
+      const at::Tensor* a = usable(it[t], &dev);
+      if (!a) return done(type_error("theta / v tensors must be contiguous fp32 HIP tensors on the model's device"));
+      if (a->numel() != sz[t]) return done(value_error("theta / v must match the model tensors' sizes"));
+      out[t] = a->data_ptr<float>();
+    }
+  }
+  std::vector<const float*> sp((size_t)ns * nt);
+  std::vector<float> w(ns);
+  PyObject** mi = PySequence_Fast_ITEMS(fm);
+  PyObject** wi = PySequence_Fast_ITEMS(fw);
+  for (Py_ssize_t m = 0; m < ns; ++m) {
+    const double wd = PyFloat_AsDouble(wi[m]);
+    if (wd == -1.0 && PyErr_Occurred()) return done(nullptr);
+    w[m] = (float)wd;  // (rounded to fp32 at the boundary, as torch's add_(alpha=...) does)
+    PyObject* msg = mi[m];
+    if (key != Py_None) {
+      msg = PyObject_GetItem(msg, key);  // (new reference)
+      if (!msg) return done(nullptr);
+      keep.push_back(msg);
+    }
+    PyObject* f = PySequence_Fast(msg, "a message is a sequence of tensors");
+    if (!f) return done(nullptr);
+    keep.push_back(f);
+    if (PySequence_Fast_GET_SIZE(f) != nt) return done(value_error("every message has one tensor per model tensor"));
+    PyObject** it = PySequence_Fast_ITEMS(f);
+    for (Py_ssize_t t = 0; t < nt; ++t) {
+      const at::Tensor* a = usable(it[t], &dev);
+      if (!a) return done(type_error("message tensors must be contiguous fp32 HIP tensors on the model's device"));
+      if (a->numel() != sz[t]) return done(value_error("message tensors must match the model tensors' sizes"));
+      sp[(size_t)m * nt + t] = a->data_ptr<float>();
+    }
+  }
+  void* st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+  int rc = FLC_OK;
+  Py_BEGIN_ALLOW_THREADS
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  Py_ssize_t m0 = 0;
+  do {  // chained launches of <= 16 messages: the optimizer step with the last one only
+    const Py_ssize_t cnt = ns - m0 < kMaxSrc ? ns - m0 : kMaxSrc;
+    const bool last = m0 + cnt >= ns;
+    rc = flc_model_fold(dp.data(), sp.data() + (size_t)m0 * nt, w.data() + m0, (int)cnt, sz.data(), (int)nt,
+                        m0 == 0 ? init_mode : 2, (float)beta, last && !tp.empty() ? tp.data() : nullptr,
+                        last && !vp.empty() ? vp.data() : nullptr, last ? opt : FLC_OPT_AVG, lr, beta2, tau, st);
+    m0 += cnt;
+  } while (rc == FLC_OK && m0 < ns);
+  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  Py_END_ALLOW_THREADS
+  if (rc != FLC_OK) {
+    PyErr_Format(PyExc_RuntimeError, "flc_model_fold failed with status %d: %s", rc, flc_last_error());
+    return done(nullptr);
+  }
+  return done((Py_INCREF(Py_None), Py_None));
+}
+
+PyMethodDef kMethods[] = {
+    {"model_fold", model_fold, METH_VARARGS,
+     "model_fold(dsts, msgs, key, weights, init_mode, beta, theta, v, opt, lr, beta2, tau): flc_model_fold on Python "
+     "lists of HIP tensors, launched on the current stream of the model's device"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_flcfold", nullptr, -1, kMethods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__flcfold(void) { return PyModule_Create(&kModule); }

@@ -284,6 +284,7 @@ def test_model_fold_ctypes_checks_sizes(monkeypatch):
     from fl_sim_amd import codec
 
     monkeypatch.setattr(codec, "_MODEL_FOLD_OP", [None])
+    monkeypatch.setattr(codec, "_PYFOLD", [None])
     d = [torch.zeros(5), torch.zeros(3)]
     msgs = [[torch.zeros(5), torch.zeros(3)]]
     with pytest.raises(ValueError, match="one weight per message"):
@@ -292,3 +293,18 @@ def test_model_fold_ctypes_checks_sizes(monkeypatch):
         codec.model_fold(d, msgs, [0.5], 0, theta=[torch.zeros(5), torch.zeros(4)])
     with pytest.raises(ValueError, match="v must"):
         codec.model_fold(d, msgs, [0.5], 0, theta=[torch.zeros(5), torch.zeros(3)], v=[torch.zeros(5)], opt="adam")
+
+
+def test_pyfold_module_checks_without_gpu():
+    """fl_sim_amd._flcfold (csrc/pyfold.cpp) loads and rejects what the fold does not take before anything runs: host
+    tensors (TypeError, the callers' cue to move messages), count and size mismatches (ValueError)."""
+    import torch
+
+    from fl_sim_amd import _flcfold
+
+    d = [torch.zeros(5), torch.zeros(3)]
+    with pytest.raises(TypeError, match="HIP"):
+        _flcfold.model_fold(d, [d], None, [0.5], 0, 0.0, None, None, 0, 1.0, 0.0, 0.0)
+    with pytest.raises(ValueError, match="one weight per message"):
+        _flcfold.model_fold(d, [d], None, [0.5, 0.5], 0, 0.0, None, None, 0, 1.0, 0.0, 0.0)
+    _flcfold.model_fold([], [], None, [], 0, 0.0, None, None, 0, 1.0, 0.0, 0.0)  # nothing to fold

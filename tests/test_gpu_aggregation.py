@@ -281,12 +281,16 @@ def _views(shapes, g, scale=1.0, misalign=False):
     return out
 
 
-@pytest.fixture(params=["torch_op", "ctypes"])
+@pytest.fixture(params=["pyfold", "torch_op", "ctypes"])
 def fold_path(request, monkeypatch):
-    """codec.model_fold through torch.ops.flcodec.model_fold_ (the default when libflcodec_torch.so is built) and
-    through the ctypes binding: the same C-ABI call behind both"""
+    """codec.model_fold through fl_sim_amd._flcfold (the default when built: Python lists straight into the C ABI),
+    through torch.ops.flcodec.model_fold_ and through the ctypes binding: the same C-ABI call behind all three"""
     from fl_sim_amd import codec
 
+    if request.param == "pyfold":
+        assert codec._pyfold() is not None
+        return request.param
+    monkeypatch.setattr(codec, "_PYFOLD", [None])
     if request.param == "ctypes":
         monkeypatch.setattr(codec, "_MODEL_FOLD_OP", [None])
     else:
@@ -328,12 +332,40 @@ def test_model_fold_equals_per_tensor_calls(opt, n_msgs, misalign, fold_path):
         assert all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(a, b))
 
 
+@pytest.mark.parametrize("opt", ["avg", "adam"])
+@pytest.mark.parametrize("n_msgs", [17, 40])
+def test_pyfold_chained_launches_equal_per_tensor_calls(opt, n_msgs):
+    """More than 16 messages through fl_sim_amd._flcfold: chained flc_model_fold launches (init mode 2 after the first,
+    the optimizer step with the last) equal flc_weighted_sum + flc_fedopt_step per tensor bit for bit."""
+    from fl_sim_amd import codec
+
+    assert codec._pyfold() is not None
+    shapes = [(16, 1, 5, 5), (16,), (256, 1568), (10,), (4097,)]
+    g = torch.Generator(device="cuda").manual_seed(n_msgs)
+    theta = _views(shapes, g)
+    delta = _views(shapes, g, 1e-3)
+    v = [t.abs() * 1e-2 + 1e-6 for t in _views(shapes, g)]
+    msgs = [_views(shapes, g, 1e-3) for _ in range(n_msgs)]
+    w = [float(np.float32(0.01 * (i + 1))) for i in range(n_msgs)]
+    th2, d2, v2 = [t.clone() for t in theta], [t.clone() for t in delta], [t.clone() for t in v]
+    codec.model_fold(delta, msgs, w, 0, 0.9, theta=theta, v=None if opt == "avg" else v, opt=opt, lr=0.01, beta2=0.99,
+                     tau=1e-3)
+    for j in range(len(shapes)):
+        codec.weighted_sum(d2[j], [m[j] for m in msgs], w, init_mode=0, beta=0.9)
+        codec.fedopt_step(th2[j], d2[j], None if opt == "avg" else v2[j], opt, 0.01, 0.99, 1e-3)
+    for a, b in zip(theta + delta + v, th2 + d2 + v2):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
 def test_model_fold_rejects_bad_arguments(fold_path):
     from fl_sim_amd import codec
 
     t = [torch.zeros(5, device="cuda")]
-    with pytest.raises(ValueError):
-        codec.model_fold(t, [t] * 17, [1.0] * 17, 0)  # more than 16 messages
+    if fold_path == "pyfold":
+        codec.model_fold(t, [t] * 17, [1.0] * 17, 0)  # more than 16 messages: chained launches
+    else:
+        with pytest.raises(ValueError):
+            codec.model_fold(t, [t] * 17, [1.0] * 17, 0)  # more than 16 messages
     with pytest.raises(ValueError):
         codec.model_fold(t, [[torch.zeros(6, device="cuda")]], [1.0], 0)  # size mismatch
     with pytest.raises(RuntimeError):
