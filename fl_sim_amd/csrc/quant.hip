@@ -403,7 +403,8 @@ template <int KIND, int BITS, bool DEC, class NormOf, class NnzAdd>
 __device__ __forceinline__ void philox_group_encode(const float (&v)[kGroup], const uint32_t (&wd)[kGroup], int64_t e0,
                                                     int valid, int64_t d, int s, double step,
                                                     uint8_t* __restrict__ codes, float* __restrict__ out, bool count,
-                                                    NormOf norm_of, NnzAdd nnz_add, bool nt = false) {
+                                                    NormOf norm_of, NnzAdd nnz_add, bool nt = false,
+                                                    const float* lvt = nullptr) {
   const int64_t r0 = e0 / d;
   const int64_t r_end = (r0 + 1) * d;
   uint64_t packed = 0;
@@ -438,7 +439,14 @@ __device__ __forceinline__ void philox_group_encode(const float (&v)[kGroup], co
     for (int j = 0; j < kGroup; ++j) {
       const uint32_t c = v[j] == 0.0f ? 0u : (((__float_as_uint(v[j]) >> 31) << (BITS - 1)) | lvl[j]);
       packed |= (uint64_t)c << (j * BITS);
-      if (DEC) o[j] = dequant<KIND, BITS>(c, nr0, s, step);
+      if (DEC) {
+        if (lvt) {  // fp32(level value) from the block's LDS table: dequant's (float)(i * step) without the fp64 work
+          const float lv = lvt[c & ((1u << (BITS - 1)) - 1u)];
+          o[j] = ((c >> (BITS - 1)) ? -lv : lv) * nr0;
+        } else {
+          o[j] = dequant<KIND, BITS>(c, nr0, s, step);
+        }
+      }
     }
   } else if (whole) {
 #pragma unroll
@@ -591,6 +599,7 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
   __shared__ uint32_t s_m[2][kFT / kWave];
   __shared__ float s_norm[2];
   __shared__ unsigned long long s_nnz[2];
+  __shared__ float s_lvt[128];  // standard dithering: fp32 level values (dequant's (float)level_value), s <= 127
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * SPAN;
   const int64_t r0 = base / d, rb = (r0 + 1) * d, rows = (n + d - 1) / d;
@@ -628,6 +637,7 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
     for (int g = 0; g < GPT; ++g) group_words(base + ((int64_t)g * kFT + tid) * kGroup, seed, counter, wd[g]);
   }
   if (tid < 2) s_nnz[tid] = 0ull;
+  if (KIND == 0 && tid <= s) s_lvt[tid] = (float)level_value<0>(tid, s, step);
   __syncthreads();
   if (tid < 2) {  // slot 0: row r0, slot 1: row r0 + 1 (0 when the block holds none of it)
     uint32_t m = 0;
@@ -677,7 +687,8 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
       philox_group_encode<KIND, BITS, DEC>(
           v[g], wd[kPre ? g : 0], e0, valid, d, s, step, codes, out, nnz != nullptr,
           [&](int64_t r) { return s_norm[r - r0]; },
-          [&](int64_t r, int cnt) { atomicAdd(&s_nnz[r - r0], (unsigned long long)cnt); }, cal & 1);
+          [&](int64_t r, int cnt) { atomicAdd(&s_nnz[r - r0], (unsigned long long)cnt); }, cal & 1,
+          KIND == 0 ? s_lvt : nullptr);
     }
   }
   if (nnz) {

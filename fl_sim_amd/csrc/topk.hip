@@ -1200,49 +1200,48 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
     // front claims in bits 0-15, back claims in 16-31) only grows, so once a claim comes back past the middle every
     // later one does too.
     __shared__ int s_ring[4];
-    const int P = NSp / 2 - w.pair_r, D = 2 * w.pair_r;
+    const int P = NSp / 2 - w.pair_r, D = 2 * w.pair_r;  // (P >= 4: the host keeps 4 static steps per block)
     unsigned* const pw = reinterpret_cast<unsigned*>(w.pairw() + (w.bid >> 1));
     const unsigned inc = rev ? 0x10000u : 1u;
     unsigned claim = 0;  // thread 0: the claim in flight (the first at the end of ordinal P - 4 >= 0)
-    // Loads are never conditional (a conditional load made the compiler copy the previous step's registers into the
-    // new ones, waiting for them) and the loop has no second copy of a step's processing (which cost the registers
-    // the kernel has none of): past the block's last step a buffer reloads the step it just processed (still in the
-    // Infinity Cache; the data is dropped), and the loop ends after the other buffer's step.
-    int sa = 0, sb = 1;  // the steps (ordinal-space: 0 = the block's first) held in va / vb
-    bool vb_ok = true;
-    int done = 0;
-    for (int i = 0;; i += 2) {
-      step_process<true, Step, SF>(va, sA + (int64_t)sa * sD + woff, pend, tf, s_wc, 0, base, fc);
-      if (tid == 0) {
-        if (i + 3 >= P) {
-          const int u = (int)((claim & 0xffffu) + (claim >> 16));
-          s_ring[(i + 3) & 3] = u < D ? P + (int)(rev ? claim >> 16 : claim & 0xffffu) : -1;
-        }
-        if (i + 4 >= P) claim = __hip_atomic_fetch_add(pw, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // The loop has the static loop's shape (a buffer is reloaded right before the other one is processed) and the
+    // same peeled first iteration.  Loads are never conditional (a conditional load made the compiler copy the
+    // previous step's registers into the new ones, waiting for them) and a step's processing has no second copy (its
+    // registers are all taken): past the block's last step a buffer reloads the step the other buffer holds (still in
+    // the Infinity Cache; the data is dropped), and the loop ends after that buffer's step.
+    auto post = [&](int j) {  // end of ordinal j (thread 0): ring[j + 3] <- claim(j + 3); claim(j + 4) issued
+      if (tid != 0) return;
+      if (j + 3 >= P) {
+        const int u = (int)((claim & 0xffffu) + (claim >> 16));
+        s_ring[(j + 3) & 3] = u < D ? P + (int)(rev ? claim >> 16 : claim & 0xffffu) : -1;
       }
-      const int n2 = i + 2 < P ? i + 2 : __builtin_amdgcn_readfirstlane(s_ring[(i + 2) & 3]);
-      x.template load<true>(cur, sA + (int64_t)(n2 >= 0 ? n2 : sa) * sD + woff, pend, lane, va);
-      if (!vb_ok) {
+      if (j + 4 >= P) claim = __hip_atomic_fetch_add(pw, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    step_process<true, Step, SF>(va, sA + woff, pend, tf, s_wc, 0, base, fc);  // ordinals 0, 1: static (P >= 4)
+    post(0);
+    x.template load<true>(cur, sA + 2 * sD + woff, pend, lane, va);
+    step_process<true, Step, SF>(vb, sA + sD + woff, pend, tf, s_wc, 1, base, fc);
+    post(1);
+    int sa = 2;  // the ordinal va holds (ordinal-space step index: 0 = the block's first)
+    int done = 0;
+    for (int i = 2;; i += 2) {
+      const int n1 = i + 1 < P ? i + 1 : __builtin_amdgcn_readfirstlane(s_ring[(i + 1) & 3]);
+      x.template load<true>(cur, sA + (int64_t)(n1 >= 0 ? n1 : sa) * sD + woff, pend, lane, vb);
+      step_process<true, Step, SF>(va, sA + (int64_t)sa * sD + woff, pend, tf, s_wc, 0, base, fc);
+      post(i);
+      if (n1 < 0) {
         done = i + 1;
         break;
       }
-      step_process<true, Step, SF>(vb, sA + (int64_t)sb * sD + woff, pend, tf, s_wc, 1, base, fc);
-      if (tid == 0) {
-        if (i + 4 >= P) {
-          const int u = (int)((claim & 0xffffu) + (claim >> 16));
-          s_ring[(i + 4) & 3] = u < D ? P + (int)(rev ? claim >> 16 : claim & 0xffffu) : -1;
-        }
-        if (i + 5 >= P) claim = __hip_atomic_fetch_add(pw, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      const int n3 = i + 3 < P ? i + 3 : __builtin_amdgcn_readfirstlane(s_ring[(i + 3) & 3]);
-      x.template load<true>(cur, sA + (int64_t)(n3 >= 0 ? n3 : sb) * sD + woff, pend, lane, vb);
+      const int n2 = i + 2 < P ? i + 2 : __builtin_amdgcn_readfirstlane(s_ring[(i + 2) & 3]);
+      x.template load<true>(cur, sA + (int64_t)(n2 >= 0 ? n2 : n1) * sD + woff, pend, lane, va);
+      step_process<true, Step, SF>(vb, sA + (int64_t)n1 * sD + woff, pend, tf, s_wc, 1, base, fc);
+      post(i + 1);
       if (n2 < 0) {
         done = i + 2;
         break;
       }
       sa = n2;
-      sb = n3;
-      vb_ok = n3 >= 0;
     }
     // the block's range: `done` steps from its end of the pair's range
     b0 = rev ? ps + 2 * w.M - (int64_t)done * kBS : ps;
