@@ -84,9 +84,14 @@ class _Mirror:
                 view.copy_(t.detach())
                 t.data = view  # same values, shape, dtype and device: the storage is now the pinned buffer
         self.key = _ptr_key(groups)
+        # the device views, made once (a view costs ~1-2 us of host time, a model has ~10-100 tensors)
+        self.views = [[self.dev[off:off + _numel(s_)].view(s_) for off, s_ in zip(self.offs[gi], self.shapes[gi])]
+                      for gi in range(len(groups))]
+        # the read and written ranges of consecutive groups merge into one copy each way
+        self.span = (self.ranges[0][0], self.ranges[-1][1])
 
     def dev_views(self, gi: int) -> List[torch.Tensor]:
-        return [self.dev[off:off + _numel(s)].view(s) for off, s in zip(self.offs[gi], self.shapes[gi])]
+        return self.views[gi]
 
 
 def _numel(shape) -> int:
@@ -97,7 +102,9 @@ def _numel(shape) -> int:
 
 
 def _ptr_key(groups: Sequence[Sequence[torch.Tensor]]) -> tuple:
-    return tuple((t.data_ptr(), tuple(t.shape), t.dtype) for g in groups for t in g)
+    """(data pointer, element count) of every tensor: a tensor whose storage was reassigned or re-viewed to another
+    size no longer matches (a view of the same size and pointer keeps its values where the mirror expects them)."""
+    return tuple((t.data_ptr(), t.numel()) for g in groups for t in g)
 
 
 _MIRRORS: "collections.OrderedDict[tuple, _Mirror]" = collections.OrderedDict()
@@ -146,10 +153,13 @@ def _staging(dtype: torch.dtype, slot: int, n: int) -> torch.Tensor:
 
 
 def stage_messages(msgs: Sequence[Sequence[torch.Tensor]], device: torch.device,
-                   dtype: torch.dtype) -> List[List[torch.Tensor]]:
+                   dtype: torch.dtype) -> Sequence[Sequence[torch.Tensor]]:
     """Every message's tensors on ``device``: device tensors there already are used as they are, host tensors are
     packed into one pinned buffer and sent in one copy, tensors on another HIP device are moved.  Stream-ordered on
-    ``device``'s current stream."""
+    ``device``'s current stream.  Messages already on HIP devices (the reference's clients on cuda:i mod N) are
+    returned as they are: the fold takes them in place or moves the ones on another device itself."""
+    if all(len(m) == 0 or m[0].is_cuda for m in msgs):
+        return msgs
     host = [(i, j, t) for i, m in enumerate(msgs) for j, t in enumerate(m) if t.device.type == "cpu"]
     out = [[t.detach() if (t.device == device) else None for t in m] for m in msgs]
     for i, m in enumerate(msgs):
@@ -187,11 +197,15 @@ def staged(groups: Sequence[Sequence[torch.Tensor]], read: Sequence[bool], write
         device = _device_for(msgs)
     with torch.cuda.device(device):
         stream = torch.cuda.current_stream(device)
-        if m is not None:  # adopted: one copy per group's range, nothing packed on the host
-            for gi, rd in enumerate(read):
-                if rd:
-                    a, b = m.ranges[gi]
-                    m.dev[a:b].copy_(m.host[a:b], non_blocking=True)
+        if m is not None:  # adopted: one copy of the groups' contiguous span, nothing packed on the host
+            if all(read):
+                a, b = m.span
+                m.dev[a:b].copy_(m.host[a:b], non_blocking=True)
+            else:
+                for gi, rd in enumerate(read):
+                    if rd:
+                        a, b = m.ranges[gi]
+                        m.dev[a:b].copy_(m.host[a:b], non_blocking=True)
             dgroups = [m.dev_views(gi) for gi in range(len(groups))]
             hbuf, dbuf, ranges, offs = m.host, m.dev, m.ranges, m.offs
         else:  # packed through the staging buffer
@@ -208,10 +222,14 @@ def staged(groups: Sequence[Sequence[torch.Tensor]], read: Sequence[bool], write
                        for gi, g in enumerate(groups)]
         dmsgs = stage_messages(msgs, device, dtype)
         yield dgroups, dmsgs
-        for gi, wr in enumerate(write):
-            if wr:
-                a, b = ranges[gi]
-                hbuf[a:b].copy_(dbuf[a:b], non_blocking=True)
+        if m is not None and all(write):
+            a, b = m.span
+            hbuf[a:b].copy_(dbuf[a:b], non_blocking=True)
+        else:
+            for gi, wr in enumerate(write):
+                if wr:
+                    a, b = ranges[gi]
+                    hbuf[a:b].copy_(dbuf[a:b], non_blocking=True)
         stream.synchronize()
         if m is None:
             for gi, g in enumerate(groups):

@@ -55,3 +55,37 @@ for name, fn in legs:
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"{name}: {(t2 - t0) * 1e6 / 200:.2f} us/call, host enqueue {(t1 - t0) * 1e6 / 200:.2f} us/call", flush=True)
+
+# the reference's placement: the server model and its FedOpt state in host memory, the messages on the device
+import types  # noqa: E402
+
+from fl_sim_amd.aggregation import FedOptUpdateMixin  # noqa: E402
+
+
+class HostServer(FedOptUpdateMixin):
+    pass
+
+
+hs = HostServer()
+hs.model = torch.nn.Module()
+for i, sh in enumerate(SHAPES):
+    hs.model.register_parameter(f"p{i}", torch.nn.Parameter(torch.randn(sh)))
+hs.delta_parameters = [torch.zeros(sh) for sh in SHAPES]
+hs.v_parameters = None
+hs.config = types.SimpleNamespace(optimizer="avg", lr=1.0, betas=(0.0, 1.0), tau=1e-3)
+hs._received_messages = msgs
+for _ in range(10):
+    hs.update()
+t0 = time.perf_counter()
+for _ in range(100):
+    hs.update()
+print(f"host_server_fedavg: {(time.perf_counter() - t0) * 1e6 / 100:.2f} us/call (host to host, synchronised)", flush=True)
+import cProfile  # noqa: E402
+import pstats  # noqa: E402
+
+pr = cProfile.Profile()
+pr.enable()
+for _ in range(50):
+    hs.update()
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(12)
