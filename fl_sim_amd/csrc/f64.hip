@@ -411,7 +411,23 @@ __global__ __launch_bounds__(kT) void quant64_decode_kernel(const uint8_t* __res
 }
 
 // ------------------------------------------------------------------------------------------------
-// top-k on fp64 (compressors.py:293-296): out = x on the K largest, +0 elsewhere
+// top-k on fp64 (compressors.py:293-296: out = x.copy(); out[np.argsort(out)[:-K]] = 0): out = x on the K largest,
+// +0 elsewhere; among the ties of the K-th largest, the highest indices are kept (the float32 encoder's rule).
+//
+// Four launches; on the common path x is read once and out written once (the HBM floor: 16 B per element):
+//   sample    one block: S strided keys; their r_lo-th and r_hi-th largest, kept to their top 24 bits, bound a band
+//             [t_lo, t_hi) that holds the K-th largest key with ~4 sigma (+16) of the sample to spare on each side
+//   filter    one block per 8192-element chunk: every key >= t_lo appended to the chunk's segment (the value's bits
+//             and its u16 position), keys >= t_hi counted per chunk (no global atomics: every count a plain store)
+//   select    one block per CU, grid-synchronised: each block bins the band keys of its chunks' segments (2048 bins,
+//             LDS, then global atomics of its nonzero bins: 256 blocks), one grid barrier, the bin holding the K-th
+//             largest is found (every block the same one) and its keys appended to one list; the last block to
+//             finish selects the exact K-th key T among them, counts its ties and, when only some are kept, the index
+//             threshold of the highest-index ones.  When the band fails (the sample missed on either side, a segment
+//             overflowed, the bin held more keys than the list) or is off (n < 64 Ki, k near n), the same blocks run
+//             the exact radix select over x instead: 8 digit passes of the key, up to 8 of the tie index
+//   emit      one block per chunk: a 64 KB LDS tile zeroed, the chunk's kept candidates scattered into it, the tile
+//             written out whole (after the fallback: x read again and kept in place)
 // ------------------------------------------------------------------------------------------------
 // order-preserving key of a double: NaN largest, -0 == +0
 __device__ __forceinline__ unsigned long long order_key64(double v) {
@@ -421,37 +437,71 @@ __device__ __forceinline__ unsigned long long order_key64(double v) {
   return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
 }
 
-constexpr int kDigits = 8;  // 8-bit digits, most significant first
-constexpr int kSample64 = 8192;   // sample keys of the top-k floor
-constexpr int kFloorDigits = 3;   // the floor keeps the sample's r-th key to its top 24 bits (a floor below it)
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+constexpr int kDigits = 8;          // 8-bit digits of a 64-bit key, most significant first
+constexpr int kSample64 = 16384;    // sample keys
+constexpr int kSampleDigits = 3;    // the band's ends keep the sample keys' top 24 bits
+constexpr int kBand = 2048;         // band histogram bins
+constexpr int kBinCap = 16384;      // keys of the K-th largest's bin the gather's list holds
+constexpr int kGT = 1024;           // threads of the sample, gather and fallback blocks
+constexpr int kGNW = kGT / kWave;
+constexpr int kMaxG64 = 1024;       // blocks of the grid-synchronised select (one flag each)
+constexpr int kSampleBlocks = 64;   // blocks loading the sample
+constexpr unsigned long long kOvf = 1ull << 44;  // (n < 2^44)
+static_assert(kBand == 2 * kGT, "gather: two band bins per thread");
+static_assert(kSample64 % kGT == 0 && kBinCap % kGT == 0, "whole keys per thread");
+
 struct Sel64 {
-  // after q digit passes: the resolved high digits of the K-th largest key, its rank among the keys sharing them
-  // (from the top, 1-based), and the size of the last digit's bin (after all kDigits passes: the ties of T)
-  unsigned long long pre[kDigits + 1];
-  long long rem[kDigits + 1], cnt[kDigits + 1];
-  unsigned long long t_lo;  // candidate floor key (from the sample)
-  int mode;                 // 0: the digit passes run over the candidates, 1: over x itself
-  int ovf;                  // a chunk had more candidates than its segment holds
-  unsigned hist[kDigits][256];
+  unsigned long long stamps[32];      // diagnostic builds (FLC_SELECT_STAMPS): phase times, s_memrealtime
+  unsigned long long t_lo, t_hi;      // the band
+  int sh;                             // band bin of a band key: (key - t_lo) >> sh
+  int mode;                           // the sample's: 0 the band is on, 1 off (read-only in the select kernel)
+  int fb;                             // the select's: 1 when T came from the passes over x (the emit reads x again)
+  int err;                            // a grid barrier timed out (lost co-residency)
+  unsigned nbin;                      // the bin's list: keys appended
+  unsigned long long T;               // the K-th largest key
+  long long need, ties;               // ties of T kept / present
+  long long ithr;                     // the kept ties: index >= ithr
+  unsigned long long flags[kMaxG64];  // grid barriers (zeroed by the sample kernel: targets 1, 2, ... in each call)
+  unsigned long long pab[kMaxG64];    // per block: keys >= t_hi in its chunks + kOvf per overflowed segment
+  unsigned hist[kBand];               // the band histogram (slice b summed by block b)
+  unsigned fhist[2 * kDigits][256];   // the fallback's digit histograms: key digits, then tie-index digits
+  unsigned long long bkey[kBinCap];   // the K-th largest's bin: keys (less the bin's base) and their indices
+  long long bidx[kBinCap];
   unsigned long long sample[kSample64];
 };
 
-// LDS histogram add of one key per lane; a wave whose counted keys all fall in one bin (the common case in the high
-// digits, where the keys share their sign and exponent) adds once
+#ifdef FLC_SELECT_STAMPS  // (tools/stamps64.py)
+#define STAMP64(cond, i)                                                                      \
+  do {                                                                                        \
+    if ((cond) && threadIdx.x == 0) const_cast<Sel64*>(st)->stamps[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define STAMP64(cond, i) \
+  do {                   \
+  } while (0)
+#endif
+
+// LDS histogram add of one key per lane.  Lanes adding to one address serialise (a wave of keys sharing their sign
+// and exponent — the high digits of most data — is a 64-way conflict), so the wave's first two bins are added once
+// each with their lane counts, and only the lanes left over add one by one
 __device__ __forceinline__ void hist_add64(unsigned* h, unsigned bin, bool in) {
-  const unsigned long long m = __ballot(in);
-  if (m == 0ull) return;
-  const int first = __builtin_ctzll(m);
-  const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)bin, first);
-  if (__ballot(in && bin != b0) == 0ull) {
-    if ((int)(threadIdx.x & (kWave - 1)) == first) atomicAdd(&h[b0], (unsigned)__popcll(m));
-  } else if (in) {
-    atomicAdd(&h[bin], 1u);
+  unsigned long long m = __ballot(in);
+  const int lane = (int)(threadIdx.x & (kWave - 1));
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (m == 0ull) return;
+    const int first = __builtin_ctzll(m);
+    const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)bin, first);
+    const unsigned long long same = __ballot(in && bin == b0) & m;
+    if (lane == first) atomicAdd(&h[b0], (unsigned)__popcll(same));
+    m &= ~same;
   }
+  if ((m >> lane) & 1ull) atomicAdd(&h[bin], 1u);
 }
 
 // block-wide (NW waves): the bin of a 256-bin histogram (count of bin 255 - t in thread t < 256, 0 elsewhere)
-// holding rank `rem` from the top.  Returns, in every thread, (digit, count above it, its count).
+// holding rank `rem` from the top.  Returns, in every thread, (digit, count above it, its count) in s_res.
 template <int NW>
 __device__ __forceinline__ void pick256(long long c, long long rem, long long* s_scan, long long* s_res) {
   long long tot;
@@ -464,256 +514,588 @@ __device__ __forceinline__ void pick256(long long c, long long rem, long long* s
   __syncthreads();
 }
 
-// state q + 1 from state q and the q-th pass's histogram (every block of a kernel computes it the same way; the
-// caller's block 0 stores it for the next kernel)
-__device__ __forceinline__ void sel64_step(const Sel64* __restrict__ st, int q, long long* s_scan, long long* s_res,
-                                           unsigned long long& pre, long long& rem, long long& cnt) {
-  const long long c = threadIdx.x < 256 ? (long long)st->hist[q][255 - threadIdx.x] : 0ll;
-  pre = st->pre[q];
-  rem = st->rem[q];
-  pick256<kNW>(c, rem, s_scan, s_res);
-  pre = (pre << 8) | (unsigned long long)s_res[0];
-  rem -= s_res[1];
-  cnt = s_res[2];
+// a wave's slots for its lanes with `in` set, from an LDS (or global) counter: the lane's slot, or any value when !in
+__device__ __forceinline__ unsigned wave_append(unsigned* counter, bool in, unsigned long long m) {
+  unsigned base = 0u;
+  if ((threadIdx.x & (kWave - 1)) == 0) base = atomicAdd(counter, (unsigned)__popcll(m));
+  base = (unsigned)__builtin_amdgcn_readlane((int)base, 0);
+  return base + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-// block 0 resets the state; with S > 0 the blocks also take S evenly strided keys (the float32 encoder's sample
-// positions)
-__global__ __launch_bounds__(kT) void sel64_init_kernel(const double* __restrict__ x, int64_t n, int S, long long k,
-                                                        int mode, Sel64* __restrict__ st) {
-  if (blockIdx.x == 0) {
-    for (int i = threadIdx.x; i < kDigits * 256; i += kT) (&st->hist[0][0])[i] = 0u;
-    if (threadIdx.x == 0) {
-      st->pre[0] = 0ull;
-      st->rem[0] = k;
-      st->cnt[0] = 0;
-      st->t_lo = 0ull;
-      st->mode = mode;
-      st->ovf = 0;
-    }
+// the bin of a kBand-bin histogram holding rank r from the top (bin j's count in h(j)): every thread gets (bin, rank
+// in it, its count) in s_out; bin -1 when the histogram holds fewer than r keys.  Thread t holds bins kBand - 1 - 2t
+// and kBand - 2 - 2t (1024 threads).
+template <class H>
+__device__ __forceinline__ void pick_band(H h, long long r, long long* s_scan, long long* s_out) {
+  const int tid = threadIdx.x;
+  const long long ha = h(kBand - 1 - 2 * tid), hb = h(kBand - 2 - 2 * tid);
+  if (tid == 0) s_out[0] = -1;
+  long long tot;
+  const long long ex = block_excl_scan<long long, kGNW>(ha + hb, s_scan, &tot);  // (barriers: s_out[0] set)
+  if (r >= 1 && ex < r && ex + ha + hb >= r) {
+    const bool first = ex + ha >= r;
+    s_out[0] = first ? kBand - 1 - 2 * tid : kBand - 2 - 2 * tid;
+    s_out[1] = first ? r - ex : r - ex - ha;
+    s_out[2] = first ? ha : hb;
   }
-  const int j = blockIdx.x * kT + threadIdx.x;
-  if (j >= S) return;
-  const int64_t pos = (int64_t)(((double)j + 0.5) * (double)n / (double)S);
-  st->sample[j] = order_key64(x[pos < n ? pos : n - 1]);
+  __syncthreads();
 }
 
-// one block: t_lo = the r-th largest sample key truncated to its top 24 bits (three digit passes over the sample
-// held in registers), so that count(key >= t_lo) >= ~k + 4 sigma over the whole vector
-__global__ __launch_bounds__(1024) void sel64_floor_kernel(int S, long long r, Sel64* __restrict__ st) {
-  constexpr int kPer = kSample64 / 1024, kW = 1024 / kWave;
-  __shared__ unsigned s_h[256];
-  __shared__ long long s_scan[kW], s_res[3];
+// the shift that maps key offsets 0 .. maxoff onto at most 2^bits bins
+__device__ __forceinline__ int range_shift64(unsigned long long maxoff, int bits) {
+  if (maxoff == 0ull) return 0;
+  const int len = 64 - __clzll((long long)maxoff);
+  return len > bits ? len - bits : 0;
+}
+
+// The sample's S keys, loaded by kSampleBlocks blocks (scattered loads from one CU wait on its address translation a
+// page at a time)
+__global__ __launch_bounds__(kT) void sel64_sample_kernel(const double* __restrict__ x, int64_t n, int S,
+                                                          Sel64* __restrict__ st) {
+  STAMP64(blockIdx.x == 0, 0);
+  for (int j = blockIdx.x * kT + threadIdx.x; j < S; j += gridDim.x * kT) {
+    const int64_t pos = (int64_t)(((double)j + 0.5) * (double)n / (double)S);
+    st->sample[j] = order_key64(x[pos < n ? pos : n - 1]);
+  }
+}
+
+// One block: the state reset, and the band from the sample's r_lo-th and r_hi-th largest keys (r_hi <= 0: no
+// ceiling).  S = 0 (the band off): the reset only.
+//   r_lo <= 1024 (k up to ~6 % of n): B = the smallest thread maximum of the 16 keys each thread holds, so at least
+//   1024 sample keys lie at or above it; one 2048-bin histogram of the keys in [B, max] locates both ranks (few
+//   keys, spread over many bins: no LDS atomic contention), and a bin holding more than 8 keys is refined once inside
+//   it.  The floor is the floor of rank r_lo's bin, the ceiling the end of rank r_hi's bin.
+//   Otherwise: three 8-bit digit passes per rank (the keys' top 24 bits).
+__global__ __launch_bounds__(kGT) void sel64_floor_kernel(int S, long long r_lo, long long r_hi, Sel64* __restrict__ st) {
+  constexpr int kPer = kSample64 / kGT;
+  __shared__ unsigned s_h[2][256];
+  __shared__ unsigned s_hb[2][kBand];
+  __shared__ long long s_scan[kGNW], s_res[3], s_out[2][3];
+  __shared__ unsigned long long s_mm[2][kGNW];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
+  STAMP64(true, 1);
+  for (int i = tid; i < 2 * kDigits * 256; i += kGT) (&st->fhist[0][0])[i] = 0u;
+  for (int i = tid; i < kBand; i += kGT) st->hist[i] = 0u;
+  for (int i = tid; i < kMaxG64; i += kGT) st->flags[i] = 0ull;
+  if (tid == 0) {
+    st->mode = S > 0 ? 0 : 1;
+    st->fb = 0;
+    st->err = 0;
+    st->nbin = 0u;
+    st->T = 0ull;
+    st->need = st->ties = st->ithr = 0;
+  }
+  if (S <= 0) return;
   unsigned long long key[kPer];
 #pragma unroll
   for (int i = 0; i < kPer; ++i) {
-    const int j = i * 1024 + threadIdx.x;
+    const int j = i * kGT + tid;
     key[i] = j < S ? st->sample[j] : 0ull;
   }
-  unsigned long long prefix = 0ull;
-  long long rem = r;
-  for (int pass = 0; pass < kFloorDigits; ++pass) {
-    if (threadIdx.x < 256) s_h[threadIdx.x] = 0u;
-    __syncthreads();
-    const int sh = 56 - 8 * pass;
+  const bool hi = r_hi > 0;
+  unsigned long long t_lo, t_hi;
+  if (r_lo <= kGT && S == kSample64) {
+    unsigned long long m = 0ull;
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const bool in = i * 1024 + (int)threadIdx.x < S && (pass == 0 || (key[i] >> (sh + 8)) == prefix);
-      hist_add64(s_h, (unsigned)(key[i] >> sh) & 255u, in);
+    for (int i = 0; i < kPer; ++i) m = key[i] > m ? key[i] : m;
+    unsigned long long mn = m, mx = m;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
     }
+    if (lane == 0) {
+      s_mm[0][wid] = mn;
+      s_mm[1][wid] = mx;
+    }
+    for (int i = tid; i < 2 * kBand; i += kGT) (&s_hb[0][0])[i] = 0u;
     __syncthreads();
-    pick256<kW>(threadIdx.x < 256 ? (long long)s_h[255 - threadIdx.x] : 0ll, rem, s_scan, s_res);
-    prefix = (prefix << 8) | (unsigned long long)s_res[0];
-    rem -= s_res[1];
-    __syncthreads();  // (s_res and s_h are rewritten by the next pass)
+    unsigned long long B = ~0ull, M = 0ull;
+#pragma unroll
+    for (int w = 0; w < kGNW; ++w) {
+      B = s_mm[0][w] < B ? s_mm[0][w] : B;
+      M = s_mm[1][w] > M ? s_mm[1][w] : M;
+    }
+    const int sh = range_shift64(M - B, 11);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+      if (key[i] >= B) atomicAdd(&s_hb[0][(unsigned)((key[i] - B) >> sh)], 1u);
+    __syncthreads();
+    pick_band([&](int j) { return (long long)s_hb[0][j]; }, r_lo, s_scan, s_out[0]);
+    if (hi) pick_band([&](int j) { return (long long)s_hb[0][j]; }, r_hi, s_scan, s_out[1]);
+    unsigned long long lo0 = B + ((unsigned long long)s_out[0][0] << sh);
+    unsigned long long lo1 = hi ? B + ((unsigned long long)s_out[1][0] << sh) : 0ull;
+    int sh_hi = sh;
+    const bool ref0 = sh > 0 && s_out[0][2] > 8, ref1 = hi && sh > 0 && s_out[1][2] > 8;  // (block-uniform)
+    if (ref0 || ref1) {  // one finer pass inside the bins holding more than 8 keys
+      const int sh2 = sh > 11 ? sh - 11 : 0;
+      const unsigned long long bw = 1ull << sh;
+      __syncthreads();
+      for (int i = tid; i < 2 * kBand; i += kGT) (&s_hb[0][0])[i] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        if (ref0 && key[i] >= lo0 && key[i] - lo0 < bw) atomicAdd(&s_hb[0][(unsigned)((key[i] - lo0) >> sh2)], 1u);
+        if (ref1 && key[i] >= lo1 && key[i] - lo1 < bw) atomicAdd(&s_hb[1][(unsigned)((key[i] - lo1) >> sh2)], 1u);
+      }
+      __syncthreads();
+      const long long q0 = s_out[0][1], q1 = s_out[1][1];
+      __syncthreads();
+      if (ref0) {
+        pick_band([&](int j) { return (long long)s_hb[0][j]; }, q0, s_scan, s_out[0]);
+        lo0 += (unsigned long long)s_out[0][0] << sh2;
+      }
+      if (ref1) {
+        pick_band([&](int j) { return (long long)s_hb[1][j]; }, q1, s_scan, s_out[1]);
+        lo1 += (unsigned long long)s_out[1][0] << sh2;
+        sh_hi = sh2;
+      }
+    }
+    t_lo = lo0;
+    const unsigned long long e1 = lo1 + (1ull << sh_hi);
+    t_hi = !hi || e1 < lo1 ? ~0ull : e1;  // (saturated at the top of the key range)
+  } else {
+    unsigned long long plo = 0ull, phi = 0ull;
+    long long rlo = r_lo, rhi = r_hi;
+    for (int pass = 0; pass < kSampleDigits; ++pass) {
+      if (tid < 256) {
+        s_h[0][tid] = 0u;
+        s_h[1][tid] = 0u;
+      }
+      __syncthreads();
+      const int sh = 56 - 8 * pass;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const bool v = i * kGT + tid < S;
+        const unsigned d = (unsigned)(key[i] >> sh) & 255u;
+        hist_add64(s_h[0], d, v && (pass == 0 || (key[i] >> (sh + 8)) == plo));
+        if (hi) hist_add64(s_h[1], d, v && (pass == 0 || (key[i] >> (sh + 8)) == phi));
+      }
+      __syncthreads();
+      pick256<kGNW>(tid < 256 ? (long long)s_h[0][255 - tid] : 0ll, rlo, s_scan, s_res);
+      plo = (plo << 8) | (unsigned long long)s_res[0];
+      rlo -= s_res[1];
+      __syncthreads();  // (s_res is rewritten next)
+      if (hi) {
+        pick256<kGNW>(tid < 256 ? (long long)s_h[1][255 - tid] : 0ll, rhi, s_scan, s_res);
+        phi = (phi << 8) | (unsigned long long)s_res[0];
+        rhi -= s_res[1];
+        __syncthreads();
+      }
+    }
+    constexpr int low = 64 - 8 * kSampleDigits;
+    t_lo = plo << low;
+    t_hi = (!hi || phi == (1ull << (8 * kSampleDigits)) - 1ull) ? ~0ull : (phi + 1ull) << low;
   }
-  if (threadIdx.x == 0) st->t_lo = prefix << (64 - 8 * kFloorDigits);
+  if (tid == 0) {
+    st->t_lo = t_lo;
+    st->t_hi = t_hi;
+    st->sh = range_shift64(t_hi - t_lo - 1ull, 11);  // (t_hi > t_lo)
+  }
+  STAMP64(true, 2);
 }
 
-// the candidates (key >= t_lo) of each 8192-element chunk appended to the chunk's own segment (no global atomics);
-// counts[c] = the chunk's candidate count (a count beyond the segment flags st->ovf: the passes then run over x)
+// the candidates (key >= t_lo) of each 8192-element chunk appended to the chunk's own segment (value bits, position);
+// counts[c] = the chunk's candidates (more than the segment holds: the select falls back), above[c] = its keys >= t_hi
 __global__ __launch_bounds__(kT) void sel64_filter_kernel(const double* __restrict__ x, int64_t n, int segcap,
-                                                          Sel64* __restrict__ st, unsigned long long* __restrict__ seg,
-                                                          int* __restrict__ counts) {
-  // (the digit passes only histogram the candidates: their order inside a segment is free, so each wave appends
-  // through one LDS counter, without block-wide barriers)
+                                                          const Sel64* __restrict__ st,
+                                                          unsigned long long* __restrict__ seg,
+                                                          unsigned short* __restrict__ segi, int* __restrict__ counts,
+                                                          int* __restrict__ above) {
   __shared__ unsigned s_n;
-  if (threadIdx.x == 0) s_n = 0u;
-  __syncthreads();
-  const unsigned long long t_lo = st->t_lo;
-  unsigned long long* my = seg + (size_t)blockIdx.x * segcap;
-  const int lane = threadIdx.x & (kWave - 1);
+  __shared__ int s_red[kNW];
+  const int tid = threadIdx.x;
+  STAMP64(blockIdx.x == 0, 3);
+  if (tid == 0) s_n = 0u;
+  const unsigned long long t_lo = st->t_lo, t_hi = st->t_hi;
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  double v[kIt][kE];  // the chunk's 32 elements of this thread, all loads in flight at once
+#pragma unroll
   for (int it = 0; it < kIt; ++it) {
-    const int64_t e0 = (int64_t)blockIdx.x * kChunk + ((int64_t)it * kT + threadIdx.x) * kE;
-    double v[kE] = {0.0, 0.0, 0.0, 0.0};
-    if (e0 < n) load4(x, e0, n, v);
+    const int64_t e0 = c0 + ((int64_t)it * kT + tid) * kE;
+    if (e0 < n) load4(x, e0, n, v[it]);
+    else
+#pragma unroll
+      for (int j = 0; j < kE; ++j) v[it][j] = 0.0;
+  }
+  __syncthreads();
+  unsigned long long* my = seg + (size_t)blockIdx.x * segcap;
+  unsigned short* myi = segi + (size_t)blockIdx.x * segcap;
+  int ab = 0;
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
 #pragma unroll
     for (int j = 0; j < kE; ++j) {
-      const unsigned long long key = order_key64(v[j]);
-      const bool in = e0 + j < n && key >= t_lo;
+      const int loc = (it * kT + tid) * kE + j;
+      const unsigned long long key = order_key64(v[it][j]);
+      const bool in = c0 + loc < n && key >= t_lo;
       const unsigned long long m = __ballot(in);
       if (m == 0ull) continue;
-      unsigned base = 0;
-      if (lane == 0) base = atomicAdd(&s_n, (unsigned)__popcll(m));
-      base = (unsigned)__builtin_amdgcn_readlane((int)base, 0);
-      const unsigned p = base + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-      if (in && p < (unsigned)segcap) my[p] = key;
+      const unsigned p = wave_append(&s_n, in, m);
+      if (in) {
+        if (p < (unsigned)segcap) {
+          my[p] = (unsigned long long)__double_as_longlong(v[it][j]);
+          myi[p] = (unsigned short)loc;
+        }
+        ab += key >= t_hi ? 1 : 0;
+      }
+    }
+  }
+  ab = block_sum<int, kNW>(ab, s_red);  // (a barrier: s_n final)
+  if (tid == 0) {
+    counts[blockIdx.x] = (int)s_n;
+    above[blockIdx.x] = ab;
+  }
+#ifdef FLC_SELECT_STAMPS
+  if (tid == 0 && blockIdx.x == 0) const_cast<Sel64*>(st)->stamps[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
+// block-wide radix select of the rem-th largest among the cnt values v[q] (slot q * kGT + tid, values < 2^bits;
+// `eq` restricts the count to the lanes' flagged values): returns the value; rem becomes its rank among its equals,
+// cnt their number
+template <int PER>
+__device__ __forceinline__ unsigned long long block_select(const unsigned long long (&v)[PER], const bool (&ok)[PER],
+                                                           int bits, long long& rem, long long& cnt, unsigned* s_h,
+                                                           long long* s_scan, long long* s_res) {
+  const int tid = threadIdx.x;
+  unsigned long long pre = 0ull;
+  for (int hb = bits; hb > 0;) {
+    const int w = hb >= 8 ? 8 : hb, lo = hb - w;
+    if (tid < 256) s_h[tid] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+      hist_add64(s_h, (unsigned)(v[q] >> lo) & ((1u << w) - 1u), ok[q] && (hb >= 64 || (v[q] >> hb) == pre));
+    __syncthreads();
+    pick256<kGNW>(tid < 256 ? (long long)s_h[255 - tid] : 0ll, rem, s_scan, s_res);
+    pre = (pre << w) | (unsigned long long)s_res[0];
+    rem -= s_res[1];
+    cnt = s_res[2];
+    __syncthreads();
+    hb = lo;
+  }
+  return pre;
+}
+
+// The K-th largest among a short list of cnt <= blockDim.x keys (s_d: offsets in the bin, s_i: their indices, in
+// LDS), rank rem0 from the top: each key's rank by comparing it with all others (a broadcast LDS read per step).
+// Returns T's offset dt, its rank among its ties (rem), their number, and the index threshold of the kept ties.
+__device__ __forceinline__ void rank_small(const unsigned long long* s_d, const long long* s_i, int cnt, long long rem0,
+                                           long long* s_sel, unsigned long long& dt, long long& rem, long long& ties,
+                                           long long& ithr) {
+  const int tid = threadIdx.x;
+  if (tid < cnt) {
+    const unsigned long long my = s_d[tid];
+    long long gt = 0, eq = 0;
+    for (int j = 0; j < cnt; ++j) {
+      gt += s_d[j] > my ? 1 : 0;
+      eq += s_d[j] == my ? 1 : 0;
+    }
+    if (gt < rem0 && rem0 <= gt + eq) {  // (every copy of T writes the same values)
+      s_sel[0] = (long long)my;
+      s_sel[1] = rem0 - gt;
+      s_sel[2] = eq;
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    counts[blockIdx.x] = (int)s_n;
-    if (s_n > (unsigned)segcap) atomicOr(&st->ovf, 1);
+  dt = (unsigned long long)s_sel[0];
+  rem = s_sel[1];
+  ties = s_sel[2];
+  ithr = 0;
+  if (rem < ties) {  // keep the rem ties with the highest indices: the one with rem - 1 tie indices above it
+    if (tid < cnt && s_d[tid] == dt) {
+      const long long ix = s_i[tid];
+      long long gi = 0;
+      for (int j = 0; j < cnt; ++j) gi += (s_d[j] == dt && s_i[j] > ix) ? 1 : 0;
+      if (gi == rem - 1) s_sel[3] = ix;
+    }
+    __syncthreads();
+    ithr = s_sel[3];
   }
 }
 
-// digit pass `pass`: the previous pass's digit resolved first (state pass from state pass - 1), then mode 0 over the
-// chunk segments (block b takes chunks b, b + grid, ...: slots i < counts[c]), mode 1 over x
-__global__ __launch_bounds__(kT) void sel64_hist_kernel(const double* __restrict__ x, int64_t n, int pass,
-                                                        Sel64* __restrict__ st, const unsigned long long* __restrict__ seg,
-                                                        const int* __restrict__ counts, int64_t nch, int segcap) {
-  __shared__ unsigned s_h[256];
-  __shared__ long long s_scan[kNW], s_res[3];
-  __shared__ int s_mode;
-  s_h[threadIdx.x] = 0u;
-  unsigned long long prefix = 0ull;
-  if (pass == 0) {
-    // the candidates serve unless a segment overflowed or the floor admitted fewer than k elements (the sample
-    // missed): every block sums the chunk counts itself (block 0 records the decision for the later passes)
-    long long c = 0;
-    if (st->mode == 0)
-      for (int64_t i = threadIdx.x; i < nch; i += kT) c += counts[i];
-    c = block_sum<long long, kNW>(c, s_scan);
-    if (threadIdx.x == 0) {
-      s_mode = (st->mode != 0 || st->ovf || c < st->rem[0]) ? 1 : 0;
-      if (blockIdx.x == 0) st->mode = s_mode;
-    }
-  } else {
-    if (threadIdx.x == 0) s_mode = st->mode;
-  }
-  if (pass > 0) {
-    long long rem, cnt;
-    sel64_step(st, pass - 1, s_scan, s_res, prefix, rem, cnt);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      st->pre[pass] = prefix;
-      st->rem[pass] = rem;
-      st->cnt[pass] = cnt;
+// the select's grid barrier: this block's stores and atomics drained, its flag raised to `target`, every flag polled
+__device__ __forceinline__ void grid_arrive64(Sel64* st, unsigned long long target) {
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(st->flags + blockIdx.x, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void grid_sync64(Sel64* st, unsigned long long target) {
+  grid_arrive64(st, target);
+  const int tid = threadIdx.x;
+  if (tid < kWave) {
+    const int G = (int)gridDim.x;
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < kMaxG64 / kWave; ++i) {
+        const int b = tid + i * kWave;
+        if (i * kWave < G) {  // (uniform)
+          const unsigned long long f =
+              __hip_atomic_load(st->flags + (b < G ? b : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= b >= G || f >= target;
+        }
+      }
+      if (__ballot(!ok) == 0ull) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {  // ~1 s: a block never arrived (lost co-residency); flag it and let the launch drain
+        if (tid == 0) atomicOr(&st->err, 1);
+        break;
+      }
     }
   }
   __syncthreads();
-  const int sh = 56 - 8 * pass;
-  auto add = [&](unsigned long long key, bool valid) {
-    hist_add64(s_h, (unsigned)(key >> sh) & 255u, valid && (pass == 0 || (key >> (sh + 8)) == prefix));
-  };
-  if (s_mode == 0) {
-    for (int64_t c = blockIdx.x; c < nch; c += gridDim.x) {
-      const int cnt = counts[c];
-      const unsigned long long* sc = seg + (size_t)c * segcap;
-      for (int i0 = 0; i0 < cnt; i0 += kT) {  // (block-uniform bounds)
-        const int i = i0 + (int)threadIdx.x;
-        add(i < cnt ? sc[i] : 0ull, i < cnt);
+}
+
+// T, its ties and the tie-index threshold: from the band when it holds the K-th largest (block b's chunks are
+// b * 16 + w, + G * 16, ... for its waves w: one wave per chunk; three grid barriers, block 0 selects T from the
+// bin's list), else from the passes over x
+__global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restrict__ x, int64_t n, long long k,
+                                                           int segcap, Sel64* __restrict__ st,
+                                                           const unsigned long long* __restrict__ seg,
+                                                           const unsigned short* __restrict__ segi,
+                                                           const int* __restrict__ counts,
+                                                           const int* __restrict__ above, int64_t nch) {
+  constexpr int kPer = kBinCap / kGT;
+  __shared__ unsigned s_hb[kBand];
+  __shared__ unsigned s_h[256];
+  __shared__ long long s_scan[kGNW], s_res[3], s_bin[3];
+  __shared__ unsigned long long s_ab;
+  __shared__ unsigned long long s_d[kGT];
+  __shared__ long long s_i[kGT], s_sel[4];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
+  const int G = (int)gridDim.x;
+  unsigned long long target = 0ull;
+  STAMP64(blockIdx.x == 0, 5);
+  bool band = st->mode == 0;
+  if (band) {
+    // 1. this block's band histogram, keys above the band and overflows, from its chunks' segments
+    for (int i = tid; i < kBand; i += kGT) s_hb[i] = 0u;
+    if (tid == 0) s_ab = 0ull;
+    __syncthreads();
+    const unsigned long long t_lo = st->t_lo, t_hi = st->t_hi;
+    const int sh = st->sh;
+    for (int64_t ch = (int64_t)blockIdx.x * kGNW + wid; ch < nch; ch += (int64_t)G * kGNW) {
+      const int c = counts[ch];
+      const unsigned long long* sc = seg + (size_t)ch * segcap;
+      for (int i = lane; i < min(c, segcap); i += kWave) {
+        const unsigned long long key = order_key64(__longlong_as_double((long long)sc[i]));
+        if (key < t_hi) atomicAdd(&s_hb[(unsigned)((key - t_lo) >> sh)], 1u);  // (key >= t_lo: a candidate)
       }
+      if (lane == 0) atomicAdd(&s_ab, (unsigned long long)above[ch] + (c > segcap ? kOvf : 0ull));
     }
-  } else {
-    for (int64_t i0 = (int64_t)blockIdx.x * kT * 2; i0 < n; i0 += (int64_t)gridDim.x * kT * 2) {
-      const int64_t i = i0 + 2 * threadIdx.x;
-      double v[2] = {0.0, 0.0};
+    __syncthreads();
+    // 2. the block's nonzero bins added to the global histogram (zeroed by the floor kernel), its count of keys above
+    //    the band and overflows published; one grid barrier
+    for (int i = tid; i < kBand; i += kGT)
+      if (s_hb[i]) atomicAdd(&st->hist[i], s_hb[i]);
+    if (tid == 0) st_sc1(&st->pab[blockIdx.x], s_ab);
+    STAMP64(blockIdx.x == 0, 6);
+    grid_sync64(st, ++target);
+    STAMP64(blockIdx.x == 0, 7);
+    // 3. the bin of the K-th largest (every block the same)
+    unsigned long long ab = 0ull;
+    for (int s = tid; s < G; s += kGT) ab += ld_sc1(&st->pab[s]);
+    ab = block_sum<unsigned long long, kGNW>(ab, reinterpret_cast<unsigned long long*>(s_scan));
+    const bool ovf = ab >= kOvf;
+    // (the K-th largest's rank among the band keys: k less the keys above the band)
+    pick_band([&](int j) { return (long long)ld_sc1(&st->hist[j]); }, k - (long long)(ab & (kOvf - 1ull)), s_scan,
+              s_bin);
+    const long long bin = s_bin[0], rem0 = s_bin[1], cnt0 = s_bin[2];
+    band = !ovf && bin >= 0 && cnt0 <= kBinCap;  // bin < 0: the sample's ceiling was too low or its floor too high
+    STAMP64(blockIdx.x == 0, 10);
+    if (band) {
+      // 4. the bin's keys to the list; the last block selects T among them
+      const unsigned long long lo_b = t_lo + ((unsigned long long)bin << sh), wb = 1ull << sh;
+      for (int64_t ch = (int64_t)blockIdx.x * kGNW + wid; ch < nch; ch += (int64_t)G * kGNW) {
+        const int c = counts[ch];
+        const unsigned long long* sc = seg + (size_t)ch * segcap;
+        const unsigned short* si = segi + (size_t)ch * segcap;
+        for (int i0 = 0; i0 < c; i0 += kWave) {  // (wave-uniform bounds)
+          const int i = i0 + lane;
+          const unsigned long long key = i < c ? order_key64(__longlong_as_double((long long)sc[i])) : 0ull;
+          const bool in = i < c && key >= lo_b && key - lo_b < wb;
+          const unsigned long long m = __ballot(in);
+          if (m == 0ull) continue;
+          const unsigned p = wave_append(&st->nbin, in, m);
+          if (in && p < (unsigned)kBinCap) {
+            st_sc1(&st->bkey[p], key - lo_b);
+            st_sc1(&st->bidx[p], (long long)(ch * kChunk + si[i]));
+          }
+        }
+      }
+      STAMP64(blockIdx.x == 0, 11);
+      if (blockIdx.x != 0) {  // (block 0 alone waits for every block's appends, then selects T)
+        grid_arrive64(st, ++target);
+        return;
+      }
+      grid_sync64(st, ++target);
+      STAMP64(true, 12);
+      // (block 0: every list entry is in)
+      const long long cnt = min((long long)ld_sc1(&st->nbin), cnt0);
+      unsigned long long dt;
+      long long rem, ties, ithr = 0;
+      if (cnt <= kGT) {  // each key's rank by comparing it with all others
+        if (tid < cnt) {
+          s_d[tid] = ld_sc1(&st->bkey[tid]);
+          s_i[tid] = ld_sc1(&st->bidx[tid]);
+        }
+        __syncthreads();
+        rank_small(s_d, s_i, (int)cnt, rem0, s_sel, dt, rem, ties, ithr);
+      } else {  // a radix select over the list (up to kBinCap keys)
+        unsigned long long d[kPer];
+        bool ok[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+          const int p = q * kGT + tid;
+          ok[q] = p < cnt;
+          d[q] = ok[q] ? ld_sc1(&st->bkey[p]) : 0ull;
+        }
+        rem = rem0;
+        ties = cnt;
+        dt = block_select<kPer>(d, ok, sh, rem, ties, s_h, s_scan, s_res);
+        if (rem < ties) {  // keep the rem ties with the highest indices: ithr = the rem-th largest index among them
+          unsigned long long ix[kPer];
+#pragma unroll
+          for (int q = 0; q < kPer; ++q) {
+            ok[q] = ok[q] && d[q] == dt;
+            ix[q] = ok[q] ? (unsigned long long)ld_sc1(&st->bidx[q * kGT + tid]) : 0ull;
+          }
+          long long ir = rem, ic = ties;
+          ithr = (long long)block_select<kPer>(ix, ok, 64 - __clzll((long long)(n - 1 > 0 ? n - 1 : 1)), ir, ic,
+                                               s_h, s_scan, s_res);
+        }
+      }
+      STAMP64(true, 13);
+      if (tid == 0) {
+        st->T = lo_b + dt;
+        st->need = rem;
+        st->ties = ties;
+        st->ithr = ithr;
+      }
+      return;
+    }
+  }
+  // the fallback: the exact radix select over x (every block reached this point with the same decision)
+  // one digit pass: `digit(i, key)` returns the element's digit, or -1 when it is not counted
+  auto pass = [&](int slot, long long rem, auto digit) {
+    if (tid < 256) s_h[tid] = 0u;
+    __syncthreads();
+    for (int64_t i0 = (int64_t)blockIdx.x * kGT * 2; i0 < n; i0 += (int64_t)G * kGT * 2) {
+      const int64_t i = i0 + 2 * tid;
+      double v0 = 0.0, v1 = 0.0;
       if (i + 2 <= n) {
         const double2 a = *reinterpret_cast<const double2*>(x + i);
-        v[0] = a.x;
-        v[1] = a.y;
+        v0 = a.x;
+        v1 = a.y;
       } else if (i < n) {
-        v[0] = x[i];
+        v0 = x[i];
       }
-      add(order_key64(v[0]), i < n);
-      add(order_key64(v[1]), i + 1 < n);
+      const int d0 = i < n ? digit(i, order_key64(v0)) : -1;
+      const int d1 = i + 1 < n ? digit(i + 1, order_key64(v1)) : -1;
+      hist_add64(s_h, (unsigned)d0, d0 >= 0);
+      hist_add64(s_h, (unsigned)d1, d1 >= 0);
     }
+    __syncthreads();
+    if (tid < 256 && s_h[tid]) atomicAdd(&st->fhist[slot][tid], s_h[tid]);
+    grid_sync64(st, ++target);
+    pick256<kGNW>(tid < 256 ? (long long)ld_sc1(&st->fhist[slot][255 - tid]) : 0ll, rem, s_scan, s_res);
+  };
+  unsigned long long T = 0ull;
+  long long need = k, ties = 0;
+  for (int q = 0; q < kDigits; ++q) {
+    const int sh = 56 - 8 * q;
+    pass(q, need, [&](int64_t, unsigned long long key) {
+      return (q == 0 || (key >> (sh + 8)) == T) ? (int)((key >> sh) & 255u) : -1;
+    });
+    T = (T << 8) | (unsigned long long)s_res[0];
+    need -= s_res[1];
+    ties = s_res[2];
+    __syncthreads();
   }
-  __syncthreads();
-  if (s_h[threadIdx.x]) atomicAdd(&st->hist[pass][threadIdx.x], s_h[threadIdx.x]);
+  long long ithr = 0;
+  if (need < ties) {  // the need-th largest index among the ties of T
+    const int bits = 64 - __clzll((long long)(n - 1 > 0 ? n - 1 : 1));
+    unsigned long long ip = 0ull;
+    long long ir = need;
+    for (int hb = bits, q = 0; hb > 0; ++q) {
+      const int w = hb >= 8 ? 8 : hb, lo = hb - w;
+      pass(kDigits + q, ir, [&](int64_t i, unsigned long long key) {
+        return (key == T && ((unsigned long long)i >> hb) == ip) ? (int)(((unsigned long long)i >> lo) & ((1u << w) - 1u))
+                                                                 : -1;
+      });
+      ip = (ip << w) | (unsigned long long)s_res[0];
+      ir -= s_res[1];
+      __syncthreads();
+      hb = lo;
+    }
+    ithr = (long long)ip;
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    st->T = T;
+    st->need = need;
+    st->ties = ties;
+    st->ithr = ithr;
+    st->fb = 1;
+  }
 }
 
-// ties (keys == T) per chunk, for the highest-index rule; nothing to count when every tie is kept (need == ties)
-__global__ __launch_bounds__(kT) void sel64_ties_kernel(const double* __restrict__ x, int64_t n, Sel64* __restrict__ st,
-                                                        int* __restrict__ counts) {
-  __shared__ int s_red[kNW];
-  __shared__ long long s_scan[kNW], s_res[3];
-  unsigned long long T;
-  long long need, ties;
-  sel64_step(st, kDigits - 1, s_scan, s_res, T, need, ties);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->pre[kDigits] = T;
-    st->rem[kDigits] = need;
-    st->cnt[kDigits] = ties;
-  }
-  if (need == ties) {
-    if (threadIdx.x == 0) counts[blockIdx.x] = 0;
+// dense write: keep key > T, and the ties of T at index >= ithr
+__global__ __launch_bounds__(kT) void sel64_emit_kernel(const double* __restrict__ x, int64_t n, int segcap,
+                                                        const Sel64* __restrict__ st,
+                                                        const unsigned long long* __restrict__ seg,
+                                                        const unsigned short* __restrict__ segi,
+                                                        const int* __restrict__ counts, double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) unsigned long long s_tile[kChunk];  // 64 KB
+  const int tid = threadIdx.x;
+  const unsigned long long T = st->T;
+  const long long ithr = st->ithr;
+  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+#ifdef FLC_SELECT_STAMPS
+  if (tid == 0 && blockIdx.x == 0) const_cast<Sel64*>(st)->stamps[14] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (!st->fb) {  // the chunk's candidates (all of them in its segment) scattered into a zeroed tile
+    u64x2* t2 = reinterpret_cast<u64x2*>(s_tile);
+    for (int i = tid; i < kChunk / 2; i += kT) t2[i] = u64x2{0ull, 0ull};
+    __syncthreads();
+    const int cc = counts[blockIdx.x];
+    const unsigned long long* sc = seg + (size_t)blockIdx.x * segcap;
+    const unsigned short* si = segi + (size_t)blockIdx.x * segcap;
+    for (int i = tid; i < cc; i += kT) {
+      const unsigned long long b = sc[i];
+      const int loc = si[i];
+      const unsigned long long key = order_key64(__longlong_as_double((long long)b));
+      if (key > T || (key == T && c0 + loc >= ithr)) s_tile[loc] = b;
+    }
+    __syncthreads();
+    double2* o2 = reinterpret_cast<double2*>(out + c0);
+    for (int i = tid; i < kChunk / 2; i += kT) {
+      const int64_t e = c0 + 2 * i;
+      if (e + 2 <= n) {
+        const u64x2 b = t2[i];
+        // (non-temporal: the 200 MB of output are written through, not left in the memory-side cache for the next
+        // call's filter pass to evict — measured 131 -> 107 us per 25 M call)
+        __builtin_nontemporal_store(b, reinterpret_cast<u64x2*>(o2) + i);  // (one 16-B store)
+      } else if (e < n) {
+        out[e] = __longlong_as_double((long long)s_tile[2 * i]);
+      }
+    }
     return;
   }
-  int cnt = 0;
   for (int it = 0; it < kIt; ++it) {
-    const int64_t e0 = (int64_t)blockIdx.x * kChunk + ((int64_t)it * kT + threadIdx.x) * kE;
+    const int64_t e0 = c0 + ((int64_t)it * kT + tid) * kE;
     if (e0 >= n) break;
     double v[kE];
     load4(x, e0, n, v);
 #pragma unroll
-    for (int j = 0; j < kE; ++j) cnt += (e0 + j < n && order_key64(v[j]) == T) ? 1 : 0;
-  }
-  const int tot = block_sum<int, kNW>(cnt, s_red);
-  if (threadIdx.x == 0) counts[blockIdx.x] = tot;
-}
-
-// dense write: keep key > T, and the `rem` ties with the highest indices (tie rank from the top < rem)
-__global__ __launch_bounds__(kT) void sel64_emit_kernel(const double* __restrict__ x, int64_t n,
-                                                        const Sel64* __restrict__ st,
-                                                        const long long* __restrict__ offsets, int64_t nchunks,
-                                                        double* __restrict__ out) {
-  __shared__ long long s_scan[kNW];
-  const unsigned long long T = st->pre[kDigits];
-  const long long need = st->rem[kDigits];
-  // ties after this chunk = total - ties up to the end of this chunk (all 0 when every tie is kept: then
-  // `higher` below is negative, hence < need, for every tie)
-  if (need == st->cnt[kDigits]) {  // every tie kept (the common case): key >= T, no tie ranks
-    for (int it = 0; it < kIt; ++it) {
-      const int64_t e0 = (int64_t)blockIdx.x * kChunk + ((int64_t)it * kT + threadIdx.x) * kE;
-      if (e0 >= n) break;
-      double v[kE];
-      load4(x, e0, n, v);
-#pragma unroll
-      for (int j = 0; j < kE; ++j) v[j] = order_key64(v[j]) >= T ? v[j] : 0.0;
-      store4(out, e0, n, v);
-    }
-    return;
-  }
-  long long after = offsets[nchunks] - offsets[blockIdx.x];
-  for (int it = 0; it < kIt; ++it) {
-    const int64_t e0 = (int64_t)blockIdx.x * kChunk + ((int64_t)it * kT + threadIdx.x) * kE;
-    double v[kE];
-    if (e0 < n) load4(x, e0, n, v);
-    else
-#pragma unroll
-      for (int j = 0; j < kE; ++j) v[j] = 0.0;
-    int c[kE], cnt = 0;
-    unsigned long long key[kE];
-#pragma unroll
     for (int j = 0; j < kE; ++j) {
-      key[j] = order_key64(v[j]);
-      c[j] = (e0 + j < n && key[j] == T) ? 1 : 0;
-      cnt += c[j];
+      const unsigned long long key = order_key64(v[j]);
+      v[j] = (key > T || (key == T && e0 + j >= ithr)) ? v[j] : 0.0;
     }
-    long long tot;
-    const long long before = block_excl_scan<long long, kNW>((long long)cnt, s_scan, &tot);
-    // ties with a higher index than element j: those after this iteration, and those after it inside it
-    long long higher = after - before - cnt;  // (after counts this iteration's ties too)
-    double o[kE];
-#pragma unroll
-    for (int j = kE - 1; j >= 0; --j) {
-      const bool keep = key[j] > T || (c[j] && higher < need);
-      higher += c[j];
-      o[j] = keep ? v[j] : 0.0;
-    }
-    after -= tot;
-    if (e0 < n) store4(out, e0, n, o);
+    store4(out, e0, n, v);
   }
 }
 
@@ -758,10 +1140,11 @@ int flc_randk_apply_f64(const double* x, int64_t n, const int32_t* idx, int64_t 
 }  // extern "C"
 
 namespace {
-// the top-k filter's geometry: sample size, the floor's rank in the sample, and each chunk's candidate segment
+// the top-k band's geometry: sample size, the sample ranks of its floor and ceiling, and each chunk's candidate
+// segment
 struct Filt64 {
   int S;
-  long long r_lo;
+  long long r_lo, r_hi;
   bool on;
   int segcap;
 };
@@ -769,9 +1152,10 @@ Filt64 filt64(int64_t n, int64_t k) {
   Filt64 f{};
   if (n < 65536 || k <= 0 || k >= n) return f;
   f.S = (int)std::min<int64_t>(n, kSample64);
-  const double m = (double)f.S * (double)k / (double)n;
-  f.r_lo = (long long)ceil(m + 4.0 * sqrt(m) + 16.0);
+  const double m = (double)f.S * (double)k / (double)n, sd = 4.0 * sqrt(m) + 16.0;
+  f.r_lo = (long long)ceil(m + sd);
   if (f.r_lo >= f.S) return f;
+  f.r_hi = std::max<long long>(0, (long long)floor(m - sd));
   const double frac = (double)f.r_lo / (double)f.S;
   f.segcap = (int)align_up((size_t)std::min<double>(kChunk, ceil(2.0 * frac * kChunk) + 256.0), 64);
   f.on = true;
@@ -783,7 +1167,9 @@ struct Ws64 {
   long long* offsets;
   unsigned long long* part;
   Sel64* sel;
-  unsigned long long* seg;  // top-k candidate segments: [chunks][segcap]
+  unsigned long long* seg;  // top-k candidate segments: [chunks][segcap] value bits
+  unsigned short* segi;     //   ... and positions in the chunk
+  int* above;               // top-k: keys above the band per chunk
   size_t need;
 };
 Ws64 carve64(void* ws, size_t bytes, int64_t n, int64_t k = 0) {
@@ -793,9 +1179,11 @@ Ws64 carve64(void* ws, size_t bytes, int64_t n, int64_t k = 0) {
   w.counts = c.take<int>((size_t)nch);
   w.offsets = c.take<long long>((size_t)nch + 1);
   w.part = c.take<unsigned long long>((size_t)nch);
-  w.sel = c.take<Sel64>(1);
+  w.sel = c.take<Sel64>(k > 0 ? 1 : 0);
   const Filt64 f = filt64(n, k);
   w.seg = c.take<unsigned long long>(f.on ? (size_t)nch * f.segcap : 0);
+  w.segi = c.take<unsigned short>(f.on ? (size_t)nch * f.segcap : 0);
+  w.above = c.take<int>(f.on ? (size_t)nch : 0);
   w.need = c.off;
   return w;
 }
@@ -929,27 +1317,25 @@ int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void*
   hipStream_t st = as_stream(stream);
   const int64_t nch = cdiv(n, kChunk);
   const Filt64 f = filt64(n, k);
-  // the candidates: a sample's floor t_lo (count(key >= t_lo) ~ k + 4 sigma), one filtering pass into per-chunk
-  // segments; the digit passes then read the candidates (~1.3 k keys) instead of x, unless a segment overflowed or the
-  // floor admitted fewer than k elements (then they read x: the same result)
-  FLC_LAUNCH("sel64_init", sel64_init_kernel, dim3((unsigned)std::max<int64_t>(1, cdiv(f.S, kT))), dim3(kT), 0, st, x,
-             n, f.on ? f.S : 0, (long long)k, f.on ? 0 : 1, w.sel);
-  if (f.on) {
-    FLC_LAUNCH("sel64_floor", sel64_floor_kernel, dim3(1), dim3(1024), 0, st, f.S, f.r_lo, w.sel);
-    FLC_LAUNCH("sel64_filter", sel64_filter_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, f.segcap, w.sel, w.seg,
-               w.counts);
+  int dev = 0;
+  const int cus = std::min(stream_cus(st, &dev), kMaxG64);
+  if (f.on) FLC_LAUNCH("sel64_sample", sel64_sample_kernel, dim3(kSampleBlocks), dim3(kT), 0, st, x, n, f.S, w.sel);
+  FLC_LAUNCH("sel64_floor", sel64_floor_kernel, dim3(1), dim3(kGT), 0, st, f.on ? f.S : 0, f.r_lo, f.r_hi, w.sel);
+  if (f.on)
+    FLC_LAUNCH("sel64_filter", sel64_filter_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, f.segcap,
+               (const Sel64*)w.sel, w.seg, w.segi, w.counts, w.above);
+  {  // (grid-synchronised: one block per CU, all resident)
+    Coresident co(st, dev);
+    if (co.status()) return co.status();
+    FLC_LAUNCH("sel64_select", sel64_select_kernel, dim3((unsigned)cus), dim3(kGT), 0, st, x, n, (long long)k,
+               f.on ? f.segcap : 0, w.sel, (const unsigned long long*)w.seg, (const unsigned short*)w.segi,
+               (const int*)w.counts, (const int*)w.above, f.on ? nch : 0);
+    const int rc = co.finish();
+    if (rc) return rc;
   }
-  // (the candidate passes need few blocks: each block flushes up to 256 bins with global atomics; the fallback over x
-  // streams with them too)
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 2), kT), 512);
-  // (each pass first resolves the previous pass's digit; the ties kernel resolves the last one)
-  for (int pass = 0; pass < kDigits; ++pass)
-    FLC_LAUNCH("sel64_hist", sel64_hist_kernel, dim3(grid), dim3(kT), 0, st, x, n, pass, w.sel,
-               (const unsigned long long*)w.seg, (const int*)w.counts, nch, f.on ? f.segcap : 1);
-  FLC_LAUNCH("sel64_ties", sel64_ties_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, w.sel, w.counts);
-  FLC_LAUNCH("scan64", scan64_kernel, dim3(1), dim3(1024), 0, st, w.counts, w.offsets, nch);
-  FLC_LAUNCH("sel64_emit", sel64_emit_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, (const Sel64*)w.sel,
-             (const long long*)w.offsets, nch, out);
+  FLC_LAUNCH("sel64_emit", sel64_emit_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, f.on ? f.segcap : 0,
+             (const Sel64*)w.sel, (const unsigned long long*)w.seg, (const unsigned short*)w.segi,
+             (const int*)w.counts, out);
   return FLC_OK;
 }
 

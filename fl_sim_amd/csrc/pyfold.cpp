@@ -10,9 +10,15 @@
 // step fused into the last one — the same fmaf chain as one launch).  Nothing is launched before every tensor of
 // the call has passed its checks.  Errors: TypeError for a tensor the fold does not take (the caller then moves
 // messages or folds per tensor), ValueError for mismatched sizes or counts.
+//
+// `alias(host_tensor, device_index)`: a HIP-device tensor over the same memory as a pinned host tensor, for the host
+// server's zero-copy staging (hoststage.py): pinned host memory is mapped into every device's address space at the
+// same address (checked here with hipPointerGetAttributes before the alias is made), so the fold kernels read and write
+// the server's host tensors in place over PCIe.  The alias keeps the host storage alive.
 #include <Python.h>
 #include <torch/csrc/autograd/python_variable.h>
 #include <c10/hip/HIPStream.h>
+#include <ATen/ATen.h>
 
 #include <vector>
 
@@ -150,10 +156,38 @@ PyObject* model_fold(PyObject*, PyObject* args) {
   return done((Py_INCREF(Py_None), Py_None));
 }
 
+void release_storage(void* ctx) { delete static_cast<c10::Storage*>(ctx); }
+
+// alias(host_tensor, device_index) -> tensor on cuda:device_index over the same bytes (see the header)
+PyObject* alias(PyObject*, PyObject* args) {
+  PyObject* o;
+  int dev;
+  if (!PyArg_ParseTuple(args, "Oi", &o, &dev)) return nullptr;
+  if (!THPVariable_Check(o)) return type_error("alias takes a tensor");
+  const at::Tensor& t = THPVariable_Unpack(o);
+  if (!t.is_cpu() || !t.is_contiguous() || !t.is_pinned()) return type_error("alias takes a contiguous pinned host tensor");
+  void* p = t.data_ptr();
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || a.devicePointer != p) {
+    (void)hipGetLastError();
+    PyErr_SetString(PyExc_RuntimeError, "the pinned buffer is not mapped at its host address on the device");
+    return nullptr;
+  }
+  const size_t nbytes = (size_t)t.numel() * t.element_size();
+  auto* keep = new c10::Storage(t.storage());
+  c10::DataPtr dp(p, keep, &release_storage, c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)dev));
+  c10::Storage st(c10::Storage::use_byte_size_t(), nbytes, std::move(dp), /*allocator=*/nullptr, /*resizable=*/false);
+  at::Tensor d = at::empty({0}, t.options().device(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)dev)).pinned_memory(false));
+  d.set_(st, 0, t.sizes(), t.strides());
+  return THPVariable_Wrap(d);
+}
+
 PyMethodDef kMethods[] = {
     {"model_fold", model_fold, METH_VARARGS,
      "model_fold(dsts, msgs, key, weights, init_mode, beta, theta, v, opt, lr, beta2, tau): flc_model_fold on Python "
      "lists of HIP tensors, launched on the current stream of the model's device"},
+    {"alias", alias, METH_VARARGS,
+     "alias(host_tensor, device_index): a HIP-device tensor over a pinned host tensor's memory (zero-copy)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_flcfold", nullptr, -1, kMethods};

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import collections
 import contextlib
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -69,14 +70,36 @@ def _device_for(msgs: Sequence[Sequence[torch.Tensor]]) -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
+def _zero_copy_alias(host: torch.Tensor, device: torch.device) -> Optional[torch.Tensor]:
+    """A device tensor over the pinned buffer's own memory (``_flcfold.alias``: checked to be mapped at its host
+    address), or None when zero-copy staging is off (``FLC_HOST_ZEROCOPY=0``) or not available."""
+    if os.environ.get("FLC_HOST_ZEROCOPY", "1") == "0":
+        return None
+    global ZERO_COPY_ERROR
+    try:
+        from . import _flcfold as mod
+    except ImportError as e:
+        ZERO_COPY_ERROR = f"ImportError: {e}"
+        return None
+    try:
+        return mod.alias(host, device.index if device.index is not None else torch.cuda.current_device())
+    except (RuntimeError, TypeError) as e:
+        ZERO_COPY_ERROR = f"{type(e).__name__}: {e}"
+        return None
+
+
 class _Mirror:
-    """Adopted groups: one pinned host buffer (the tensors' storage) and one device buffer of the same layout."""
+    """Adopted groups: one pinned host buffer (the tensors' storage), and either a device alias of that buffer
+    (zero-copy: the kernels read and write it in place over PCIe) or a device buffer of the same layout."""
 
     def __init__(self, groups: Sequence[Sequence[torch.Tensor]], device: torch.device):
         self.dtype = groups[0][0].dtype
+        self.device = device
         self.offs, self.ranges, total = _layout(groups)
         self.host = torch.empty(max(total, 1), dtype=self.dtype, pin_memory=True)
-        self.dev = torch.empty(max(total, 1), dtype=self.dtype, device=device)
+        alias = _zero_copy_alias(self.host, device)
+        self.zero_copy = alias is not None
+        self.dev = alias if alias is not None else torch.empty(max(total, 1), dtype=self.dtype, device=device)
         self.shapes = [[tuple(t.shape) for t in g] for g in groups]
         for g, o in zip(groups, self.offs):
             for t, off in zip(g, o):
@@ -107,6 +130,7 @@ def _ptr_key(groups: Sequence[Sequence[torch.Tensor]]) -> tuple:
     return tuple((t.data_ptr(), t.numel()) for g in groups for t in g)
 
 
+ZERO_COPY_ERROR: Optional[str] = None  # why the last alias attempt failed (diagnostics)
 _MIRRORS: "collections.OrderedDict[tuple, _Mirror]" = collections.OrderedDict()
 _STAGING: Dict[Tuple[torch.dtype, int], torch.Tensor] = {}  # (dtype, slot) -> pinned staging buffer
 
@@ -191,12 +215,17 @@ def staged(groups: Sequence[Sequence[torch.Tensor]], read: Sequence[bool], write
     dtype = next(t.dtype for g in groups for t in g)
     m = _lookup([g for g in groups if g])
     if m is not None and all(len(g) for g in groups):
-        device = m.dev.device
+        device = m.device
     else:
         m = None
         device = _device_for(msgs)
     with torch.cuda.device(device):
         stream = torch.cuda.current_stream(device)
+        if m is not None and m.zero_copy:  # adopted, zero-copy: the kernels work on the host buffer itself
+            dmsgs = stage_messages(msgs, device, dtype)
+            yield [m.dev_views(gi) for gi in range(len(groups))], dmsgs
+            stream.synchronize()
+            return
         if m is not None:  # adopted: one copy of the groups' contiguous span, nothing packed on the host
             if all(read):
                 a, b = m.span

@@ -217,12 +217,52 @@ def test_f64_topk_filter_fallbacks():
     for K in (n // 100, 12_345):
         exp, _ = ref.topk(x, K)
         assert g64.same_bits(codec.topk_dense_f64(torch.from_numpy(x).to(DEV), K).cpu().numpy(), exp)
-    S = 32768
+    S = 16384  # f64.hip kSample64
     y = np.full(n, -1.0)
     y[((np.arange(S) + 0.5) * n / S).astype(np.int64)] = 0.0  # the sample positions
+    # n / 2, S + 5: the floor admits fewer than k; S - 5: the band resolves T = 0 among S ties (tie-index threshold)
     for K in (n // 2, S + 5, S - 5):
         exp, _ = ref.topk(y, K)
         assert g64.same_bits(codec.topk_dense_f64(torch.from_numpy(y).to(DEV), K).cpu().numpy(), exp)
+    # the sample's ceiling too low: k + 100 large values, none at a sample position (more than k keys above the band)
+    z = y.copy()
+    free = np.setdiff1d(np.arange(n), ((np.arange(S) + 0.5) * n / S).astype(np.int64))
+    K = 5000
+    z[np.random.default_rng(3).choice(free, K + 100, replace=False)] = 5.0
+    exp, _ = ref.topk(z, K)
+    assert g64.same_bits(codec.topk_dense_f64(torch.from_numpy(z).to(DEV), K).cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("n_ties", [3, 5000, 16384, 16385, 100_000])
+def test_f64_topk_ties_of_the_kth_value(n_ties):
+    """The K-th largest value repeated n_ties times at random positions, k cutting through the ties: the band's bin
+    list resolves the highest-index ties itself up to its capacity (16384 keys of the bin), the fallback beyond."""
+    from fl_sim_amd import codec
+
+    n = 2_000_003
+    g = np.random.default_rng(n_ties)
+    x = g.standard_normal(n) * 1e-3
+    v = np.sort(x)[-20_000]  # the value at rank 20000 from the top
+    pos = g.choice(n, n_ties, replace=False)
+    x[pos] = v
+    above = int((x > v).sum())
+    for K in (above + 1, above + max(1, n_ties // 2), above + n_ties):
+        exp, _ = ref.topk(x, K)
+        assert g64.same_bits(codec.topk_dense_f64(torch.from_numpy(x).to(DEV), K).cpu().numpy(), exp), K
+
+
+def test_f64_topk_full_size_25m():
+    """The headline size of the float64 top-k (BASELINE configs[2]'s 25 M, float64): 1 % and 0.1 % against numpy's
+    argsort (the oracle), on gaussian and heavy-tailed vectors."""
+    from fl_sim_amd import codec
+
+    n = 25_000_000
+    g = np.random.default_rng(25)
+    for x in (g.standard_normal(n) * 1e-3, g.standard_cauchy(n) * 1e-4):
+        xd = torch.from_numpy(x).to(DEV)
+        for K in (n // 100, n // 1000):
+            exp, _ = ref.topk(x, K)
+            assert g64.same_bits(codec.topk_dense_f64(xd, K).cpu().numpy(), exp), K
 
 
 def test_f64_device_tensor_in_device_tensor_out():

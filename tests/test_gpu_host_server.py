@@ -35,6 +35,18 @@ def _msgs_on(msgs, key, where):
     return [{**m, key: [t.to(where) for t in m[key]]} for m in msgs]
 
 
+@pytest.fixture(autouse=True, params=["zero_copy", "copy"])
+def staging_mode(request, monkeypatch):
+    """Every test under both stagings of an adopted server: the kernels on the pinned host buffer itself (zero-copy,
+    the default) and one copy each way through a device buffer (FLC_HOST_ZEROCOPY=0)."""
+    from fl_sim_amd import hoststage
+
+    monkeypatch.setenv("FLC_HOST_ZEROCOPY", "1" if request.param == "zero_copy" else "0")
+    hoststage._MIRRORS.clear()
+    yield request.param
+    hoststage._MIRRORS.clear()
+
+
 class _Cfg:
     def __init__(self, **kw):
         self.__dict__.update(kw)
@@ -264,3 +276,18 @@ def test_host_server_pinned_parameters_behave_as_cpu_tensors():
     s.model.load_state_dict(sd)
     assert np.array_equal(_flat(s.model.parameters()), before)
     assert all(p.is_pinned() for p in s.model.parameters()), "load_state_dict copies in place"
+
+
+def test_host_server_zero_copy_is_taken(staging_mode):
+    """The adopted mirror of a host server works on the pinned buffer in place when zero-copy is on (the device alias
+    shares the host tensors' memory), and keeps a separate device buffer when it is off."""
+    from fl_sim_amd import hoststage
+
+    params = [torch.randn(5, 7), torch.randn(3)]
+    m = hoststage.adopt([params], torch.device("cuda", 0))
+    assert m is not None and m.zero_copy == (staging_mode == "zero_copy"), hoststage.ZERO_COPY_ERROR
+    if m.zero_copy:
+        assert m.dev.is_cuda and m.dev.data_ptr() == m.host.data_ptr() == params[0].data_ptr()
+        m.dev_views(0)[1].fill_(2.5)  # a device-side write lands in the host tensor itself
+        torch.cuda.synchronize()
+        assert torch.equal(params[1], torch.full((3,), 2.5))
