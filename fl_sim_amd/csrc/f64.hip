@@ -15,8 +15,10 @@
 //                                    (lv(s) - lv(s+1)), lower level iff u < p, value lv * sign * norm
 //                                    (compressors.py:339-357, 376-393); 8-bit codes sign << 7 | level
 //   topk_dense                       out = x on the K largest (ties: the highest indices, as the float32 encoder),
-//                                    0 elsewhere (compressors.py:293-296): a radix select over 64-bit order keys,
-//                                    eight 8-bit digit passes, then one counting pass and the dense write
+//                                    0 elsewhere (compressors.py:293-296): a band around the K-th largest key from
+//                                    a sample, one filter pass into per-chunk candidate segments, the exact key
+//                                    from the band's bin, a tiled dense write (below); an exact radix select over
+//                                    x whenever the band misses
 // Uniforms: compat mode takes u[r] for the r-th consumer in index order (the reference's random.random() calls);
 // philox mode the word of the element's own index (the float32 codec's stream).  Every kernel streams its input
 // with 16-B loads (two doubles per load); all are HBM-bound element-wise or counting passes (no MFMA).
@@ -414,20 +416,23 @@ __global__ __launch_bounds__(kT) void quant64_decode_kernel(const uint8_t* __res
 // top-k on fp64 (compressors.py:293-296: out = x.copy(); out[np.argsort(out)[:-K]] = 0): out = x on the K largest,
 // +0 elsewhere; among the ties of the K-th largest, the highest indices are kept (the float32 encoder's rule).
 //
-// Four launches; on the common path x is read once and out written once (the HBM floor: 16 B per element):
-//   sample    one block: S strided keys; their r_lo-th and r_hi-th largest, kept to their top 24 bits, bound a band
-//             [t_lo, t_hi) that holds the K-th largest key with ~4 sigma (+16) of the sample to spare on each side
-//   filter    one block per 8192-element chunk: every key >= t_lo appended to the chunk's segment (the value's bits
-//             and its u16 position), keys >= t_hi counted per chunk (no global atomics: every count a plain store)
-//   select    one block per CU, grid-synchronised: each block bins the band keys of its chunks' segments (2048 bins,
-//             LDS, then global atomics of its nonzero bins: 256 blocks), one grid barrier, the bin holding the K-th
-//             largest is found (every block the same one) and its keys appended to one list; the last block to
-//             finish selects the exact K-th key T among them, counts its ties and, when only some are kept, the index
-//             threshold of the highest-index ones.  When the band fails (the sample missed on either side, a segment
-//             overflowed, the bin held more keys than the list) or is off (n < 64 Ki, k near n), the same blocks run
-//             the exact radix select over x instead: 8 digit passes of the key, up to 8 of the tie index
+// Three launches; on the common path x is read once and out written once (the HBM floor: 16 B per element):
+//   prep      kSampleBlocks blocks: S strided sample keys (order-preserving 64-bit keys); block 0 resets the state
+//   select    one block of 1024 threads per CU, grid-synchronised (block b takes chunks b, b + G, ...):
+//             every block finds, identically, a band [t_lo, t_hi) from the sample's r_lo-th and r_hi-th largest keys
+//             (the K-th largest lies inside it with ~4 sigma (+16) of the sample to spare on each side); then the
+//             filter pass over its 8192-element chunks (8 elements per thread, the next chunk's loads in flight):
+//             every key >= t_lo appended to the chunk's segment (the value's bits and its u16 position), keys
+//             >= t_hi counted, band keys binned into a 2048-bin LDS histogram; the block's nonzero bins go to the
+//             global histogram (memory-side atomics, one block per CU), then ONE grid barrier; every block finds
+//             the bin holding the K-th largest and appends its keys in that bin to one list; block 0 waits for all
+//             appends and selects the exact K-th key T among them (~100 keys: each key's rank by comparison), its
+//             ties and, when only some are kept, the index threshold of the highest-index ones.  When the band
+//             fails (the sample missed on either side, a segment overflowed, the bin held more keys than the
+//             list) or is off (n < 64 Ki, k near n), the same blocks run the exact radix select over x instead:
+//             8 digit passes of the key, up to 8 of the tie index, a grid barrier each
 //   emit      one block per chunk: a 64 KB LDS tile zeroed, the chunk's kept candidates scattered into it, the tile
-//             written out whole (after the fallback: x read again and kept in place)
+//             written out whole with non-temporal 16-B stores (after the fallback: x read again, kept in place)
 // ------------------------------------------------------------------------------------------------
 // order-preserving key of a double: NaN largest, -0 == +0
 __device__ __forceinline__ unsigned long long order_key64(double v) {
@@ -447,24 +452,22 @@ constexpr int kGT = 1024;           // threads of the sample, gather and fallbac
 constexpr int kGNW = kGT / kWave;
 constexpr int kMaxG64 = 1024;       // blocks of the grid-synchronised select (one flag each)
 constexpr int kSampleBlocks = 64;   // blocks loading the sample
+constexpr int kMaxCPB = 2048;       // chunks per select block (more: the band is off, the passes over x run)
 constexpr unsigned long long kOvf = 1ull << 44;  // (n < 2^44)
 static_assert(kBand == 2 * kGT, "gather: two band bins per thread");
 static_assert(kSample64 % kGT == 0 && kBinCap % kGT == 0, "whole keys per thread");
 
 struct Sel64 {
   unsigned long long stamps[32];      // diagnostic builds (FLC_SELECT_STAMPS): phase times, s_memrealtime
-  unsigned long long t_lo, t_hi;      // the band
-  int sh;                             // band bin of a band key: (key - t_lo) >> sh
-  int mode;                           // the sample's: 0 the band is on, 1 off (read-only in the select kernel)
-  int fb;                             // the select's: 1 when T came from the passes over x (the emit reads x again)
+  int fb;                             // 1 when T came from the passes over x (the emit reads x again)
   int err;                            // a grid barrier timed out (lost co-residency)
   unsigned nbin;                      // the bin's list: keys appended
   unsigned long long T;               // the K-th largest key
   long long need, ties;               // ties of T kept / present
   long long ithr;                     // the kept ties: index >= ithr
-  unsigned long long flags[kMaxG64];  // grid barriers (zeroed by the sample kernel: targets 1, 2, ... in each call)
-  unsigned long long pab[kMaxG64];    // per block: keys >= t_hi in its chunks + kOvf per overflowed segment
-  unsigned hist[kBand];               // the band histogram (slice b summed by block b)
+  unsigned long long flags[kMaxG64];  // grid barriers (zeroed by the prep kernel: targets 1, 2, ... in each call)
+  unsigned long long pab[kMaxG64];    // per block: keys >= t_hi in its chunks + kOvf if a segment overflowed
+  unsigned hist[kBand];               // the band histogram
   unsigned fhist[2 * kDigits][256];   // the fallback's digit histograms: key digits, then tie-index digits
   unsigned long long bkey[kBinCap];   // the K-th largest's bin: keys (less the bin's base) and their indices
   long long bidx[kBinCap];
@@ -549,43 +552,52 @@ __device__ __forceinline__ int range_shift64(unsigned long long maxoff, int bits
 }
 
 // The sample's S keys, loaded by kSampleBlocks blocks (scattered loads from one CU wait on its address translation a
-// page at a time)
-__global__ __launch_bounds__(kT) void sel64_sample_kernel(const double* __restrict__ x, int64_t n, int S,
-                                                          Sel64* __restrict__ st) {
+// page at a time); block 0 also resets the state the select kernel accumulates into
+__global__ __launch_bounds__(kT) void sel64_prep_kernel(const double* __restrict__ x, int64_t n, int S,
+                                                        Sel64* __restrict__ st) {
+  const int tid = threadIdx.x;
   STAMP64(blockIdx.x == 0, 0);
-  for (int j = blockIdx.x * kT + threadIdx.x; j < S; j += gridDim.x * kT) {
+  if (blockIdx.x == 0) {
+    for (int i = tid; i < 2 * kDigits * 256; i += kT) (&st->fhist[0][0])[i] = 0u;
+    for (int i = tid; i < kBand; i += kT) st->hist[i] = 0u;
+    for (int i = tid; i < kMaxG64; i += kT) st->flags[i] = 0ull;
+    if (tid == 0) {
+      st->fb = 0;
+      st->err = 0;
+      st->nbin = 0u;
+      st->T = 0ull;
+      st->need = st->ties = st->ithr = 0;
+    }
+  }
+  for (int j = blockIdx.x * kT + tid; j < S; j += gridDim.x * kT) {
     const int64_t pos = (int64_t)(((double)j + 0.5) * (double)n / (double)S);
     st->sample[j] = order_key64(x[pos < n ? pos : n - 1]);
   }
 }
 
-// One block: the state reset, and the band from the sample's r_lo-th and r_hi-th largest keys (r_hi <= 0: no
-// ceiling).  S = 0 (the band off): the reset only.
+// the select kernel's LDS
+struct SelLds {
+  unsigned hb[2][kBand];  // the band's histograms (sample), then the band histogram of the block's chunks (hb[0])
+  unsigned h[2][256];
+  unsigned long long d[kGT];  // the K-th largest's bin list (block 0)
+  long long i[kGT];
+  unsigned long long mm[2][kGNW];
+  long long scan[kGNW], res[3], out[2][3], sel[4];
+  unsigned cn[kMaxCPB];  // the candidates of the block's chunks
+  int ovf;
+};
+
+// The band [t_lo, t_hi) from the sample's r_lo-th and r_hi-th largest keys (r_hi <= 0: no ceiling); every block of
+// the select kernel computes the same one from the same keys.
 //   r_lo <= 1024 (k up to ~6 % of n): B = the smallest thread maximum of the 16 keys each thread holds, so at least
 //   1024 sample keys lie at or above it; one 2048-bin histogram of the keys in [B, max] locates both ranks (few
 //   keys, spread over many bins: no LDS atomic contention), and a bin holding more than 8 keys is refined once inside
 //   it.  The floor is the floor of rank r_lo's bin, the ceiling the end of rank r_hi's bin.
 //   Otherwise: three 8-bit digit passes per rank (the keys' top 24 bits).
-__global__ __launch_bounds__(kGT) void sel64_floor_kernel(int S, long long r_lo, long long r_hi, Sel64* __restrict__ st) {
+__device__ __forceinline__ void sample_band(const Sel64* __restrict__ st, int S, long long r_lo, long long r_hi,
+                                            SelLds& L, unsigned long long& t_lo, unsigned long long& t_hi) {
   constexpr int kPer = kSample64 / kGT;
-  __shared__ unsigned s_h[2][256];
-  __shared__ unsigned s_hb[2][kBand];
-  __shared__ long long s_scan[kGNW], s_res[3], s_out[2][3];
-  __shared__ unsigned long long s_mm[2][kGNW];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
-  STAMP64(true, 1);
-  for (int i = tid; i < 2 * kDigits * 256; i += kGT) (&st->fhist[0][0])[i] = 0u;
-  for (int i = tid; i < kBand; i += kGT) st->hist[i] = 0u;
-  for (int i = tid; i < kMaxG64; i += kGT) st->flags[i] = 0ull;
-  if (tid == 0) {
-    st->mode = S > 0 ? 0 : 1;
-    st->fb = 0;
-    st->err = 0;
-    st->nbin = 0u;
-    st->T = 0ull;
-    st->need = st->ties = st->ithr = 0;
-  }
-  if (S <= 0) return;
   unsigned long long key[kPer];
 #pragma unroll
   for (int i = 0; i < kPer; ++i) {
@@ -593,7 +605,6 @@ __global__ __launch_bounds__(kGT) void sel64_floor_kernel(int S, long long r_lo,
     key[i] = j < S ? st->sample[j] : 0ull;
   }
   const bool hi = r_hi > 0;
-  unsigned long long t_lo, t_hi;
   if (r_lo <= kGT && S == kSample64) {
     unsigned long long m = 0ull;
 #pragma unroll
@@ -606,49 +617,49 @@ __global__ __launch_bounds__(kGT) void sel64_floor_kernel(int S, long long r_lo,
       mx = b > mx ? b : mx;
     }
     if (lane == 0) {
-      s_mm[0][wid] = mn;
-      s_mm[1][wid] = mx;
+      L.mm[0][wid] = mn;
+      L.mm[1][wid] = mx;
     }
-    for (int i = tid; i < 2 * kBand; i += kGT) (&s_hb[0][0])[i] = 0u;
+    for (int i = tid; i < 2 * kBand; i += kGT) (&L.hb[0][0])[i] = 0u;
     __syncthreads();
     unsigned long long B = ~0ull, M = 0ull;
 #pragma unroll
     for (int w = 0; w < kGNW; ++w) {
-      B = s_mm[0][w] < B ? s_mm[0][w] : B;
-      M = s_mm[1][w] > M ? s_mm[1][w] : M;
+      B = L.mm[0][w] < B ? L.mm[0][w] : B;
+      M = L.mm[1][w] > M ? L.mm[1][w] : M;
     }
     const int sh = range_shift64(M - B, 11);
 #pragma unroll
     for (int i = 0; i < kPer; ++i)
-      if (key[i] >= B) atomicAdd(&s_hb[0][(unsigned)((key[i] - B) >> sh)], 1u);
+      if (key[i] >= B) atomicAdd(&L.hb[0][(unsigned)((key[i] - B) >> sh)], 1u);
     __syncthreads();
-    pick_band([&](int j) { return (long long)s_hb[0][j]; }, r_lo, s_scan, s_out[0]);
-    if (hi) pick_band([&](int j) { return (long long)s_hb[0][j]; }, r_hi, s_scan, s_out[1]);
-    unsigned long long lo0 = B + ((unsigned long long)s_out[0][0] << sh);
-    unsigned long long lo1 = hi ? B + ((unsigned long long)s_out[1][0] << sh) : 0ull;
+    pick_band([&](int j) { return (long long)L.hb[0][j]; }, r_lo, L.scan, L.out[0]);
+    if (hi) pick_band([&](int j) { return (long long)L.hb[0][j]; }, r_hi, L.scan, L.out[1]);
+    unsigned long long lo0 = B + ((unsigned long long)L.out[0][0] << sh);
+    unsigned long long lo1 = hi ? B + ((unsigned long long)L.out[1][0] << sh) : 0ull;
     int sh_hi = sh;
-    const bool ref0 = sh > 0 && s_out[0][2] > 8, ref1 = hi && sh > 0 && s_out[1][2] > 8;  // (block-uniform)
+    const bool ref0 = sh > 0 && L.out[0][2] > 8, ref1 = hi && sh > 0 && L.out[1][2] > 8;  // (block-uniform)
     if (ref0 || ref1) {  // one finer pass inside the bins holding more than 8 keys
       const int sh2 = sh > 11 ? sh - 11 : 0;
       const unsigned long long bw = 1ull << sh;
       __syncthreads();
-      for (int i = tid; i < 2 * kBand; i += kGT) (&s_hb[0][0])[i] = 0u;
+      for (int i = tid; i < 2 * kBand; i += kGT) (&L.hb[0][0])[i] = 0u;
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
-        if (ref0 && key[i] >= lo0 && key[i] - lo0 < bw) atomicAdd(&s_hb[0][(unsigned)((key[i] - lo0) >> sh2)], 1u);
-        if (ref1 && key[i] >= lo1 && key[i] - lo1 < bw) atomicAdd(&s_hb[1][(unsigned)((key[i] - lo1) >> sh2)], 1u);
+        if (ref0 && key[i] >= lo0 && key[i] - lo0 < bw) atomicAdd(&L.hb[0][(unsigned)((key[i] - lo0) >> sh2)], 1u);
+        if (ref1 && key[i] >= lo1 && key[i] - lo1 < bw) atomicAdd(&L.hb[1][(unsigned)((key[i] - lo1) >> sh2)], 1u);
       }
       __syncthreads();
-      const long long q0 = s_out[0][1], q1 = s_out[1][1];
+      const long long q0 = L.out[0][1], q1 = L.out[1][1];
       __syncthreads();
       if (ref0) {
-        pick_band([&](int j) { return (long long)s_hb[0][j]; }, q0, s_scan, s_out[0]);
-        lo0 += (unsigned long long)s_out[0][0] << sh2;
+        pick_band([&](int j) { return (long long)L.hb[0][j]; }, q0, L.scan, L.out[0]);
+        lo0 += (unsigned long long)L.out[0][0] << sh2;
       }
       if (ref1) {
-        pick_band([&](int j) { return (long long)s_hb[1][j]; }, q1, s_scan, s_out[1]);
-        lo1 += (unsigned long long)s_out[1][0] << sh2;
+        pick_band([&](int j) { return (long long)L.hb[1][j]; }, q1, L.scan, L.out[1]);
+        lo1 += (unsigned long long)L.out[1][0] << sh2;
         sh_hi = sh2;
       }
     }
@@ -660,8 +671,8 @@ __global__ __launch_bounds__(kGT) void sel64_floor_kernel(int S, long long r_lo,
     long long rlo = r_lo, rhi = r_hi;
     for (int pass = 0; pass < kSampleDigits; ++pass) {
       if (tid < 256) {
-        s_h[0][tid] = 0u;
-        s_h[1][tid] = 0u;
+        L.h[0][tid] = 0u;
+        L.h[1][tid] = 0u;
       }
       __syncthreads();
       const int sh = 56 - 8 * pass;
@@ -669,18 +680,18 @@ __global__ __launch_bounds__(kGT) void sel64_floor_kernel(int S, long long r_lo,
       for (int i = 0; i < kPer; ++i) {
         const bool v = i * kGT + tid < S;
         const unsigned d = (unsigned)(key[i] >> sh) & 255u;
-        hist_add64(s_h[0], d, v && (pass == 0 || (key[i] >> (sh + 8)) == plo));
-        if (hi) hist_add64(s_h[1], d, v && (pass == 0 || (key[i] >> (sh + 8)) == phi));
+        hist_add64(L.h[0], d, v && (pass == 0 || (key[i] >> (sh + 8)) == plo));
+        if (hi) hist_add64(L.h[1], d, v && (pass == 0 || (key[i] >> (sh + 8)) == phi));
       }
       __syncthreads();
-      pick256<kGNW>(tid < 256 ? (long long)s_h[0][255 - tid] : 0ll, rlo, s_scan, s_res);
-      plo = (plo << 8) | (unsigned long long)s_res[0];
-      rlo -= s_res[1];
-      __syncthreads();  // (s_res is rewritten next)
+      pick256<kGNW>(tid < 256 ? (long long)L.h[0][255 - tid] : 0ll, rlo, L.scan, L.res);
+      plo = (plo << 8) | (unsigned long long)L.res[0];
+      rlo -= L.res[1];
+      __syncthreads();  // (res is rewritten next)
       if (hi) {
-        pick256<kGNW>(tid < 256 ? (long long)s_h[1][255 - tid] : 0ll, rhi, s_scan, s_res);
-        phi = (phi << 8) | (unsigned long long)s_res[0];
-        rhi -= s_res[1];
+        pick256<kGNW>(tid < 256 ? (long long)L.h[1][255 - tid] : 0ll, rhi, L.scan, L.res);
+        phi = (phi << 8) | (unsigned long long)L.res[0];
+        rhi -= L.res[1];
         __syncthreads();
       }
     }
@@ -688,68 +699,7 @@ __global__ __launch_bounds__(kGT) void sel64_floor_kernel(int S, long long r_lo,
     t_lo = plo << low;
     t_hi = (!hi || phi == (1ull << (8 * kSampleDigits)) - 1ull) ? ~0ull : (phi + 1ull) << low;
   }
-  if (tid == 0) {
-    st->t_lo = t_lo;
-    st->t_hi = t_hi;
-    st->sh = range_shift64(t_hi - t_lo - 1ull, 11);  // (t_hi > t_lo)
-  }
-  STAMP64(true, 2);
-}
-
-// the candidates (key >= t_lo) of each 8192-element chunk appended to the chunk's own segment (value bits, position);
-// counts[c] = the chunk's candidates (more than the segment holds: the select falls back), above[c] = its keys >= t_hi
-__global__ __launch_bounds__(kT) void sel64_filter_kernel(const double* __restrict__ x, int64_t n, int segcap,
-                                                          const Sel64* __restrict__ st,
-                                                          unsigned long long* __restrict__ seg,
-                                                          unsigned short* __restrict__ segi, int* __restrict__ counts,
-                                                          int* __restrict__ above) {
-  __shared__ unsigned s_n;
-  __shared__ int s_red[kNW];
-  const int tid = threadIdx.x;
-  STAMP64(blockIdx.x == 0, 3);
-  if (tid == 0) s_n = 0u;
-  const unsigned long long t_lo = st->t_lo, t_hi = st->t_hi;
-  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
-  double v[kIt][kE];  // the chunk's 32 elements of this thread, all loads in flight at once
-#pragma unroll
-  for (int it = 0; it < kIt; ++it) {
-    const int64_t e0 = c0 + ((int64_t)it * kT + tid) * kE;
-    if (e0 < n) load4(x, e0, n, v[it]);
-    else
-#pragma unroll
-      for (int j = 0; j < kE; ++j) v[it][j] = 0.0;
-  }
-  __syncthreads();
-  unsigned long long* my = seg + (size_t)blockIdx.x * segcap;
-  unsigned short* myi = segi + (size_t)blockIdx.x * segcap;
-  int ab = 0;
-#pragma unroll
-  for (int it = 0; it < kIt; ++it) {
-#pragma unroll
-    for (int j = 0; j < kE; ++j) {
-      const int loc = (it * kT + tid) * kE + j;
-      const unsigned long long key = order_key64(v[it][j]);
-      const bool in = c0 + loc < n && key >= t_lo;
-      const unsigned long long m = __ballot(in);
-      if (m == 0ull) continue;
-      const unsigned p = wave_append(&s_n, in, m);
-      if (in) {
-        if (p < (unsigned)segcap) {
-          my[p] = (unsigned long long)__double_as_longlong(v[it][j]);
-          myi[p] = (unsigned short)loc;
-        }
-        ab += key >= t_hi ? 1 : 0;
-      }
-    }
-  }
-  ab = block_sum<int, kNW>(ab, s_red);  // (a barrier: s_n final)
-  if (tid == 0) {
-    counts[blockIdx.x] = (int)s_n;
-    above[blockIdx.x] = ab;
-  }
-#ifdef FLC_SELECT_STAMPS
-  if (tid == 0 && blockIdx.x == 0) const_cast<Sel64*>(st)->stamps[4] = __builtin_amdgcn_s_memrealtime();
-#endif
+  __syncthreads();  // (L is reused by the caller)
 }
 
 // block-wide radix select of the rem-th largest among the cnt values v[q] (slot q * kGT + tid, values < 2^bits;
@@ -850,52 +800,117 @@ __device__ __forceinline__ void grid_sync64(Sel64* st, unsigned long long target
   __syncthreads();
 }
 
-// T, its ties and the tie-index threshold: from the band when it holds the K-th largest (block b's chunks are
-// b * 16 + w, + G * 16, ... for its waves w: one wave per chunk; three grid barriers, block 0 selects T from the
-// bin's list), else from the passes over x
-__global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restrict__ x, int64_t n, long long k,
-                                                           int segcap, Sel64* __restrict__ st,
-                                                           const unsigned long long* __restrict__ seg,
-                                                           const unsigned short* __restrict__ segi,
-                                                           const int* __restrict__ counts,
-                                                           const int* __restrict__ above, int64_t nch) {
+// The select, one block per CU (grid-synchronised; block b takes chunks b, b + G, ...):
+//   1. the band from the sample (every block the same);
+//   2. the filter pass: each chunk's 8192 elements (8 per thread, the next chunk's loads in flight while this one is
+//      processed), every key >= t_lo appended to the chunk's segment, the keys above the band counted and the band
+//      keys binned (LDS);
+//   3. the block's nonzero bins added to the global histogram, its above / overflow count published; a grid barrier;
+//   4. the bin of the K-th largest (every block the same), its keys appended to one list, block 0 waits for every
+//      block's appends and selects T among them;
+// else (the band off or failed) the exact radix select over x.
+__global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restrict__ x, int64_t n, long long k, int S,
+                                                           long long r_lo, long long r_hi, int segcap,
+                                                           Sel64* __restrict__ st, unsigned long long* __restrict__ seg,
+                                                           unsigned short* __restrict__ segi, int* __restrict__ counts,
+                                                           int64_t nch) {
   constexpr int kPer = kBinCap / kGT;
-  __shared__ unsigned s_hb[kBand];
-  __shared__ unsigned s_h[256];
-  __shared__ long long s_scan[kGNW], s_res[3], s_bin[3];
-  __shared__ unsigned long long s_ab;
-  __shared__ unsigned long long s_d[kGT];
-  __shared__ long long s_i[kGT], s_sel[4];
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
+  constexpr int kR = kChunk / (2 * kGT);  // 16-B loads per thread per chunk (4)
+  __shared__ SelLds L;
+  unsigned* const s_h = L.h[0];
+  long long* const s_scan = L.scan;
+  long long* const s_res = L.res;
+  long long* const s_bin = L.out[0];
+  unsigned long long* const s_d = L.d;
+  long long* const s_i = L.i;
+  long long* const s_sel = L.sel;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int G = (int)gridDim.x;
   unsigned long long target = 0ull;
   STAMP64(blockIdx.x == 0, 5);
-  bool band = st->mode == 0;
+  bool band = S > 0;
   if (band) {
-    // 1. this block's band histogram, keys above the band and overflows, from its chunks' segments
-    for (int i = tid; i < kBand; i += kGT) s_hb[i] = 0u;
-    if (tid == 0) s_ab = 0ull;
+    // 1. the band
+    unsigned long long t_lo, t_hi;
+    sample_band(st, S, r_lo, r_hi, L, t_lo, t_hi);
+    const int sh = range_shift64(t_hi - t_lo - 1ull, 11);  // (t_hi > t_lo)
+    STAMP64(blockIdx.x == 0, 6);
+    // 2. the filter pass over the block's chunks: chunk q of the block (ch = b + q G) appends through its own LDS
+    //    counter, so the waves never wait for each other; three register sets rotate (the loop unrolled three
+    //    times, no copies), two chunks' loads in flight while one is processed (a fourth set spills)
+    for (int i = tid; i < kBand; i += kGT) L.hb[0][i] = 0u;
+    for (int i = tid; i < kMaxCPB; i += kGT) L.cn[i] = 0u;
+    if (tid == 0) L.ovf = 0;
     __syncthreads();
-    const unsigned long long t_lo = st->t_lo, t_hi = st->t_hi;
-    const int sh = st->sh;
-    for (int64_t ch = (int64_t)blockIdx.x * kGNW + wid; ch < nch; ch += (int64_t)G * kGNW) {
-      const int c = counts[ch];
-      const unsigned long long* sc = seg + (size_t)ch * segcap;
-      for (int i = lane; i < min(c, segcap); i += kWave) {
-        const unsigned long long key = order_key64(__longlong_as_double((long long)sc[i]));
-        if (key < t_hi) atomicAdd(&s_hb[(unsigned)((key - t_lo) >> sh)], 1u);  // (key >= t_lo: a candidate)
+    unsigned long long above = 0ull;
+    auto load_chunk = [&](int64_t ch, double2 (&v)[kR]) {
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int64_t e = ch * kChunk + 2 * ((int64_t)r * kGT + tid);
+        if (ch < nch && e + 2 <= n) {
+          v[r] = *reinterpret_cast<const double2*>(x + e);
+        } else {
+          v[r].x = ch < nch && e < n ? x[e] : 0.0;
+          v[r].y = 0.0;
+        }
       }
-      if (lane == 0) atomicAdd(&s_ab, (unsigned long long)above[ch] + (c > segcap ? kOvf : 0ull));
+    };
+    auto chunk_work = [&](int64_t ch, int q, const double2 (&cv)[kR]) {
+      unsigned long long* my = seg + (size_t)ch * segcap;
+      unsigned short* myi = segi + (size_t)ch * segcap;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const double v = j ? cv[r].y : cv[r].x;
+          const int loc = 2 * (r * kGT + tid) + j;
+          const unsigned long long key = order_key64(v);
+          const bool in = ch * kChunk + loc < n && key >= t_lo;
+          const unsigned long long m = __ballot(in);
+          if (m == 0ull) continue;
+          const unsigned p = wave_append(&L.cn[q], in, m);
+          if (in) {
+            if (p < (unsigned)segcap) {
+              my[p] = (unsigned long long)__double_as_longlong(v);
+              myi[p] = (unsigned short)loc;
+            }
+            if (key >= t_hi) ++above;
+            else atomicAdd(&L.hb[0][(unsigned)((key - t_lo) >> sh)], 1u);
+          }
+        }
+      }
+    };
+    {
+      double2 va[kR], vb[kR], vc[kR];
+      const int64_t c0 = blockIdx.x;
+      load_chunk(c0, va);
+      load_chunk(c0 + G, vb);
+      for (int q = 0; c0 + (int64_t)q * G < nch; q += 3) {
+        const int64_t ch = c0 + (int64_t)q * G;
+        load_chunk(ch + 2 * G, vc);
+        chunk_work(ch, q, va);
+        if (ch + G >= nch) break;
+        load_chunk(ch + 3 * G, va);
+        chunk_work(ch + G, q + 1, vb);
+        if (ch + 2 * G >= nch) break;
+        load_chunk(ch + 4 * G, vb);
+        chunk_work(ch + 2 * G, q + 2, vc);
+      }
     }
     __syncthreads();
-    // 2. the block's nonzero bins added to the global histogram (zeroed by the floor kernel), its count of keys above
-    //    the band and overflows published; one grid barrier
+    for (int q = tid; blockIdx.x + (int64_t)q * G < nch; q += kGT) {
+      counts[blockIdx.x + (int64_t)q * G] = (int)L.cn[q];
+      if (L.cn[q] > (unsigned)segcap) L.ovf = 1;  // (benign race: every writer stores 1)
+    }
+    __syncthreads();
+    // 3. the block's band histogram into the global one, its above / overflow count published; one grid barrier
+    above = block_sum<unsigned long long, kGNW>(above, reinterpret_cast<unsigned long long*>(s_scan));
     for (int i = tid; i < kBand; i += kGT)
-      if (s_hb[i]) atomicAdd(&st->hist[i], s_hb[i]);
-    if (tid == 0) st_sc1(&st->pab[blockIdx.x], s_ab);
-    STAMP64(blockIdx.x == 0, 6);
-    grid_sync64(st, ++target);
+      if (L.hb[0][i]) atomicAdd(&st->hist[i], L.hb[0][i]);
+    if (tid == 0) st_sc1(&st->pab[blockIdx.x], above + (L.ovf ? kOvf : 0ull));
     STAMP64(blockIdx.x == 0, 7);
+    grid_sync64(st, ++target);
+    STAMP64(blockIdx.x == 0, 8);
     // 3. the bin of the K-th largest (every block the same)
     unsigned long long ab = 0ull;
     for (int s = tid; s < G; s += kGT) ab += ld_sc1(&st->pab[s]);
@@ -910,8 +925,8 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
     if (band) {
       // 4. the bin's keys to the list; the last block selects T among them
       const unsigned long long lo_b = t_lo + ((unsigned long long)bin << sh), wb = 1ull << sh;
-      for (int64_t ch = (int64_t)blockIdx.x * kGNW + wid; ch < nch; ch += (int64_t)G * kGNW) {
-        const int c = counts[ch];
+      for (int64_t ch = blockIdx.x + (int64_t)G * (tid >> 6); ch < nch; ch += (int64_t)G * kGNW) {
+        const int c = counts[ch];  // (this block's own chunks: written by it above, in its XCD's L2)
         const unsigned long long* sc = seg + (size_t)ch * segcap;
         const unsigned short* si = segi + (size_t)ch * segcap;
         for (int i0 = 0; i0 < c; i0 += kWave) {  // (wave-uniform bounds)
@@ -1169,7 +1184,6 @@ struct Ws64 {
   Sel64* sel;
   unsigned long long* seg;  // top-k candidate segments: [chunks][segcap] value bits
   unsigned short* segi;     //   ... and positions in the chunk
-  int* above;               // top-k: keys above the band per chunk
   size_t need;
 };
 Ws64 carve64(void* ws, size_t bytes, int64_t n, int64_t k = 0) {
@@ -1183,7 +1197,6 @@ Ws64 carve64(void* ws, size_t bytes, int64_t n, int64_t k = 0) {
   const Filt64 f = filt64(n, k);
   w.seg = c.take<unsigned long long>(f.on ? (size_t)nch * f.segcap : 0);
   w.segi = c.take<unsigned short>(f.on ? (size_t)nch * f.segcap : 0);
-  w.above = c.take<int>(f.on ? (size_t)nch : 0);
   w.need = c.off;
   return w;
 }
@@ -1316,20 +1329,17 @@ int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void*
   if (!ws || w.need > ws_bytes) return fail(FLC_EWORKSPACE, "flc_topk_dense_f64: workspace %zu < %zu", ws_bytes, w.need);
   hipStream_t st = as_stream(stream);
   const int64_t nch = cdiv(n, kChunk);
-  const Filt64 f = filt64(n, k);
+  Filt64 f = filt64(n, k);
   int dev = 0;
   const int cus = std::min(stream_cus(st, &dev), kMaxG64);
-  if (f.on) FLC_LAUNCH("sel64_sample", sel64_sample_kernel, dim3(kSampleBlocks), dim3(kT), 0, st, x, n, f.S, w.sel);
-  FLC_LAUNCH("sel64_floor", sel64_floor_kernel, dim3(1), dim3(kGT), 0, st, f.on ? f.S : 0, f.r_lo, f.r_hi, w.sel);
-  if (f.on)
-    FLC_LAUNCH("sel64_filter", sel64_filter_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, f.segcap,
-               (const Sel64*)w.sel, w.seg, w.segi, w.counts, w.above);
+  if (cdiv(nch, cus) > kMaxCPB) f.on = false;  // (more chunks per block than its LDS counters: the exact passes)
+  FLC_LAUNCH("sel64_prep", sel64_prep_kernel, dim3(f.on ? (unsigned)kSampleBlocks : 1u), dim3(kT), 0, st, x, n,
+             f.on ? f.S : 0, w.sel);
   {  // (grid-synchronised: one block per CU, all resident)
     Coresident co(st, dev);
     if (co.status()) return co.status();
     FLC_LAUNCH("sel64_select", sel64_select_kernel, dim3((unsigned)cus), dim3(kGT), 0, st, x, n, (long long)k,
-               f.on ? f.segcap : 0, w.sel, (const unsigned long long*)w.seg, (const unsigned short*)w.segi,
-               (const int*)w.counts, (const int*)w.above, f.on ? nch : 0);
+               f.on ? f.S : 0, f.r_lo, f.r_hi, f.on ? f.segcap : 0, w.sel, w.seg, w.segi, w.counts, f.on ? nch : 0);
     const int rc = co.finish();
     if (rc) return rc;
   }

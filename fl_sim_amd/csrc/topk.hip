@@ -6,26 +6,30 @@
 // highest indices are kept (stable ascending argsort order; the reference's own argsort is unstable,
 // so any tie choice satisfies it — see DESIGN.md).
 //
-// Three launches; block b of the filter and of the select owns the element range [b M, (b + 1) M):
+// Two launches (the default, "fused" path); block b of the encode owns the element range [b M, (b + 1) M):
 //   sample   32 K strided keys of x (order-preserving uint32 keys).
-//   filter   one block of 1024 threads per CU.  Every block derives, identically, from the sample a
-//            candidate floor t_lo (count(key >= t_lo) ~ k + 4 sigma: ~1.27 k candidates at k/n = 1 %)
-//            and a likely ceiling t_hi of the k-th largest key; then the one HBM pass over its range
-//            (4 B/element): 16 waves stream 16 K-element block steps (4 float4 per lane, the next step
-//            in flight), one float compare per element, ballot/mbcnt compaction, the step's 16 wave
-//            counts exchanged through LDS so that the block's candidates land in index order in LDS;
-//            candidates in [t_lo, t_hi) are binned into a 2048-bin LDS histogram on the fly.  At the
-//            end the candidates go to the block's staging slot (<= 16 K; beyond, only counted) and the
-//            histogram, above-the-band count, max key and candidate count are added to global
-//            memory (memory-side atomics).  The kernel boundary is the grid-wide hand-off.
-//   select   one block of 1024 threads per CU, its own register budget: the summed histogram picks
-//            the bin holding the k-th largest key; every block publishes its candidates inside that
-//            bin (~3 each at the headline) and its count above it; after ONE exchange every block
-//            resolves the exact k-th largest key T among those keys and its own output offset
-//            locally, then writes its slice of the kept entries in index order: idx[k] + val[k] or
-//            idx[k] + codes[k] with the dithering fused.  Rare paths (a list overflow, a re-range,
-//            a floor that admitted fewer than k elements — then every block reads its x range
-//            directly) fall back to histogram rounds, each one exchange.
+//   encode   one block of 1024 threads per CU (topk_select_kernel<STACKED, FUSED = true>), in two phases:
+//     filter phase (filter_phase): every block derives, identically, from the sample a candidate floor t_lo
+//            (count(key >= t_lo) ~ k + 4 sigma: ~1.27 k candidates at k/n = 1 %) and a likely ceiling t_hi of the
+//            k-th largest key; then the one HBM pass over its range (4 B/element): 16 waves stream 16 K-element
+//            block steps (4 float4 per lane, the next step in flight), one float compare per element,
+//            ballot/mbcnt compaction, the step's 16 wave counts exchanged through LDS so that the block's
+//            candidates land in index order in LDS (past its 16 K LDS slots, in an HBM overflow area);
+//            candidates in [t_lo, t_hi) are binned into a 2048-bin LDS histogram on the fly.  At the end the
+//            histogram, above-the-band count, max key and candidate count are added to global memory
+//            (memory-side atomics), followed by ONE grid exchange.
+//     select phase: the summed histogram picks the bin holding the k-th largest key; every block publishes its
+//            candidates inside that bin (~3 each at the headline) and its count above it; after one more exchange
+//            every block resolves the exact k-th largest key T among those keys and its own output offset
+//            locally, then writes its slice of the kept entries in index order from LDS: idx[k] + val[k] or
+//            idx[k] + codes[k] with the dithering fused, and the tile pointers.  Rare paths (a list overflow, a
+//            re-range, a floor that admitted fewer than k elements — then every block reads its x range directly)
+//            fall back to histogram rounds, each one exchange.
+// Calibration builds keep the earlier split form (FLC_TOPK_SPLIT=1: a separate filter kernel staging the
+// candidates through HBM, the kernel boundary as the hand-off); FLC_PAIR=1 turns on the paired filter pass (blocks
+// 2j and 2j + 1 stream their joint range from both ends and claim the middle steps at run time; bit-identical,
+// measured no faster: DESIGN.md §8).  The batched encoders (flc_stacked_encode_batch*) run one fused select per
+// client on its share of the CUs, in one launch.
 // An exchange: the block drains its stores/atomics, raises its own flag to the exchange's epoch
 // (call * 32 + phase, from a call counter in the workspace), one wave polls all flags.  The histograms
 // are zeroed by the select at the end of each call; the workspace is zero-initialised once by its
@@ -2179,6 +2183,49 @@ BatchGeom batch_geometry(int64_t n, int64_t k, int n_clients, int cus, size_t ex
   return b;
 }
 
+// Pinned staging of the host-built tables (batch entries, delta pointer tables): a ring of slots per device, each
+// reused only after the copy out of it has completed (an event per slot; with kRing slots the wait is for a call
+// kRing calls back).  A copy from pageable memory goes through the runtime's own staging and can hold the host
+// until the device reaches it.
+constexpr int kRing = 32;
+struct TableRing {
+  std::mutex mu;
+  char* buf[kRing] = {};
+  size_t cap[kRing] = {};
+  hipEvent_t ev[kRing] = {};
+  bool pending[kRing] = {};
+  int next = 0;
+};
+TableRing& table_ring(int dev) {
+  static TableRing rings[64];
+  return rings[dev < 0 || dev >= 64 ? 0 : dev];
+}
+// copy `bytes` from `src` to the device address `dst`, stream-ordered on `st` (of device `dev`), through a pinned slot
+int copy_table(int dev, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  TableRing& r = table_ring(dev);
+  std::lock_guard<std::mutex> lk(r.mu);
+  const int s = r.next;
+  r.next = (s + 1) % kRing;
+  if (r.pending[s]) {
+    FLC_CHECK_HIP(hipEventSynchronize(r.ev[s]));
+    r.pending[s] = false;
+  }
+  if (r.cap[s] < bytes) {
+    if (r.buf[s]) FLC_CHECK_HIP(hipHostFree(r.buf[s]));
+    r.buf[s] = nullptr;
+    r.cap[s] = 0;
+    const size_t cap = std::max<size_t>(align_up(bytes, 4096), 16384);
+    FLC_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.buf[s]), cap, hipHostMallocDefault));
+    r.cap[s] = cap;
+  }
+  if (!r.ev[s]) FLC_CHECK_HIP(hipEventCreateWithFlags(&r.ev[s], hipEventDisableTiming));
+  std::memcpy(r.buf[s], src, bytes);
+  FLC_CHECK_HIP(hipMemcpyAsync(dst, r.buf[s], bytes, hipMemcpyHostToDevice, st));
+  FLC_CHECK_HIP(hipEventRecord(r.ev[s], st));
+  r.pending[s] = true;
+  return FLC_OK;
+}
+
 // host: the entries, then `extra` (already holding device addresses inside the workspace), in one copy
 template <class Src, bool STACKED = true>
 int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, const std::vector<char>& extra, int64_t n,
@@ -2194,7 +2241,7 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
   std::vector<char> host(bg.extra_off - bg.table_off + extra.size(), 0);
   std::memcpy(host.data(), ents.data(), ents.size() * sizeof(BatchEntry));
   if (!extra.empty()) std::memcpy(host.data() + (bg.extra_off - bg.table_off), extra.data(), extra.size());
-  FLC_CHECK_HIP(hipMemcpyAsync(tab, host.data(), host.size(), hipMemcpyHostToDevice, st));
+  if (const int rc = copy_table(dev, tab, host.data(), host.size(), st)) return rc;
   // each call starts its headers from zero (state, flags, histograms; one launch): no history is carried between
   // calls, so the header / staging split may move with the client count
   static_assert(kOffBlk % 16 == 0 && kOffStage % 16 == 0, "16-B zeroing of the headers");
@@ -2321,7 +2368,9 @@ int flc_stacked_encode_delta(const float* const* local, const float* const* glob
   std::memcpy(host.data() + off.size() * 8 + (size_t)n_tensors * 8, global, (size_t)n_tensors * 8);
   char* tab = static_cast<char*>(ws) + enc;
   hipStream_t st = as_stream(stream);
-  FLC_CHECK_HIP(hipMemcpyAsync(tab, host.data(), host.size(), hipMemcpyHostToDevice, st));
+  int dev = 0;
+  (void)stream_cus(st, &dev);
+  if (const int rc = copy_table(dev, tab, host.data(), host.size(), st)) return rc;
   DeltaSrc src;
   src.t.off = reinterpret_cast<const long long*>(tab);
   src.t.lp = reinterpret_cast<const float* const*>(tab + off.size() * 8);

@@ -40,6 +40,9 @@ SHORT = {
     "quant_encode_kernel": "quant_encode",
     "quant_decode_kernel": "quant_decode",
     "weighted_sum_kernel": "weighted_sum",
+    "sel64_select_kernel": "sel64_select",
+    "sel64_emit_kernel": "sel64_emit",
+    "sel64_prep_kernel": "sel64_prep",
 }
 
 
