@@ -431,8 +431,9 @@ __global__ __launch_bounds__(kT) void quant64_decode_kernel(const uint8_t* __res
 //             fails (the sample missed on either side, a segment overflowed, the bin held more keys than the
 //             list) or is off (n < 64 Ki, k near n), the same blocks run the exact radix select over x instead:
 //             8 digit passes of the key, up to 8 of the tie index, a grid barrier each
-//   emit      one block per chunk: a 64 KB LDS tile zeroed, the chunk's kept candidates scattered into it, the tile
-//             written out whole with non-temporal 16-B stores (after the fallback: x read again, kept in place)
+//   emit      one 64-lane wave per 1024-element piece: an 8 KB LDS tile zeroed, the piece's kept candidates
+//             scattered into it, the tile written out whole with non-temporal 16-B stores (after the fallback: x read
+//             again, kept in place)
 // ------------------------------------------------------------------------------------------------
 // order-preserving key of a double: NaN largest, -0 == +0
 __device__ __forceinline__ unsigned long long order_key64(double v) {
@@ -534,14 +535,15 @@ __device__ __forceinline__ void pick_band(H h, long long r, long long* s_scan, l
   const long long ha = h(kBand - 1 - 2 * tid), hb = h(kBand - 2 - 2 * tid);
   if (tid == 0) s_out[0] = -1;
   long long tot;
-  const long long ex = block_excl_scan<long long, kGNW>(ha + hb, s_scan, &tot);  // (barriers: s_out[0] set)
+  // (LDS-only barriers: global loads the caller has in flight stay in flight)
+  const long long ex = block_excl_scan_lds<long long, kGNW>(ha + hb, s_scan, &tot);  // (barriers: s_out[0] set)
   if (r >= 1 && ex < r && ex + ha + hb >= r) {
     const bool first = ex + ha >= r;
     s_out[0] = first ? kBand - 1 - 2 * tid : kBand - 2 - 2 * tid;
     s_out[1] = first ? r - ex : r - ex - ha;
     s_out[2] = first ? ha : hb;
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // the shift that maps key offsets 0 .. maxoff onto at most 2^bits bins
@@ -621,7 +623,7 @@ __device__ __forceinline__ void sample_band(const Sel64* __restrict__ st, int S,
       L.mm[1][wid] = mx;
     }
     for (int i = tid; i < 2 * kBand; i += kGT) (&L.hb[0][0])[i] = 0u;
-    __syncthreads();
+    lds_barrier();
     unsigned long long B = ~0ull, M = 0ull;
 #pragma unroll
     for (int w = 0; w < kGNW; ++w) {
@@ -632,7 +634,7 @@ __device__ __forceinline__ void sample_band(const Sel64* __restrict__ st, int S,
 #pragma unroll
     for (int i = 0; i < kPer; ++i)
       if (key[i] >= B) atomicAdd(&L.hb[0][(unsigned)((key[i] - B) >> sh)], 1u);
-    __syncthreads();
+    lds_barrier();
     pick_band([&](int j) { return (long long)L.hb[0][j]; }, r_lo, L.scan, L.out[0]);
     if (hi) pick_band([&](int j) { return (long long)L.hb[0][j]; }, r_hi, L.scan, L.out[1]);
     unsigned long long lo0 = B + ((unsigned long long)L.out[0][0] << sh);
@@ -642,17 +644,17 @@ __device__ __forceinline__ void sample_band(const Sel64* __restrict__ st, int S,
     if (ref0 || ref1) {  // one finer pass inside the bins holding more than 8 keys
       const int sh2 = sh > 11 ? sh - 11 : 0;
       const unsigned long long bw = 1ull << sh;
-      __syncthreads();
+      lds_barrier();
       for (int i = tid; i < 2 * kBand; i += kGT) (&L.hb[0][0])[i] = 0u;
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
         if (ref0 && key[i] >= lo0 && key[i] - lo0 < bw) atomicAdd(&L.hb[0][(unsigned)((key[i] - lo0) >> sh2)], 1u);
         if (ref1 && key[i] >= lo1 && key[i] - lo1 < bw) atomicAdd(&L.hb[1][(unsigned)((key[i] - lo1) >> sh2)], 1u);
       }
-      __syncthreads();
+      lds_barrier();
       const long long q0 = L.out[0][1], q1 = L.out[1][1];
-      __syncthreads();
+      lds_barrier();
       if (ref0) {
         pick_band([&](int j) { return (long long)L.hb[0][j]; }, q0, L.scan, L.out[0]);
         lo0 += (unsigned long long)L.out[0][0] << sh2;
@@ -699,7 +701,7 @@ __device__ __forceinline__ void sample_band(const Sel64* __restrict__ st, int S,
     t_lo = plo << low;
     t_hi = (!hi || phi == (1ull << (8 * kSampleDigits)) - 1ull) ? ~0ull : (phi + 1ull) << low;
   }
-  __syncthreads();  // (L is reused by the caller)
+  lds_barrier();  // (L is reused by the caller)
 }
 
 // block-wide radix select of the rem-th largest among the cnt values v[q] (slot q * kGT + tid, values < 2^bits;
@@ -830,19 +832,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
   STAMP64(blockIdx.x == 0, 5);
   bool band = S > 0;
   if (band) {
-    // 1. the band
-    unsigned long long t_lo, t_hi;
-    sample_band(st, S, r_lo, r_hi, L, t_lo, t_hi);
-    const int sh = range_shift64(t_hi - t_lo - 1ull, 11);  // (t_hi > t_lo)
-    STAMP64(blockIdx.x == 0, 6);
-    // 2. the filter pass over the block's chunks: chunk q of the block (ch = b + q G) appends through its own LDS
-    //    counter, so the waves never wait for each other; three register sets rotate (the loop unrolled three
-    //    times, no copies), two chunks' loads in flight while one is processed (a fourth set spills)
-    for (int i = tid; i < kBand; i += kGT) L.hb[0][i] = 0u;
-    for (int i = tid; i < kMaxCPB; i += kGT) L.cn[i] = 0u;
-    if (tid == 0) L.ovf = 0;
-    __syncthreads();
-    unsigned long long above = 0ull;
+    // 1. the band (the block's first chunk already streaming: its loads do not depend on it)
     auto load_chunk = [&](int64_t ch, double2 (&v)[kR]) {
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
@@ -855,6 +845,22 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
         }
       }
     };
+    double2 va[kR], vb[kR], vc[kR];
+    const int64_t c0 = blockIdx.x;
+    load_chunk(c0, va);  // (a second chunk held across the band's keys would spill)
+    unsigned long long t_lo, t_hi;
+    sample_band(st, S, r_lo, r_hi, L, t_lo, t_hi);
+    load_chunk(c0 + G, vb);
+    const int sh = range_shift64(t_hi - t_lo - 1ull, 11);  // (t_hi > t_lo)
+    STAMP64(blockIdx.x == 0, 6);
+    // 2. the filter pass over the block's chunks: chunk q of the block (ch = b + q G) appends through its own LDS
+    //    counter, so the waves never wait for each other; three register sets rotate (the loop unrolled three
+    //    times, no copies), two chunks' loads in flight while one is processed (a fourth set spills)
+    for (int i = tid; i < kBand; i += kGT) L.hb[0][i] = 0u;
+    for (int i = tid; i < kMaxCPB; i += kGT) L.cn[i] = 0u;
+    if (tid == 0) L.ovf = 0;
+    lds_barrier();
+    unsigned long long above = 0ull;
     auto chunk_work = [&](int64_t ch, int q, const double2 (&cv)[kR]) {
       unsigned long long* my = seg + (size_t)ch * segcap;
       unsigned short* myi = segi + (size_t)ch * segcap;
@@ -881,10 +887,6 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
       }
     };
     {
-      double2 va[kR], vb[kR], vc[kR];
-      const int64_t c0 = blockIdx.x;
-      load_chunk(c0, va);
-      load_chunk(c0 + G, vb);
       for (int q = 0; c0 + (int64_t)q * G < nch; q += 3) {
         const int64_t ch = c0 + (int64_t)q * G;
         load_chunk(ch + 2 * G, vc);
@@ -1058,59 +1060,66 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
   }
 }
 
-// dense write: keep key > T, and the ties of T at index >= ithr
-__global__ __launch_bounds__(kT) void sel64_emit_kernel(const double* __restrict__ x, int64_t n, int segcap,
-                                                        const Sel64* __restrict__ st,
-                                                        const unsigned long long* __restrict__ seg,
-                                                        const unsigned short* __restrict__ segi,
-                                                        const int* __restrict__ counts, double* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) unsigned long long s_tile[kChunk];  // 64 KB
-  const int tid = threadIdx.x;
+// dense write: keep key > T, and the ties of T at index >= ithr.  One 64-lane wave per 1024-element piece (8 KB of
+// output: the write shape of the float32 decode, whose short one-wave workgroups write fastest), eight per chunk:
+// a zeroed LDS tile, the chunk's candidates of this piece scattered into it (each wave scans the chunk's ~100-entry
+// segment), the tile written with non-temporal 16-B stores — the 200 MB of output are written through, not left in
+// the memory-side cache for the next call's filter pass to evict (measured: 131 -> 107-109 us per 25 M call).
+constexpr int kPiece = 1024;
+constexpr int kPieces = kChunk / kPiece;
+__global__ __launch_bounds__(kWave) void sel64_emit_kernel(const double* __restrict__ x, int64_t n, int segcap,
+                                                           const Sel64* __restrict__ st,
+                                                           const unsigned long long* __restrict__ seg,
+                                                           const unsigned short* __restrict__ segi,
+                                                           const int* __restrict__ counts, double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) unsigned long long s_tile[kPiece];  // 8 KB
+  const int lane = threadIdx.x;
   const unsigned long long T = st->T;
   const long long ithr = st->ithr;
-  const int64_t c0 = (int64_t)blockIdx.x * kChunk;
+  const int64_t p = blockIdx.x, c = p / kPieces;
+  const int sub = (int)(p - c * kPieces);
+  const int64_t e0 = p * kPiece;
 #ifdef FLC_SELECT_STAMPS
-  if (tid == 0 && blockIdx.x == 0) const_cast<Sel64*>(st)->stamps[14] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && blockIdx.x == 0) const_cast<Sel64*>(st)->stamps[14] = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (!st->fb) {  // the chunk's candidates (all of them in its segment) scattered into a zeroed tile
+  if (!st->fb) {  // the piece's candidates (all of them in its chunk's segment) scattered into a zeroed tile
     u64x2* t2 = reinterpret_cast<u64x2*>(s_tile);
-    for (int i = tid; i < kChunk / 2; i += kT) t2[i] = u64x2{0ull, 0ull};
-    __syncthreads();
-    const int cc = counts[blockIdx.x];
-    const unsigned long long* sc = seg + (size_t)blockIdx.x * segcap;
-    const unsigned short* si = segi + (size_t)blockIdx.x * segcap;
-    for (int i = tid; i < cc; i += kT) {
-      const unsigned long long b = sc[i];
+#pragma unroll
+    for (int u = 0; u < kPiece / 2 / kWave; ++u) t2[lane + u * kWave] = u64x2{0ull, 0ull};
+    const int cc = counts[c];
+    const unsigned long long* sc = seg + (size_t)c * segcap;
+    const unsigned short* si = segi + (size_t)c * segcap;
+    for (int i = lane; i < cc; i += kWave) {
       const int loc = si[i];
+      const unsigned long long b = sc[i];
       const unsigned long long key = order_key64(__longlong_as_double((long long)b));
-      if (key > T || (key == T && c0 + loc >= ithr)) s_tile[loc] = b;
+      if ((loc / kPiece) == sub && (key > T || (key == T && c * kChunk + loc >= ithr))) s_tile[loc % kPiece] = b;
     }
-    __syncthreads();
-    double2* o2 = reinterpret_cast<double2*>(out + c0);
-    for (int i = tid; i < kChunk / 2; i += kT) {
-      const int64_t e = c0 + 2 * i;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < kPiece / 2 / kWave; ++u) {
+      const int q = lane + u * kWave;
+      const int64_t e = e0 + 2 * q;
       if (e + 2 <= n) {
-        const u64x2 b = t2[i];
-        // (non-temporal: the 200 MB of output are written through, not left in the memory-side cache for the next
-        // call's filter pass to evict — measured 131 -> 107 us per 25 M call)
-        __builtin_nontemporal_store(b, reinterpret_cast<u64x2*>(o2) + i);  // (one 16-B store)
+        __builtin_nontemporal_store(t2[q], reinterpret_cast<u64x2*>(out + e));  // (one 16-B store)
       } else if (e < n) {
-        out[e] = __longlong_as_double((long long)s_tile[2 * i]);
+        out[e] = __longlong_as_double((long long)s_tile[2 * q]);
       }
     }
     return;
   }
-  for (int it = 0; it < kIt; ++it) {
-    const int64_t e0 = c0 + ((int64_t)it * kT + tid) * kE;
-    if (e0 >= n) break;
-    double v[kE];
-    load4(x, e0, n, v);
+  for (int u = 0; u < kPiece / 2 / kWave; ++u) {  // (after the fallback: x read again, kept in place)
+    const int64_t e = e0 + 2 * (lane + u * kWave);
+    if (e >= n) break;
+    double v[2] = {x[e], e + 1 < n ? x[e + 1] : 0.0};
 #pragma unroll
-    for (int j = 0; j < kE; ++j) {
+    for (int j = 0; j < 2; ++j) {
       const unsigned long long key = order_key64(v[j]);
-      v[j] = (key > T || (key == T && e0 + j >= ithr)) ? v[j] : 0.0;
+      v[j] = (key > T || (key == T && e + j >= ithr)) ? v[j] : 0.0;
     }
-    store4(out, e0, n, v);
+    out[e] = v[0];
+    if (e + 1 < n) out[e + 1] = v[1];
   }
 }
 
@@ -1343,7 +1352,8 @@ int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void*
     const int rc = co.finish();
     if (rc) return rc;
   }
-  FLC_LAUNCH("sel64_emit", sel64_emit_kernel, dim3((unsigned)nch), dim3(kT), 0, st, x, n, f.on ? f.segcap : 0,
+  FLC_LAUNCH("sel64_emit", sel64_emit_kernel, dim3((unsigned)cdiv(n, kPiece)), dim3(kWave), 0, st, x, n,
+             f.on ? f.segcap : 0,
              (const Sel64*)w.sel, (const unsigned long long*)w.seg, (const unsigned short*)w.segi,
              (const int*)w.counts, out);
   return FLC_OK;

@@ -66,7 +66,8 @@ constexpr int kHistStride = kHistBins + 64;   // bins, [kHistBins] above-the-ran
 constexpr int kMaxSlots = 12;                 // histogram rounds per call (normal + fallback pass)
 constexpr int kEpochStride = 32;              // exchanges per call < 32
 constexpr int kMaxBlocks = 1024;              // <= kET (per-block words are read one per thread)
-constexpr int kInbin = 32;                    // in-bin keys a block may publish (more: histogram rounds)
+constexpr int kInbin = 32;                    // in-bin keys a block may publish (more: histogram rounds) ...
+constexpr int kInbinMax = 256;                //   ... or up to kInbinAll / blocks when a select has few blocks
 constexpr int kInbinAll = 1024;               // in-bin keys of all blocks resolved locally
 constexpr int kTile = FLC_TILE;               // outputs per tile of the CSR tile pointers
 constexpr int kTileLog = 10;
@@ -166,7 +167,11 @@ SampleSetup sample_setup(int64_t n, int64_t k, int s_max = kSample) {
   s.S = (int)(n < s_max ? n : s_max);
   const double m = (double)s.S * (double)k / (double)n;
   s.rank_lo = (long long)ceil(m + 4.0 * sqrt(m) + 16.0);
-  const double rh = floor(m - 4.0 * sqrt(m) - 16.0);
+  // the ceiling: 4 sigma + 16 below m, or (small m: a batched client's 4 K-key sample at k = 1 % has m = 41) just
+  // 4 sigma — without a ceiling the band reaches the top of the key range and its bins are too coarse for the in-bin
+  // lists (histogram rounds follow); a ceiling that admits k keys or more only costs those rounds
+  double rh = floor(m - 4.0 * sqrt(m) - 16.0);
+  if (rh < 1.0) rh = floor(m - 4.0 * sqrt(m));
   s.rank_hi = rh >= 1.0 ? (long long)rh : 0;
   s.take_all = (s.rank_lo >= s.S) ? 1 : 0;
   if (s.take_all) s.rank_lo = s.S;
@@ -1076,13 +1081,29 @@ __device__ __forceinline__ DeltaSrc batch_src(const DeltaSrc& proto, const Batch
   return d;
 }
 
-// batched: `per` blocks sample each client into its own header
+// batched: `per` blocks sample each client into its own header (and zero the client's header for its select: the
+// state, the flags of its nb blocks, the histograms and accumulators — the `per` blocks of a client each take a
+// slice; the sample keys lie past kOffBlk)
 template <class Src>
 __global__ __launch_bounds__(256) void topk_sample_batch_kernel(Src proto, const BatchEntry* __restrict__ tab,
                                                                 int64_t n, int S, EncWs w, int per) {
-  const int g = (int)blockIdx.x / per;
+  const int g = (int)blockIdx.x / per, sub = (int)blockIdx.x - g * per;
   w.base += (size_t)g * kOffStage;
-  sample_one(batch_src(proto, tab[g]), n, S, w, ((int)blockIdx.x - g * per) * 256 + (int)threadIdx.x);
+  {
+    constexpr int kW0 = (int)(kOffFlags / 16), kWH = (int)(kOffHist / 16), kWE = (int)(kOffBlk / 16);
+    const int wf = (int)((size_t)w.nb * kFlagStride * 4 + 15) / 16;  // the select's flags
+    const int nz = kW0 + wf + (kWE - kWH);
+    uint4* p = reinterpret_cast<uint4*>(w.base);
+    for (int i = sub * 256 + (int)threadIdx.x; i < nz; i += per * 256) {
+      const int q = i < kW0 + wf ? i : kWH + (i - kW0 - wf);
+      if (q == 0 && g == 0) {  // header 0: the call counter only — its error word (errp) stays sticky
+        reinterpret_cast<unsigned long long*>(p)[0] = 0ull;
+        continue;
+      }
+      p[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  sample_one(batch_src(proto, tab[g]), n, S, w, sub * 256 + (int)threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1582,12 +1603,15 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     // among those keys and forms its own prefix locally: no second histogram round and no separate
     // count exchange.  Falls through to the histogram rounds if any list overflows.
     __shared__ unsigned s_nl;
-    __shared__ unsigned s_mykey[kInbin], s_mywv[kInbin];
+    __shared__ unsigned s_mykey[kInbinMax], s_mywv[kInbinMax];
     if (tid == 0) s_nl = 0u;
     __syncthreads();
     const unsigned lo0 = cur.lo;
     const unsigned long long wd0 = cur.width;
-    unsigned* my_list = w.inbin() + (size_t)w.bid * kInbin;
+    // a block's list slots: 32, or more when the select has few blocks (a batched client's 2-4: its in-bin keys per
+    // block are many more, and the gathered list still holds kInbinAll)
+    const unsigned cap = (unsigned)max(kInbin, min(kInbinMax, kInbinAll / max(w.nb, 1)));
+    unsigned* my_list = w.inbin() + (size_t)w.bid * cap;
     // scanned in the compaction's wave ranges: the count above the bin per wave range plus the wave of
     // each of my in-bin keys give the compaction its per-wave strict / tie counts once T is known
     unsigned gtw = 0;
@@ -1603,7 +1627,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
         if (lane == 0) base_l = atomicAdd(&s_nl, (unsigned)__popcll(bm));
         base_l = (unsigned)__builtin_amdgcn_readlane((int)base_l, 0);
         const unsigned q = base_l + __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u));
-        if (f && q < (unsigned)kInbin) {  // write-through: read by other XCDs after the exchange
+        if (f && q < cap) {  // write-through: read by other XCDs after the exchange
           __hip_atomic_store(my_list + q, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           s_mykey[q] = key;
           s_mywv[q] = (unsigned)wid;
@@ -1656,7 +1680,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     __shared__ unsigned s_nb[kMaxBlocks];
     __shared__ unsigned s_ovf, s_nall;
     constexpr int kLW = 8;  // list words per thread per batch (G <= 256: one batch)
-    const int words = w.nb * kInbin;
+    const int words = w.nb * (int)cap;
     unsigned long long meta = 0;
     unsigned lw[kLW];
     if (tid < w.nb) meta = ld_mem64(&w.blk_cnt()[tid]);
@@ -1673,7 +1697,7 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
       s_nb[tid] = nb;
       my_gt = meta & 0xffffffffull;
       pre_gt = tid < w.bid ? my_gt : 0ull;
-      if (nb > (unsigned)kInbin) atomicOr(&s_ovf, 1u);
+      if (nb > cap) atomicOr(&s_ovf, 1u);
     }
     __syncthreads();
     if (s_ovf == 0u) {
@@ -1688,8 +1712,8 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
 #pragma unroll
         for (int i = 0; i < kLW; ++i) {
           const int j = c0 + i * kET + tid;
-          const int bb = j / kInbin;
-          const bool v = j < words && (unsigned)(j % kInbin) < s_nb[bb < w.nb ? bb : 0];
+          const int bb = j / (int)cap;
+          const bool v = j < words && (unsigned)(j % (int)cap) < s_nb[bb < w.nb ? bb : 0];
           const unsigned long long bm = __ballot(v);
           if (bm) {
             unsigned base_l = 0;
@@ -2242,11 +2266,15 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
   std::memcpy(host.data(), ents.data(), ents.size() * sizeof(BatchEntry));
   if (!extra.empty()) std::memcpy(host.data() + (bg.extra_off - bg.table_off), extra.data(), extra.size());
   if (const int rc = copy_table(dev, tab, host.data(), host.size(), st)) return rc;
-  // each call starts its headers from zero (state, flags, histograms; one launch): no history is carried between
-  // calls, so the header / staging split may move with the client count
-  static_assert(kOffBlk % 16 == 0 && kOffStage % 16 == 0, "16-B zeroing of the headers");
-  FLC_LAUNCH("zero_headers", zero_headers_kernel, dim3(8, (unsigned)bg.chunk), dim3(256), 0, st, base,
-             (int)(kOffBlk / 16));
+  // each call starts its headers from zero (state, flags, histograms): no history is carried between calls, so the
+  // header / staging split may move with the client count
+  const SampleSetup ss = sample_setup(n, k, batch_sample_cap(n));
+  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
+  static_assert(kOffBlk % 16 == 0 && kOffStage % 16 == 0 && kOffFlags % 16 == 0 && kOffHist % 16 == 0,
+                "16-B zeroing of the headers");
+  if (ss.take_all)  // (otherwise every chunk's sample launch zeroes its clients' headers)
+    FLC_LAUNCH("zero_headers", zero_headers_kernel, dim3(8, (unsigned)bg.chunk), dim3(256), 0, st, base,
+               (int)(kOffBlk / 16));
   EncWs w;
   w.base = base;
   w.var = base + (size_t)bg.chunk * kOffStage;
@@ -2258,8 +2286,6 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
   w.vstride = bg.vstride;
   w.pair_r = 0;  // (batched selects keep static ranges: a client's few blocks)
   w.errp = reinterpret_cast<unsigned long long*>(base + kOffSt + offsetof(EncState, err));
-  const SampleSetup ss = sample_setup(n, k, batch_sample_cap(n));
-  const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   Coresident co(st, dev);
   if (co.status()) return co.status();
   for (int c0 = 0; c0 < C; c0 += bg.chunk) {

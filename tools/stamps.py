@@ -26,13 +26,17 @@ if os.environ.get("DELTA"):  # f1: the delta-fused encode over 64 tensors (local
     glo = [torch.randn(s, device="cuda", generator=gen) for s in sizes]
     loc = [gl + xp for gl, xp in zip(glo, torch.split(x, sizes))]
     encode = lambda it: codec.stacked_encode_delta(loc, glo, k, 127, seed=1, counter=it)
+elif os.environ.get("BATCH"):  # the batched encode of 100 clients x 1 M: client 0's header (block 0 of client 0)
+    gen = torch.Generator(device="cuda").manual_seed(seed + 2)
+    xs = [torch.randn(1_000_000, device="cuda", generator=gen) * 1e-3 for _ in range(int(os.environ["BATCH"]))]
+    encode = lambda it: codec.stacked_encode_batch(xs, 10_000, 127, seeds=list(range(len(xs))), counter=it)  # noqa: E731
 else:
     encode = lambda it: codec.stacked_encode(x, k, 127, 1, it)
 names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "decide", "write+tiles"]
 for it in range(int(os.environ.get("ITERS", "12"))):
     encode(it)
     torch.cuda.synchronize()
-    ws = [t for key, t in codec._WS.items() if key[2] == "topk"][0]
+    ws = [t for key, t in codec._WS.items() if key[2] == ("topk_batch" if os.environ.get("BATCH") else "topk")][0]
     st = ws[STAMP_OFF:STAMP_OFF + 16 * 8].cpu().numpy().view(np.uint64).astype(np.int64)
     if it < 2:
         continue
