@@ -2188,8 +2188,8 @@ struct BatchGeom {
   size_t table_off, extra_off, need;
 };
 
-// keys per client of a batched call's sample: n / 128 rounded down to a power of two, within [4096, kSample]
-// (a 1 M-element client samples 8 K keys; 25 M and more the full 32 K)
+// keys per client of a batched call's sample: n / 256 rounded down to a power of two, within [4096, kSample]
+// (a 1 M-element client samples 4 K keys; 8 M and more the full 32 K)
 int batch_sample_cap(int64_t n) {
   int s = 4096;
   while (s < kSample && (int64_t)s * 2 * 128 <= n) s *= 2;
