@@ -431,9 +431,9 @@ __global__ __launch_bounds__(kT) void quant64_decode_kernel(const uint8_t* __res
 //             fails (the sample missed on either side, a segment overflowed, the bin held more keys than the
 //             list) or is off (n < 64 Ki, k near n), the same blocks run the exact radix select over x instead:
 //             8 digit passes of the key, up to 8 of the tie index, a grid barrier each
-//   emit      one 64-lane wave per 1024-element piece: an 8 KB LDS tile zeroed, the piece's kept candidates
-//             scattered into it, the tile written out whole with non-temporal 16-B stores (after the fallback: x read
-//             again, kept in place)
+//   emit      one 64-lane wave per 256-element piece: a 2 KB LDS tile zeroed, the piece's kept candidates
+//             scattered into it, the tile written out whole with non-temporal 16-B stores (after the fallback, or
+//             with long segments: x read again, kept in place)
 // ------------------------------------------------------------------------------------------------
 // order-preserving key of a double: NaN largest, -0 == +0
 __device__ __forceinline__ unsigned long long order_key64(double v) {
@@ -460,6 +460,9 @@ static_assert(kSample64 % kGT == 0 && kBinCap % kGT == 0, "whole keys per thread
 
 struct Sel64 {
   unsigned long long stamps[32];      // diagnostic builds (FLC_SELECT_STAMPS): phase times, s_memrealtime
+#ifdef FLC_SELECT_STAMPS
+  unsigned long long bstamps[2][kMaxG64];  // per block: filter pass done, histogram flushed
+#endif
   int fb;                             // 1 when T came from the passes over x (the emit reads x again)
   int err;                            // a grid barrier timed out (lost co-residency)
   unsigned nbin;                      // the bin's list: keys appended
@@ -476,6 +479,7 @@ struct Sel64 {
 };
 
 #ifdef FLC_SELECT_STAMPS  // (tools/stamps64.py)
+static_assert(offsetof(Sel64, bstamps) == 256, "tools/stamps64.py reads the per-block stamps at this offset");
 #define STAMP64(cond, i)                                                                      \
   do {                                                                                        \
     if ((cond) && threadIdx.x == 0) const_cast<Sel64*>(st)->stamps[i] = __builtin_amdgcn_s_memrealtime(); \
@@ -546,6 +550,27 @@ __device__ __forceinline__ void pick_band(H h, long long r, long long* s_scan, l
   lds_barrier();
 }
 
+// pick_band for two ranks of one histogram (r < 1: none), one scan: results in s_out[0] and s_out[1]
+template <class H>
+__device__ __forceinline__ void pick_band2(H h, long long r0, long long r1, long long* s_scan, long long (*s_out)[3]) {
+  const int tid = threadIdx.x;
+  const long long ha = h(kBand - 1 - 2 * tid), hb = h(kBand - 2 - 2 * tid);
+  if (tid == 0) s_out[0][0] = s_out[1][0] = -1;
+  long long tot;
+  const long long ex = block_excl_scan_lds<long long, kGNW>(ha + hb, s_scan, &tot);  // (barriers: s_out[.][0] set)
+  auto put = [&](long long r, long long* o) {
+    if (r >= 1 && ex < r && ex + ha + hb >= r) {
+      const bool first = ex + ha >= r;
+      o[0] = first ? kBand - 1 - 2 * tid : kBand - 2 - 2 * tid;
+      o[1] = first ? r - ex : r - ex - ha;
+      o[2] = first ? ha : hb;
+    }
+  };
+  put(r0, s_out[0]);
+  put(r1, s_out[1]);
+  lds_barrier();
+}
+
 // the shift that maps key offsets 0 .. maxoff onto at most 2^bits bins
 __device__ __forceinline__ int range_shift64(unsigned long long maxoff, int bits) {
   if (maxoff == 0ull) return 0;
@@ -596,16 +621,19 @@ struct SelLds {
 //   keys, spread over many bins: no LDS atomic contention), and a bin holding more than 8 keys is refined once inside
 //   it.  The floor is the floor of rank r_lo's bin, the ceiling the end of rank r_hi's bin.
 //   Otherwise: three 8-bit digit passes per rank (the keys' top 24 bits).
-__device__ __forceinline__ void sample_band(const Sel64* __restrict__ st, int S, long long r_lo, long long r_hi,
-                                            SelLds& L, unsigned long long& t_lo, unsigned long long& t_hi) {
-  constexpr int kPer = kSample64 / kGT;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
-  unsigned long long key[kPer];
+constexpr int kSPer = kSample64 / kGT;  // sample keys per thread
+__device__ __forceinline__ void sample_keys(const Sel64* __restrict__ st, int S, unsigned long long (&key)[kSPer]) {
 #pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const int j = i * kGT + tid;
+  for (int i = 0; i < kSPer; ++i) {
+    const int j = i * kGT + (int)threadIdx.x;
     key[i] = j < S ? st->sample[j] : 0ull;
   }
+}
+__device__ __forceinline__ void sample_band(const Sel64* st, const unsigned long long (&key)[kSPer], int S,
+                                            long long r_lo, long long r_hi, SelLds& L, unsigned long long& t_lo,
+                                            unsigned long long& t_hi) {
+  constexpr int kPer = kSPer;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   const bool hi = r_hi > 0;
   if (r_lo <= kGT && S == kSample64) {
     unsigned long long m = 0ull;
@@ -624,6 +652,7 @@ __device__ __forceinline__ void sample_band(const Sel64* __restrict__ st, int S,
     }
     for (int i = tid; i < 2 * kBand; i += kGT) (&L.hb[0][0])[i] = 0u;
     lds_barrier();
+    STAMP64(blockIdx.x == 0, 16);
     unsigned long long B = ~0ull, M = 0ull;
 #pragma unroll
     for (int w = 0; w < kGNW; ++w) {
@@ -635,11 +664,12 @@ __device__ __forceinline__ void sample_band(const Sel64* __restrict__ st, int S,
     for (int i = 0; i < kPer; ++i)
       if (key[i] >= B) atomicAdd(&L.hb[0][(unsigned)((key[i] - B) >> sh)], 1u);
     lds_barrier();
-    pick_band([&](int j) { return (long long)L.hb[0][j]; }, r_lo, L.scan, L.out[0]);
-    if (hi) pick_band([&](int j) { return (long long)L.hb[0][j]; }, r_hi, L.scan, L.out[1]);
+    STAMP64(blockIdx.x == 0, 17);
+    pick_band2([&](int j) { return (long long)L.hb[0][j]; }, r_lo, hi ? r_hi : 0ll, L.scan, L.out);
     unsigned long long lo0 = B + ((unsigned long long)L.out[0][0] << sh);
     unsigned long long lo1 = hi ? B + ((unsigned long long)L.out[1][0] << sh) : 0ull;
     int sh_hi = sh;
+    STAMP64(blockIdx.x == 0, 18);
     const bool ref0 = sh > 0 && L.out[0][2] > 8, ref1 = hi && sh > 0 && L.out[1][2] > 8;  // (block-uniform)
     if (ref0 || ref1) {  // one finer pass inside the bins holding more than 8 keys
       const int sh2 = sh > 11 ? sh - 11 : 0;
@@ -732,24 +762,33 @@ __device__ __forceinline__ unsigned long long block_select(const unsigned long l
 }
 
 // The K-th largest among a short list of cnt <= blockDim.x keys (s_d: offsets in the bin, s_i: their indices, in
-// LDS), rank rem0 from the top: each key's rank by comparing it with all others (a broadcast LDS read per step).
-// Returns T's offset dt, its rank among its ties (rem), their number, and the index threshold of the kept ties.
+// LDS), rank rem0 from the top: each key's rank by comparing it with all others, P threads per key (P * cnt <= 1024,
+// each comparing a P-th of the list; their counts summed across the P adjacent lanes).  Returns T's offset dt, its rank
+// among its ties (rem), their number, and the index threshold of the kept ties.
 __device__ __forceinline__ void rank_small(const unsigned long long* s_d, const long long* s_i, int cnt, long long rem0,
                                            long long* s_sel, unsigned long long& dt, long long& rem, long long& ties,
                                            long long& ithr) {
   const int tid = threadIdx.x;
-  if (tid < cnt) {
-    const unsigned long long my = s_d[tid];
-    long long gt = 0, eq = 0;
-    for (int j = 0; j < cnt; ++j) {
-      gt += s_d[j] > my ? 1 : 0;
-      eq += s_d[j] == my ? 1 : 0;
+  int P = 1;  // (uniform; a power of two <= 64, so a key's threads are adjacent lanes of one wave)
+  while (P < kWave && 2 * P * cnt <= kGT) P *= 2;
+  const int q = tid / P, part = tid & (P - 1);
+  const unsigned long long my = q < cnt ? s_d[q] : 0ull;
+  int gt = 0, eq = 0;
+  if (q < cnt) {
+    for (int j = part; j < cnt; j += P) {
+      const unsigned long long o = s_d[j];
+      gt += o > my ? 1 : 0;
+      eq += o == my ? 1 : 0;
     }
-    if (gt < rem0 && rem0 <= gt + eq) {  // (every copy of T writes the same values)
-      s_sel[0] = (long long)my;
-      s_sel[1] = rem0 - gt;
-      s_sel[2] = eq;
-    }
+  }
+  for (int o = 1; o < P; o <<= 1) {
+    gt += __shfl_xor(gt, o);
+    eq += __shfl_xor(eq, o);
+  }
+  if (q < cnt && part == 0 && gt < rem0 && rem0 <= gt + eq) {  // (every copy of T writes the same values)
+    s_sel[0] = (long long)my;
+    s_sel[1] = rem0 - gt;
+    s_sel[2] = eq;
   }
   __syncthreads();
   dt = (unsigned long long)s_sel[0];
@@ -757,12 +796,14 @@ __device__ __forceinline__ void rank_small(const unsigned long long* s_d, const 
   ties = s_sel[2];
   ithr = 0;
   if (rem < ties) {  // keep the rem ties with the highest indices: the one with rem - 1 tie indices above it
-    if (tid < cnt && s_d[tid] == dt) {
-      const long long ix = s_i[tid];
-      long long gi = 0;
-      for (int j = 0; j < cnt; ++j) gi += (s_d[j] == dt && s_i[j] > ix) ? 1 : 0;
-      if (gi == rem - 1) s_sel[3] = ix;
+    const bool tie = q < cnt && my == dt;
+    const long long ix = tie ? s_i[q] : 0ll;
+    int gi = 0;
+    if (tie) {
+      for (int j = part; j < cnt; j += P) gi += (s_d[j] == dt && s_i[j] > ix) ? 1 : 0;
     }
+    for (int o = 1; o < P; o <<= 1) gi += __shfl_xor(gi, o);
+    if (tie && part == 0 && gi == rem - 1) s_sel[3] = ix;
     __syncthreads();
     ithr = s_sel[3];
   }
@@ -833,23 +874,32 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
   bool band = S > 0;
   if (band) {
     // 1. the band (the block's first chunk already streaming: its loads do not depend on it)
+    // Branch-free loads: every chunk is four 16-B loads per thread, the pairs past the end clamped onto the last
+    // aligned pair (their elements are masked by index, an odd n's last element taken from xlast).  A load under a
+    // branch leaves the compiler unsure how many loads follow an earlier one, and it then waits for all of them:
+    // with the tail's branch, every chunk's processing waited for the loads of the next one too.
+    // (The chunk's base is uniform and the lane's offset 32-bit: few registers, so the three sets fit unspilled.)
+    const int64_t nl2 = (n & ~1ll) - 2;  // (n >= 64 Ki here)
+    const double xlast = x[n - 1];
     auto load_chunk = [&](int64_t ch, double2 (&v)[kR]) {
+      // (a chunk past the end loads chunk 0, never processed; the last chunk's pairs past nl2 load the pair at nl2)
+      const int64_t cb = ch < nch ? min(ch * kChunk, nl2) : 0;
+      const unsigned lim = (unsigned)min<int64_t>(kChunk - 2, nl2 - cb);
+      const double* xb = x + cb;
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
-        const int64_t e = ch * kChunk + 2 * ((int64_t)r * kGT + tid);
-        if (ch < nch && e + 2 <= n) {
-          v[r] = *reinterpret_cast<const double2*>(x + e);
-        } else {
-          v[r].x = ch < nch && e < n ? x[e] : 0.0;
-          v[r].y = 0.0;
-        }
+        const unsigned o = 2u * (unsigned)(r * kGT + tid);
+        v[r] = *reinterpret_cast<const double2*>(xb + (o <= lim ? o : lim));
       }
     };
     double2 va[kR], vb[kR], vc[kR];
     const int64_t c0 = blockIdx.x;
+    // (the sample's keys are loaded first: loads complete in order, so keys issued behind the chunk would wait for it)
+    unsigned long long skey[kSPer];
+    sample_keys(st, S, skey);
     load_chunk(c0, va);  // (a second chunk held across the band's keys would spill)
     unsigned long long t_lo, t_hi;
-    sample_band(st, S, r_lo, r_hi, L, t_lo, t_hi);
+    sample_band(st, skey, S, r_lo, r_hi, L, t_lo, t_hi);
     load_chunk(c0 + G, vb);
     const int sh = range_shift64(t_hi - t_lo - 1ull, 11);  // (t_hi > t_lo)
     STAMP64(blockIdx.x == 0, 6);
@@ -860,18 +910,19 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
     for (int i = tid; i < kMaxCPB; i += kGT) L.cn[i] = 0u;
     if (tid == 0) L.ovf = 0;
     lds_barrier();
-    unsigned long long above = 0ull;
+    unsigned above = 0u;  // (at most 8 per chunk)
     auto chunk_work = [&](int64_t ch, int q, const double2 (&cv)[kR]) {
       unsigned long long* my = seg + (size_t)ch * segcap;
       unsigned short* myi = segi + (size_t)ch * segcap;
+      const int rem = (int)min<int64_t>(n - ch * kChunk, kChunk + 1);  // (the chunk's elements; uniform)
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const double v = j ? cv[r].y : cv[r].x;
           const int loc = 2 * (r * kGT + tid) + j;
+          const double v = loc == rem - 1 ? xlast : j ? cv[r].y : cv[r].x;
           const unsigned long long key = order_key64(v);
-          const bool in = ch * kChunk + loc < n && key >= t_lo;
+          const bool in = loc < rem && key >= t_lo;
           const unsigned long long m = __ballot(in);
           if (m == 0ull) continue;
           const unsigned p = wave_append(&L.cn[q], in, m);
@@ -900,17 +951,24 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
       }
     }
     __syncthreads();
+#ifdef FLC_SELECT_STAMPS
+    if (tid == 0) const_cast<Sel64*>(st)->bstamps[0][blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int q = tid; blockIdx.x + (int64_t)q * G < nch; q += kGT) {
       counts[blockIdx.x + (int64_t)q * G] = (int)L.cn[q];
       if (L.cn[q] > (unsigned)segcap) L.ovf = 1;  // (benign race: every writer stores 1)
     }
     __syncthreads();
     // 3. the block's band histogram into the global one, its above / overflow count published; one grid barrier
-    above = block_sum<unsigned long long, kGNW>(above, reinterpret_cast<unsigned long long*>(s_scan));
+    const unsigned long long ab_blk =
+        block_sum<unsigned long long, kGNW>((unsigned long long)above, reinterpret_cast<unsigned long long*>(s_scan));
     for (int i = tid; i < kBand; i += kGT)
       if (L.hb[0][i]) atomicAdd(&st->hist[i], L.hb[0][i]);
-    if (tid == 0) st_sc1(&st->pab[blockIdx.x], above + (L.ovf ? kOvf : 0ull));
+    if (tid == 0) st_sc1(&st->pab[blockIdx.x], ab_blk + (L.ovf ? kOvf : 0ull));
     STAMP64(blockIdx.x == 0, 7);
+#ifdef FLC_SELECT_STAMPS
+    if (tid == 0) const_cast<Sel64*>(st)->bstamps[1][blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
     grid_sync64(st, ++target);
     STAMP64(blockIdx.x == 0, 8);
     // 3. the bin of the K-th largest (every block the same)
@@ -961,6 +1019,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
           s_i[tid] = ld_sc1(&st->bidx[tid]);
         }
         __syncthreads();
+        STAMP64(true, 15);
         rank_small(s_d, s_i, (int)cnt, rem0, s_sel, dt, rem, ties, ithr);
       } else {  // a radix select over the list (up to kBinCap keys)
         unsigned long long d[kPer];
@@ -1060,12 +1119,22 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
   }
 }
 
-// dense write: keep key > T, and the ties of T at index >= ithr.  One 64-lane wave per 1024-element piece (8 KB of
-// output: the write shape of the float32 decode, whose short one-wave workgroups write fastest), eight per chunk:
-// a zeroed LDS tile, the chunk's candidates of this piece scattered into it (each wave scans the chunk's ~100-entry
-// segment), the tile written with non-temporal 16-B stores — the 200 MB of output are written through, not left in
-// the memory-side cache for the next call's filter pass to evict (measured: 131 -> 107-109 us per 25 M call).
-constexpr int kPiece = 1024;
+// dense write: keep key > T, and the ties of T at index >= ithr.  One 64-lane wave per 256-element piece (2 KB of
+// output), 32 per chunk: a zeroed LDS tile, the chunk's candidates of this piece scattered into it (each wave scans
+// the chunk's ~150-entry segment, its first 64 entries loaded with the state: one round trip before the stores), the
+// tile written with non-temporal 16-B stores — the 200 MB of output are written through, not left in the
+// memory-side cache for the next call's filter pass to evict (measured: 131 -> 107-109 us per 25 M call).  The wave
+// is short so that many are in flight: pieces of 1024 / 512 / 256 / 128 elements took 41 / ~35 / 29.6 / ~47 us at
+// 25 M, k = 1 % (the 128-element pieces rescan the segment 64 times).  Segments longer than kEmitSegMax (k above
+// ~4.5 % of n) would be rescanned as often: x is read again instead (12 % of n: 165 us against 217 us).
+#ifndef FLC_EMIT_PIECE
+#define FLC_EMIT_PIECE 256
+#endif
+constexpr int kPiece = FLC_EMIT_PIECE;
+#ifndef FLC_EMIT_SEG_MAX
+#define FLC_EMIT_SEG_MAX 1024
+#endif
+constexpr int kEmitSegMax = FLC_EMIT_SEG_MAX;
 constexpr int kPieces = kChunk / kPiece;
 __global__ __launch_bounds__(kWave) void sel64_emit_kernel(const double* __restrict__ x, int64_t n, int segcap,
                                                            const Sel64* __restrict__ st,
@@ -1082,19 +1151,26 @@ __global__ __launch_bounds__(kWave) void sel64_emit_kernel(const double* __restr
 #ifdef FLC_SELECT_STAMPS
   if (lane == 0 && blockIdx.x == 0) const_cast<Sel64*>(st)->stamps[14] = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (!st->fb) {  // the piece's candidates (all of them in its chunk's segment) scattered into a zeroed tile
+  // (the chunk's count and first 64 segment entries are loaded with the state, not after it: one round trip)
+  const unsigned long long* sc = seg + (size_t)c * segcap;
+  const unsigned short* si = segi + (size_t)c * segcap;
+  int cc = 0, loc0 = 0;
+  unsigned long long b0 = 0ull;
+  if (segcap > 0) {  // (the band on: every chunk's count written by the select, its segment allocated)
+    cc = counts[c];
+    b0 = sc[lane];
+    loc0 = si[lane];
+  }
+  if (segcap > 0 && !st->fb) {  // the piece's candidates (all in its chunk's segment) scattered into a zeroed tile
     u64x2* t2 = reinterpret_cast<u64x2*>(s_tile);
 #pragma unroll
     for (int u = 0; u < kPiece / 2 / kWave; ++u) t2[lane + u * kWave] = u64x2{0ull, 0ull};
-    const int cc = counts[c];
-    const unsigned long long* sc = seg + (size_t)c * segcap;
-    const unsigned short* si = segi + (size_t)c * segcap;
-    for (int i = lane; i < cc; i += kWave) {
-      const int loc = si[i];
-      const unsigned long long b = sc[i];
+    auto put = [&](int loc, unsigned long long b) {
       const unsigned long long key = order_key64(__longlong_as_double((long long)b));
       if ((loc / kPiece) == sub && (key > T || (key == T && c * kChunk + loc >= ithr))) s_tile[loc % kPiece] = b;
-    }
+    };
+    if (lane < cc) put(loc0, b0);
+    for (int i = lane + kWave; i < cc; i += kWave) put(si[i], sc[i]);
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -1109,17 +1185,28 @@ __global__ __launch_bounds__(kWave) void sel64_emit_kernel(const double* __restr
     }
     return;
   }
-  for (int u = 0; u < kPiece / 2 / kWave; ++u) {  // (after the fallback: x read again, kept in place)
-    const int64_t e = e0 + 2 * (lane + u * kWave);
-    if (e >= n) break;
-    double v[2] = {x[e], e + 1 < n ? x[e + 1] : 0.0};
+  // (after the fallback, or with long segments: x read again, kept in place)
+  double2 v[kPiece / 2 / kWave];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const unsigned long long key = order_key64(v[j]);
-      v[j] = (key > T || (key == T && e + j >= ithr)) ? v[j] : 0.0;
+  for (int u = 0; u < kPiece / 2 / kWave; ++u) {
+    const int64_t e = e0 + 2 * (lane + u * kWave);
+    const int64_t ec = e + 2 <= n ? e : (n & ~1ll) - 2;  // (branch-free loads: the pairs past the end re-read one)
+    v[u] = n >= 2 ? *reinterpret_cast<const double2*>(x + ec) : double2{x[0], 0.0};
+  }
+#pragma unroll
+  for (int u = 0; u < kPiece / 2 / kWave; ++u) {
+    const int64_t e = e0 + 2 * (lane + u * kWave);
+    auto keep = [&](double d, int64_t i) {
+      const unsigned long long key = order_key64(d);
+      return (key > T || (key == T && i >= ithr)) ? d : 0.0;
+    };
+    if (e + 2 <= n) {
+      __builtin_nontemporal_store(u64x2{(unsigned long long)__double_as_longlong(keep(v[u].x, e)),
+                                        (unsigned long long)__double_as_longlong(keep(v[u].y, e + 1))},
+                                  reinterpret_cast<u64x2*>(out + e));
+    } else if (e < n) {  // (the odd last element)
+      out[e] = keep(x[e], e);
     }
-    out[e] = v[0];
-    if (e + 1 < n) out[e + 1] = v[1];
   }
 }
 
@@ -1352,8 +1439,9 @@ int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void*
     const int rc = co.finish();
     if (rc) return rc;
   }
+  // (segments longer than kEmitSegMax: x is read again instead, every piece's wave would scan its chunk's segment)
   FLC_LAUNCH("sel64_emit", sel64_emit_kernel, dim3((unsigned)cdiv(n, kPiece)), dim3(kWave), 0, st, x, n,
-             f.on ? f.segcap : 0,
+             f.on && f.segcap <= kEmitSegMax ? f.segcap : 0,
              (const Sel64*)w.sel, (const unsigned long long*)w.seg, (const unsigned short*)w.segi,
              (const int*)w.counts, out);
   return FLC_OK;

@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fl_sim_amd import codec  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 25_000_000
-k = n // 100
+k = int(n * float(sys.argv[2]) / 100) if len(sys.argv) > 2 else n // 100  # (argument 2: k in % of n)
 x = torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(5), device="cuda", dtype=torch.float64)
 out = codec.topk_dense_f64(x, k)
 exp = torch.zeros_like(x)
