@@ -2208,64 +2208,84 @@ BatchGeom batch_geometry(int64_t n, int64_t k, int n_clients, int cus, size_t ex
 }
 
 // Pinned staging of the host-built tables (batch entries, delta pointer tables): a ring of slots per device, each
-// reused only after the copy out of it has completed (an event per slot; with kRing slots the wait is for a call
-// kRing calls back).  A copy from pageable memory goes through the runtime's own staging and can hold the host
-// until the device reaches it.
-constexpr int kRing = 32;
+// reused only after the last stream operation reading it has completed.  An event is recorded after every kEvery-th
+// slot's use only (each record put a ≈ 5.6 µs gap before the stream's next kernel); reusing slot s waits for the event
+// of slot s | (kEvery - 1), used after s in the previous lap — with kRing slots that is a call ≥ kRing - kEvery calls
+// back, normally long complete.  A copy from pageable memory goes through the runtime's own staging and can hold the
+// host until the device reaches it.  The batch entry table is not copied at all: pinned memory is mapped into the
+// device's address space, and each block reads its client's entry once, in place (one PCIe read at the kernel's
+// start instead of a copy and the dispatch gap behind it: ≈ 10 µs per call, §3.1b).
+constexpr int kRing = 32, kEvery = 8;
+static_assert(kRing % kEvery == 0 && (kEvery & (kEvery - 1)) == 0, "event slots");
 struct TableRing {
   std::mutex mu;
   char* buf[kRing] = {};
+  char* dptr[kRing] = {};  // the slot's device address
   size_t cap[kRing] = {};
   hipEvent_t ev[kRing] = {};
-  bool pending[kRing] = {};
+  hipStream_t st_of[kRing] = {};  // the stream of the slot's last use
+  bool used[kRing] = {};          // ... which may still be in flight
+  bool rec[kRing] = {};           // an event was recorded after it
   int next = 0;
 };
 TableRing& table_ring(int dev) {
   static TableRing rings[64];
   return rings[dev < 0 || dev >= 64 ? 0 : dev];
 }
-// copy `bytes` from `src` to the device address `dst`, stream-ordered on `st` (of device `dev`), through a pinned slot
-int copy_table(int dev, void* dst, const void* src, size_t bytes, hipStream_t st) {
+// `bytes` of `src` into the next pinned slot: *dev_ptr = its device address; table_done() after the last launch or copy
+// that reads it
+int stage_table(int dev, const void* src, size_t bytes, char** dev_ptr, char** host_ptr, int* slot) {
   TableRing& r = table_ring(dev);
   std::lock_guard<std::mutex> lk(r.mu);
-  const int s = r.next;
+  const int s = r.next, q = s | (kEvery - 1);
   r.next = (s + 1) % kRing;
-  if (r.pending[s]) {
-    FLC_CHECK_HIP(hipEventSynchronize(r.ev[s]));
-    r.pending[s] = false;
+  if (r.used[s]) {  // slot q was used after s in the previous lap: its event covers s when both ran on one stream
+    if (r.rec[q] && r.st_of[q] == r.st_of[s]) FLC_CHECK_HIP(hipEventSynchronize(r.ev[q]));
+    else FLC_CHECK_HIP(hipDeviceSynchronize());  // (streams mixed in one lap: rare; the stream may be gone)
+    r.used[s] = false;
   }
   if (r.cap[s] < bytes) {
     if (r.buf[s]) FLC_CHECK_HIP(hipHostFree(r.buf[s]));
-    r.buf[s] = nullptr;
+    r.buf[s] = r.dptr[s] = nullptr;
     r.cap[s] = 0;
     const size_t cap = std::max<size_t>(align_up(bytes, 4096), 16384);
     FLC_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.buf[s]), cap, hipHostMallocDefault));
     r.cap[s] = cap;
+    void* d = nullptr;
+    FLC_CHECK_HIP(hipHostGetDevicePointer(&d, r.buf[s], 0));
+    r.dptr[s] = static_cast<char*>(d);
   }
   if (!r.ev[s]) FLC_CHECK_HIP(hipEventCreateWithFlags(&r.ev[s], hipEventDisableTiming));
   std::memcpy(r.buf[s], src, bytes);
-  FLC_CHECK_HIP(hipMemcpyAsync(dst, r.buf[s], bytes, hipMemcpyHostToDevice, st));
-  FLC_CHECK_HIP(hipEventRecord(r.ev[s], st));
-  r.pending[s] = true;
+  *dev_ptr = r.dptr[s];
+  if (host_ptr) *host_ptr = r.buf[s];
+  *slot = s;
   return FLC_OK;
 }
+int table_done(int dev, int slot, hipStream_t st) {
+  TableRing& r = table_ring(dev);
+  std::lock_guard<std::mutex> lk(r.mu);
+  r.st_of[slot] = st;
+  r.used[slot] = true;
+  r.rec[slot] = (slot & (kEvery - 1)) == kEvery - 1;
+  if (r.rec[slot]) FLC_CHECK_HIP(hipEventRecord(r.ev[slot], st));
+  return FLC_OK;
+}
+// copy `bytes` from `src` to the device address `dst`, stream-ordered on `st` (of device `dev`), through a pinned slot
+int copy_table(int dev, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  char *d = nullptr, *h = nullptr;
+  int slot = 0;
+  if (const int rc = stage_table(dev, src, bytes, &d, &h, &slot)) return rc;
+  const hipError_t e = hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, st);
+  const int rc = table_done(dev, slot, st);
+  FLC_CHECK_HIP(e);
+  return rc;
+}
 
-// host: the entries, then `extra` (already holding device addresses inside the workspace), in one copy
-template <class Src, bool STACKED = true>
-int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, const std::vector<char>& extra, int64_t n,
-                      int64_t k, int levels, uint64_t counter, void* ws, size_t ws_bytes, hipStream_t st,
-                      const char* who) {
-  int dev = 0;
-  const int cus = stream_cus(st, &dev);
-  const int C = (int)ents.size();
-  const BatchGeom bg = batch_geometry(n, k, C, cus, extra.size());
-  if (!ws || bg.need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, bg.need);
-  char* base = static_cast<char*>(ws);
-  BatchEntry* tab = reinterpret_cast<BatchEntry*>(base + bg.table_off);
-  std::vector<char> host(bg.extra_off - bg.table_off + extra.size(), 0);
-  std::memcpy(host.data(), ents.data(), ents.size() * sizeof(BatchEntry));
-  if (!extra.empty()) std::memcpy(host.data() + (bg.extra_off - bg.table_off), extra.data(), extra.size());
-  if (const int rc = copy_table(dev, tab, host.data(), host.size(), st)) return rc;
+// the batched launches over the clients in chunks of bg.chunk (tab: the entry table, device-readable)
+template <class Src, bool STACKED>
+int launch_topk_batch_chunks(const Src& proto, const BatchEntry* tab, int C, const BatchGeom& bg, int64_t n, int64_t k,
+                             int levels, uint64_t counter, char* base, hipStream_t st, int dev) {
   // each call starts its headers from zero (state, flags, histograms): no history is carried between calls, so the
   // header / staging split may move with the client count
   const SampleSetup ss = sample_setup(n, k, batch_sample_cap(n));
@@ -2303,6 +2323,39 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
   }
   return co.finish();
 }
+
+// host: the entries read in place from a pinned slot; with `extra` (already holding device addresses inside the
+// workspace) both copied into the workspace in one copy
+template <class Src, bool STACKED = true>
+int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, const std::vector<char>& extra, int64_t n,
+                      int64_t k, int levels, uint64_t counter, void* ws, size_t ws_bytes, hipStream_t st,
+                      const char* who) {
+  int dev = 0;
+  const int cus = stream_cus(st, &dev);
+  const int C = (int)ents.size();
+  const BatchGeom bg = batch_geometry(n, k, C, cus, extra.size());
+  if (!ws || bg.need > ws_bytes) return fail(FLC_EWORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, bg.need);
+  char* base = static_cast<char*>(ws);
+  const BatchEntry* tab = reinterpret_cast<const BatchEntry*>(base + bg.table_off);
+  int slot = -1;  // the entries read in place from a pinned slot (no extra tables), or copied with them
+  if (extra.empty()) {
+    char* d = nullptr;
+    if (const int rc = stage_table(dev, ents.data(), ents.size() * sizeof(BatchEntry), &d, nullptr, &slot)) return rc;
+    tab = reinterpret_cast<const BatchEntry*>(d);
+  } else {  // (the delta tables are read throughout the pass: device memory)
+    std::vector<char> host(bg.extra_off - bg.table_off + extra.size(), 0);
+    std::memcpy(host.data(), ents.data(), ents.size() * sizeof(BatchEntry));
+    std::memcpy(host.data() + (bg.extra_off - bg.table_off), extra.data(), extra.size());
+    if (const int rc = copy_table(dev, base + bg.table_off, host.data(), host.size(), st)) return rc;
+  }
+  const int rc = launch_topk_batch_chunks<Src, STACKED>(proto, tab, C, bg, n, k, levels, counter, base, st, dev);
+  if (slot >= 0) {
+    const int rc2 = table_done(dev, slot, st);
+    if (rc == FLC_OK) return rc2;
+  }
+  return rc;
+}
+
 
 int check_topk(const float* x, int64_t n, int64_t k, const char* who) {
   if (!x || n <= 0) return fail(FLC_EINVAL, "%s: bad arguments", who);
