@@ -181,7 +181,9 @@ def test_f64_dithering_philox_matches_oracle(D, kind, L, p):
     assert g64.same_bits(dec, exp)
 
 
-@pytest.mark.parametrize("D,K", [(10, 3), (4096, 41), (100_003, 1000), (4_000_000, 40_000), (1_000_000, 999_999)])
+# (1 M at 3 % / 5 % / 10 % and 2 M + 1 at 25 %: the band on, the emit from the segments below segcap 1024, from x above)
+@pytest.mark.parametrize("D,K", [(10, 3), (4096, 41), (100_003, 1000), (4_000_000, 40_000), (1_000_000, 999_999),
+                                 (1_000_000, 30_000), (1_000_000, 50_000), (1_000_000, 100_000), (2_000_001, 500_000)])
 def test_f64_topk_matches_oracle(D, K):
     from fl_sim_amd import codec
 
