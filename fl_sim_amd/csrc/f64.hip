@@ -878,7 +878,9 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
     // aligned pair (their elements are masked by index, an odd n's last element taken from xlast).  A load under a
     // branch leaves the compiler unsure how many loads follow an earlier one, and it then waits for all of them:
     // with the tail's branch, every chunk's processing waited for the loads of the next one too.
-    // (The chunk's base is uniform and the lane's offset 32-bit: few registers, so the three sets fit unspilled.)
+    // (The chunk's base is uniform and the lane's offset 32-bit: few registers, so the three sets fit unspilled.  The
+    // loads are non-temporal, as in the float32 pass: on fresh inputs 98-99 us per 25 M call against 104 us with
+    // cached loads; only an input still resident in the memory-side cache from the previous call reads faster cached.)
     const int64_t nl2 = (n & ~1ll) - 2;  // (n >= 64 Ki here)
     const double xlast = x[n - 1];
     auto load_chunk = [&](int64_t ch, double2 (&v)[kR]) {
@@ -889,7 +891,9 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         const unsigned o = 2u * (unsigned)(r * kGT + tid);
-        v[r] = *reinterpret_cast<const double2*>(xb + (o <= lim ? o : lim));
+        const u64x2 t = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(xb + (o <= lim ? o : lim)));
+        v[r].x = __longlong_as_double((long long)t.x);
+        v[r].y = __longlong_as_double((long long)t.y);
       }
     };
     double2 va[kR], vb[kR], vc[kR];

@@ -18,6 +18,9 @@ from fl_sim_amd import codec  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 25_000_000
 k = n // 100
 x = torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(5), device="cuda", dtype=torch.float64)
+# ROTATE=3: three distinct inputs in rotation (not cache-resident)
+xs = [x] + [torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(6 + i), device="cuda",
+                        dtype=torch.float64) for i in range(int(os.environ.get("ROTATE", "1")) - 1)]
 nch = -(-n // 8192)
 al = lambda v: -(-v // 256) * 256  # noqa: E731
 off = al(nch * 4) + al((nch + 1) * 8) + al(nch * 8)  # carve64: counts, offsets, part, then Sel64
@@ -26,7 +29,7 @@ names = ["prep0", "", "", "", "", "sel0", "band", "filtered", "bar1", "", "bin",
 G = torch.cuda.get_device_properties(0).multi_processor_count
 rows, blk = [], []
 for it in range(12):
-    codec.topk_dense_f64(x, k)
+    codec.topk_dense_f64(xs[it % len(xs)], k)
     torch.cuda.synchronize()
     ws = codec._WS[(0, codec._stream(x.device), "f64")]
     st = ws[off:off + 19 * 8].cpu().numpy().view(np.uint64).astype(np.int64)
