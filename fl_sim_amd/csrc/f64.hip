@@ -475,7 +475,7 @@ struct Sel64 {
   unsigned fhist[2 * kDigits][256];   // the fallback's digit histograms: key digits, then tie-index digits
   unsigned long long bkey[kBinCap];   // the K-th largest's bin: keys (less the bin's base) and their indices
   long long bidx[kBinCap];
-  unsigned long long sample[kSample64];
+  unsigned sample[kSample64];         // the sample's keys, top 32 bits (the band needs no more; half the bytes)
 };
 
 #ifdef FLC_SELECT_STAMPS  // (tools/stamps64.py)
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(kT) void sel64_prep_kernel(const double* __restrict
   }
   for (int j = blockIdx.x * kT + tid; j < S; j += gridDim.x * kT) {
     const int64_t pos = (int64_t)(((double)j + 0.5) * (double)n / (double)S);
-    st->sample[j] = order_key64(x[pos < n ? pos : n - 1]);
+    st->sample[j] = (unsigned)(order_key64(x[pos < n ? pos : n - 1]) >> 32);
   }
 }
 
@@ -626,7 +626,7 @@ __device__ __forceinline__ void sample_keys(const Sel64* __restrict__ st, int S,
 #pragma unroll
   for (int i = 0; i < kSPer; ++i) {
     const int j = i * kGT + (int)threadIdx.x;
-    key[i] = j < S ? st->sample[j] : 0ull;
+    key[i] = j < S ? (unsigned long long)st->sample[j] << 32 : 0ull;  // (truncated: key' <= key)
   }
 }
 __device__ __forceinline__ void sample_band(const Sel64* st, const unsigned long long (&key)[kSPer], int S,
@@ -695,9 +695,12 @@ __device__ __forceinline__ void sample_band(const Sel64* st, const unsigned long
         sh_hi = sh2;
       }
     }
-    t_lo = lo0;
+    t_lo = lo0;  // (from truncated keys: at least as many true keys lie at or above it)
     const unsigned long long e1 = lo1 + (1ull << sh_hi);
-    t_hi = !hi || e1 < lo1 ? ~0ull : e1;  // (saturated at the top of the key range)
+    // (rounded up to a multiple of 2^32, so that key >= t_hi exactly when the truncated key is: the ceiling's rank
+    // holds for the true keys too)
+    const unsigned long long e2 = (e1 + 0xffffffffull) & ~0xffffffffull;
+    t_hi = !hi || e1 < lo1 || e2 < e1 ? ~0ull : e2;  // (saturated at the top of the key range)
   } else {
     unsigned long long plo = 0ull, phi = 0ull;
     long long rlo = r_lo, rhi = r_hi;
