@@ -59,6 +59,7 @@ SIGNATURES = {
     "flc_natural_decode": (c_int, [c_void_p, c_int64, c_float, c_int, c_void_p, c_void_p]),
     "flc_topk_workspace_size": (c_size_t, [c_int64, c_int64]),
     "flc_topk_status": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "flc_ring_selftest": (c_int, [POINTER(c_int32), c_int, POINTER(c_int32), c_int]),
     "flc_topk_encode": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_sparse_decode_workspace_size": (c_size_t, [c_int64]),
     "flc_sparse_decode": (
@@ -149,6 +150,7 @@ SIGNATURES = {
     "flc_scale_div_f64": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_void_p]),
     "flc_randk_apply_f64": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_double, c_void_p, c_void_p]),
     "flc_f64_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "flc_f64_status": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "flc_count_consumers_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "flc_natural_f64": (
         c_int, [c_void_p, c_int64, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]

@@ -78,19 +78,21 @@ def _fold(dsts: Sequence[torch.Tensor], msg_tensors: Sequence, weights: Sequence
     if key is not None:
         msg_tensors = [m[key] for m in msg_tensors]
     cap = codec.MODEL_FOLD_MAX_SRC
+    launched = False  # a launch has written the model: from then on a failure has no clean fallback
     try:
         if len(msg_tensors) > cap:
             for c0 in range(0, len(msg_tensors) - cap, cap):
                 _fold_one(dev, dsts, msg_tensors[c0:c0 + cap], weights[c0:c0 + cap], init_mode if c0 == 0 else 2,
                           beta)
-                init_mode = 2  # (the first launch has run: the chain continues from the stored partial sums)
+                launched = True
+                init_mode = 2  # (the chain continues from the stored partial sums)
             last = (len(msg_tensors) - 1) // cap * cap
             _fold_one(dev, dsts, msg_tensors[last:], weights[last:], 2, beta, **step)
             return True
         _fold_one(dev, dsts, msg_tensors, weights, init_mode, beta, **step)
     except TypeError:
-        if init_mode == 2 and len(msg_tensors) > cap:
-            raise  # (a later chunk's tensors failed after the first launch ran: no clean fallback)
+        if launched:
+            raise  # (a later chunk's tensors failed after an earlier launch ran)
         return False  # a model tensor the fold does not take (dtype, device, layout): per-tensor launches
     return True
 
@@ -181,11 +183,20 @@ def update_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Ma
             grads = [g.to("cpu") for g in dgs]
     else:
         g0s = messages[0]["gradients"]
-        devs = {mp.device if mp.device.type == "cuda" else g.device for mp, g in zip(model_params, g0s)}
-        if len(devs) != 1 or next(iter(devs)).type != "cuda":
-            raise TypeError("update_gradients: the model and the gradients must live on one HIP device, or the model "
-                            "in host memory")
-        grads = _gradients_on(next(iter(devs)), messages)
+        devs = [mp.device if mp.device.type == "cuda" else g.device for mp, g in zip(model_params, g0s)]
+        if len(set(devs)) == 1 and devs[0].type == "cuda":
+            grads = _gradients_on(devs[0], messages)
+        else:  # parameters spread over several HIP devices (the reference accepts any placement): per tensor, each
+            # gradient folded on its own parameter's device
+            total_samples = sum([m["train_samples"] for m in messages])
+            weights = [m["train_samples"] / total_samples for m in messages]
+            grads = []
+            for j, d in enumerate(devs):
+                if d.type != "cuda":
+                    raise TypeError(f"update_gradients: parameter {j} and its gradients are not on a HIP device")
+                g = torch.empty(g0s[j].shape, dtype=g0s[j].dtype, device=d)
+                codec.weighted_sum(g, [_on(m["gradients"][j], d) for m in messages], weights, init_mode=1)
+                grads.append(g)
     for mp, g in zip(model_params, grads):
         if isinstance(mp, torch.Tensor) and mp.requires_grad:
             mp.grad = g

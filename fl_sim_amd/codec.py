@@ -218,7 +218,8 @@ TOPK_CHECK = os.environ.get("FLC_TOPK_CHECK", "0") not in ("", "0")
 TOPK_ERRORS = {1: "digit not found", 2: "count mismatch", 4: "exchange spin timeout"}
 _TOPK_KINDS = ("topk", "topk_batch")  # single-client and batched encoder workspaces (never shared)
 # every workspace kind whose kernels run a grid exchange, and the entry point reading its sticky error word
-_STATUS_FN = {"topk": "flc_topk_status", "topk_batch": "flc_topk_status", "quant": "flc_quant_status"}
+_STATUS_FN = {"topk": "flc_topk_status", "topk_batch": "flc_topk_status", "quant": "flc_quant_status",
+              "f64": "flc_f64_status"}
 
 
 def _status(device: torch.device, kinds: Sequence[str], reset: bool = True) -> int:
@@ -271,7 +272,7 @@ def _after_encode(device: torch.device, kinds: Sequence[str] = _TOPK_KINDS) -> N
         err = _status(device, kinds)
         if err:
             bits = ", ".join(v for b, v in TOPK_ERRORS.items() if err & b)
-            what = "quantizer" if tuple(kinds) == ("quant",) else "top-k encode"
+            what = {("quant",): "quantizer", ("f64",): "float64 top-k select"}.get(tuple(kinds), "top-k encode")
             raise _lib.FlcError(f"{what} lost co-residency or failed ({bits}); its output may be wrong")
 
 
@@ -1018,4 +1019,5 @@ def topk_dense_f64(x: torch.Tensor, k: int) -> torch.Tensor:
     out = torch.empty_like(x)
     ws = _ws64(x, k)
     call("flc_topk_dense_f64", _p(x), x.numel(), int(k), _p(out), _p(ws), ws.numel(), _stream(x.device))
+    _after_encode(x.device, ("f64",))
     return out

@@ -818,7 +818,7 @@ __device__ __forceinline__ void grid_arrive64(Sel64* st, unsigned long long targ
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(st->flags + blockIdx.x, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void grid_sync64(Sel64* st, unsigned long long target) {
+__device__ __forceinline__ void grid_sync64(Sel64* st, unsigned long long target, unsigned spin_lim) {
   grid_arrive64(st, target);
   const int tid = threadIdx.x;
   if (tid < kWave) {
@@ -837,7 +837,9 @@ __device__ __forceinline__ void grid_sync64(Sel64* st, unsigned long long target
       }
       if (__ballot(!ok) == 0ull) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) {  // ~1 s: a block never arrived (lost co-residency); flag it and let the launch drain
+      // ~1 s (spin_lim = 2^22): a block never arrived (lost co-residency); flag it and let the launch drain.  (spin_lim 0,
+      // a test knob: the first barrier reports a timeout whatever the flags say)
+      if (spin_lim == 0u || ++spins > spin_lim) {
         if (tid == 0) atomicOr(&st->err, 1);
         break;
       }
@@ -859,7 +861,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
                                                            long long r_lo, long long r_hi, int segcap,
                                                            Sel64* __restrict__ st, unsigned long long* __restrict__ seg,
                                                            unsigned short* __restrict__ segi, int* __restrict__ counts,
-                                                           int64_t nch) {
+                                                           int64_t nch, unsigned spin_lim) {
   constexpr int kPer = kBinCap / kGT;
   constexpr int kR = kChunk / (2 * kGT);  // 16-B loads per thread per chunk (4)
   __shared__ SelLds L;
@@ -976,7 +978,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
 #ifdef FLC_SELECT_STAMPS
     if (tid == 0) const_cast<Sel64*>(st)->bstamps[1][blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
-    grid_sync64(st, ++target);
+    grid_sync64(st, ++target, spin_lim);
     STAMP64(blockIdx.x == 0, 8);
     // 3. the bin of the K-th largest (every block the same)
     unsigned long long ab = 0ull;
@@ -1014,7 +1016,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
         grid_arrive64(st, ++target);
         return;
       }
-      grid_sync64(st, ++target);
+      grid_sync64(st, ++target, spin_lim);
       STAMP64(true, 12);
       // (block 0: every list entry is in)
       const long long cnt = min((long long)ld_sc1(&st->nbin), cnt0);
@@ -1084,7 +1086,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
     }
     __syncthreads();
     if (tid < 256 && s_h[tid]) atomicAdd(&st->fhist[slot][tid], s_h[tid]);
-    grid_sync64(st, ++target);
+    grid_sync64(st, ++target, spin_lim);
     pick256<kGNW>(tid < 256 ? (long long)ld_sc1(&st->fhist[slot][255 - tid]) : 0ll, rem, s_scan, s_res);
   };
   unsigned long long T = 0ull;
@@ -1147,9 +1149,14 @@ __global__ __launch_bounds__(kWave) void sel64_emit_kernel(const double* __restr
                                                            const Sel64* __restrict__ st,
                                                            const unsigned long long* __restrict__ seg,
                                                            const unsigned short* __restrict__ segi,
-                                                           const int* __restrict__ counts, double* __restrict__ out) {
+                                                           const int* __restrict__ counts, double* __restrict__ out,
+                                                           unsigned long long* __restrict__ sticky) {
   __shared__ __attribute__((aligned(16))) unsigned long long s_tile[kPiece];  // 8 KB
   const int lane = threadIdx.x;
+  // the select's barrier timeout (this call's output is invalid) into the workspace's sticky error word (bit 4, as the
+  // float32 encoders report it), which flc_f64_status reads
+  if (blockIdx.x == 0 && lane == 0 && st->err)
+    __hip_atomic_fetch_or(sticky, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long T = st->T;
   const long long ithr = st->ithr;
   const int64_t p = blockIdx.x, c = p / kPieces;
@@ -1280,7 +1287,15 @@ Filt64 filt64(int64_t n, int64_t k) {
   return f;
 }
 
+// FLC_F64_FORCE_TIMEOUT=1 (tests only): the select's first grid barrier reports a timeout, so that the error path
+// (Sel64::err -> the sticky word -> flc_f64_status -> the caller's check) can be exercised
+bool force_timeout64() {
+  static const bool on = getenv("FLC_F64_FORCE_TIMEOUT") && atoi(getenv("FLC_F64_FORCE_TIMEOUT")) == 1;
+  return on;
+}
+
 struct Ws64 {
+  unsigned long long* sticky;  // the sticky error word (flc_f64_status): first in every float64 workspace
   int* counts;
   long long* offsets;
   unsigned long long* part;
@@ -1293,6 +1308,7 @@ Ws64 carve64(void* ws, size_t bytes, int64_t n, int64_t k = 0) {
   Carver c(ws, bytes);
   const int64_t nch = cdiv(n < 1 ? 1 : n, kChunk);
   Ws64 w;
+  w.sticky = c.take<unsigned long long>(32);
   w.counts = c.take<int>((size_t)nch);
   w.offsets = c.take<long long>((size_t)nch + 1);
   w.part = c.take<unsigned long long>((size_t)nch);
@@ -1442,7 +1458,8 @@ int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void*
     Coresident co(st, dev);
     if (co.status()) return co.status();
     FLC_LAUNCH("sel64_select", sel64_select_kernel, dim3((unsigned)cus), dim3(kGT), 0, st, x, n, (long long)k,
-               f.on ? f.S : 0, f.r_lo, f.r_hi, f.on ? f.segcap : 0, w.sel, w.seg, w.segi, w.counts, f.on ? nch : 0);
+               f.on ? f.S : 0, f.r_lo, f.r_hi, f.on ? f.segcap : 0, w.sel, w.seg, w.segi, w.counts, f.on ? nch : 0,
+               force_timeout64() ? 0u : (1u << 22));
     const int rc = co.finish();
     if (rc) return rc;
   }
@@ -1450,7 +1467,15 @@ int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void*
   FLC_LAUNCH("sel64_emit", sel64_emit_kernel, dim3((unsigned)cdiv(n, kPiece)), dim3(kWave), 0, st, x, n,
              f.on && f.segcap <= kEmitSegMax ? f.segcap : 0,
              (const Sel64*)w.sel, (const unsigned long long*)w.seg, (const unsigned short*)w.segi,
-             (const int*)w.counts, out);
+             (const int*)w.counts, out, w.sticky);
+  return FLC_OK;
+}
+
+int flc_f64_status(void* ws, uint64_t* err_out, int reset, void* stream) {
+  if (!ws || !err_out) return fail(FLC_EINVAL, "flc_f64_status: null workspace or output");
+  hipStream_t st = as_stream(stream);
+  FLC_CHECK_HIP(hipMemcpyAsync(err_out, ws, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+  if (reset) FLC_CHECK_HIP(hipMemsetAsync(ws, 0, sizeof(uint64_t), st));
   return FLC_OK;
 }
 

@@ -64,7 +64,8 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave_kernel(const int* __
                                                                    int levels, double step,
                                                                    const float* __restrict__ norm_ptr, int64_t n,
                                                                    float weight, float* __restrict__ out,
-                                                                   const unsigned* __restrict__ tile_start) {
+                                                                   const unsigned* __restrict__ tile_start,
+                                                                   unsigned k) {
   constexpr int TILE = 1024;
   __shared__ __attribute__((aligned(16))) float s_tile[TILE];
   const int lane = threadIdx.x;
@@ -77,7 +78,8 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave_kernel(const int* __
       acc[u] = e + 4 <= n ? *reinterpret_cast<const float4*>(out + e) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  const unsigned lo = tile_start[blockIdx.x], hi = tile_start[blockIdx.x + 1];
+  // (entries clamped to [0, k): a malformed tile pointer never reads past the wire; scalar)
+  const unsigned lo = min(tile_start[blockIdx.x], k), hi = min(tile_start[blockIdx.x + 1], k);
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
 #pragma unroll
   for (int u = 0; u < 4; ++u) tile4[lane + u * kWave] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
                                                                     const float* __restrict__ norm_ptr, int64_t n,
                                                                     float weight, float* __restrict__ out,
                                                                     const unsigned* __restrict__ tile_start,
-                                                                    int64_t ntiles) {
+                                                                    int64_t ntiles, unsigned k) {
   constexpr int TILE = 1024;
   __shared__ __attribute__((aligned(16))) float s_tile[NT * TILE];
   const int lane = threadIdx.x;
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
   const int64_t t0 = tb * TILE;
   unsigned ts[NT + 1];
 #pragma unroll
-  for (int i = 0; i <= NT; ++i) ts[i] = tile_start[tb + i < ntiles ? tb + i : ntiles];
+  for (int i = 0; i <= NT; ++i) ts[i] = min(tile_start[tb + i < ntiles ? tb + i : ntiles], k);  // (clamped: see above)
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
 #pragma unroll
   for (int u = 0; u < 4 * NT; ++u) tile4[lane + u * kWave] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -253,28 +255,29 @@ int launch_decode_wave(const int32_t* idx, const float* val, const uint8_t* code
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   if (accumulate)
     FLC_LAUNCH(name, (sparse_decode_wave_kernel<MODE, true>), dim3((unsigned)ntiles), dim3(kWave), 0, st, idx, val,
-               codes, scale, levels, step, norm, n, weight, out, tile_start);
+               codes, scale, levels, step, norm, n, weight, out, tile_start, (unsigned)k);
   else
     FLC_LAUNCH(name, (sparse_decode_wave_kernel<MODE, false>), dim3((unsigned)ntiles), dim3(kWave), 0, st, idx, val,
-               codes, scale, levels, step, norm, n, weight, out, tile_start);
+               codes, scale, levels, step, norm, n, weight, out, tile_start, (unsigned)k);
   return FLC_OK;
 }
 
 // decode over given 1024-output tile pointers (no tile_index pass): one wave per two tiles, or, when
 // accumulating, one wave per tile (its slice of `out` read first)
 template <int MODE>
-int launch_decode_tiles(const int32_t* idx, const float* val, const uint8_t* codes, float scale, int levels,
+int launch_decode_tiles(const int32_t* idx, const float* val, const uint8_t* codes, int64_t k, float scale, int levels,
                         const float* norm, int64_t n, float weight, int accumulate, float* out,
                         const unsigned* tile_start, hipStream_t st, const char* name) {
   if (!aligned16(out)) return fail(FLC_EINVAL, "%s: out must be 16-B aligned", name);
+  if (k >= (1ll << 31)) return fail(FLC_EINVAL, "%s: k must be < 2^31", name);
   const int64_t ntiles = cdiv(n, (int64_t)FLC_TILE);
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   if (accumulate)
     FLC_LAUNCH(name, (sparse_decode_wave_kernel<MODE, true>), dim3((unsigned)ntiles), dim3(kWave), 0, st, idx, val,
-               codes, scale, levels, step, norm, n, weight, out, tile_start);
+               codes, scale, levels, step, norm, n, weight, out, tile_start, (unsigned)k);
   else
     FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, 2>), dim3((unsigned)cdiv(ntiles, 2)), dim3(kWave), 0, st, idx,
-               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles);
+               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, (unsigned)k);
   return FLC_OK;
 }
 
@@ -294,7 +297,7 @@ int launch_decode_wave2(const int32_t* idx, const float* val, const uint8_t* cod
              (long long)ntiles, tile_start);
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, NT>), dim3((unsigned)cdiv(ntiles, NT)), dim3(kWave), 0, st, idx,
-             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles);
+             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, (unsigned)k);
   return FLC_OK;
 }
 
@@ -331,7 +334,7 @@ int flc_sparse_decode_tiled(const int32_t* idx, const float* val, int64_t k, flo
   if (!out || !tiles || n <= 0 || k < 0 || (k > 0 && (!idx || !val)))
     return fail(FLC_EINVAL, "flc_sparse_decode_tiled: bad arguments");
   if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_sparse_decode_tiled: n must be < 2^31");
-  return launch_decode_tiles<0>(idx, val, nullptr, scale, 0, nullptr, n, weight, accumulate, out, tiles,
+  return launch_decode_tiles<0>(idx, val, nullptr, k, scale, 0, nullptr, n, weight, accumulate, out, tiles,
                                 as_stream(stream), "sparse_decode");
 }
 
@@ -341,7 +344,7 @@ int flc_stacked_decode_tiled(const int32_t* idx, const uint8_t* codes, int64_t k
     return fail(FLC_EINVAL, "flc_stacked_decode_tiled: bad arguments");
   if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_stacked_decode_tiled: n must be < 2^31");
   if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_stacked_decode_tiled: levels must be in [1, 127]");
-  return launch_decode_tiles<1>(idx, nullptr, codes, 1.0f, levels, norm, n, weight, accumulate, out, tiles,
+  return launch_decode_tiles<1>(idx, nullptr, codes, k, 1.0f, levels, norm, n, weight, accumulate, out, tiles,
                                 as_stream(stream), "stacked_decode");
 }
 

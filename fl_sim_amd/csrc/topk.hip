@@ -2210,52 +2210,111 @@ BatchGeom batch_geometry(int64_t n, int64_t k, int n_clients, int cus, size_t ex
 // Pinned staging of the host-built tables (batch entries, delta pointer tables): a ring of slots per device, each
 // reused only after the last stream operation reading it has completed.  An event is recorded after every kEvery-th
 // slot's use only (each record put a ≈ 5.6 µs gap before the stream's next kernel); reusing slot s waits for the event
-// of slot s | (kEvery - 1), used after s in the previous lap — with kRing slots that is a call ≥ kRing - kEvery calls
+// of slot q = s | (kEvery - 1), used after s in the previous lap — with kRing slots that is a call ≥ kRing - kEvery calls
 // back, normally long complete.  A copy from pageable memory goes through the runtime's own staging and can hold the
 // host until the device reaches it.  The batch entry table is not copied at all: pinned memory is mapped into the
 // device's address space, and each block reads its client's entry once, in place (one PCIe read at the kernel's
 // start instead of a copy and the dispatch gap behind it: ≈ 10 µs per call, §3.1b).
+//
+// The bookkeeping (RingBook, pure host logic: flc_ring_selftest drives it without a device) records at STAGE time
+// that a slot is in use and in which lap, and clears its event mark; table_done then records the stream and, every
+// kEvery-th slot, the event.  q's event covers s only when q was staged and done in the same lap as s (after s) on
+// the same stream: a stage that never reached table_done (an error return between the two), or a recorded event from
+// an earlier lap, cannot stand for s.  Otherwise the reuse drains the ring's device (made current for the call).
+// Under stream capture the ring is not used at all (a captured graph reads a host slot at replay time, laps later):
+// the tables go into the device workspace through kernel arguments (fill_table), see stage_or_fill.
 constexpr int kRing = 32, kEvery = 8;
 static_assert(kRing % kEvery == 0 && (kEvery & (kEvery - 1)) == 0, "event slots");
+struct RingBook {
+  enum Wait { kNone = 0, kEvent = 1, kDrain = 2 };
+  unsigned long long lap_of[kRing] = {};  // lap of the slot's latest stage (valid when used)
+  const void* st_of[kRing] = {};          // stream of its latest use (set by done; null: not done)
+  bool used[kRing] = {};                  // staged, and not yet known complete
+  bool rec[kRing] = {};                   // an event was recorded after its latest use (set by done)
+  unsigned long long lap = 0;
+  int next = 0;
+  // the next slot to stage into and how to make it free: *wait_slot = the slot whose event to wait for (kEvent)
+  int stage(Wait* how, int* wait_slot) {
+    const int s = next, q = s | (kEvery - 1);
+    *how = kNone;
+    *wait_slot = -1;
+    if (used[s]) {
+      if (rec[q] && used[q] && lap_of[q] == lap_of[s] && st_of[s] != nullptr && st_of[q] == st_of[s]) {
+        *how = kEvent;
+        *wait_slot = q;
+      } else {
+        *how = kDrain;
+      }
+    }
+    return s;
+  }
+  // the wait for slot s is done (or none was needed): s is staged in the current lap
+  void staged(int s, Wait how) {
+    if (how == kDrain)  // the whole device drained: every earlier use is complete
+      for (int i = 0; i < kRing; ++i) used[i] = false;
+    used[s] = true;
+    lap_of[s] = lap;
+    st_of[s] = nullptr;
+    rec[s] = false;
+    next = (s + 1) % kRing;
+    if (next == 0) ++lap;
+  }
+  // the last stream operation reading slot s is enqueued on `st`; returns true when an event is to be recorded
+  bool done(int s, const void* st) {
+    st_of[s] = st;
+    rec[s] = (s & (kEvery - 1)) == kEvery - 1;
+    return rec[s];
+  }
+};
 struct TableRing {
   std::mutex mu;
+  RingBook book;
   char* buf[kRing] = {};
   char* dptr[kRing] = {};  // the slot's device address
   size_t cap[kRing] = {};
   hipEvent_t ev[kRing] = {};
-  hipStream_t st_of[kRing] = {};  // the stream of the slot's last use
-  bool used[kRing] = {};          // ... which may still be in flight
-  bool rec[kRing] = {};           // an event was recorded after it
-  int next = 0;
 };
 TableRing& table_ring(int dev) {
   static TableRing rings[64];
   return rings[dev < 0 || dev >= 64 ? 0 : dev];
+}
+// run `f` with `dev` current (the ring's slots, events and drains belong to that device, not to the calling
+// thread's current one), restoring the previous device
+template <class F>
+hipError_t on_device(int dev, F&& f) {
+  int cur = -1;
+  hipError_t e = hipGetDevice(&cur);
+  if (e != hipSuccess) return e;
+  if (cur != dev && (e = hipSetDevice(dev)) != hipSuccess) return e;
+  const hipError_t r = f();
+  const hipError_t e2 = cur != dev ? hipSetDevice(cur) : hipSuccess;
+  return r != hipSuccess ? r : e2;
 }
 // `bytes` of `src` into the next pinned slot: *dev_ptr = its device address; table_done() after the last launch or copy
 // that reads it
 int stage_table(int dev, const void* src, size_t bytes, char** dev_ptr, char** host_ptr, int* slot) {
   TableRing& r = table_ring(dev);
   std::lock_guard<std::mutex> lk(r.mu);
-  const int s = r.next, q = s | (kEvery - 1);
-  r.next = (s + 1) % kRing;
-  if (r.used[s]) {  // slot q was used after s in the previous lap: its event covers s when both ran on one stream
-    if (r.rec[q] && r.st_of[q] == r.st_of[s]) FLC_CHECK_HIP(hipEventSynchronize(r.ev[q]));
-    else FLC_CHECK_HIP(hipDeviceSynchronize());  // (streams mixed in one lap: rare; the stream may be gone)
-    r.used[s] = false;
-  }
+  RingBook::Wait how;
+  int q = -1;
+  const int s = r.book.stage(&how, &q);
+  if (how == RingBook::kEvent) FLC_CHECK_HIP(hipEventSynchronize(r.ev[q]));
+  else if (how == RingBook::kDrain) FLC_CHECK_HIP(on_device(dev, [] { return hipDeviceSynchronize(); }));
   if (r.cap[s] < bytes) {
     if (r.buf[s]) FLC_CHECK_HIP(hipHostFree(r.buf[s]));
     r.buf[s] = r.dptr[s] = nullptr;
     r.cap[s] = 0;
     const size_t cap = std::max<size_t>(align_up(bytes, 4096), 16384);
-    FLC_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.buf[s]), cap, hipHostMallocDefault));
+    FLC_CHECK_HIP(on_device(dev, [&] {
+      return hipHostMalloc(reinterpret_cast<void**>(&r.buf[s]), cap, hipHostMallocDefault);
+    }));
     r.cap[s] = cap;
     void* d = nullptr;
     FLC_CHECK_HIP(hipHostGetDevicePointer(&d, r.buf[s], 0));
     r.dptr[s] = static_cast<char*>(d);
   }
-  if (!r.ev[s]) FLC_CHECK_HIP(hipEventCreateWithFlags(&r.ev[s], hipEventDisableTiming));
+  if (!r.ev[s]) FLC_CHECK_HIP(on_device(dev, [&] { return hipEventCreateWithFlags(&r.ev[s], hipEventDisableTiming); }));
+  r.book.staged(s, how);
   std::memcpy(r.buf[s], src, bytes);
   *dev_ptr = r.dptr[s];
   if (host_ptr) *host_ptr = r.buf[s];
@@ -2265,14 +2324,42 @@ int stage_table(int dev, const void* src, size_t bytes, char** dev_ptr, char** h
 int table_done(int dev, int slot, hipStream_t st) {
   TableRing& r = table_ring(dev);
   std::lock_guard<std::mutex> lk(r.mu);
-  r.st_of[slot] = st;
-  r.used[slot] = true;
-  r.rec[slot] = (slot & (kEvery - 1)) == kEvery - 1;
-  if (r.rec[slot]) FLC_CHECK_HIP(hipEventRecord(r.ev[slot], st));
+  if (r.book.done(slot, st)) FLC_CHECK_HIP(hipEventRecord(r.ev[slot], st));
   return FLC_OK;
 }
+
+// Under stream capture: `bytes` (a multiple of 4) of `src` written to the device address `dst` by kernels whose
+// arguments carry the bytes (2 KB per launch), so the captured graph holds the table itself
+struct TableChunk {
+  unsigned w[512];
+};
+__global__ __launch_bounds__(256) void fill_table_kernel(unsigned* __restrict__ dst, TableChunk c, int words) {
+  for (int i = (int)threadIdx.x; i < words; i += 256) dst[i] = c.w[i];
+}
+int fill_table(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  const size_t words = (bytes + 3) / 4;
+  for (size_t w0 = 0; w0 < words; w0 += 512) {
+    TableChunk c;
+    const size_t nw = std::min<size_t>(512, words - w0);
+    std::memset(&c, 0, sizeof(c));
+    std::memcpy(c.w, static_cast<const char*>(src) + 4 * w0, std::min(bytes - 4 * w0, 4 * nw));
+    FLC_LAUNCH("fill_table", fill_table_kernel, dim3(1), dim3(256), 0, st, static_cast<unsigned*>(dst) + w0, c, (int)nw);
+  }
+  return FLC_OK;
+}
+int capturing(hipStream_t st, bool* cap) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  FLC_CHECK_HIP(hipStreamIsCapturing(st, &cs));
+  *cap = cs != hipStreamCaptureStatusNone;
+  return FLC_OK;
+}
+
 // copy `bytes` from `src` to the device address `dst`, stream-ordered on `st` (of device `dev`), through a pinned slot
+// (under capture: through kernel arguments)
 int copy_table(int dev, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  bool cap = false;
+  if (const int rc = capturing(st, &cap)) return rc;
+  if (cap) return fill_table(dst, src, bytes, st);
   char *d = nullptr, *h = nullptr;
   int slot = 0;
   if (const int rc = stage_table(dev, src, bytes, &d, &h, &slot)) return rc;
@@ -2338,7 +2425,11 @@ int launch_topk_batch(const Src& proto, const std::vector<BatchEntry>& ents, con
   char* base = static_cast<char*>(ws);
   const BatchEntry* tab = reinterpret_cast<const BatchEntry*>(base + bg.table_off);
   int slot = -1;  // the entries read in place from a pinned slot (no extra tables), or copied with them
-  if (extra.empty()) {
+  bool cap = false;
+  if (const int rc = capturing(st, &cap)) return rc;
+  if (extra.empty() && cap) {  // (under capture: into the workspace, through kernel arguments)
+    if (const int rc = fill_table(base + bg.table_off, ents.data(), ents.size() * sizeof(BatchEntry), st)) return rc;
+  } else if (extra.empty()) {
     char* d = nullptr;
     if (const int rc = stage_table(dev, ents.data(), ents.size() * sizeof(BatchEntry), &d, nullptr, &slot)) return rc;
     tab = reinterpret_cast<const BatchEntry*>(d);
@@ -2552,6 +2643,35 @@ int flc_stacked_encode_delta_batch(const float* const* local, const float* const
     ents[c] = BatchEntry{dx + o_lp + (size_t)c * n_tensors * 8, seeds[c], idx[c], codes[c], norm[c],
                          tiles ? tiles[c] : nullptr, nullptr};
   return launch_topk_batch(proto, ents, extra, n, k, levels, counter, ws, ws_bytes, as_stream(stream), who);
+}
+
+// the pinned table ring's bookkeeping on its own (no device): ops are triples (kind, slot, stream id); kind 0 stages
+// (writes the triple slot, wait kind 0 none / 1 event / 2 drain, event slot to `out`), kind 1 marks `slot` done on
+// stream `stream id` (ids > 0); returns the number of triples written, or -1 on a bad op
+int flc_ring_selftest(const int32_t* ops, int n_ops, int32_t* out, int n_out) {
+  if (!ops || n_ops < 0 || (!out && n_out > 0)) return -1;
+  RingBook b;
+  int w = 0;
+  for (int i = 0; i < n_ops; ++i) {
+    const int32_t kind = ops[3 * i], slot = ops[3 * i + 1], sid = ops[3 * i + 2];
+    if (kind == 0) {
+      RingBook::Wait how;
+      int q = -1;
+      const int s = b.stage(&how, &q);
+      b.staged(s, how);
+      if (w >= n_out) return -1;
+      out[3 * w] = s;
+      out[3 * w + 1] = (int32_t)how;
+      out[3 * w + 2] = q;
+      ++w;
+    } else if (kind == 1) {
+      if (slot < 0 || slot >= kRing || sid <= 0) return -1;
+      (void)b.done(slot, reinterpret_cast<const void*>((uintptr_t)sid));
+    } else {
+      return -1;
+    }
+  }
+  return w;
 }
 
 int flc_topk_status(void* ws, uint64_t* err_out, int reset, void* stream) {

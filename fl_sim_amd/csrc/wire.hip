@@ -67,7 +67,7 @@ template <bool SPARSE>
 __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t* __restrict__ wires, int64_t stride,
                                                                    WireLayout L, FoldArgs a, int nw, int levels,
                                                                    double step, int64_t n, int acc_in,
-                                                                   float* __restrict__ out) {
+                                                                   float* __restrict__ out, unsigned k) {
   __shared__ __attribute__((aligned(16))) float s_tile[FLC_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t s_last[SPARSE ? FLC_TILE : 4];  // sparse: last writer + 1 (0: none)
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
@@ -102,8 +102,10 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
     rec = wires + (int64_t)a.slot[lane] * stride;
     wl = a.w[lane];
     const unsigned* tiles = reinterpret_cast<const unsigned*>(rec + L.tiles);
-    lo = tiles[t];
-    cnt = tiles[t + 1] - lo;
+    // (clamped to the record's k entries: a malformed or unwritten tile pointer never reads past the record)
+    lo = min(tiles[t], k);
+    const unsigned hi = min(tiles[t + 1], k);
+    cnt = hi > lo ? hi - lo : 0u;
     nrm = *reinterpret_cast<const float*>(rec + L.norm);
   }
   const unsigned long long pos = __ballot(lane < nw && !std::signbit(wl));  // sign-clear weights (sparse: -0 rule)
@@ -293,7 +295,7 @@ int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slo
                            int64_t n, int64_t k, int levels, int accumulate, float* out, void* stream) {
   if (!wires || !slots || !weights || !out || n_wires < 1 || n <= 0 || k < 0)
     return fail(FLC_EINVAL, "flc_stacked_fold_wires: bad arguments");
-  if (n >= (1ll << 31)) return fail(FLC_EINVAL, "flc_stacked_fold_wires: n must be < 2^31");
+  if (n >= (1ll << 31) || k >= (1ll << 31)) return fail(FLC_EINVAL, "flc_stacked_fold_wires: n and k must be < 2^31");
   if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_stacked_fold_wires: levels must be in [1, 127]");
   size_t need = 0;
   const WireLayout L = wire_layout(n, k, &need);
@@ -321,10 +323,10 @@ int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slo
     const int acc_in = (c0 > 0 || accumulate) ? 1 : 0;
     if (sparse)
       FLC_LAUNCH("stacked_fold_wires", stacked_fold_wires_kernel<true>, dim3((unsigned)ntiles), dim3(kWave), 0, st,
-                 static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, acc_in, out);
+                 static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, acc_in, out, (unsigned)k);
     else
       FLC_LAUNCH("stacked_fold_wires", stacked_fold_wires_kernel<false>, dim3((unsigned)ntiles), dim3(kWave), 0, st,
-                 static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, acc_in, out);
+                 static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, acc_in, out, (unsigned)k);
   }
   return FLC_OK;
 }

@@ -216,7 +216,8 @@ class HostWirePipeline:
         if self.srv is None or self.srv.shape[0] < m:
             self.srv = torch.empty(m, self.stride, dtype=torch.uint8, device=self.device)
         srv = self.srv
-        srv.record_stream(self.s_h2d)
+        srv.record_stream(self.s_h2d)  # (written on s_h2d, read by the fold on s_comp: both uses recorded, so a
+        srv.record_stream(self.s_comp)  #  regrown buffer is not handed out while either still touches it)
         with torch.cuda.stream(self.s_h2d):
             self.s_h2d.wait_stream(self.s_comp)  # the previous fold has read the record buffer
             for i, w in enumerate(wires):

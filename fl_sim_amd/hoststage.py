@@ -210,6 +210,8 @@ def staged(groups: Sequence[Sequence[torch.Tensor]], read: Sequence[bool], write
            msgs: Sequence[Sequence[torch.Tensor]] = ()):
     """Stage host-resident groups for one aggregation call.  Yields ``(device groups, device messages)``; on a clean
     exit the groups marked ``write`` are copied back into the host tensors in place (and the stream synchronised).
+    On an error the stream is synchronised as well; with the copy staging the host tensors are left untouched, with
+    zero-copy staging the kernels that ran before the error have already updated them in place (no rollback).
     ``read[g]`` False skips the host→device copy of a group the call only writes."""
     groups = [list(g) for g in groups]
     dtype = next(t.dtype for g in groups for t in g)
@@ -223,8 +225,10 @@ def staged(groups: Sequence[Sequence[torch.Tensor]], read: Sequence[bool], write
         stream = torch.cuda.current_stream(device)
         if m is not None and m.zero_copy:  # adopted, zero-copy: the kernels work on the host buffer itself
             dmsgs = stage_messages(msgs, device, dtype)
-            yield [m.dev_views(gi) for gi in range(len(groups))], dmsgs
-            stream.synchronize()
+            try:  # (on an error the launches already made have written the host tensors: not rolled back)
+                yield [m.dev_views(gi) for gi in range(len(groups))], dmsgs
+            finally:
+                stream.synchronize()
             return
         if m is not None:  # adopted: one copy of the groups' contiguous span, nothing packed on the host
             if all(read):
@@ -250,7 +254,13 @@ def staged(groups: Sequence[Sequence[torch.Tensor]], read: Sequence[bool], write
             dgroups = [[dbuf[off:off + t.numel()].view(t.shape) for t, off in zip(g, offs[gi])]
                        for gi, g in enumerate(groups)]
         dmsgs = stage_messages(msgs, device, dtype)
-        yield dgroups, dmsgs
+        try:
+            yield dgroups, dmsgs
+        except BaseException:
+            # the host tensors stay as they were (nothing is copied back), but the H2D copies queued above may still
+            # be reading the shared pinned staging buffers that the next call overwrites from the host: drain first
+            stream.synchronize()
+            raise
         if m is not None and all(write):
             a, b = m.span
             hbuf[a:b].copy_(dbuf[a:b], non_blocking=True)

@@ -148,6 +148,11 @@ int flc_natural_decode(const uint16_t* codes, int64_t n, float weight, int accum
  * have shared the device (fl_sim_amd does when FLC_TOPK_CHECK=1, and the GPU tests after every test). */
 /* *err_out (device uint64) = the workspace's sticky error word; reset != 0 clears it (stream-ordered) */
 int flc_topk_status(void* ws, uint64_t* err_out, int reset, void* stream);
+/* Test hook (host only, no device): the batched encoders' pinned table ring (a ring of 32 host slots whose reuse
+ * waits for an event recorded after every 8th slot's use, or drains the device) driven by `n_ops` triples
+ * (kind, slot, stream id): kind 0 stages the next slot and writes (slot, wait 0 none / 1 event / 2 drain, event slot)
+ * to `out`; kind 1 marks `slot` done on stream `stream id` (> 0).  Returns the triples written, or -1. */
+int flc_ring_selftest(const int32_t* ops, int n_ops, int32_t* out, int n_out);
 size_t flc_topk_workspace_size(int64_t n, int64_t k);
 int flc_topk_encode(const float* x, int64_t n, int64_t k, int32_t* idx, float* val, void* ws,
                     size_t ws_bytes, void* stream);
@@ -341,6 +346,10 @@ int flc_quant_f64(const double* x, int64_t n, int kind, int levels, const double
 int flc_quant_decode_f64(const uint8_t* codes, int64_t n, int kind, int levels, const double* norm, double* out,
                          void* stream);
 int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void* ws, size_t ws_bytes, void* stream);
+/* the float64 workspace's sticky error word (4: flc_topk_dense_f64's grid-synchronised select timed out at a barrier,
+ * i.e. its blocks were not all resident — the output of that call is invalid), as flc_topk_status reports the float32
+ * encoders'; copied to *err_out (device uint64), zeroed with reset */
+int flc_f64_status(void* ws, uint64_t* err_out, int reset, void* stream);
 
 /* ------------------------------------------------------------------ client delta
  * FedOptClient.communicate (_fedopt.py:294-297): delta_t = clone(local_t) then add_(global_t, alpha=-1), i.e.

@@ -309,3 +309,75 @@ def test_pyfold_module_checks_without_gpu():
     with pytest.raises(ValueError, match="one weight per message"):
         _flcfold.model_fold(d, [d], None, [0.5, 0.5], 0, 0.0, None, None, 0, 1.0, 0.0, 0.0)
     _flcfold.model_fold([], [], None, [], 0, 0.0, None, None, 0, 1.0, 0.0, 0.0)  # nothing to fold
+
+
+def _ring(ops):
+    """Drive the batched encoders' pinned table ring bookkeeping (flc_ring_selftest, no device): ops are ("s",) to
+    stage the next slot or ("d", slot, stream) to mark a slot done; returns [(slot, wait, event_slot)] per stage."""
+    lib = _lib.load()
+    flat = []
+    for op in ops:
+        flat += [0, 0, 0] if op[0] == "s" else [1, op[1], op[2]]
+    n = len(ops)
+    a = (ctypes.c_int32 * max(1, 3 * n))(*flat)
+    out = (ctypes.c_int32 * max(1, 3 * n))()
+    w = lib.flc_ring_selftest(a, n, out, n)
+    assert w >= 0
+    return [tuple(out[3 * i:3 * i + 3]) for i in range(w)]
+
+
+def _lap(stream=1, skip_done=()):
+    """One lap of 32 stage + done pairs on one stream (slots in `skip_done` staged but never done: an error return
+    between stage_table and table_done)."""
+    ops = []
+    for s in range(32):
+        ops.append(("s",))
+        if s not in skip_done:
+            ops.append(("d", s, stream))
+    return ops
+
+
+NONE, EVENT, DRAIN = 0, 1, 2
+
+
+def test_table_ring_reuse_waits_for_the_covering_event():
+    """Second lap on one stream: slot s waits for the event of slot s | 7 (recorded after it in the first lap)."""
+    res = _ring(_lap() + _lap())
+    assert [r[0] for r in res] == list(range(32)) * 2
+    assert all(r[1] == NONE for r in res[:32])
+    for s, (slot, wait, q) in enumerate(res[32:]):
+        assert slot == s and wait == EVENT and q == (s | 7)
+
+
+def test_table_ring_stage_without_done_never_trusts_a_stale_event():
+    """Verdict r04 item 8: slot q = 7's stage in lap 2 fails before table_done.  In lap 3, slots 0..7 (covered by q in
+    lap 2) must not wait on q's event from lap 1: they drain the device instead."""
+    ops = _lap() + _lap(skip_done={7}) + _lap()
+    res = _ring(ops)
+    lap3 = res[64:]
+    assert lap3[0][1] == DRAIN  # slot 0: q = 7 never completed its lap-2 use
+    # after the drain every earlier use is complete: the next slots of the lap need no wait at all
+    assert all(r[1] == NONE for r in lap3[1:8])
+    # slots 8.. were staged in lap 2 *before* the drain: complete now, no wait either
+    assert all(r[1] == NONE for r in lap3[8:32])
+
+
+def test_table_ring_mixed_streams_drain():
+    """A slot used on stream 2 whose covering slot ran on stream 1: the event does not cover it -> drain."""
+    ops = []
+    for s in range(32):
+        ops += [("s",), ("d", s, 2 if s == 3 else 1)]
+    ops += [("s",)] * 4
+    res = _ring(ops)
+    assert [r[1] for r in res[32:35]] == [EVENT, EVENT, EVENT]
+    assert res[35][1] == DRAIN
+
+
+def test_table_ring_event_from_an_earlier_lap_is_not_used():
+    """Slot 7 done in lap 1 but its lap-2 stage never done; slot 0 of lap 2 done.  Reusing slot 0 in lap 3 must not
+    take slot 7's lap-1 event (recorded before slot 0's lap-2 use)."""
+    ops = _lap() + [("s",), ("d", 0, 1)]
+    ops += [op for s in range(1, 32) for op in ([("s",)] if s == 7 else [("s",), ("d", s, 1)])]
+    ops += [("s",)]
+    res = _ring(ops)
+    assert res[-1][0] == 0 and res[-1][1] == DRAIN

@@ -11,6 +11,7 @@ step stays float64.  Checked here:
   elements, with ties, zeros, NaN and signed zeros; float64 device tensors in, float64 device tensors out.
 """
 
+import os
 import random
 
 import numpy as np
@@ -357,3 +358,34 @@ def test_f64_adaptive_many_special_chunks_vs_oracle(structured):
     assert st["sequential"] == 0 and st["special"] > 256, st
     if not structured:
         assert st["taken"] >= st["special"] - 8, st
+
+
+def test_f64_topk_select_timeout_is_reported():
+    """ADVICE r04: a lost co-residency in the grid-synchronised float64 select (Sel64::err) reaches the workspace's
+    sticky error word, flc_f64_status reads it (codec.topk_status_all), and with FLC_TOPK_CHECK=1 the call raises.
+    FLC_F64_FORCE_TIMEOUT=1 (read once per process: a child) makes the first grid barrier report a timeout."""
+    import subprocess
+    import sys
+
+    child = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from fl_sim_amd import codec, _lib
+x = torch.randn(1 << 20, device="cuda", dtype=torch.float64)
+codec.TOPK_CHECK = False
+codec.topk_dense_f64(x, 1 << 13)
+print("status", max(codec.topk_status_all(reset=True).values()))
+codec.TOPK_CHECK = True
+try:
+    codec.topk_dense_f64(x, 1 << 13)
+    print("no error")
+except _lib.FlcError as e:
+    print("raised", "float64 top-k" in str(e))
+print("status", max(codec.topk_status_all(reset=True).values()))
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FLC_F64_FORCE_TIMEOUT="1")
+    r = subprocess.run([sys.executable, "-c", child, root], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln and not ln.startswith("/opt")]
+    assert lines == ["status 4", "raised True", "status 0"], lines

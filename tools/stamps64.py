@@ -23,7 +23,7 @@ xs = [x] + [torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(
                         dtype=torch.float64) for i in range(int(os.environ.get("ROTATE", "1")) - 1)]
 nch = -(-n // 8192)
 al = lambda v: -(-v // 256) * 256  # noqa: E731
-off = al(nch * 4) + al((nch + 1) * 8) + al(nch * 8)  # carve64: counts, offsets, part, then Sel64
+off = al(32 * 8) + al(nch * 4) + al((nch + 1) * 8) + al(nch * 8)  # carve64: sticky word, counts, offsets, part, then Sel64
 names = ["prep0", "", "", "", "", "sel0", "band", "filtered", "bar1", "", "bin", "append", "bar2", "T", "emit0",
          "list", "keys", "shist", "spick"]
 G = torch.cuda.get_device_properties(0).multi_processor_count
