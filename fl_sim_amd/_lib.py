@@ -23,6 +23,7 @@ FLC_NORM_INF = 0
 FLC_NORM_L2 = 2
 FLC_OPT = {"avg": 0, "adagrad": 1, "yogi": 2, "adam": 3}
 FLC_PROX_NONE, FLC_PROX_L1, FLC_PROX_SCALE = 0, 1, 2
+FLC_SRV_FEDDYN, FLC_SRV_PFEDME = 1, 2
 
 # name -> (restype, argtypes); must list every function declared in include/flcodec.h
 SIGNATURES = {
@@ -168,6 +169,8 @@ SIGNATURES = {
     "flc_fedopt_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
     "flc_model_fold": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
                                c_int, c_double, c_double, c_double, c_void_p]),
+    "flc_model_fold_server": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                                      c_int, c_float, c_double, c_void_p]),
     "flc_delta_flatten": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "flc_feddr_combine": (
         c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_int, c_float, c_void_p]

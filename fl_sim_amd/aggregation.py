@@ -348,6 +348,58 @@ def feddr_update(model_params: Sequence[torch.Tensor], y_params: Sequence[torch.
             codec.weighted_sum(sp, [], [], init_mode=0, beta=f)
 
 
+def feddyn_update(model_params: Sequence[torch.Tensor], h_params: Sequence[torch.Tensor], messages: Sequence[Mapping],
+                  mu: float, num_clients: int) -> None:
+    """feddyn/_feddyn.py:172-184: ``h += -mu/N · (p_m − θ)`` for each message in order (θ still the old model), then
+    ``avg_parameters()``; line 184 (``p = p.add(h, alpha=-1/mu)``) rebinds a local name and leaves the model as it is,
+    so nothing follows.  Up to 16 messages: one launch for h and θ together (every operand read once); more: h in
+    chained launches against the unchanged θ, then the chained average."""
+    model_params, h_params = list(model_params), list(h_params)
+    if len(messages) == 0:
+        return  # (no h update; avg_parameters returns early)
+    if hoststage.is_host(model_params):
+        with hoststage.staged([model_params, h_params], [True, True], [True, True],
+                              [m["parameters"] for m in messages]) as ((dps, dhs), dm):
+            feddyn_update(dps, dhs, [{"parameters": d, "train_samples": m["train_samples"]}
+                                     for m, d in zip(messages, dm)], mu, num_clients)
+        return
+    ps = _params(model_params)
+    dev = ps[0].device
+    alpha = -mu / num_clients
+    srcs = [[_on(t, dev) for t in m["parameters"]] for m in messages]
+    w = [1 / len(messages)] * len(messages)
+    cap = codec.MODEL_FOLD_MAX_SRC
+    if len(srcs) <= cap:
+        codec.model_fold_server(ps, h_params, srcs, w, "feddyn", True, 0, 0.0, alpha)
+        return
+    for c0 in range(0, len(srcs), cap):
+        codec.model_fold_server(ps, h_params, srcs[c0:c0 + cap], w[c0:c0 + cap], "feddyn", False, 0, 0.0, alpha)
+    avg_parameters(ps, [{"parameters": s_, "train_samples": m["train_samples"]} for s_, m in zip(srcs, messages)])
+
+
+def pfedme_update(model_params: Sequence[torch.Tensor], messages: Sequence[Mapping], beta: float) -> None:
+    """pfedme/_pfedme.py:166-175: the previous model saved, ``avg_parameters()``, then
+    ``θ = fl(θ · β) + (1 − β) · θ_prev`` (mul_ then add_ with alpha: one rounding, then one fma).  Up to 16 messages in
+    one launch (θ_prev held in registers, never stored); more: θ saved, the chained average, then the blend."""
+    model_params = list(model_params)
+    if hoststage.is_host(model_params):
+        with hoststage.staged([model_params], [True], [True], [m["parameters"] for m in messages]) as ((dps,), dm):
+            pfedme_update(dps, [{"parameters": d, "train_samples": m["train_samples"]} for m, d in zip(messages, dm)],
+                          beta)
+        return
+    ps = _params(model_params)
+    dev = ps[0].device
+    srcs = [[_on(t, dev) for t in m["parameters"]] for m in messages]
+    w = [1 / len(messages)] * len(messages) if messages else []
+    if len(srcs) <= codec.MODEL_FOLD_MAX_SRC:
+        # (no message: avg_parameters returns before its mul_(inertia): the blend of θ with itself, init 2)
+        codec.model_fold_server(ps, ps, srcs, w, "pfedme", True, 0 if srcs else 2, 0.0, beta)
+        return
+    saved = [p.detach().clone() for p in ps]
+    avg_parameters(ps, [{"parameters": s_, "train_samples": m["train_samples"]} for s_, m in zip(srcs, messages)])
+    codec.model_fold_server(ps, saved, [], [], "pfedme", False, 2, 0.0, beta)
+
+
 def _adopt(groups, messages_tensors=()) -> None:
     """The mixins own the server's tensors: a host-resident server's groups are adopted into one pinned buffer with a
     device mirror (hoststage.adopt), so each update stages them with one copy each way."""
@@ -415,3 +467,21 @@ class FedDRUpdateMixin:
         feddr_update(list(self.model.parameters()), self._y_parameters, self._x_til_parameters,
                      self._received_messages, self.config.alpha, self.config.eta, self.config.num_clients,
                      self.config.reg_type)
+
+
+class FedDynUpdateMixin:
+    """Device ``update()`` for the reference's ``FedDynServer`` (feddyn/_feddyn.py:172-184), for a server model on a
+    HIP device or in host memory (h kept next to the model)."""
+
+    def update(self) -> None:
+        _adopt([list(self.model.parameters()), self.h_params], [m["parameters"] for m in self._received_messages])
+        feddyn_update(list(self.model.parameters()), self.h_params, self._received_messages, self.config.mu,
+                      self.config.num_clients)
+
+
+class pFedMeUpdateMixin:  # noqa: N801 (the reference's class name: pFedMeServer)
+    """Device ``update()`` for the reference's ``pFedMeServer`` (pfedme/_pfedme.py:166-175)."""
+
+    def update(self) -> None:
+        _adopt([list(self.model.parameters())], [m["parameters"] for m in self._received_messages])
+        pfedme_update(list(self.model.parameters()), self._received_messages, self.config.beta)

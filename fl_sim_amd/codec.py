@@ -787,6 +787,41 @@ def _pyfold():
     return _PYFOLD[0]
 
 
+def model_fold_server(theta: Sequence[torch.Tensor], aux: Sequence[torch.Tensor],
+                      srcs: Sequence[Sequence[torch.Tensor]], weights: Sequence[float], kind: str, fold: bool = True,
+                      init_mode: int = 0, inertia: float = 0.0, c: float = 0.0) -> None:
+    """FedDyn's / pFedMe's server update of a whole model in one launch (flc_model_fold_server): ``kind`` "feddyn"
+    (aux = h; c = -mu / num_clients) or "pfedme" (aux = the saved model when ``fold`` is False; c = beta).  ``srcs[m]``
+    is message m's tensor list, at most 16 messages; every tensor a contiguous fp32 tensor on theta's device."""
+    import ctypes
+
+    nt, ns = len(theta), len(srcs)
+    if ns > MODEL_FOLD_MAX_SRC:
+        raise ValueError(f"model_fold_server takes at most {MODEL_FOLD_MAX_SRC} messages")
+    if len(aux) != nt or len(weights) != ns or any(len(m) != nt for m in srcs):
+        raise ValueError("one aux tensor per model tensor, one weight per message, one tensor per model tensor each")
+    if nt == 0:
+        return
+    f32, dev = torch.float32, theta[0].get_device()
+    sizes = [t.numel() for t in theta]
+
+    def ptrs(ts):
+        out = []
+        for t, n in zip(ts, sizes):
+            if not (t.is_cuda and t.dtype is f32 and t.is_contiguous() and t.get_device() == dev and t.numel() == n):
+                raise TypeError("model_fold_server: contiguous fp32 HIP tensors of the model's sizes on one device")
+            out.append(t.data_ptr())
+        return out
+
+    sp = [q for m in srcs for q in ptrs(m)]
+    P = ctypes.c_void_p
+    vp = lambda a: ctypes.cast(a, P)  # noqa: E731
+    call("flc_model_fold_server", vp((P * nt)(*ptrs(theta))), vp((P * nt)(*ptrs(aux))), vp((P * max(len(sp), 1))(*sp)),
+         vp((ctypes.c_float * max(ns, 1))(*[float(w) for w in weights])), ns, vp((ctypes.c_int64 * nt)(*sizes)), nt,
+         {"feddyn": _lib.FLC_SRV_FEDDYN, "pfedme": _lib.FLC_SRV_PFEDME}[kind], int(bool(fold)), int(init_mode),
+         float(inertia), float(c), _stream(theta[0].device))
+
+
 def model_fold(dsts: Sequence[torch.Tensor], srcs: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
                init_mode: int, beta: float = 0.0, theta: Optional[Sequence[torch.Tensor]] = None,
                v: Optional[Sequence[torch.Tensor]] = None, opt: str = "avg", lr: float = 1.0, beta2: float = 0.0,

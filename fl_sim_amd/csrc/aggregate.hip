@@ -337,6 +337,90 @@ __global__ __launch_bounds__(kThreads) void model_fold_kernel(ModelPack p, float
   }
 }
 
+// FedDyn / pFedMe server updates on a whole model in one pass (flc_model_fold_server), the model pack as in
+// model_fold_kernel with `theta` holding the second per-element state (FedDyn's h, pFedMe's saved θ):
+//   KIND 1 FedDyn (feddyn/_feddyn.py:172-184): per message m in order h = fmaf(c, fl(src_m - θ0), h)
+//          (hp.add_(mp - p, alpha=-mu/N) with the model still at θ0); FOLD: θ = the avg fold of θ0 (INIT 0: θ0 * beta
+//          first, avg_parameters' mul_(inertia)), line 184's p.add(...) is dropped by the reference (no effect);
+//   KIND 2 pFedMe (pfedme/_pfedme.py:166-175): FOLD: a = the avg fold of θ0 (INIT 0, or INIT 2 with no message:
+//          avg_parameters returns early), then θ = fmaf(c2, θ0, fl(a * c)) (mul_(beta).add_(prev, alpha=1-beta));
+//          !FOLD (more messages than one launch folds: the fold ran in chained model_fold launches, θ0 saved in
+//          `theta`): θ = fmaf(c2, saved, fl(θ * c)).
+// Every step rounds where the reference's torch CPU ops round (add_(alpha) is one fma, mul_ and the subtraction one
+// rounding each); nothing else is contracted (-ffp-contract=off).
+template <int KIND, bool FOLD, int INIT>
+__device__ __forceinline__ float server_elem(float th0, float* __restrict__ aux, const ModelPack& p, int t, int64_t e,
+                                             float beta, float c, float c2) {
+  if (KIND == 1) {
+    float h = *aux;
+    for (int m = 0; m < p.ns; ++m) h = fmaf(c, p.src[m][t][e] - th0, h);
+    *aux = h;
+    if (!FOLD) return th0;
+  }
+  float a = th0;
+  if (FOLD) {
+    a = INIT == 0 ? th0 * beta : th0;
+    for (int m = 0; m < p.ns; ++m) a = fmaf(p.w[m], p.src[m][t][e], a);
+  }
+  if (KIND == 2) return fmaf(c2, FOLD ? th0 : *aux, a * c);
+  return a;
+}
+
+template <int KIND, bool FOLD, int INIT>
+__global__ __launch_bounds__(kThreads) void server_fold_kernel(ModelPack p, float beta, float c, float c2) {
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < p.nt && p.blk0[t + 1] <= b) ++t;  // uniform: <= kModelT steps
+  float* __restrict__ dst = p.dst[t];
+  float* __restrict__ aux = p.theta[t];
+  const int64_t n = p.n[t];
+  const int64_t c0 = (int64_t)(b - p.blk0[t]) * kModelChunk;
+  const int64_t c1 = c0 + kModelChunk < n ? c0 + kModelChunk : n;
+  if ((p.vec >> t) & 1u) {
+    for (int64_t i = c0 + 4 * (int64_t)threadIdx.x; i < c1; i += 4 * kThreads) {
+      if (i + 4 > c1) {  // the tensor's n % 4 tail
+        for (int64_t e = i; e < c1; ++e) dst[e] = server_elem<KIND, FOLD, INIT>(dst[e], aux + e, p, t, e, beta, c, c2);
+        break;
+      }
+      // every operand's float4 loaded first, then the chains in message order (weighted_sum's shape)
+      float4 sv[kMaxSrc];
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m)
+        if (m < p.ns) sv[m] = *reinterpret_cast<const float4*>(p.src[m][t] + i);
+      const float4 t0 = *reinterpret_cast<const float4*>(dst + i);
+      float4 x = *reinterpret_cast<const float4*>(aux + i);  // FedDyn: h; pFedMe !FOLD: the saved θ0
+      float4 a = t0;
+      if (KIND == 1) {
+#pragma unroll
+        for (int m = 0; m < kMaxSrc; ++m)
+          if (m < p.ns)
+            x = make_float4(fmaf(c, sv[m].x - t0.x, x.x), fmaf(c, sv[m].y - t0.y, x.y), fmaf(c, sv[m].z - t0.z, x.z),
+                            fmaf(c, sv[m].w - t0.w, x.w));
+        *reinterpret_cast<float4*>(aux + i) = x;
+      }
+      if (FOLD) {
+        if (INIT == 0) a = make_float4(t0.x * beta, t0.y * beta, t0.z * beta, t0.w * beta);
+#pragma unroll
+        for (int m = 0; m < kMaxSrc; ++m) {
+          if (m < p.ns) {
+            const float w = p.w[m];
+            a = make_float4(fmaf(w, sv[m].x, a.x), fmaf(w, sv[m].y, a.y), fmaf(w, sv[m].z, a.z), fmaf(w, sv[m].w, a.w));
+          }
+        }
+      }
+      if (KIND == 2) {
+        const float4 pr = FOLD ? t0 : x;
+        a = make_float4(fmaf(c2, pr.x, a.x * c), fmaf(c2, pr.y, a.y * c), fmaf(c2, pr.z, a.z * c),
+                        fmaf(c2, pr.w, a.w * c));
+      }
+      if (KIND == 2 || FOLD) *reinterpret_cast<float4*>(dst + i) = a;
+    }
+    return;
+  }
+  for (int64_t e = c0 + threadIdx.x; e < c1; e += kThreads)
+    dst[e] = server_elem<KIND, FOLD, INIT>(dst[e], aux + e, p, t, e, beta, c, c2);
+}
+
 // up to 64 blocks of 256 threads per CU of a 256-CU device, grid-stride beyond (tools/wsum_probe.hip, 8 x 25 M:
 // 16 K blocks 160-162 us against 169-170 us for 4 K, 163 us for one float4 per thread; profiles/r03/r03p_wsum2.txt)
 unsigned grid_for(int64_t work) {
@@ -444,6 +528,63 @@ int flc_model_fold(float* const* dst, const float* const* srcs, const float* wei
     else { FLC_MF_OPT(2); }
 #undef FLC_MF_OPT
 #undef FLC_MF
+  }
+  return FLC_OK;
+}
+
+int flc_model_fold_server(float* const* theta, float* const* aux, const float* const* srcs, const float* weights,
+                          int n_src, const int64_t* sizes, int n_tensors, int kind, int fold, int init_mode,
+                          float inertia, double c, void* stream) {
+  if (n_tensors < 0 || (n_tensors > 0 && (!theta || !aux || !sizes)) || n_src < 0 || n_src > kMaxSrc ||
+      (n_src > 0 && (!srcs || !weights)))
+    return fail(FLC_EINVAL, "flc_model_fold_server: bad arguments (at most %d sources)", kMaxSrc);
+  if (kind != FLC_SRV_FEDDYN && kind != FLC_SRV_PFEDME) return fail(FLC_EINVAL, "flc_model_fold_server: unknown kind %d", kind);
+  if (init_mode != 0 && init_mode != 2) return fail(FLC_EINVAL, "flc_model_fold_server: init_mode must be 0 or 2");
+  if (kind == FLC_SRV_PFEDME && !fold && n_src != 0)
+    return fail(FLC_EINVAL, "flc_model_fold_server: the pFedMe blend alone takes no sources");
+  hipStream_t st = as_stream(stream);
+  // the reference's scalars are Python doubles cast to fp32 by torch: FedDyn alpha = -mu/N, pFedMe beta and 1 - beta
+  const float cf = (float)c, c2f = (float)(1.0 - c);
+  for (int t0 = 0; t0 < n_tensors; t0 += kModelT) {
+    ModelPack p{};
+    p.ns = n_src;
+    for (int m = 0; m < n_src; ++m) p.w[m] = weights[m];
+    int blocks = 0;
+    for (int t = t0; t < std::min(n_tensors, t0 + kModelT); ++t) {
+      if (sizes[t] < 0) return fail(FLC_EINVAL, "flc_model_fold_server: negative size for tensor %d", t);
+      if (sizes[t] == 0) continue;
+      if (!theta[t] || !aux[t]) return fail(FLC_EINVAL, "flc_model_fold_server: null pointer for tensor %d", t);
+      const int i = p.nt++;
+      p.dst[i] = theta[t];
+      p.theta[i] = aux[t];
+      p.n[i] = sizes[t];
+      bool vec = aligned16(theta[t]) && aligned16(aux[t]);
+      for (int m = 0; m < n_src; ++m) {
+        const float* sp = srcs[(size_t)m * n_tensors + t];
+        if (!sp) return fail(FLC_EINVAL, "flc_model_fold_server: null source %d of tensor %d", m, t);
+        p.src[m][i] = sp;
+        vec = vec && aligned16(sp);
+      }
+      if (vec) p.vec |= 1u << i;
+      p.blk0[i] = blocks;
+      const int64_t nb = cdiv(sizes[t], kModelChunk);
+      if (blocks + nb > 0x7fffffff) return fail(FLC_EINVAL, "flc_model_fold_server: too many elements");
+      blocks += (int)nb;
+    }
+    p.blk0[p.nt] = blocks;
+    if (blocks == 0) continue;
+#define FLC_SF(K, F, I) \
+  FLC_LAUNCH("model_fold_server", (server_fold_kernel<K, F, I>), dim3(blocks), dim3(kThreads), 0, st, p, inertia, cf, c2f)
+    if (kind == FLC_SRV_FEDDYN) {
+      if (!fold) FLC_SF(FLC_SRV_FEDDYN, false, 0);
+      else if (init_mode == 0) FLC_SF(FLC_SRV_FEDDYN, true, 0);
+      else FLC_SF(FLC_SRV_FEDDYN, true, 2);
+    } else {
+      if (!fold) FLC_SF(FLC_SRV_PFEDME, false, 2);
+      else if (init_mode == 0) FLC_SF(FLC_SRV_PFEDME, true, 0);
+      else FLC_SF(FLC_SRV_PFEDME, true, 2);
+    }
+#undef FLC_SF
   }
   return FLC_OK;
 }

@@ -378,6 +378,20 @@ int flc_weighted_sum(const float* const* srcs, const float* weights, int n_src, 
 int flc_model_fold(float* const* dst, const float* const* srcs, const float* weights, int n_src, const int64_t* sizes,
                    int n_tensors, int init_mode, float beta, float* const* theta, float* const* v, int opt, double lr,
                    double beta2, double tau, void* stream);
+/* FedDyn's and pFedMe's server updates on a whole model, one pass per <= 16 tensors and <= 16 messages
+ * (theta = the model, aux = the per-element second state; srcs[m * n_tensors + t] = message m's tensor t):
+ *   FLC_SRV_FEDDYN (feddyn/_feddyn.py:172-184): h = aux, for each message in order h = fmaf(c, fl(src - theta0), h)
+ *     with c = fp32(-mu / num_clients); with `fold`, theta = the avg_parameters fold of theta0 in the same pass
+ *     (init_mode 0: theta0 * inertia first, then fmaf(weights[m], src, .) in order); line 184's result is discarded
+ *     by the reference, so nothing follows.  Without `fold` only h is updated (theta read-only: the chained form).
+ *   FLC_SRV_PFEDME (pfedme/_pfedme.py:166-175): with `fold`, a = the avg fold of theta0 (init_mode 0, or 2 when the
+ *     round has no message: avg_parameters returns early), then theta = fmaf(fp32(1 - c), theta0, fl(a * fp32(c)))
+ *     with c = beta; without `fold` (no sources: the fold ran in chained flc_model_fold launches and aux holds the
+ *     saved theta0) theta = fmaf(fp32(1 - c), aux, fl(theta * fp32(c))). */
+enum flc_server_kind { FLC_SRV_FEDDYN = 1, FLC_SRV_PFEDME = 2 };
+int flc_model_fold_server(float* const* theta, float* const* aux, const float* const* srcs, const float* weights,
+                          int n_src, const int64_t* sizes, int n_tensors, int kind, int fold, int init_mode,
+                          float inertia, double c, void* stream);
 /* the rest of FedOptServer.update after the delta average (_fedopt.py:212-265):
  *   avg:     theta = fmaf(lr, delta, theta)
  *   adagrad: v = v + delta^2;                               theta += lr * delta / (sqrt(v) + tau)

@@ -5,7 +5,8 @@ torch-CPU restatement of the reference's server aggregation, operation for opera
 and ``FedOptServer.update`` with its avg/adagrad/yogi/adam tails (fl_sim/algorithms/fedopt/
 _fedopt.py:196-265); the f4 variants ``SCAFFOLDServer.update`` (scaffold/_scaffold.py:158-167), ``IFCAServer.update``
 (ifca/_ifca.py:167-195) and ``FedDRServer.update`` (feddr/_feddr.py:166-190) with the regularizers' proximal steps
-(regularizers/regularizers.py:146-200).  It runs the same torch CPU kernels the reference runs (``mul_``, ``add_`` with
+(regularizers/regularizers.py:146-200); and (round 5) ``FedDynServer.update`` (feddyn/_feddyn.py:172-184) and
+``pFedMeServer.update`` (pfedme/_pfedme.py:166-175).  It runs the same torch CPU kernels the reference runs (``mul_``, ``add_`` with
 ``alpha``, ``addcmul_``, ``addcdiv_``), so it rounds exactly where the reference rounds.  Pinned by
 ``tests/golden/agg.npz`` and ``agg_variants.npz``, produced by executing the reference's own method bodies
 (``tests/golden/gen_golden.py``).
@@ -144,3 +145,18 @@ def client_delta(local_params, cached_params):
     for dp, rp in zip(deltas, cached_params):
         dp.add_(rp, alpha=-1)
     return deltas
+
+
+def feddyn_update(params, h_params, messages, mu: float, num_clients: int) -> None:
+    for m in messages:  # feddyn/_feddyn.py:174-180: h updated against the model before the average
+        for hp, p, mp in zip(h_params, params, m["parameters"]):
+            hp.add_(mp - p, alpha=-mu / num_clients)
+    avg_parameters(params, messages)  # _feddyn.py:182
+    # _feddyn.py:183-184: `p = p.add(...)` rebinds a local name; the model is not changed
+
+
+def pfedme_update(params, messages, beta: float) -> None:
+    previous = [p.detach().clone() for p in params]  # pfedme/_pfedme.py:166-167
+    avg_parameters(params, messages)  # _pfedme.py:170
+    for pre, p in zip(previous, params):  # _pfedme.py:173-174
+        p.mul_(beta).add_(pre.detach().clone(), alpha=1 - beta)

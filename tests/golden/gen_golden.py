@@ -14,7 +14,8 @@ Aggregation fixtures (``agg_*.npz``): FedOptServer.update (avg/adam/yogi/adagrad
 (size_aware x inertia) and update_gradients on small model shapes (full arrays) and on the
 cnn_femmist_tiny shapes of config 1 (SHA-256 of the outputs).
 
-Variant fixtures (``agg_variants.npz``): SCAFFOLDServer.update, IFCAServer.update (centers and the
+Variant fixtures (``agg_variants.npz``): FedDynServer.update, pFedMeServer.update (round 5),
+SCAFFOLDServer.update, IFCAServer.update (centers and the
 client-id bookkeeping), FedDRServer.update under each constructible regularizer, and FedOptClient.communicate's
 client delta, same shapes.
 
@@ -635,6 +636,8 @@ IFCA_CLUSTER_OF = [0, 2, 0, 0, 2, 3, 0, 2, 3, 0]  # cluster 1 receives no messag
 IFCA_PREV_IDS = {0: [0, 2, 11, 12], 1: [13, 14], 2: [1, 4, 15], 3: [5, 8]}
 FEDDR_REGS = ("l1_norm", "l2_norm", "l2_norm_squared", "none")
 SCAFFOLD_CFG = dict(lr=0.05, num_clients=20)
+FEDDYN_CFG = dict(mu=0.01, num_clients=20)
+PFEDME_BETAS = (1.0, 0.7)
 FEDDR_CFG = dict(alpha=0.9, eta=0.05, num_clients=10)
 
 
@@ -657,6 +660,25 @@ def feddr_inputs(shapes):
     ys = [p.detach().clone() for p in make_model(shapes, 31).parameters()]
     xts = [p.detach().clone() for p in make_model(shapes, 32).parameters()]
     return params, ys, xts, variant_msgs(shapes, FEDDR_CFG["num_clients"], 12, ("x_hat_delta",))
+
+
+def feddyn_inputs(shapes, n_msgs=10):
+    """(model params, h_params, messages) of the FedDyn fixture: a nonzero h from an earlier round."""
+    params = [p.detach().clone() for p in make_model(shapes, 50).parameters()]
+    g = torch.Generator().manual_seed(51)
+    hs = [torch.randn(sh, generator=g) * 1e-3 for sh in shapes]
+    msgs = variant_msgs(shapes, n_msgs, 52, ("parameters",))
+    for m in msgs:  # client models near the server's
+        m["parameters"] = [p + d for p, d in zip(params, m["parameters"])]
+    return params, hs, msgs
+
+
+def pfedme_inputs(shapes, n_msgs=10):
+    params = [p.detach().clone() for p in make_model(shapes, 60).parameters()]
+    msgs = variant_msgs(shapes, n_msgs, 61, ("parameters",))
+    for m in msgs:
+        m["parameters"] = [p + d for p, d in zip(params, m["parameters"])]
+    return params, msgs
 
 
 def delta_inputs(shapes):
@@ -714,6 +736,38 @@ def gen_variants():
             put(f"feddr_{reg}_{tag}|theta", list(s.model.parameters()))
             put(f"feddr_{reg}_{tag}|y", s._y_parameters)
             put(f"feddr_{reg}_{tag}|xtil", s._x_til_parameters)
+        # FedDynServer.update (feddyn/_feddyn.py:172-184) and pFedMeServer.update (pfedme/_pfedme.py:166-175), on top
+        # of the reference's own avg_parameters / add_parameters; 10 messages (one launch) and 20 (chained)
+        srv_avg = compile_methods("fl_sim/nodes.py", "Server", ("add_parameters", "avg_parameters"), ns)
+        node = compile_methods("fl_sim/nodes.py", "Node", ("get_detached_model_parameters",), ns)
+        feddyn = compile_methods("fl_sim/algorithms/feddyn/_feddyn.py", "FedDynServer", ("update",), ns)["update"]
+        pfedme = compile_methods("fl_sim/algorithms/pfedme/_pfedme.py", "pFedMeServer", ("update",), ns)["update"]
+
+        def server_ns(params):
+            s = types.SimpleNamespace(device=torch.device("cpu"))
+            s.model = torch.nn.Module()
+            for i, t in enumerate(params):
+                s.model.register_parameter(f"p{i}", torch.nn.Parameter(t.clone()))
+            for name, fn in {**srv_avg, **node}.items():
+                setattr(s, name, types.MethodType(fn, s))
+            return s
+
+        for nm in (10, 20, 0):
+            params, hs, msgs = feddyn_inputs(shapes, nm)
+            s = server_ns(params)
+            s.config = types.SimpleNamespace(**FEDDYN_CFG)
+            s.h_params, s._received_messages = hs, msgs
+            feddyn(s)
+            put(f"feddyn_{nm}_{tag}|theta", list(s.model.parameters()))
+            put(f"feddyn_{nm}_{tag}|h", s.h_params)
+            for beta in PFEDME_BETAS:
+                params, msgs = pfedme_inputs(shapes, nm)
+                s = server_ns(params)
+                s.config = types.SimpleNamespace(beta=beta)
+                s._received_messages = msgs
+                pfedme(s)
+                put(f"pfedme_{beta}_{nm}_{tag}|theta", list(s.model.parameters()))
+
         # FedOptClient.communicate (_fedopt.py:294-307): the per-tensor client delta (f1)
         comm = compile_methods("fl_sim/algorithms/fedopt/_fedopt.py", "FedOptClient", ("communicate",),
                                {**ns, "ClientMessage": dict})["communicate"]

@@ -384,3 +384,61 @@ def test_fold_with_host_messages_equals_device_messages(fold_path):
     aggregation.avg_parameters(a, host_msgs, True, 0.3)
     aggregation.avg_parameters(b, _msgs_dev(host_msgs, "parameters"), True, 0.3)
     assert all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(a, b))
+
+
+# ------------------------------------------------------------------- FedDyn / pFedMe server updates (round 5)
+from tests.golden.gen_golden import FEDDYN_CFG, PFEDME_BETAS, feddyn_inputs, pfedme_inputs  # noqa: E402
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+@pytest.mark.parametrize("nm", [10, 20, 0])
+def test_feddyn_update_matches_reference(tag, shapes, nm):
+    """FedDynServer.update (feddyn/_feddyn.py:172-184): h and θ in one launch (10 messages) or chained (20), against
+    the reference's own outputs, bit for bit (line 184's discarded result included: θ is the average)."""
+    from fl_sim_amd import aggregation
+
+    params, hs, msgs = feddyn_inputs(shapes, nm)
+    params, hs = _dev(params), _dev(hs)
+    aggregation.feddyn_update(params, hs, _msgs_dev(msgs, "parameters"), FEDDYN_CFG["mu"], FEDDYN_CFG["num_clients"])
+    assert _golden_v(f"feddyn_{nm}_{tag}|h", hs)[0], "h must be bit-exact"
+    assert _golden_v(f"feddyn_{nm}_{tag}|theta", params)[0], "theta must be bit-exact"
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+@pytest.mark.parametrize("nm", [10, 20, 0])
+@pytest.mark.parametrize("beta", PFEDME_BETAS)
+def test_pfedme_update_matches_reference(tag, shapes, nm, beta):
+    """pFedMeServer.update (pfedme/_pfedme.py:166-175): the average and the β blend with the saved model in one launch
+    (10 messages; 0: the blend of θ with itself), or the chained average and one blend pass (20)."""
+    from fl_sim_amd import aggregation
+
+    params, msgs = pfedme_inputs(shapes, nm)
+    params = _dev(params)
+    aggregation.pfedme_update(params, _msgs_dev(msgs, "parameters"), beta)
+    assert _golden_v(f"pfedme_{beta}_{nm}_{tag}|theta", params)[0], "theta must be bit-exact"
+
+
+def test_model_fold_server_misaligned_and_odd_tensors_equal_the_oracle():
+    """The fused server pass on views that are not 16-B aligned and tensors of odd sizes (the scalar path) against
+    the oracle's torch ops, both kinds."""
+    from fl_sim_amd import aggregation
+
+    shapes = [(7,), (3, 5), (1,), (1029,), (4, 4, 3)]
+    for kind in ("feddyn", "pfedme"):
+        params, hs, msgs = feddyn_inputs(shapes, 5)
+        big = torch.zeros(sum(int(np.prod(s)) for s in shapes) + 1, device="cuda")
+        views, off = [], 1  # (offset 1: every view 4-B aligned, none 16-B aligned)
+        for p in params:
+            v = big[off:off + p.numel()].view(p.shape)
+            v.copy_(p)
+            views.append(v)
+            off += p.numel()
+        dh = _dev(hs)
+        if kind == "feddyn":
+            agg_ref.feddyn_update(params, hs, msgs, 0.05, 7)
+            aggregation.feddyn_update(views, dh, _msgs_dev(msgs, "parameters"), 0.05, 7)
+            assert gc.same_bits(_flat(dh), _flat(hs))
+        else:
+            agg_ref.pfedme_update(params, msgs, 0.3)
+            aggregation.pfedme_update(views, _msgs_dev(msgs, "parameters"), 0.3)
+        assert gc.same_bits(_flat(views), _flat(params)), kind

@@ -257,6 +257,55 @@ def test_host_server_feddr_matches_reference(tag, shapes, reg):
     assert _sha(list(s.model.parameters())) == str(AGGV[f"feddr_{reg}_{tag}|theta|sha"])
 
 
+from tests.golden.gen_golden import FEDDYN_CFG, PFEDME_BETAS, feddyn_inputs, pfedme_inputs  # noqa: E402
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+@pytest.mark.parametrize("nm", [10, 20])
+@pytest.mark.parametrize("where", ["host", "cuda"])
+def test_host_server_feddyn_matches_reference(tag, shapes, nm, where):
+    """FedDynServer.update on the reference's CPU server (model and h in host memory), messages on the device or the
+    host: the mixin's result equals the reference's bit for bit."""
+    from fl_sim_amd.aggregation import AggregationMixin, FedDynUpdateMixin
+
+    class Server(FedDynUpdateMixin, AggregationMixin):
+        pass
+
+    params, hs, msgs = feddyn_inputs(shapes, nm)
+    s = Server()
+    s.model = torch.nn.Module()
+    for i, p in enumerate(params):
+        s.model.register_parameter(f"p{i}", torch.nn.Parameter(p.clone()))
+    s.h_params = [t.clone() for t in hs]
+    s._received_messages = _msgs_on(msgs, "parameters", where)
+    s.config = _Cfg(**FEDDYN_CFG)
+    s.update()
+    assert all(p.device.type == "cpu" for p in s.model.parameters()) and all(h.device.type == "cpu" for h in s.h_params)
+    assert _sha(s.h_params) == str(AGGV[f"feddyn_{nm}_{tag}|h|sha"])
+    assert _sha(list(s.model.parameters())) == str(AGGV[f"feddyn_{nm}_{tag}|theta|sha"])
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+@pytest.mark.parametrize("nm", [10, 20, 0])
+@pytest.mark.parametrize("beta", PFEDME_BETAS)
+def test_host_server_pfedme_matches_reference(tag, shapes, nm, beta):
+    from fl_sim_amd.aggregation import AggregationMixin, pFedMeUpdateMixin
+
+    class Server(pFedMeUpdateMixin, AggregationMixin):
+        pass
+
+    params, msgs = pfedme_inputs(shapes, nm)
+    s = Server()
+    s.model = torch.nn.Module()
+    for i, p in enumerate(params):
+        s.model.register_parameter(f"p{i}", torch.nn.Parameter(p.clone()))
+    s._received_messages = _msgs_on(msgs, "parameters", "cuda")
+    s.config = _Cfg(beta=beta)
+    s.update()
+    assert all(p.device.type == "cpu" for p in s.model.parameters())
+    assert _sha(list(s.model.parameters())) == str(AGGV[f"pfedme_{beta}_{nm}_{tag}|theta|sha"])
+
+
 def test_host_server_pinned_parameters_behave_as_cpu_tensors():
     """Adoption moves the storage into pinned host memory: the model still runs on the CPU (forward, in-place ops,
     state_dict round trip) with unchanged values."""

@@ -182,3 +182,25 @@ def test_client_delta_oracle_matches_reference(tag, shapes):
 
     local, cached = delta_inputs(shapes)
     _check_v(f"delta_{tag}|delta", agg_ref.client_delta(local, cached))
+
+
+# ------------------------------------------------------------------- FedDyn / pFedMe server updates (round 5)
+from tests.golden.gen_golden import FEDDYN_CFG, PFEDME_BETAS, feddyn_inputs, pfedme_inputs  # noqa: E402
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+@pytest.mark.parametrize("nm", [10, 20, 0])
+def test_feddyn_oracle_matches_reference(tag, shapes, nm):
+    params, hs, msgs = feddyn_inputs(shapes, nm)
+    agg_ref.feddyn_update(params, hs, msgs, FEDDYN_CFG["mu"], FEDDYN_CFG["num_clients"])
+    _check_v(f"feddyn_{nm}_{tag}|theta", params)
+    _check_v(f"feddyn_{nm}_{tag}|h", hs)
+
+
+@pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
+@pytest.mark.parametrize("nm", [10, 20, 0])
+@pytest.mark.parametrize("beta", PFEDME_BETAS)
+def test_pfedme_oracle_matches_reference(tag, shapes, nm, beta):
+    params, msgs = pfedme_inputs(shapes, nm)
+    agg_ref.pfedme_update(params, msgs, beta)
+    _check_v(f"pfedme_{beta}_{nm}_{tag}|theta", params)
