@@ -60,6 +60,8 @@ constexpr int kBlockStep = kENW * kWaveSpan;  // 16384 elements per block step
 constexpr int kCap = 16384;                   // candidates per block kept in LDS
 constexpr int kSample = 32768;
 constexpr int kSPT = kSample / kET;           // 32 sample keys per thread
+constexpr int kTopPer = 8;                    // compact sample: the 8 largest keys of each 64-key wave of the sample ...
+constexpr int kSampTop = kSample / 64 * kTopPer;  // ... 4096 keys, 4 per encode thread (single-client calls)
 constexpr int kHistBits = 11;
 constexpr int kHistBins = 1 << kHistBits;
 constexpr int kHistStride = kHistBins + 64;   // bins, [kHistBins] above-the-range count, [+1] max key
@@ -100,7 +102,8 @@ constexpr size_t kOffBlk = al256(kOffAcc + 64);
 constexpr size_t kOffStamps = al256(kOffBlk + (size_t)kMaxBlocks * 8);
 constexpr size_t kOffBlkT = al256(kOffStamps + 128);   // [kMaxBlocks][4] per-block times (diagnostic build)
 constexpr size_t kOffSample = al256(kOffBlkT + (size_t)kMaxBlocks * 32);
-constexpr size_t kOffInbin = al256(kOffSample + (size_t)kSample * 4);
+constexpr size_t kOffSampTop = al256(kOffSample + (size_t)kSample * 4);
+constexpr size_t kOffInbin = al256(kOffSampTop + (size_t)kSampTop * 4);
 constexpr size_t kOffBlkC = al256(kOffInbin + (size_t)kMaxBlocks * kInbin * 4);
 constexpr size_t kOffPair = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // per block pair: its step-claim word
 constexpr size_t kOffStage = al256(kOffPair + (size_t)(kMaxBlocks / 2) * 8);  // + G * kCap * 8 (keys, then indices)
@@ -120,6 +123,7 @@ struct EncWs {
   int bid, nb;    // this block's index in its select, the blocks of its select (set in the kernel prologue)
   size_t vstride; // batched: bytes between two clients' staging / overflow areas
   int pair_r;     // paired pass (see filter_phase): dynamic steps per block side, 0 = static ranges
+  int compact;    // the sample kernel wrote the compact sample (samptop): the floor / ceiling start from it
   unsigned long long* errp;
   __device__ EncState* st() const { return reinterpret_cast<EncState*>(base + kOffSt); }
   __device__ unsigned* flags() const { return reinterpret_cast<unsigned*>(base + kOffFlags); }
@@ -129,6 +133,7 @@ struct EncWs {
   __device__ unsigned long long* stamps() const { return reinterpret_cast<unsigned long long*>(base + kOffStamps); }
   __device__ unsigned long long* blkt() const { return reinterpret_cast<unsigned long long*>(base + kOffBlkT); }
   __device__ unsigned* sample() const { return reinterpret_cast<unsigned*>(base + kOffSample); }
+  __device__ unsigned* samptop() const { return reinterpret_cast<unsigned*>(base + kOffSampTop); }
   __device__ unsigned* inbin() const { return reinterpret_cast<unsigned*>(base + kOffInbin); }
   __device__ unsigned* blk_c() const { return reinterpret_cast<unsigned*>(base + kOffBlkC); }  // candidates / block
   __device__ unsigned long long* pairw() const { return reinterpret_cast<unsigned long long*>(base + kOffPair); }  // (32 bits used)
@@ -216,6 +221,7 @@ EncWs carve_enc(void* ws, int64_t n, int64_t k, int cus, size_t* need) {
   w.nb = g.G;
   w.vstride = 0;
   w.pair_r = 0;
+  w.compact = 0;
   w.errp = reinterpret_cast<unsigned long long*>(w.base + kOffSt + offsetof(EncState, err));
   *need = kOffStage + vb;
   return w;
@@ -344,6 +350,7 @@ struct SampleLds {
   unsigned digit[2];
   long long rem[2];
   unsigned err;
+  unsigned bad;  // compact sample: some wave of the sample holds more keys above the floor than its 8 listed
 };
 
 // sample index of a thread's key slot i: 16-B runs, so the coherent read is 8 x 16 B per thread
@@ -373,18 +380,26 @@ __device__ __forceinline__ void load_sample_keys(const unsigned* sample, int S, 
 // the end of rank_hi's bin (fewer than rank_hi sample keys at or above it).
 // Two halves: the histogram (the keys' last use in registers: the caller issues the second HBM step
 // in their place) and the pick (the rare refinement re-reads the keys).
-__device__ __forceinline__ void sample_fast_hist(const unsigned (&keys)[kSPT], int S, SampleLds& L, unsigned* s_hist,
+// N = kSPT: the full sample (slot i valid when sample_j(i) < S); N = 4: the compact sample (every slot valid)
+template <int N>
+__device__ __forceinline__ bool sample_slot_valid(int i, int S) { return N != kSPT || sample_j(i) < S; }
+
+template <int N>
+__device__ __forceinline__ void sample_fast_hist(const unsigned (&keys)[N], int S, SampleLds& L, unsigned* s_hist,
                                                  unsigned* B_out, int* sh_out) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   unsigned m = 0;
 #pragma unroll
-  for (int i = 0; i < kSPT; ++i) m = keys[i] > m ? keys[i] : m;  // invalid slots hold key 0
+  for (int i = 0; i < N; ++i) m = keys[i] > m ? keys[i] : m;  // invalid slots hold key 0
   const unsigned wmn = wave_min_u32(m), wmx = wave_max_u32(m);
   if (lane == 0) {
     L.wmin[wid] = wmn;
     L.wmax[wid] = wmx;
   }
-  if (tid == 0) L.err = 0;
+  if (tid == 0) {
+    L.err = 0;
+    L.bad = 0;
+  }
   for (int i = tid; i < kHistBins; i += kET) {
     s_hist[i] = 0u;
     L.hist2[i] = 0u;
@@ -398,12 +413,14 @@ __device__ __forceinline__ void sample_fast_hist(const unsigned (&keys)[kSPT], i
   }
   const int sh = range_shift((unsigned long long)mx - B + 1ull, kHistBits);
 #pragma unroll
-  for (int i = 0; i < kSPT; ++i)
-    if (sample_j(i) < S && keys[i] >= B) atomicAdd(&s_hist[(keys[i] - B) >> sh], 1u);
+  for (int i = 0; i < N; ++i)
+    if (sample_slot_valid<N>(i, S) && keys[i] >= B) atomicAdd(&s_hist[(keys[i] - B) >> sh], 1u);
   *B_out = B;
   *sh_out = sh;
 }
 
+// (N = 4: `sample` is the compact sample, the refinement re-reads the thread's 4 keys of it)
+template <int N>
 __device__ __forceinline__ bool sample_fast_pick(const unsigned* sample, int S, long long rank_lo, long long rank_hi,
                                                  unsigned B, int sh, SampleLds& L, unsigned* s_hist,
                                                  unsigned long long* s_red, unsigned* t_lo_out,
@@ -419,8 +436,14 @@ __device__ __forceinline__ bool sample_fast_pick(const unsigned* sample, int S, 
   int sh_hi = sh;
   const bool ref0 = sh > 0 && s_hist[d0] > 8u, ref1 = two && sh > 0 && s_hist[d1] > 8u;  // block-uniform
   if (ref0 || ref1) {
-    unsigned keys[kSPT];
-    load_sample_keys(sample, S, keys);
+    unsigned keys[N];
+    if constexpr (N == kSPT) {
+      load_sample_keys(sample, S, keys);
+    } else {
+      static_assert(N == 4, "compact sample: 4 keys per thread");
+      const uint4 t4 = *reinterpret_cast<const uint4*>(sample + 4 * tid);
+      keys[0] = t4.x; keys[1] = t4.y; keys[2] = t4.z; keys[3] = t4.w;
+    }
     const long long r0 = L.rem[0], r1 = two ? L.rem[1] : 0;
     const int sh2 = sh > kHistBits ? sh - kHistBits : 0;
     const unsigned long long bw = 1ull << sh;
@@ -428,8 +451,8 @@ __device__ __forceinline__ bool sample_fast_pick(const unsigned* sample, int S, 
     for (int i = tid; i < kHistBins; i += kET) s_hist[i] = 0u;
     lds_barrier();
 #pragma unroll
-    for (int i = 0; i < kSPT; ++i) {
-      if (sample_j(i) >= S) continue;
+    for (int i = 0; i < N; ++i) {
+      if (!sample_slot_valid<N>(i, S)) continue;
       const unsigned long long rel0 = (unsigned long long)keys[i] - lo0, rel1 = (unsigned long long)keys[i] - lo1;
       if (ref0 && keys[i] >= lo0 && rel0 < bw) atomicAdd(&s_hist[(unsigned)(rel0 >> sh2)], 1u);
       if (ref1 && keys[i] >= lo1 && rel1 < bw) atomicAdd(&L.hist2[(unsigned)(rel1 >> sh2)], 1u);
@@ -1022,10 +1045,12 @@ __device__ __forceinline__ unsigned long long* stamp_lds() {
 // sample kernel
 // ------------------------------------------------------------------------------------------------
 template <class Src>
-__device__ __forceinline__ void sample_one(const Src& x, int64_t n, int S, const EncWs& w, int j) {
-  if (j >= S) return;
+__device__ __forceinline__ unsigned sample_one(const Src& x, int64_t n, int S, const EncWs& w, int j) {
+  if (j >= S) return 0u;
   const int64_t pos = (S == n) ? (int64_t)j : (int64_t)(((double)j + 0.5) * (double)n / (double)S);
-  w.sample()[j] = order_key(__float_as_uint(x.get(pos < n ? pos : n - 1)));
+  const unsigned key = order_key(__float_as_uint(x.get(pos < n ? pos : n - 1)));
+  w.sample()[j] = key;
+  return key;
 }
 
 template <class Src>
@@ -1033,7 +1058,20 @@ __global__ __launch_bounds__(256) void topk_sample_kernel(Src x, int64_t n, int 
 #ifdef FLC_SELECT_STAMPS  // diagnostic timeline: each sample block's start and end (blkt rows 512 + b)
   if (threadIdx.x == 0 && blockIdx.x < 256) w.blkt()[(512 + blockIdx.x) * 4] = __builtin_amdgcn_s_memrealtime();
 #endif
-  sample_one(x, n, S, w, blockIdx.x * 256 + threadIdx.x);
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  unsigned key = sample_one(x, n, S, w, j);
+  if (w.compact) {  // (S == kSample: every lane holds a key) the wave's 8 largest keys, descending: the compact sample
+    const int lane = (int)(threadIdx.x & (kWave - 1));
+    unsigned mine = 0u;
+#pragma unroll
+    for (int r = 0; r < kTopPer; ++r) {
+      const unsigned m = wave_max_u32(key);
+      if (lane == r) mine = m;
+      const unsigned long long at = __ballot(key == m);
+      if (lane == __ffsll((long long)at) - 1) key = 0u;  // one instance of it leaves the wave's set
+    }
+    if (lane < kTopPer) w.samptop()[(j >> 6) * kTopPer + lane] = mine;
+  }
   // the paired pass's step-claim words start every call from zero (this kernel precedes the encode in the stream)
   if (w.pair_r > 0 && blockIdx.x == 0)
     for (int i = (int)threadIdx.x; i < (w.nb + 1) / 2; i += 256) w.pairw()[i] = 0ull;
@@ -1103,7 +1141,7 @@ __global__ __launch_bounds__(256) void topk_sample_batch_kernel(Src proto, const
       p[q] = make_uint4(0u, 0u, 0u, 0u);
     }
   }
-  sample_one(batch_src(proto, tab[g]), n, S, w, sub * 256 + (int)threadIdx.x);
+  (void)sample_one(batch_src(proto, tab[g]), n, S, w, sub * 256 + (int)threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1167,7 +1205,26 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
     if (w.bid == 0 && tid == 0) w.st()->sample_path = 2ull;
   } else {
     bool ok = false;
-    {
+    const bool fast = rank_lo <= kET;  // grid-uniform
+    if (PAIR && w.compact && fast) {  // (single-client selects only: PAIR = !BATCH; the batched ones skip the code)
+      // The compact sample (the 8 largest keys of each 64-key wave of the sample, 4096 keys: 4 per thread, one 16-B
+      // load instead of eight): the floor and the ceiling from it, both HBM steps issued right behind that load.
+      // The floor's rank among the compact keys is a lower bound of its rank in the full sample; the two agree when
+      // no wave of the sample has its 8th largest key at or above the floor (else, rarely — clustered inputs — the
+      // general pick over the full sample runs).  Either way the floor only sets how many candidates are kept.
+      const uint4 c4 = *reinterpret_cast<const uint4*>(w.samptop() + 4 * tid);
+      x.template load<false>(cur, wb0, pend, lane, va);
+      x.template load<false>(cur, wb0 + sD, pend, lane, vb);
+      unsigned keys[4] = {c4.x, c4.y, c4.z, c4.w};
+      unsigned B = 0;
+      int shB = 0;
+      sample_fast_hist<4>(keys, S, SL, s_hist, &B, &shB);
+      STAMP(1);
+      ok = sample_fast_pick<4>(w.samptop(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
+      if (ok && (tid & 1) && c4.w >= t_lo) SL.bad = 1u;  // (odd threads hold keys 4-7 of a wave: .w its 8th largest)
+      lds_barrier();
+      ok = ok && SL.bad == 0u;
+    } else {
       unsigned keys[kSPT];
       load_sample_keys(w.sample(), S, keys);
       // the first two steps stream while the floor / ceiling are picked (unconditional, clamped
@@ -1176,11 +1233,10 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
       x.template load<false>(cur, wb0, pend, lane, va);
       unsigned B = 0;
       int shB = 0;
-      const bool fast = rank_lo <= kET;  // grid-uniform
-      if (fast) sample_fast_hist(keys, S, SL, s_hist, &B, &shB);
+      if (fast) sample_fast_hist<kSPT>(keys, S, SL, s_hist, &B, &shB);
       STAMP(1);
       x.template load<false>(cur, wb0 + sD, pend, lane, vb);
-      if (fast) ok = sample_fast_pick(w.sample(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
+      if (fast) ok = sample_fast_pick<kSPT>(w.sample(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
     }
     if (!ok) sample_general(w.sample(), S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
     if (w.bid == 0 && tid == 0) w.st()->sample_path = ok ? 0ull : 1ull;
@@ -2156,6 +2212,9 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
     const int ns = (int)(2 * g.M / ((int64_t)kENW * Src::SF * 256));
     w.pair_r = std::max(0, std::min(ns / 2 - 4, std::max(4, ns / 16)));
   }
+  // the compact sample when the full 32 K keys are taken (FLC_COMPACT_SAMPLE=0: calibration A/B only)
+  static const bool compact_on = !getenv("FLC_COMPACT_SAMPLE") || atoi(getenv("FLC_COMPACT_SAMPLE")) != 0;
+  w.compact = (compact_on && !ss.take_all && ss.S == kSample) ? 1 : 0;
   if (!ss.take_all)
     FLC_LAUNCH("topk_sample", topk_sample_kernel<Src>, dim3((unsigned)cdiv(ss.S, 256)), dim3(256), 0, st, x, n, ss.S, w);
   if (split)
@@ -2392,6 +2451,7 @@ int launch_topk_batch_chunks(const Src& proto, const BatchEntry* tab, int C, con
   w.nb = bg.g.G;
   w.vstride = bg.vstride;
   w.pair_r = 0;  // (batched selects keep static ranges: a client's few blocks)
+  w.compact = 0;  // (and the full sample: the batched sample kernel writes no compact one)
   w.errp = reinterpret_cast<unsigned long long*>(base + kOffSt + offsetof(EncState, err));
   Coresident co(st, dev);
   if (co.status()) return co.status();
