@@ -559,11 +559,14 @@ constexpr int kMaxFused = 1024;  // blocks (flags)
 // level) and drained with s_waitcnt vmcnt(0) before the flag is raised; readers load it the same way — no release /
 // acquire fence, which on gfx950 writes back / invalidates the whole L2 (measured 6-8 us over 510 blocks, quant.hip's
 // dropped ticket fold).  The exchange of topk.hip, for one kernel with its own flag region.
-__device__ __forceinline__ void fused_exchange(const QuantWs& ws, unsigned long long epoch) {
+// (split in two: the block's flag raised by fused_arrive, the poll in fused_wait — the block's own work in between)
+__device__ __forceinline__ void fused_arrive(const QuantWs& ws, unsigned long long epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(ws.flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fused_wait(const QuantWs& ws, unsigned long long epoch) {
   const int tid = threadIdx.x;
-  if (tid == 0) __hip_atomic_store(ws.flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid < kWave) {
     const int G = (int)gridDim.x;
     unsigned spins = 0;
@@ -628,23 +631,25 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
     s_m[0][wid] = m0;
     s_m[1][wid] = m1;
   }
-  // the Philox words do not depend on the norm: computed here, before the exchange, so the VALU work of the encode
-  // overlaps the wait for the slowest block instead of following it (GPT = 2; at 4 they would not fit the registers)
-  constexpr bool kPre = GPT <= 2;
-  uint32_t wd[kPre ? GPT : 1][kGroup];
-  if constexpr (kPre) {
-#pragma unroll
-    for (int g = 0; g < GPT; ++g) group_words(base + ((int64_t)g * kFT + tid) * kGroup, seed, counter, wd[g]);
-  }
   if (tid < 2) s_nnz[tid] = 0ull;
-  if (KIND == 0 && tid <= s) s_lvt[tid] = (float)level_value<0>(tid, s, step);
   __syncthreads();
   if (tid < 2) {  // slot 0: row r0, slot 1: row r0 + 1 (0 when the block holds none of it)
     uint32_t m = 0;
     for (int w = 0; w < kFT / kWave; ++w) m = s_m[tid][w] > m ? s_m[tid][w] : m;
     __hip_atomic_store(ws.blkmax + 2 * blockIdx.x + tid, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (!(cal & 2)) fused_exchange(ws, epoch);
+  if (!(cal & 2)) fused_arrive(ws, epoch);
+  // The Philox words and the level table do not depend on the norm: computed after this block's flag is up and
+  // before its poll, so that they fill the wait for the slowest block instead of delaying this block's arrival
+  // (GPT = 2; at 4 they would not fit the registers)
+  constexpr bool kPre = GPT <= 2;
+  uint32_t wd[kPre ? GPT : 1][kGroup];
+  if constexpr (kPre) {
+#pragma unroll
+    for (int g = 0; g < GPT; ++g) group_words(base + ((int64_t)g * kFT + tid) * kGroup, seed, counter, wd[g]);
+  }
+  if (KIND == 0 && tid <= s) s_lvt[tid] = (float)level_value<0>(tid, s, step);
+  if (!(cal & 2)) fused_wait(ws, epoch);
   else __syncthreads();
   if (tid < kWave) {  // wave 0: each row's max over the blocks holding it
 #pragma unroll
