@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "grad-codec GB/s (device-resident encode+decode), flat fp32 delta, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: 6.29 TB/s measured (float4 copy)
 XGMI_GBS = 7 * 153.0  # 7 xGMI links x ~153 GB/s per GPU
 D_HEADLINE = 268_435_456
 LEVELS = 127
@@ -379,6 +380,23 @@ def aggregation_extras(dev, world: int, rank: int) -> dict:
                   "D2H back into the same CPU tensors, stream synchronised; cpu_torch is the reference's CPU update "
                   "with its messages already in host memory")
     out["aggregation_config0_host_server"] = hl
+    # FedDyn's and pFedMe's server updates (feddyn/_feddyn.py:172-184, pfedme/_pfedme.py:166-175): one
+    # flc_model_fold_server launch each, device-resident, same model and messages (as client parameters)
+    pm = [{"train_samples": m["train_samples"], "parameters": [t + p for t, p in zip(m["delta_parameters"], th0)]}
+          for m in msgs0]
+    h0 = [torch.zeros(sh, device=dev) for sh in CONFIG0_SHAPES]
+    srv = {"feddyn_update": (lambda: fagg.feddyn_update(th0, h0, pm, 0.01, 20), (n0 + 4) * 4 * d0),
+           "pfedme_update": (lambda: fagg.pfedme_update(th0, pm, 0.7), (n0 + 2) * 4 * d0)}
+    sl = {"model": line["model"]}
+    for name, (fn, nbytes) in srv.items():
+        ms_s, _ = timed(fn, 50, 10, world)
+        ms_s = max_over_ranks(ms_s, world)
+        sl[name] = {"us": round(ms_s * 1e3, 2), "GB_s": round(nbytes / (ms_s * 1e-3) / 1e9, 1),
+                    "algorithmic_bytes": nbytes}
+    sl["bytes_formula"] = ("FedDyn (n + 4) * 4 * D: the n messages, theta and h read, theta and h written; pFedMe "
+                           "(n + 2) * 4 * D: the n messages and theta read, theta written (the saved model never leaves "
+                           "the registers)")
+    out["aggregation_config0_feddyn_pfedme"] = sl
     del th0, dl0, v0, msgs0
     # 8 x 25 M: distinct sources (a repeated source would be served from the caches)
     n8 = 25_000_000
@@ -474,6 +492,11 @@ def main():
         roof["stream_copy_GB_s"] = round(cp, 1)
         roof["frac_of_stream_copy"] = round(roof["achieved"] / cp, 4)
         roof["value_frac_of_stream_copy"] = round(value / world / cp, 4)
+        # the guide's measured float4 copy (MI355X_MICROARCH.md: 6.29 TB/s), beside the box's own copy: the best copy
+        # shape found here (tools/copyprobe.hip, profiles/r05/r05b_copyprobe.txt) reaches 5.9 TB/s, below the codec's
+        # own decode write stream, so this copy is a reference point, not a ceiling
+        roof["guide_copy_GB_s"] = GUIDE_COPY_GBS
+        roof["value_frac_of_guide_copy"] = round(value / world / GUIDE_COPY_GBS, 4)
     extra = {}
     parity = None  # set by the configs[3] legs (skipped with --skip-extra)
     if probe_ms:

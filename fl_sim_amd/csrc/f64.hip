@@ -476,6 +476,7 @@ struct Sel64 {
   unsigned long long bkey[kBinCap];   // the K-th largest's bin: keys (less the bin's base) and their indices
   long long bidx[kBinCap];
   unsigned sample[kSample64];         // the sample's keys, top 32 bits (the band needs no more; half the bytes)
+  unsigned top[kSample64 / 64 * 8];   // the compact sample: each 64-key wave's 8 largest (top 32 bits), descending
 };
 
 #ifdef FLC_SELECT_STAMPS  // (tools/stamps64.py)
@@ -598,7 +599,21 @@ __global__ __launch_bounds__(kT) void sel64_prep_kernel(const double* __restrict
   }
   for (int j = blockIdx.x * kT + tid; j < S; j += gridDim.x * kT) {
     const int64_t pos = (int64_t)(((double)j + 0.5) * (double)n / (double)S);
-    st->sample[j] = (unsigned)(order_key64(x[pos < n ? pos : n - 1]) >> 32);
+    unsigned key = (unsigned)(order_key64(x[pos < n ? pos : n - 1]) >> 32);
+    st->sample[j] = key;
+    if (S == kSample64 && gridDim.x * kT == kSample64) {  // (one key per thread: every lane of the wave holds one)
+      // the compact sample: the wave's 8 largest keys, descending (topk.hip's compact sample for float32)
+      const int lane = tid & (kWave - 1);
+      unsigned mine = 0u;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const unsigned m = wave_max_u32(key);
+        if (lane == r) mine = m;
+        const unsigned long long at = __ballot(key == m);
+        if (lane == __ffsll((long long)at) - 1) key = 0u;
+      }
+      if (lane < 8) st->top[(j >> 6) * 8 + lane] = mine;
+    }
   }
 }
 
@@ -612,6 +627,7 @@ struct SelLds {
   long long scan[kGNW], res[3], out[2][3], sel[4];
   unsigned cn[kMaxCPB];  // the candidates of the block's chunks
   int ovf;
+  int bad;  // the compact sample's band is not exact (a wave of the sample holds more keys above the floor)
 };
 
 // The band [t_lo, t_hi) from the sample's r_lo-th and r_hi-th largest keys (r_hi <= 0: no ceiling); every block of
@@ -629,10 +645,12 @@ __device__ __forceinline__ void sample_keys(const Sel64* __restrict__ st, int S,
     key[i] = j < S ? (unsigned long long)st->sample[j] << 32 : 0ull;  // (truncated: key' <= key)
   }
 }
-__device__ __forceinline__ void sample_band(const Sel64* st, const unsigned long long (&key)[kSPer], int S,
+// (N = kSPer: the full sample; N = 2: the compact sample, 2048 keys, only for r_lo <= kGT)
+template <int N>
+__device__ __forceinline__ void sample_band(const Sel64* st, const unsigned long long (&key)[N], int S,
                                             long long r_lo, long long r_hi, SelLds& L, unsigned long long& t_lo,
                                             unsigned long long& t_hi) {
-  constexpr int kPer = kSPer;
+  constexpr int kPer = N;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
   const bool hi = r_hi > 0;
   if (r_lo <= kGT && S == kSample64) {
@@ -701,7 +719,7 @@ __device__ __forceinline__ void sample_band(const Sel64* st, const unsigned long
     // holds for the true keys too)
     const unsigned long long e2 = (e1 + 0xffffffffull) & ~0xffffffffull;
     t_hi = !hi || e1 < lo1 || e2 < e1 ? ~0ull : e2;  // (saturated at the top of the key range)
-  } else {
+  } else if constexpr (N == kSPer) {
     unsigned long long plo = 0ull, phi = 0ull;
     long long rlo = r_lo, rhi = r_hi;
     for (int pass = 0; pass < kSampleDigits; ++pass) {
@@ -904,11 +922,28 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
     double2 va[kR], vb[kR], vc[kR];
     const int64_t c0 = blockIdx.x;
     // (the sample's keys are loaded first: loads complete in order, so keys issued behind the chunk would wait for it)
-    unsigned long long skey[kSPer];
-    sample_keys(st, S, skey);
-    load_chunk(c0, va);  // (a second chunk held across the band's keys would spill)
     unsigned long long t_lo, t_hi;
-    sample_band(st, skey, S, r_lo, r_hi, L, t_lo, t_hi);
+    bool have_band = false;
+    if (S == kSample64 && r_lo <= kGT) {
+      // The compact sample (each 64-key wave's 8 largest, 2048 keys: one 8-B load per thread instead of 16): the band
+      // from it when no wave of the sample has its 8th largest at or above the floor (then the floor's and the
+      // ceiling's ranks among the compact keys are their ranks in the sample), else from the full sample below
+      const uint2 c2 = *reinterpret_cast<const uint2*>(st->top + 2 * tid);
+      load_chunk(c0, va);
+      if (tid == 0) L.bad = 0;
+      const unsigned long long ck[2] = {(unsigned long long)c2.x << 32, (unsigned long long)c2.y << 32};
+      sample_band<2>(st, ck, S, r_lo, r_hi, L, t_lo, t_hi);
+      if ((tid & 3) == 3 && ck[1] >= t_lo) L.bad = 1;  // (threads 4w .. 4w + 3 hold wave w's 8 keys: .y of the last, its 8th)
+      lds_barrier();
+      have_band = L.bad == 0;
+      lds_barrier();  // (L is reused by the full-sample band)
+    }
+    if (!have_band) {
+      unsigned long long skey[kSPer];
+      sample_keys(st, S, skey);
+      if (!(S == kSample64 && r_lo <= kGT)) load_chunk(c0, va);  // (a second chunk held across the band's keys would spill)
+      sample_band<kSPer>(st, skey, S, r_lo, r_hi, L, t_lo, t_hi);
+    }
     load_chunk(c0 + G, vb);
     const int sh = range_shift64(t_hi - t_lo - 1ull, 11);  // (t_hi > t_lo)
     STAMP64(blockIdx.x == 0, 6);

@@ -1,0 +1,19 @@
+"""Same-box A/B of two prebuilt libraries (FLC_LIB): tools/env_ab.py's workloads (the headline step, the encode alone,
+f1, configs[2]'s 25 M top-k step, a 25 M stacked encode), run as separate processes, interleaved A B A B A B.
+    python tools/lib_ab.py ab/libflc_A.so ab/libflc_B.so [rounds]"""
+import os
+import subprocess
+import sys
+
+libs = sys.argv[1:3]
+rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+here = os.path.dirname(os.path.abspath(__file__))
+for r in range(rounds):
+    for lib in libs:
+        env = dict(os.environ, FLC_LIB=lib, FLC_AB_LABEL=os.path.basename(lib))
+        out = subprocess.run([sys.executable, os.path.join(here, "env_ab.py"), "FLC_AB_LABEL"], env=env,
+                             capture_output=True, text=True, timeout=180)
+        if out.returncode != 0:
+            print(out.stderr[-2000:], flush=True)
+            sys.exit(1)
+        print([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1], flush=True)
