@@ -930,6 +930,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
       // ceiling's ranks among the compact keys are their ranks in the sample), else from the full sample below
       const uint2 c2 = *reinterpret_cast<const uint2*>(st->top + 2 * tid);
       load_chunk(c0, va);
+      load_chunk(c0 + G, vb);  // (two chunks in flight across the compact band: 2 keys per thread, not 16)
       if (tid == 0) L.bad = 0;
       const unsigned long long ck[2] = {(unsigned long long)c2.x << 32, (unsigned long long)c2.y << 32};
       sample_band<2>(st, ck, S, r_lo, r_hi, L, t_lo, t_hi);
@@ -944,7 +945,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
       if (!(S == kSample64 && r_lo <= kGT)) load_chunk(c0, va);  // (a second chunk held across the band's keys would spill)
       sample_band<kSPer>(st, skey, S, r_lo, r_hi, L, t_lo, t_hi);
     }
-    load_chunk(c0 + G, vb);
+    if (!(S == kSample64 && r_lo <= kGT)) load_chunk(c0 + G, vb);
     const int sh = range_shift64(t_hi - t_lo - 1ull, 11);  // (t_hi > t_lo)
     STAMP64(blockIdx.x == 0, 6);
     // 2. the filter pass over the block's chunks: chunk q of the block (ch = b + q G) appends through its own LDS
