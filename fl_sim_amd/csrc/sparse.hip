@@ -78,11 +78,16 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave_kernel(const int* __
       acc[u] = e + 4 <= n ? *reinterpret_cast<const float4*>(out + e) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  // (entries clamped to [0, k): a malformed tile pointer never reads past the wire; scalar)
-  const unsigned lo = min(tile_start[blockIdx.x], k), hi = min(tile_start[blockIdx.x + 1], k);
+  // (entries clamped to [0, k): a malformed tile pointer never reads past the wire.  Both loads are issued before the
+  // clamps — a scalar load's value is waited for with lgkmcnt(0), and a clamp scheduled between the loads made them
+  // two round trips)
+  unsigned lo = tile_start[blockIdx.x], hi = tile_start[blockIdx.x + 1];
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
 #pragma unroll
   for (int u = 0; u < 4; ++u) tile4[lane + u * kWave] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __builtin_amdgcn_sched_barrier(0);
+  lo = min(lo, k);
+  hi = min(hi, k);
   const float nrm = MODE == 1 ? *norm_ptr : 0.0f;
   for (unsigned j = lo + lane; j < hi; j += kWave) {
     const int64_t off = (int64_t)(unsigned)idx[j] - t0;
@@ -134,10 +139,13 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
   const int64_t t0 = tb * TILE;
   unsigned ts[NT + 1];
 #pragma unroll
-  for (int i = 0; i <= NT; ++i) ts[i] = min(tile_start[tb + i < ntiles ? tb + i : ntiles], k);  // (clamped: see above)
+  for (int i = 0; i <= NT; ++i) ts[i] = tile_start[tb + i < ntiles ? tb + i : ntiles];
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
 #pragma unroll
   for (int u = 0; u < 4 * NT; ++u) tile4[lane + u * kWave] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __builtin_amdgcn_sched_barrier(0);  // (every load and the zeroing issued before the clamps: see above)
+#pragma unroll
+  for (int i = 0; i <= NT; ++i) ts[i] = min(ts[i], k);
   const float nrm = MODE == 1 ? *norm_ptr : 0.0f;
   // first entry per lane of every tile in flight together, the (rare) rest afterwards
   unsigned e_idx[NT];
