@@ -17,6 +17,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "flc_device.hpp"
 #include "flc_runtime.hpp"
@@ -130,11 +131,12 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
                                                                     const float* __restrict__ norm_ptr, int64_t n,
                                                                     float weight, float* __restrict__ out,
                                                                     const unsigned* __restrict__ tile_start,
-                                                                    int64_t ntiles, unsigned k) {
+                                                                    int64_t ntiles, unsigned k, int rev) {
   constexpr int TILE = 1024;
   __shared__ __attribute__((aligned(16))) float s_tile[NT * TILE];
   const int lane = threadIdx.x;
-  const int64_t g = blockIdx.x;  // plain order (XCD-chunked orders measured no faster)
+  // plain order (XCD-chunked orders measured no faster); `rev`: from the last pair down
+  const int64_t g = rev ? (int64_t)gridDim.x - 1 - blockIdx.x : (int64_t)blockIdx.x;
   const int64_t tb = g * NT;
   const int64_t t0 = tb * TILE;
   unsigned ts[NT + 1];
@@ -283,9 +285,18 @@ int launch_decode_tiles(const int32_t* idx, const float* val, const uint8_t* cod
   if (accumulate)
     FLC_LAUNCH(name, (sparse_decode_wave_kernel<MODE, true>), dim3((unsigned)ntiles), dim3(kWave), 0, st, idx, val,
                codes, scale, levels, step, norm, n, weight, out, tile_start, (unsigned)k);
-  else
+  else {
+    // The tile order alternates from call to call (ascending, then descending, ...): a decode then starts on the
+    // lines the previous one wrote last, which are still in the 256 MiB memory-side cache, when consecutive decodes
+    // write the same output (the server's accumulator, a step loop): 179.0 -> 176.5 us per 1 GiB decode, step
+    // 386.9 -> 384.9 us (profiles/r05/r05r_alt_ab.txt).  Every tile is still written by exactly one wave: the output
+    // does not depend on the order.  FLC_DECODE_ALT=0 keeps the ascending order.
+    static const bool alt = !getenv("FLC_DECODE_ALT") || atoi(getenv("FLC_DECODE_ALT")) != 0;
+    static std::atomic<int> parity{0};
+    const int rev = alt ? (parity.fetch_xor(1, std::memory_order_relaxed) ^ 1) : 0;
     FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, 2>), dim3((unsigned)cdiv(ntiles, 2)), dim3(kWave), 0, st, idx,
-               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, (unsigned)k);
+               val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, (unsigned)k, rev);
+  }
   return FLC_OK;
 }
 
@@ -305,7 +316,7 @@ int launch_decode_wave2(const int32_t* idx, const float* val, const uint8_t* cod
              (long long)ntiles, tile_start);
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   FLC_LAUNCH(name, (sparse_decode_wave2_kernel<MODE, NT>), dim3((unsigned)cdiv(ntiles, NT)), dim3(kWave), 0, st, idx,
-             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, (unsigned)k);
+             val, codes, scale, levels, step, norm, n, weight, out, tile_start, ntiles, (unsigned)k, 0);
   return FLC_OK;
 }
 
