@@ -26,10 +26,10 @@
 //            re-range, a floor that admitted fewer than k elements — then every block reads its x range directly)
 //            fall back to histogram rounds, each one exchange.
 // Calibration builds keep the earlier split form (FLC_TOPK_SPLIT=1: a separate filter kernel staging the
-// candidates through HBM, the kernel boundary as the hand-off); FLC_PAIR=1 turns on the paired filter pass (blocks
-// 2j and 2j + 1 stream their joint range from both ends and claim the middle steps at run time; bit-identical,
-// measured no faster: DESIGN.md §8).  The batched encoders (flc_stacked_encode_batch*) run one fused select per
-// client on its share of the CUs, in one launch.
+// candidates through HBM, the kernel boundary as the hand-off).  (A paired pass — blocks 2j and 2j + 1 streaming their
+// joint range from both ends, claiming the middle steps at run time — measured no faster and was removed in round 5:
+// DESIGN.md §8.)  The batched encoders (flc_stacked_encode_batch*) run one fused select per client on its share of the
+// CUs, in one launch.
 // An exchange: the block drains its stores/atomics, raises its own flag to the exchange's epoch
 // (call * 32 + phase, from a call counter in the workspace), one wave polls all flags.  The histograms
 // are zeroed by the select at the end of each call; the workspace is zero-initialised once by its
@@ -105,8 +105,7 @@ constexpr size_t kOffSample = al256(kOffBlkT + (size_t)kMaxBlocks * 32);
 constexpr size_t kOffSampTop = al256(kOffSample + (size_t)kSample * 4);
 constexpr size_t kOffInbin = al256(kOffSampTop + (size_t)kSampTop * 4);
 constexpr size_t kOffBlkC = al256(kOffInbin + (size_t)kMaxBlocks * kInbin * 4);
-constexpr size_t kOffPair = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // per block pair: its step-claim word
-constexpr size_t kOffStage = al256(kOffPair + (size_t)(kMaxBlocks / 2) * 8);  // + G * kCap * 8 (keys, then indices)
+constexpr size_t kOffStage = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // + G * kCap * 8 (keys, then indices)
 static_assert(kOffAcc % 8 == 0, "acc words are 64-bit");
 static_assert(sizeof(EncState) <= 128, "state block");
 
@@ -122,7 +121,6 @@ struct EncWs {
   unsigned ovf;   // candidates per block kept in HBM beyond the LDS's kCap (0: none)
   int bid, nb;    // this block's index in its select, the blocks of its select (set in the kernel prologue)
   size_t vstride; // batched: bytes between two clients' staging / overflow areas
-  int pair_r;     // paired pass (see filter_phase): dynamic steps per block side, 0 = static ranges
   int compact;    // the sample kernel wrote the compact sample (samptop): the floor / ceiling start from it
   unsigned long long* errp;
   __device__ EncState* st() const { return reinterpret_cast<EncState*>(base + kOffSt); }
@@ -136,7 +134,6 @@ struct EncWs {
   __device__ unsigned* samptop() const { return reinterpret_cast<unsigned*>(base + kOffSampTop); }
   __device__ unsigned* inbin() const { return reinterpret_cast<unsigned*>(base + kOffInbin); }
   __device__ unsigned* blk_c() const { return reinterpret_cast<unsigned*>(base + kOffBlkC); }  // candidates / block
-  __device__ unsigned long long* pairw() const { return reinterpret_cast<unsigned long long*>(base + kOffPair); }  // (32 bits used)
   __device__ unsigned* stage_key(int b) const { return reinterpret_cast<unsigned*>(var) + (size_t)b * 2 * kCap; }
   __device__ unsigned* stage_idx(int b) const { return stage_key(b) + kCap; }
   __device__ unsigned* ovf_key(int b) const {
@@ -220,7 +217,6 @@ EncWs carve_enc(void* ws, int64_t n, int64_t k, int cus, size_t* need) {
   w.bid = 0;
   w.nb = g.G;
   w.vstride = 0;
-  w.pair_r = 0;
   w.compact = 0;
   w.errp = reinterpret_cast<unsigned long long*>(w.base + kOffSt + offsetof(EncState, err));
   *need = kOffStage + vb;
@@ -617,8 +613,7 @@ struct DeltaSrc {
     const int64_t r = e - t.off[sg];
     return t.lp[sg][r] - t.gp[sg][r];
   }
-  // (every cursor field through readfirstlane: wave-uniform values the compiler would otherwise keep in VGPRs, which
-  // the paired pass's second copy of the load loop could not afford)
+  // (every cursor field through readfirstlane: wave-uniform values the compiler would otherwise keep in VGPRs)
   static __device__ __forceinline__ long long rfl64(long long v) {
     return (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v) |
            ((long long)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32);
@@ -710,16 +705,11 @@ struct FilterCtx {
   unsigned above;         // per thread: candidates >= t_hi
   unsigned mk;            // per thread: max candidate key
   unsigned swept;         // (block-uniform) LDS candidates [0, swept) already in the band histogram
-  // paired pass, second block of a pair (it streams its range from the top down): candidate count r (its rank from
-  // the top of the block's range, r = rb - p for the step's ascending position p) lives at LDS slot kCap - 1 - r, so
-  // the block's candidates end up in index order in [kCap - C, kCap); past kCap they go to the HBM overflow at r - kCap
-  bool rev;
-  unsigned rb;            // (block-uniform) per step: 2 * base + tot - 1
 };
 
 // one LDS candidate into the band histogram / above count / max key
 __device__ __forceinline__ void band_bin(FilterCtx& c, unsigned p) {
-  const unsigned key = order_key(c.s_key[c.rev ? (unsigned)kCap - 1u - p : p]);
+  const unsigned key = order_key(c.s_key[p]);
   const unsigned long long rel = (unsigned long long)(key - c.t_lo);
   if (rel >= c.width0) ++c.above;
   else atomicAdd(&c.s_hist[(unsigned)(rel >> c.sh0)], 1u);
@@ -733,11 +723,10 @@ __device__ __forceinline__ void band_bin(FilterCtx& c, unsigned p) {
 template <bool OVF>
 __device__ __forceinline__ void emit(FilterCtx& c, unsigned q, unsigned e, float v) {
   const unsigned raw = __float_as_uint(v);
-  const unsigned p = c.rev ? c.rb - q : q;  // (count order: from the range's bottom, or its top for a reverse block)
+  const unsigned p = q;
   if (!OVF || p < (unsigned)kCap) {
-    const unsigned ph = c.rev ? (unsigned)kCap - 1u - p : p;
-    c.s_key[ph] = raw;
-    c.s_idx[ph] = e;
+    c.s_key[p] = raw;
+    c.s_idx[p] = e;
   } else {
     if (p - (unsigned)kCap < c.gcap) {
       c.g_key[p - kCap] = raw;
@@ -808,7 +797,6 @@ __device__ __forceinline__ void step_process(const Step& v, int64_t wb, int64_t 
   // stops the compiler from reusing the count pass's compares)
   float tf2 = tf;
   asm volatile("" : "+v"(tf2));
-  c.rb = 2u * base + tot - 1u;
   if (cnt != 0u) {
     if (base + tot <= (unsigned)kCap)  // (block-uniform) the step lands in LDS: no overflow code on the hot path
       step_write<FULL, Step, SF, false>(v, tf2, lim, lane, (unsigned)wb, base + pre, c);
@@ -985,29 +973,18 @@ struct CandSrc {
   int64_t b0;
   bool xmode;
   bool gmode;       // more candidates than LDS holds, all of them in LDS + the overflow
-  bool rev;         // gmode of a reverse block (paired pass): the overflow holds the LOWEST indices, top down
-  unsigned C;       // the block's candidates (rev gmode)
 };
 template <class Src>
 __device__ __forceinline__ void cand_get(const CandSrc<Src>& c, unsigned p, unsigned& raw, unsigned& id) {
   if (c.xmode) {
     raw = __float_as_uint(c.x.get(c.b0 + p));
     id = (unsigned)(c.b0 + p);
-  } else if (!c.gmode || (!c.rev && p < (unsigned)kCap)) {
+  } else if (!c.gmode || p < (unsigned)kCap) {
     raw = c.s_key[p];
     id = c.s_idx[p];
-  } else if (!c.rev) {  // (written by this block's waves in the filter pass, before the exchange that followed it)
+  } else {  // (written by this block's waves in the filter pass, before the exchange that followed it)
     raw = ld_mem(c.g_key + (p - kCap));
     id = ld_mem(c.g_idx + (p - kCap));
-  } else {  // reverse block, gmode: count from the top r = C - 1 - p; LDS for r < kCap, the overflow beyond
-    const unsigned r = c.C - 1u - p;
-    if (r < (unsigned)kCap) {
-      raw = c.s_key[kCap - 1u - r];
-      id = c.s_idx[kCap - 1u - r];
-    } else {
-      raw = ld_mem(c.g_key + (r - kCap));
-      id = ld_mem(c.g_idx + (r - kCap));
-    }
   }
 }
 
@@ -1072,9 +1049,6 @@ __global__ __launch_bounds__(256) void topk_sample_kernel(Src x, int64_t n, int 
     }
     if (lane < kTopPer) w.samptop()[(j >> 6) * kTopPer + lane] = mine;
   }
-  // the paired pass's step-claim words start every call from zero (this kernel precedes the encode in the stream)
-  if (w.pair_r > 0 && blockIdx.x == 0)
-    for (int i = (int)threadIdx.x; i < (w.nb + 1) / 2; i += 256) w.pairw()[i] = 0ull;
 #ifdef FLC_SELECT_STAMPS
   __syncthreads();
   if (threadIdx.x == 0 && blockIdx.x < 256) w.blkt()[(512 + blockIdx.x) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1151,13 +1125,13 @@ struct FilterOut {
   unsigned C_b;            // candidates of this block (<= kCap of them in s_key / s_idx)
   unsigned t_lo;           // floor key
   unsigned long long t_hi; // ceiling key (exclusive)
-  int64_t b0, b1;          // the block's element range (paired pass: decided during the pass)
-  bool rev;                // paired pass, second block: LDS candidates at the top (see FilterCtx)
+  int64_t b0, b1;          // the block's element range
 };
 
 // floor / ceiling from the sample, the HBM pass into the block's LDS candidate arrays, the round-0 band
 // histogram and counts; STAGE: also the staging copy of the candidates for a separate select kernel
-template <bool STAGE, class Src, bool PAIR = false>
+// (SINGLE: a single-client select, which may take the compact sample; the batched selects do not)
+template <bool STAGE, class Src, bool SINGLE = false>
 __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const EncWs& w, int S,
                                                   long long rank_lo, long long rank_hi, int take_all,
                                                   unsigned* s_key, unsigned* s_idx, unsigned* s_hist,
@@ -1173,20 +1147,6 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   constexpr int64_t kBS = kENW * kWS;       // elements per block step (M is a multiple of it)
   using Step = typename Src::Step;
   const int nsteps = (int)cdiv_dev(b1 - b0, kBS);
-  // Paired pass (w.pair_r > 0, both blocks of the pair with whole ranges): blocks 2j and 2j + 1 (neighbouring XCDs)
-  // stream the 2M elements of both ranges from the two ends towards each other — block 2j upwards from the bottom,
-  // block 2j + 1 downwards from the top — each taking its first NS / 2 - R steps statically and the 2R steps in the
-  // middle one at a time from a shared claim word.  The pair's
-  // boundary thus falls where the two meet, so a block on a slower XCD hands steps to its partner instead of making
-  // every block wait for it at the first exchange; each block's range stays contiguous and in index order, so the
-  // select and the compaction are unchanged.
-  const bool pairm = PAIR && !STAGE && w.pair_r > 0 && (int64_t)((w.bid | 1) + 1) * w.M <= n;  // (per pair)
-  const bool rev = pairm && (w.bid & 1);
-  const int64_t ps = (int64_t)(w.bid & ~1) * w.M;   // the pair's range start
-  const int NSp = (int)(2 * w.M / kBS);             // the pair's steps
-  const int64_t sA = rev ? ps + (int64_t)(NSp - 1) * kBS : b0;  // the block's first step
-  const int64_t sD = rev ? -kBS : kBS;                          // and its direction
-  const int64_t pend = pairm ? ps + 2 * w.M : b1;               // load clamp (full steps only in the paired pass)
   STAMP(0);
 
   // ---- floor / ceiling (identical in every block); the first step of the HBM pass is already in flight
@@ -1195,7 +1155,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   typename Src::Cursor cur;
   // (the wave's offset through readfirstlane: wave-uniform, so every step address and the DeltaSrc cursor stay scalar)
   const int64_t woff = (int64_t)__builtin_amdgcn_readfirstlane(wid) * kWS;
-  const int64_t wb0 = sA + woff;
+  const int64_t wb0 = b0 + woff;
   const int nfull = (int)((b1 - b0) / kBS);
   unsigned t_lo;
   unsigned long long t_hi;
@@ -1206,15 +1166,15 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   } else {
     bool ok = false;
     const bool fast = rank_lo <= kET;  // grid-uniform
-    if (PAIR && w.compact && fast) {  // (single-client selects only: PAIR = !BATCH; the batched ones skip the code)
+    if (SINGLE && w.compact && fast) {  // (single-client selects only; the batched ones skip the code)
       // The compact sample (the 8 largest keys of each 64-key wave of the sample, 4096 keys: 4 per thread, one 16-B
       // load instead of eight): the floor and the ceiling from it, both HBM steps issued right behind that load.
       // The floor's rank among the compact keys is a lower bound of its rank in the full sample; the two agree when
       // no wave of the sample has its 8th largest key at or above the floor (else, rarely — clustered inputs — the
       // general pick over the full sample runs).  Either way the floor only sets how many candidates are kept.
       const uint4 c4 = *reinterpret_cast<const uint4*>(w.samptop() + 4 * tid);
-      x.template load<false>(cur, wb0, pend, lane, va);
-      x.template load<false>(cur, wb0 + sD, pend, lane, vb);
+      x.template load<false>(cur, wb0, b1, lane, va);
+      x.template load<false>(cur, wb0 + kBS, b1, lane, vb);
       unsigned keys[4] = {c4.x, c4.y, c4.z, c4.w};
       unsigned B = 0;
       int shB = 0;
@@ -1230,12 +1190,12 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
       // the first two steps stream while the floor / ceiling are picked (unconditional, clamped
       // in-range loads, so no wait is merged in): the first right away, the second in the registers the
       // keys leave free after the histogram
-      x.template load<false>(cur, wb0, pend, lane, va);
+      x.template load<false>(cur, wb0, b1, lane, va);
       unsigned B = 0;
       int shB = 0;
       if (fast) sample_fast_hist<kSPT>(keys, S, SL, s_hist, &B, &shB);
       STAMP(1);
-      x.template load<false>(cur, wb0 + sD, pend, lane, vb);
+      x.template load<false>(cur, wb0 + kBS, b1, lane, vb);
       if (fast) ok = sample_fast_pick<kSPT>(w.sample(), S, rank_lo, rank_hi, B, shB, SL, s_hist, s_red, &t_lo, &t_hi);
     }
     if (!ok) sample_general(w.sample(), S, rank_lo, rank_hi, SL, s_hist, s_red, &t_lo, &t_hi);
@@ -1269,65 +1229,8 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   fc.above = 0;
   fc.mk = 0;
   fc.swept = 0;
-  fc.rev = rev;
-  fc.rb = 0;
   unsigned base = 0;
-  if (pairm) {
-    // ordinal i = the block's i-th step: i < P static, then one claimed step at a time (s_ring[i & 3]: its step index
-    // in the pair's range, or -1 once the middle is used up).  Thread 0 stores ordinal i + 3's claim result (issued
-    // at the end of ordinal i - 1, before the loads of ordinal i + 1, so waiting for it does not wait for those
-    // loads) into the ring and issues the claim of ordinal i + 4 at the end of ordinal i, before the loads of
-    // ordinal i + 2; the barrier inside the next step_process publishes the ring entry.  The claim word (32 bits:
-    // front claims in bits 0-15, back claims in 16-31) only grows, so once a claim comes back past the middle every
-    // later one does too.
-    __shared__ int s_ring[4];
-    const int P = NSp / 2 - w.pair_r, D = 2 * w.pair_r;  // (P >= 4: the host keeps 4 static steps per block)
-    unsigned* const pw = reinterpret_cast<unsigned*>(w.pairw() + (w.bid >> 1));
-    const unsigned inc = rev ? 0x10000u : 1u;
-    unsigned claim = 0;  // thread 0: the claim in flight (the first at the end of ordinal P - 4 >= 0)
-    // The loop has the static loop's shape (a buffer is reloaded right before the other one is processed) and the
-    // same peeled first iteration.  Loads are never conditional (a conditional load made the compiler copy the
-    // previous step's registers into the new ones, waiting for them) and a step's processing has no second copy (its
-    // registers are all taken): past the block's last step a buffer reloads the step the other buffer holds (still in
-    // the Infinity Cache; the data is dropped), and the loop ends after that buffer's step.
-    auto post = [&](int j) {  // end of ordinal j (thread 0): ring[j + 3] <- claim(j + 3); claim(j + 4) issued
-      if (tid != 0) return;
-      if (j + 3 >= P) {
-        const int u = (int)((claim & 0xffffu) + (claim >> 16));
-        s_ring[(j + 3) & 3] = u < D ? P + (int)(rev ? claim >> 16 : claim & 0xffffu) : -1;
-      }
-      if (j + 4 >= P) claim = __hip_atomic_fetch_add(pw, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    step_process<true, Step, SF>(va, sA + woff, pend, tf, s_wc, 0, base, fc);  // ordinals 0, 1: static (P >= 4)
-    post(0);
-    x.template load<true>(cur, sA + 2 * sD + woff, pend, lane, va);
-    step_process<true, Step, SF>(vb, sA + sD + woff, pend, tf, s_wc, 1, base, fc);
-    post(1);
-    int sa = 2;  // the ordinal va holds (ordinal-space step index: 0 = the block's first)
-    int done = 0;
-    for (int i = 2;; i += 2) {
-      const int n1 = i + 1 < P ? i + 1 : __builtin_amdgcn_readfirstlane(s_ring[(i + 1) & 3]);
-      x.template load<true>(cur, sA + (int64_t)(n1 >= 0 ? n1 : sa) * sD + woff, pend, lane, vb);
-      step_process<true, Step, SF>(va, sA + (int64_t)sa * sD + woff, pend, tf, s_wc, 0, base, fc);
-      post(i);
-      if (n1 < 0) {
-        done = i + 1;
-        break;
-      }
-      const int n2 = i + 2 < P ? i + 2 : __builtin_amdgcn_readfirstlane(s_ring[(i + 2) & 3]);
-      x.template load<true>(cur, sA + (int64_t)(n2 >= 0 ? n2 : n1) * sD + woff, pend, lane, va);
-      step_process<true, Step, SF>(vb, sA + (int64_t)n1 * sD + woff, pend, tf, s_wc, 1, base, fc);
-      post(i + 1);
-      if (n2 < 0) {
-        done = i + 2;
-        break;
-      }
-      sa = n2;
-    }
-    // the block's range: `done` steps from its end of the pair's range
-    b0 = rev ? ps + 2 * w.M - (int64_t)done * kBS : ps;
-    b1 = rev ? ps + 2 * w.M : ps + (int64_t)done * kBS;
-  } else {
+  {
     // full block steps in a two-deep software pipeline; every load in the loop body is unconditional
     // (a conditional prefetch makes the compiler copy the loaded registers on a side path, and the copy
     // waits for the load), and the partial tail step is peeled off
@@ -1407,7 +1310,6 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
   o.t_hi = t_hi;
   o.b0 = b0;
   o.b1 = b1;
-  o.rev = rev;
   return o;
 }
 
@@ -1477,13 +1379,12 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
 #endif
   STAMP_INIT();
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
-  int64_t b0 = (int64_t)w.bid * w.M;  // (the paired pass decides them in the filter phase)
+  int64_t b0 = (int64_t)w.bid * w.M;
   int64_t b1 = b0 + w.M < n ? b0 + w.M : n;
   unsigned* hist = w.hist();
   unsigned C_b;
   unsigned ep;
-  bool rev = false;
-  const unsigned* s_keyl = s_key;  // the block's LDS candidates in index order (a reverse block's sit at the top)
+  const unsigned* s_keyl = s_key;  // the block's LDS candidates in index order
   const unsigned* s_idxl = s_idx;
   // Philox words of the candidates (stacked), precomputed in exchange waits into the block's staging
   // area (unused by the fused path; the split path has copied its staged candidates to LDS by then):
@@ -1516,11 +1417,6 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
     C_b = fo.C_b;
     b0 = fo.b0;
     b1 = fo.b1;
-    rev = fo.rev;
-    if (rev && C_b <= (unsigned)kCap) {
-      s_keyl = s_key + (kCap - C_b);
-      s_idxl = s_idx + (kCap - C_b);
-    }
     if (tid == 0) {
       s_glob[0] = fo.t_lo;
       s_glob[1] = fo.t_hi;
@@ -1593,8 +1489,6 @@ __global__ __launch_bounds__(kET) void topk_select_kernel(Src x, int64_t n, long
   const unsigned gcap = FUSED ? w.ovf : 0u;
   src.xmode = fb || C_b > (unsigned)kCap + gcap;  // block-uniform
   src.gmode = !src.xmode && C_b > (unsigned)kCap;
-  src.rev = rev;
-  src.C = C_b;
   const unsigned ncand = src.xmode ? (unsigned)(b1 - b0) : C_b;
 
   auto flush = [&](int sl, unsigned above_t, unsigned mk_t) {
@@ -2205,13 +2099,6 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
 #else
   constexpr bool split = false;
 #endif
-  // the paired pass (filter_phase): R dynamic steps per side, about 1/16 of a pair's steps, at least 4 static steps
-  // per block (the claims run 4 steps ahead).  Off unless FLC_PAIR=1: measured slower so far
-  static const bool pair_on = getenv("FLC_PAIR") && atoi(getenv("FLC_PAIR")) == 1;
-  if (!split && !ss.take_all && pair_on) {
-    const int ns = (int)(2 * g.M / ((int64_t)kENW * Src::SF * 256));
-    w.pair_r = std::max(0, std::min(ns / 2 - 4, std::max(4, ns / 16)));
-  }
   // the compact sample when the full 32 K keys are taken (FLC_COMPACT_SAMPLE=0: calibration A/B only)
   static const bool compact_on = !getenv("FLC_COMPACT_SAMPLE") || atoi(getenv("FLC_COMPACT_SAMPLE")) != 0;
   w.compact = (compact_on && !ss.take_all && ss.S == kSample) ? 1 : 0;
@@ -2450,8 +2337,7 @@ int launch_topk_batch_chunks(const Src& proto, const BatchEntry* tab, int C, con
   w.bid = 0;
   w.nb = bg.g.G;
   w.vstride = bg.vstride;
-  w.pair_r = 0;  // (batched selects keep static ranges: a client's few blocks)
-  w.compact = 0;  // (and the full sample: the batched sample kernel writes no compact one)
+  w.compact = 0;  // (the full sample: the batched sample kernel writes no compact one)
   w.errp = reinterpret_cast<unsigned long long*>(base + kOffSt + offsetof(EncState, err));
   Coresident co(st, dev);
   if (co.status()) return co.status();

@@ -14,7 +14,7 @@ inc = [f"-I{os.path.dirname(os.path.abspath(__file__))}/../include",
        f"-I{os.path.dirname(os.path.abspath(__file__))}/../fl_sim_amd/csrc"]
 with tempfile.TemporaryDirectory() as d:
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", *inc,
-                    "--save-temps", "-c", src, "-o", f"{d}/k.o", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"],
+                    "--save-temps", "-c", src, "-o", f"{d}/k.o"],
                    cwd=d, check=True, stderr=subprocess.DEVNULL)
     s = open(glob.glob(f"{d}/*gfx950*.s")[0]).read()
 for b in s.split(".end_amdhsa_kernel"):
