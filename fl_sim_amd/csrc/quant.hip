@@ -39,22 +39,21 @@ constexpr int kRowSlots = 16;              // per-block LDS nnz slots
 
 struct QuantWs {
   unsigned long long* err;       // [1] sticky error word: 4 = a fused launch's exchange timed out (flc_quant_status)
-  unsigned long long* flags;     // [1024] fused launch: each block's arrival epoch (64-bit: never wraps)
+  unsigned long long* stamps;    // [2 * kMaxFused] fused launch: each block's max |x| bits of its (<= 2) rows, tagged
+                                 // with the call (tag << 31 | max bits)
   unsigned long long* partials;  // [rows * kNormMaxParts]
   int* chunk_counts;             // [nblocks]  (compat)
   long long* chunk_offsets;      // [nblocks]  (compat)
-  unsigned* blkmax;              // [2 * kMaxFused] fused launch: each block's max |x| bits of its (<= 2) rows
 };
 
 QuantWs carve(void* ws, size_t bytes, int64_t rows, int64_t nblocks, size_t* need) {
   Carver c(ws, bytes);
   QuantWs w;
   w.err = c.take<unsigned long long>(1);
-  w.flags = c.take<unsigned long long>(1024);
+  w.stamps = c.take<unsigned long long>(2 * 1024);
   w.partials = c.take<unsigned long long>((size_t)rows * kNormMaxParts);
   w.chunk_counts = c.take<int>((size_t)nblocks);
   w.chunk_offsets = c.take<long long>((size_t)nblocks);
-  w.blkmax = c.take<unsigned>(2 * 1024);
   *need = c.off;
   return w;
 }
@@ -546,50 +545,51 @@ __global__ __launch_bounds__(kThreads) void quant_encode_philox_kernel(
 // configs[1] in one launch (flc_quant_encode_auto with p = inf, Philox): one 1024-thread block per CU, block b owning
 // the flat span [b SPAN, (b + 1) SPAN) of the batch (SPAN = 8192 GPT elements, d >= SPAN: at most two rows per block).
 // Each thread loads its GPT groups of 8 (coalesced: group j of thread t at (j * 1024 + t) * 8) and keeps them in
-// registers; the block's max |x| of each of its rows goes to its own two workspace slots; then a grid exchange (every
-// block raises its flag to the call's epoch, one wave polls all flags); then every block folds its rows' maxima over
-// the blocks that hold them (a contiguous range, one batch of coherent loads) and encodes (+ decodes) from the
-// registers.  x is read once, the codes and the decoded batch written once: 9 B/element
+// registers; the block's max |x| of each of its rows goes to its own two workspace slots, tagged with the call; then
+// every block polls and folds its rows' maxima over the blocks that hold them (a contiguous range: one wave's coherent
+// loads, repeated until every tag is this call's) and encodes (+ decodes) from the registers.  x is read once, the codes and the decoded batch written once: 9 B/element
 // in one launch, bit-identical to the two-launch form (max is exact in any order; same Philox words, same rule).
 // ------------------------------------------------------------------------------------------------
 constexpr int kFT = 1024;
-constexpr int kMaxFused = 1024;  // blocks (flags)
+constexpr int kMaxFused = 1024;  // blocks (stamp words: 2 each)
 
-// The payload (each block's two maxima) is stored with agent-scope atomic stores (write-through to the coherent
-// level) and drained with s_waitcnt vmcnt(0) before the flag is raised; readers load it the same way — no release /
-// acquire fence, which on gfx950 writes back / invalidates the whole L2 (measured 6-8 us over 510 blocks, quant.hip's
-// dropped ticket fold).  The exchange of topk.hip, for one kernel with its own flag region.
-// (split in two: the block's flag raised by fused_arrive, the poll in fused_wait — the block's own work in between)
-__device__ __forceinline__ void fused_arrive(const QuantWs& ws, unsigned long long epoch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(ws.flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// The exchange carries its payload in its flags: each block publishes the max |x| bits of its two row slots as two
+// 64-bit words tagged with the call (tag << 31 | bits), one agent-scope atomic store each (write-through to the
+// coherent level; no release / acquire fence, which on gfx950 writes back / invalidates the whole L2 — measured 6-8 us
+// over 510 blocks, quant.hip's dropped ticket fold).  A reader polls only the words of the blocks that hold its rows,
+// until every tag is this call's: one round trip for flag and payload, and a block waits for its row neighbours, not
+// for the slowest block of the grid.  Tags are 33 bits, never 0 (a fresh workspace's words), equal to a stale word's
+// only if that word was last written 2^33 - 1 calls earlier.
+__device__ __forceinline__ unsigned long long stamp_word(unsigned long long tag, uint32_t bits) {
+  return (tag << 31) | bits;
 }
-__device__ __forceinline__ void fused_wait(const QuantWs& ws, unsigned long long epoch) {
-  const int tid = threadIdx.x;
-  if (tid < kWave) {
-    const int G = (int)gridDim.x;
+
+// wave-wide: the max of slot words [c0, c1] of row r (slot: the row is block c's first or second), polled until every
+// word carries `tag`; every lane gets the result.  Spins are bounded: a block that never arrived (lost co-residency)
+// sets the sticky error word and the launch drains.
+__device__ __forceinline__ uint32_t row_max_polled(const QuantWs& ws, int64_t r, int64_t d, int64_t SPAN, int64_t c0,
+                                                   int64_t c1, unsigned long long tag, bool poll) {
+  const int lane = threadIdx.x & (kWave - 1);
+  uint32_t m = 0;
+  for (int64_t cb = c0; cb <= c1; cb += kWave) {  // (uniform)
+    const int64_t c = cb + lane;
+    const bool mine = c <= c1;
+    const int slot = mine && (c * SPAN) / d != r ? 1 : 0;
+    const unsigned long long* wp = ws.stamps + 2 * (mine ? c : c0) + slot;
+    unsigned long long v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
-    for (;;) {
-      bool ok = true;
-#pragma unroll
-      for (int i = 0; i < kMaxFused / kWave; ++i) {
-        const int b = tid + i * kWave;
-        if (i * kWave < G) {  // (uniform)
-          const unsigned long long f =
-              __hip_atomic_load(ws.flags + (b < G ? b : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok &= b >= G || f >= epoch;  // a zeroed flag (0) or any earlier call's epoch is below this call's
-        }
-      }
-      if (__ballot(!ok) == 0ull) break;
+    while (poll && __ballot(mine && (v >> 31) != tag) != 0ull) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) {  // ~1 s: a block never arrived (lost co-residency); flag it and let the launch drain
-        if (tid == 0) __hip_atomic_fetch_or(ws.err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (mine && (v >> 31) != tag) v = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > (1u << 22)) {  // ~1 s
+        if (lane == 0) __hip_atomic_fetch_or(ws.err, 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
+    const uint32_t b = mine ? (uint32_t)(v & 0x7fffffffu) : 0u;
+    m = b > m ? b : m;
   }
-  __syncthreads();
+  return wave_max_u32(m);
 }
 
 template <int KIND, int BITS, bool DEC, int GPT>
@@ -597,7 +597,7 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
                                                           double step, float* __restrict__ norms, uint64_t seed,
                                                           uint64_t counter, uint8_t* __restrict__ codes,
                                                           long long* __restrict__ nnz, float* __restrict__ out,
-                                                          QuantWs ws, unsigned long long epoch, int cal) {
+                                                          QuantWs ws, unsigned long long tag, int cal) {
   constexpr int64_t SPAN = (int64_t)kFT * kGroup * GPT;
   __shared__ uint32_t s_m[2][kFT / kWave];
   __shared__ float s_norm[2];
@@ -636,12 +636,12 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
   if (tid < 2) {  // slot 0: row r0, slot 1: row r0 + 1 (0 when the block holds none of it)
     uint32_t m = 0;
     for (int w = 0; w < kFT / kWave; ++w) m = s_m[tid][w] > m ? s_m[tid][w] : m;
-    __hip_atomic_store(ws.blkmax + 2 * blockIdx.x + tid, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ws.stamps + 2 * blockIdx.x + tid, stamp_word(tag, m), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (!(cal & 2)) fused_arrive(ws, epoch);
-  // The Philox words and the level table do not depend on the norm: computed after this block's flag is up and
-  // before its poll, so that they fill the wait for the slowest block instead of delaying this block's arrival
-  // (GPT = 2; at 4 they would not fit the registers)
+  // The Philox words and the level table do not depend on the norm: computed after this block's words are out and
+  // before its poll, so that they fill the wait for the row's slowest block instead of delaying this block's words
+  // (GPT = 2; at 4 they would not fit the registers).  (Computed under the x loads instead: no faster.)
   constexpr bool kPre = GPT <= 2;
   uint32_t wd[kPre ? GPT : 1][kGroup];
   if constexpr (kPre) {
@@ -649,23 +649,15 @@ __global__ __launch_bounds__(kFT) void quant_fused_kernel(const float* __restric
     for (int g = 0; g < GPT; ++g) group_words(base + ((int64_t)g * kFT + tid) * kGroup, seed, counter, wd[g]);
   }
   if (KIND == 0 && tid <= s) s_lvt[tid] = (float)level_value<0>(tid, s, step);
-  if (!(cal & 2)) fused_wait(ws, epoch);
-  else __syncthreads();
-  if (tid < kWave) {  // wave 0: each row's max over the blocks holding it
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
+  // waves 0 and 1: the max of row r0 + wid over the blocks holding it (row r0 + 1 only when this block holds some of it)
+  if (wid < 2 && r0 + wid < rows && (wid == 0 || rb < base + SPAN)) {
+    {
+      const int rr = wid;
       const int64_t r = r0 + rr;
-      if (r >= rows) break;  // (uniform)
       const int64_t c0 = r * d / SPAN, c1 = ((r + 1) * d - 1) / SPAN < (int64_t)gridDim.x - 1
                                                ? ((r + 1) * d - 1) / SPAN
                                                : (int64_t)gridDim.x - 1;
-      uint32_t m = 0;
-      for (int64_t c = c0 + lane; c <= c1; c += kWave) {
-        const int slot = (c * SPAN) / d == r ? 0 : 1;  // row r is block c's first row or its second
-        const uint32_t v = __hip_atomic_load(ws.blkmax + 2 * c + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        m = v > m ? v : m;
-      }
-      m = wave_max_u32(m);
+      const uint32_t m = row_max_polled(ws, r, d, SPAN, c0, c1, tag, !(cal & 2));
       if (lane == 0) {
         s_norm[rr] = __uint_as_float(m);
         if (r * d >= base && r * d < base + SPAN) norms[r] = __uint_as_float(m);  // the block holding its 1st element
@@ -751,11 +743,11 @@ int check_quant_args(int kind, int levels, int bits) {
 
 double level_step(int levels) { return 1.0 / (double)levels; }
 
-// the one-launch encode's exchange epochs: process-wide and increasing (64-bit, so they never wrap), so a flag left by
-// any earlier call (of any shape, on any workspace) is below this call's; never 0 (a fresh workspace's flags)
-unsigned long long next_epoch() {
-  static std::atomic<unsigned long long> epochs{0};
-  return ++epochs;
+// the one-launch encode's exchange tags: process-wide, 33 bits, never 0 (a fresh workspace's words); a word left by an
+// earlier call (of any shape, on any workspace) carries another tag unless it is 2^33 - 1 calls old
+unsigned long long next_tag() {
+  static std::atomic<unsigned long long> calls{0};
+  return (calls++ % ((1ull << 33) - 1)) + 1;
 }
 
 template <int KIND, int BITS, bool DEC>
@@ -900,7 +892,7 @@ int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p,
                     : (d >= 4 * kFT * kGroup && n <= (int64_t)cus * 4 * kFT * kGroup) ? 4
                                                                                         : 0;
     if (gpt) {
-      const unsigned long long ep = next_epoch();
+      const unsigned long long ep = next_tag();
       const unsigned grid = (unsigned)cdiv(n, (int64_t)gpt * kFT * kGroup);
       const char* fname = DEC ? "quant_fused_encode_decode" : "quant_fused_encode";
 #ifdef FLC_CALIB  // calibration builds (tools/quant_cal_probe.py): 1 non-temporal stores, 2 no exchange, 4 traffic only

@@ -222,6 +222,26 @@ def test_quant_encode_auto_equals_the_separate_calls(p, kind, levels, rows, d):
     assert torch.equal(pkt.codes, pkt3.codes) and gc.same_bits(out3.cpu().numpy(), ref_out.cpu().numpy())
 
 
+def test_quant_one_launch_interleaved_shapes_share_the_exchange_words():
+    """The one-launch quantizer's exchange words are tagged per call and polled per row: shapes with different grids
+    and row layouts interleaved on one workspace (a word left by a larger grid must never pass for this call's), each
+    call equal to the separate calls, and the exchange's error word 0 at the end."""
+    codec = _codec()
+    cases = []
+    for rows, d in ((10, 417482), (1, 16384), (3, 2_000_003), (7, 16_387), (2, 1_000_000)):
+        g = np.random.default_rng(rows + d)
+        xd = torch.from_numpy((g.standard_normal((rows, d)) * 1e-3).astype(np.float32)).to(DEV)
+        norms = codec.quant_norm(xd, math.inf)
+        pkt = codec.quant_encode(xd, 0, 127, norms, 5, 1, None)
+        cases.append((xd, pkt.codes.clone(), codec.quant_decode(pkt).clone()))
+    codec.quant_status(reset=True)
+    for rep in range(3):
+        for xd, codes, out in cases[rep % 2:] + cases[: rep % 2]:
+            pkt2, out2 = codec.quant_encode_auto(xd, 0, 127, math.inf, 5, 1)
+            assert torch.equal(pkt2.codes, codes) and torch.equal(out2.view(torch.int32), out.view(torch.int32))
+    assert codec.quant_status() == 0
+
+
 def test_quant_one_launch_nan_and_zero_rows():
     """The one-launch path on rows with NaN / inf / all zeros: the norms and codes of the two-launch path."""
     codec = _codec()

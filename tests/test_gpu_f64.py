@@ -254,6 +254,28 @@ def test_f64_topk_ties_of_the_kth_value(n_ties):
         assert g64.same_bits(codec.topk_dense_f64(torch.from_numpy(x).to(DEV), K).cpu().numpy(), exp), K
 
 
+@pytest.mark.parametrize("n_ties", [100, 400, 1500])
+def test_f64_topk_clustered_ties_in_one_chunk(n_ties):
+    """Ties of the K-th value packed into one 8192-element chunk at 25 M (12 chunks per select block): 100 ties put more
+    of the bin's keys in one block than its 64 list slots (the overflow list); 400 put more band keys in one chunk than
+    its LDS slot holds (341: the block's bin keys then come from its segments); 1500 overflow the chunk's segment (the
+    band is off, the exact passes run).  k cuts through the ties each time."""
+    from fl_sim_amd import codec
+
+    n = 25_000_000
+    g = np.random.default_rng(n_ties)
+    x = g.standard_normal(n) * 1e-3
+    v = np.sort(x)[-(n // 100)]
+    c = 1234 * 8192 + 17
+    x[c: c + n_ties] = v
+    xd = torch.from_numpy(x).to(DEV)
+    above = int((x > v).sum())
+    for K in (above + n_ties // 3, above + n_ties):
+        exp, _ = ref.topk(x, K)
+        assert g64.same_bits(codec.topk_dense_f64(xd, K).cpu().numpy(), exp), K
+    assert sum(codec.topk_status_all().values()) == 0
+
+
 def test_f64_topk_full_size_25m():
     """The headline size of the float64 top-k (BASELINE configs[2]'s 25 M, float64): 1 % and 0.1 % against numpy's
     argsort (the oracle), on gaussian and heavy-tailed vectors."""
