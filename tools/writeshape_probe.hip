@@ -6,6 +6,8 @@
 //          same 4 KB pieces at the same 32 KB stride as under w4
 //   w8h:   8 KB per wave, pieces j and j + P/2 (half the array apart)
 //   w8nt:  w8 with non-temporal stores
+//   w8w2:  8 KB per workgroup of 2 waves, 4 KB per wave (wave w of workgroup j -> piece 2j + w)
+//   w16w4: 16 KB per workgroup of 4 waves, 4 KB per wave
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/writeshape_probe tools/writeshape_probe.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -38,6 +40,15 @@ __global__ __launch_bounds__(64) void wr(f32x4* __restrict__ out, long P, float 
   }
 }
 
+template <int W>
+__global__ __launch_bounds__(64 * W) void wrw(f32x4* __restrict__ out, float v) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long p0 = (long)blockIdx.x * W + w;
+  const f32x4 val = {v, v + 1.f, v + 2.f, v + 3.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) out[p0 * 256 + q * 64 + lane] = val;
+}
+
 int main() {
   const long bytes = 1l << 30, P = bytes / 4096;  // 4 KB pieces
   f32x4* out;
@@ -62,7 +73,10 @@ int main() {
     const float c = t([&] { wr<2><<<P / 2, 64>>>(out, P, 1.f); });
     const float d = t([&] { wr<3><<<P / 2, 64>>>(out, P, 1.f); });
     const float e = t([&] { wr<4><<<P / 2, 64>>>(out, P, 1.f); });
-    printf("round %d: 1 GiB of stores: w4 %.1f us | w8 %.1f | w8x %.1f | w8h %.1f | w8nt %.1f\n", round, a, b, c, d, e);
+    const float f = t([&] { wrw<2><<<P / 2, 128>>>(out, 1.f); });
+    const float g = t([&] { wrw<4><<<P / 4, 256>>>(out, 1.f); });
+    printf("round %d: 1 GiB of stores: w4 %.1f us | w8 %.1f | w8x %.1f | w8h %.1f | w8nt %.1f | w8w2 %.1f | w16w4 %.1f\n",
+           round, a, b, c, d, e, f, g);
   }
   return 0;
 }
