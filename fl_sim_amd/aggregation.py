@@ -366,9 +366,16 @@ def feddyn_update(model_params: Sequence[torch.Tensor], h_params: Sequence[torch
     ps = _params(model_params)
     dev = ps[0].device
     alpha = -mu / num_clients
-    srcs = [[_on(t, dev) for t in m["parameters"]] for m in messages]
     w = [1 / len(messages)] * len(messages)
     cap = codec.MODEL_FOLD_MAX_SRC
+    ps_ = codec._pysrv()
+    if ps_ is not None and len(messages) <= cap:
+        try:  # the common case in one C call: the messages already on the model's device
+            ps_(ps, h_params, messages, "parameters", w, _lib.FLC_SRV_FEDDYN, 1, 0, 0.0, alpha)
+            return
+        except TypeError:
+            pass  # messages elsewhere: moved below
+    srcs = [[_on(t, dev) for t in m["parameters"]] for m in messages]
     if len(srcs) <= cap:
         codec.model_fold_server(ps, h_params, srcs, w, "feddyn", True, 0, 0.0, alpha)
         return
@@ -389,8 +396,15 @@ def pfedme_update(model_params: Sequence[torch.Tensor], messages: Sequence[Mappi
         return
     ps = _params(model_params)
     dev = ps[0].device
-    srcs = [[_on(t, dev) for t in m["parameters"]] for m in messages]
     w = [1 / len(messages)] * len(messages) if messages else []
+    ps_ = codec._pysrv()
+    if ps_ is not None and len(messages) <= codec.MODEL_FOLD_MAX_SRC:
+        try:  # the common case in one C call (no message: the blend of θ with itself, init 2)
+            ps_(ps, ps, messages, "parameters", w, _lib.FLC_SRV_PFEDME, 1, 0 if messages else 2, 0.0, beta)
+            return
+        except TypeError:
+            pass  # messages elsewhere: moved below
+    srcs = [[_on(t, dev) for t in m["parameters"]] for m in messages]
     if len(srcs) <= codec.MODEL_FOLD_MAX_SRC:
         # (no message: avg_parameters returns before its mul_(inertia): the blend of θ with itself, init 2)
         codec.model_fold_server(ps, ps, srcs, w, "pfedme", True, 0 if srcs else 2, 0.0, beta)

@@ -787,6 +787,22 @@ def _pyfold():
     return _PYFOLD[0]
 
 
+_PYSRV: list = []
+
+
+def _pysrv():
+    """fl_sim_amd._flcfold.server_fold (csrc/pyfold.cpp: flc_model_fold_server on Python lists of tensors, at most 16
+    messages) when built, else None."""
+    if not _PYSRV:
+        try:
+            from . import _flcfold
+
+            _PYSRV.append(_flcfold.server_fold)
+        except (ImportError, AttributeError):
+            _PYSRV.append(None)
+    return _PYSRV[0]
+
+
 def model_fold_server(theta: Sequence[torch.Tensor], aux: Sequence[torch.Tensor],
                       srcs: Sequence[Sequence[torch.Tensor]], weights: Sequence[float], kind: str, fold: bool = True,
                       init_mode: int = 0, inertia: float = 0.0, c: float = 0.0) -> None:

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kThreads) void feddr_combine64_kernel(double* __res
 // OPT >= 0, the step of fedopt_step on the folded value — the same roundings as the two kernels, in one pass.
 // ------------------------------------------------------------------------------------------------
 constexpr int kModelT = 16;              // tensors per launch (kernel-argument budget: ~2.7 KB)
-constexpr int kModelChunk = kThreads * 16;  // elements per block
+constexpr int kModelChunk = kThreads * 4;  // elements per block: one float4 per thread, every load in flight at once
 
 struct ModelPack {
   float* dst[kModelT];

@@ -1,6 +1,7 @@
 // pyfold.cpp — `fl_sim_amd._flcfold.model_fold`: the server's whole-model fold (flc_model_fold) called straight from
 // Python lists of tensors, for the per-round host path of FedOptServer.update / avg_parameters / add_parameters /
-// update_gradients (_fedopt.py:196-240, nodes.py:1116-1180).
+// update_gradients (_fedopt.py:196-240, nodes.py:1116-1180); `server_fold`, the same for FedDyn's and pFedMe's server
+// updates (flc_model_fold_server).
 //
 // At configs[0] (cnn_femmist_tiny: 8 tensors, 10 clients) the kernel takes ~9 us, but going through the dispatcher
 // (torch.ops.flcodec.model_fold_) cost ~14 us of host time: every tensor of the 96 in the call is boxed into an IValue
@@ -156,6 +157,96 @@ PyObject* model_fold(PyObject*, PyObject* args) {
   return done((Py_INCREF(Py_None), Py_None));
 }
 
+// server_fold(theta, aux, msgs, key, weights, kind, fold, init_mode, inertia, c): flc_model_fold_server (FedDyn's h
+// fold + average, pFedMe's average + blend: feddyn/_feddyn.py:172-184, pfedme/_pfedme.py:166-175) on Python lists, at
+// most 16 messages (the caller chains longer lists).  The same checks as model_fold, the same errors.
+PyObject* server_fold(PyObject*, PyObject* args) {
+  PyObject *theta, *aux, *msgs, *key, *weights;
+  int kind, fold, init_mode;
+  double inertia, c;
+  if (!PyArg_ParseTuple(args, "OOOOOiiidd", &theta, &aux, &msgs, &key, &weights, &kind, &fold, &init_mode, &inertia,
+                        &c))
+    return nullptr;
+  std::vector<PyObject*> keep;
+  auto done = [&](PyObject* r) {
+    for (PyObject* o : keep) Py_XDECREF(o);
+    return r;
+  };
+  PyObject* ft = PySequence_Fast(theta, "theta must be a sequence of tensors");
+  if (!ft) return nullptr;
+  keep.push_back(ft);
+  PyObject* fa = PySequence_Fast(aux, "aux must be a sequence of tensors");
+  if (!fa) return done(nullptr);
+  keep.push_back(fa);
+  PyObject* fm = PySequence_Fast(msgs, "messages must be a sequence");
+  if (!fm) return done(nullptr);
+  keep.push_back(fm);
+  PyObject* fw = PySequence_Fast(weights, "weights must be a sequence of floats");
+  if (!fw) return done(nullptr);
+  keep.push_back(fw);
+  const Py_ssize_t nt = PySequence_Fast_GET_SIZE(ft), ns = PySequence_Fast_GET_SIZE(fm);
+  if (PySequence_Fast_GET_SIZE(fw) != ns) return done(value_error("one weight per message"));
+  if (PySequence_Fast_GET_SIZE(fa) != nt) return done(value_error("one aux tensor per model tensor"));
+  if (ns > kMaxSrc) return done(value_error("server_fold takes at most 16 messages"));
+  if (nt == 0) return done((Py_INCREF(Py_None), Py_None));
+  int dev = -1;
+  std::vector<float*> tp(nt), ap(nt);
+  std::vector<int64_t> sz(nt);
+  PyObject** ti = PySequence_Fast_ITEMS(ft);
+  PyObject** ai = PySequence_Fast_ITEMS(fa);
+  for (Py_ssize_t t = 0; t < nt; ++t) {
+    const at::Tensor* a = usable(ti[t], &dev);
+    if (!a) return done(type_error("model tensors must be contiguous fp32 HIP tensors on one device"));
+    tp[t] = a->data_ptr<float>();
+    sz[t] = a->numel();
+    const at::Tensor* b = usable(ai[t], &dev);
+    if (!b) return done(type_error("aux tensors must be contiguous fp32 HIP tensors on the model's device"));
+    if (b->numel() != sz[t]) return done(value_error("aux tensors must match the model tensors' sizes"));
+    ap[t] = b->data_ptr<float>();
+  }
+  std::vector<const float*> sp((size_t)(ns > 0 ? ns : 1) * nt);
+  std::vector<float> w(ns > 0 ? ns : 1);
+  PyObject** mi = PySequence_Fast_ITEMS(fm);
+  PyObject** wi = PySequence_Fast_ITEMS(fw);
+  for (Py_ssize_t m = 0; m < ns; ++m) {
+    const double wd = PyFloat_AsDouble(wi[m]);
+    if (wd == -1.0 && PyErr_Occurred()) return done(nullptr);
+    w[m] = (float)wd;
+    PyObject* msg = mi[m];
+    if (key != Py_None) {
+      msg = PyObject_GetItem(msg, key);
+      if (!msg) return done(nullptr);
+      keep.push_back(msg);
+    }
+    PyObject* f = PySequence_Fast(msg, "a message is a sequence of tensors");
+    if (!f) return done(nullptr);
+    keep.push_back(f);
+    if (PySequence_Fast_GET_SIZE(f) != nt) return done(value_error("every message has one tensor per model tensor"));
+    PyObject** it = PySequence_Fast_ITEMS(f);
+    for (Py_ssize_t t = 0; t < nt; ++t) {
+      const at::Tensor* a = usable(it[t], &dev);
+      if (!a) return done(type_error("message tensors must be contiguous fp32 HIP tensors on the model's device"));
+      if (a->numel() != sz[t]) return done(value_error("message tensors must match the model tensors' sizes"));
+      sp[(size_t)m * nt + t] = a->data_ptr<float>();
+    }
+  }
+  void* st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+  int rc = FLC_OK;
+  Py_BEGIN_ALLOW_THREADS
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  rc = flc_model_fold_server(tp.data(), ap.data(), sp.data(), w.data(), (int)ns, sz.data(), (int)nt, kind, fold,
+                             init_mode, (float)inertia, c, st);
+  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  Py_END_ALLOW_THREADS
+  if (rc != FLC_OK) {
+    PyErr_Format(PyExc_RuntimeError, "flc_model_fold_server failed with status %d: %s", rc, flc_last_error());
+    return done(nullptr);
+  }
+  return done((Py_INCREF(Py_None), Py_None));
+}
+
 void release_storage(void* ctx) { delete static_cast<c10::Storage*>(ctx); }
 
 // alias(host_tensor, device_index) -> tensor on cuda:device_index over the same bytes (see the header)
@@ -186,6 +277,9 @@ PyMethodDef kMethods[] = {
     {"model_fold", model_fold, METH_VARARGS,
      "model_fold(dsts, msgs, key, weights, init_mode, beta, theta, v, opt, lr, beta2, tau): flc_model_fold on Python "
      "lists of HIP tensors, launched on the current stream of the model's device"},
+    {"server_fold", server_fold, METH_VARARGS,
+     "server_fold(theta, aux, msgs, key, weights, kind, fold, init_mode, inertia, c): flc_model_fold_server (FedDyn / "
+     "pFedMe) on Python lists of HIP tensors, at most 16 messages, on the current stream of the model's device"},
     {"alias", alias, METH_VARARGS,
      "alias(host_tensor, device_index): a HIP-device tensor over a pinned host tensor's memory (zero-copy)"},
     {nullptr, nullptr, 0, nullptr}};

@@ -390,9 +390,22 @@ def test_fold_with_host_messages_equals_device_messages(fold_path):
 from tests.golden.gen_golden import FEDDYN_CFG, PFEDME_BETAS, feddyn_inputs, pfedme_inputs  # noqa: E402
 
 
+@pytest.fixture(params=["pyfold", "ctypes"])
+def srv_path(request, monkeypatch):
+    """FedDyn / pFedMe through fl_sim_amd._flcfold.server_fold (the default when built) and through the ctypes binding
+    of flc_model_fold_server: the same C-ABI call behind both"""
+    from fl_sim_amd import codec
+
+    if request.param == "pyfold":
+        assert codec._pysrv() is not None
+    else:
+        monkeypatch.setattr(codec, "_PYSRV", [None])
+    return request.param
+
+
 @pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
 @pytest.mark.parametrize("nm", [10, 20, 0])
-def test_feddyn_update_matches_reference(tag, shapes, nm):
+def test_feddyn_update_matches_reference(tag, shapes, nm, srv_path):
     """FedDynServer.update (feddyn/_feddyn.py:172-184): h and θ in one launch (10 messages) or chained (20), against
     the reference's own outputs, bit for bit (line 184's discarded result included: θ is the average)."""
     from fl_sim_amd import aggregation
@@ -407,7 +420,7 @@ def test_feddyn_update_matches_reference(tag, shapes, nm):
 @pytest.mark.parametrize("tag,shapes", [("small", SMALL_SHAPES), ("config1", CONFIG1_SHAPES)])
 @pytest.mark.parametrize("nm", [10, 20, 0])
 @pytest.mark.parametrize("beta", PFEDME_BETAS)
-def test_pfedme_update_matches_reference(tag, shapes, nm, beta):
+def test_pfedme_update_matches_reference(tag, shapes, nm, beta, srv_path):
     """pFedMeServer.update (pfedme/_pfedme.py:166-175): the average and the β blend with the saved model in one launch
     (10 messages; 0: the blend of θ with itself), or the chained average and one blend pass (20)."""
     from fl_sim_amd import aggregation

@@ -1,5 +1,6 @@
-"""The aggregation kernels under rocprofv3 --kernel-trace --stats (profiles/r03/*agg*): FedAvg / FedAdam server updates
-and avg_parameters at configs[0]'s model x 10 clients, and one weighted fold of 8 x 25 M (flc_weighted_sum)."""
+"""The aggregation kernels under rocprofv3 --kernel-trace --stats (profiles/r03/*agg*): FedAvg / FedDyn / pFedMe /
+FedAdam server updates and avg_parameters at configs[0]'s model x 10 clients, and one weighted fold of 8 x 25 M
+(flc_weighted_sum)."""
 import os
 import sys
 import time
@@ -21,7 +22,12 @@ msgs = [{"train_samples": 100 * (i + 1), "delta_parameters": [torch.randn(s, gen
 srcs = [torch.randn(25_000_000, generator=g, device=dev) for _ in range(8)]
 dst = torch.randn(25_000_000, generator=g, device=dev)
 w8 = [0.1 * (i + 1) for i in range(8)]
+pm = [{"train_samples": m["train_samples"], "parameters": [t + p for t, p in zip(m["delta_parameters"], th)]}
+      for m in msgs]
+h = [torch.zeros(s, device=dev) for s in SHAPES]
 legs = (("fedavg", lambda: fagg.fedopt_update(th, dl, None, msgs, "avg", 1.0, (0.0, 1.0), 1e-3)),
+        ("feddyn", lambda: fagg.feddyn_update(th, h, pm, 0.01, 20)),
+        ("pfedme", lambda: fagg.pfedme_update(th, pm, 0.7)),
         ("fedadam", lambda: fagg.fedopt_update(th, dl, v, msgs, "adam", 1e-2, (0.9, 0.99), 1e-3)),
         ("avg_parameters", lambda: fagg.avg_parameters(th, msgs, size_aware=True, key="delta_parameters")),
         ("weighted_sum_8x25M", lambda: codec.weighted_sum(dst, srcs, w8, init_mode=0, beta=0.5)))
