@@ -23,7 +23,14 @@ from ._lib import call
 _WS: Dict[Tuple[int, int, str], torch.Tensor] = {}
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(device: torch.device) -> int:
+    """The raw handle of ``device``'s current stream (torch's C accessor when present: building a Stream object per
+    call cost a few microseconds of host time on every launch of the small configs)."""
+    if _RAW_STREAM is not None:
+        return _RAW_STREAM(device.index if device.index is not None else torch.cuda.current_device())
     return torch.cuda.current_stream(device).cuda_stream
 
 
@@ -105,7 +112,7 @@ def quant_norm(x2d: torch.Tensor, p: float = math.inf) -> torch.Tensor:
     if pk is None:
         raise ValueError(f"p must be inf or 2 (got {p})")
     norms = torch.empty(rows, dtype=torch.float32, device=x2d.device)
-    nb = _lib.size("flc_quant_workspace_size", rows, d)
+    nb = _ws_size(x2d.device, "flc_quant_workspace_size", rows, d)
     ws = workspace(x2d.device, nb, "quant")
     call("flc_quant_norm", _p(x2d), rows, d, pk, _p(norms), _p(ws), ws.numel(), _stream(x2d.device))
     return norms
@@ -130,7 +137,7 @@ def quant_encode(x2d: torch.Tensor, kind: int, levels: int, norms: torch.Tensor,
     nnz = torch.empty(rows, dtype=torch.int64, device=x2d.device) if want_nnz else None
     if compat_u is not None and compat_u.dtype != torch.float64:
         raise TypeError("compat_u must be float64")
-    nb = _lib.size("flc_quant_workspace_size", rows, d)
+    nb = _ws_size(x2d.device, "flc_quant_workspace_size", rows, d)
     ws = workspace(x2d.device, nb, "quant")
     call("flc_quant_encode", _p(x2d), rows, d, kind, levels, bits, _p(norms), seed, counter, _p(compat_u),
          _p(codes), _p(nnz), _p(ws), ws.numel(), _stream(x2d.device))
@@ -151,7 +158,7 @@ def quant_encode_decode(x2d: torch.Tensor, kind: int, levels: int, norms: torch.
         out = torch.empty(rows, d, dtype=torch.float32, device=x2d.device)
     if compat_u is not None and compat_u.dtype != torch.float64:
         raise TypeError("compat_u must be float64")
-    ws = workspace(x2d.device, _lib.size("flc_quant_workspace_size", rows, d), "quant")
+    ws = workspace(x2d.device, _ws_size(x2d.device, "flc_quant_workspace_size", rows, d), "quant")
     call("flc_quant_encode_decode", _p(x2d), rows, d, kind, levels, bits, _p(norms), seed, counter, _p(compat_u),
          _p(codes), _p(nnz), _p(out), _p(ws), ws.numel(), _stream(x2d.device))
     return QuantPacket(codes, norms, rows, d, kind, levels, bits, nnz), out
@@ -171,7 +178,7 @@ def quant_encode_auto(x2d: torch.Tensor, kind: int, levels: int, p: float = math
     norms = torch.empty(rows, dtype=torch.float32, device=x2d.device)
     nnz = torch.empty(rows, dtype=torch.int64, device=x2d.device) if want_nnz else None
     out = torch.empty(rows, d, dtype=torch.float32, device=x2d.device) if decode else None
-    ws = workspace(x2d.device, _lib.size("flc_quant_workspace_size", rows, d), "quant")
+    ws = workspace(x2d.device, _ws_size(x2d.device, "flc_quant_workspace_size", rows, d), "quant")
     call("flc_quant_encode_auto", _p(x2d), rows, d, kind, levels, bits, pk, seed, counter, _p(codes), _p(norms),
          _p(nnz), _p(out), _p(ws), ws.numel(), _stream(x2d.device))
     _after_encode(x2d.device, ("quant",))
@@ -196,7 +203,7 @@ def natural_encode(x: torch.Tensor, seed: int = 0, counter: int = 0, compat_u: O
     n = x.numel()
     codes = torch.empty(n, dtype=torch.int16, device=x.device)
     nnz = torch.empty(1, dtype=torch.int64, device=x.device) if want_nnz else None
-    nb = _lib.size("flc_natural_workspace_size", n)
+    nb = _ws_size(x.device, "flc_natural_workspace_size", n)
     ws = workspace(x.device, nb, "natural")
     call("flc_natural_encode", _p(x), n, seed, counter, _p(compat_u), _p(codes), _p(nnz), _p(ws), ws.numel(),
          _stream(x.device))
@@ -331,7 +338,7 @@ def sparse_decode(idx: torch.Tensor, val: torch.Tensor, n: int, scale: float = 1
         call("flc_sparse_decode_tiled", _p(idx), _p(val), idx.numel(), scale, n, weight, int(accumulate), _p(out),
              _p(tiles), _stream(out.device))
         return out
-    ws = workspace(out.device, _lib.size("flc_sparse_decode_workspace_size", n), "decode")
+    ws = workspace(out.device, _ws_size(out.device, "flc_sparse_decode_workspace_size", n), "decode")
     call("flc_sparse_decode", _p(idx), _p(val), idx.numel(), scale, n, weight, int(accumulate), _p(out), _p(ws),
          ws.numel(), _stream(out.device))
     return out
@@ -606,7 +613,7 @@ def stacked_decode(pkt: StackedPacket, out: Optional[torch.Tensor] = None, weigh
         call("flc_stacked_decode_tiled", _p(pkt.idx), _p(pkt.codes), pkt.idx.numel(), pkt.levels, _p(pkt.norm), pkt.n,
              weight, int(accumulate), _p(out), _p(pkt.tiles), _stream(out.device))
         return out
-    ws = workspace(out.device, _lib.size("flc_sparse_decode_workspace_size", pkt.n), "decode")
+    ws = workspace(out.device, _ws_size(out.device, "flc_sparse_decode_workspace_size", pkt.n), "decode")
     call("flc_stacked_decode", _p(pkt.idx), _p(pkt.codes), pkt.idx.numel(), pkt.levels, _p(pkt.norm), pkt.n, weight,
          int(accumulate), _p(out), _p(ws), ws.numel(), _stream(out.device))
     return out
@@ -659,7 +666,7 @@ def adaptive_prepare(x: torch.Tensor) -> torch.Tensor:
     if n == 0:
         raise ValueError("'a' cannot be empty unless no samples are taken")
     status = torch.empty(1, dtype=torch.int32, device=x.device)
-    ws = workspace(x.device, _lib.size("flc_adaptive_workspace_size", n), "adaptive")
+    ws = workspace(x.device, _ws_size(x.device, "flc_adaptive_workspace_size", n), "adaptive")
     call("flc_adaptive_prepare_f64" if f64 else "flc_adaptive_prepare", _p(x), n, _p(status), _p(ws), ws.numel(),
          _stream(x.device))
     return status
@@ -676,7 +683,7 @@ def adaptive_select(x: torch.Tensor, u: float, out: Optional[torch.Tensor] = Non
     if out is None:
         out = torch.empty(n, dtype=x.dtype, device=x.device)
     index = torch.empty(1, dtype=torch.int64, device=x.device)
-    ws = workspace(x.device, _lib.size("flc_adaptive_workspace_size", n), "adaptive")
+    ws = workspace(x.device, _ws_size(x.device, "flc_adaptive_workspace_size", n), "adaptive")
     call("flc_adaptive_select_f64" if f64 else "flc_adaptive_select", _p(x), n, float(u), _p(index), _p(out), _p(ws),
          ws.numel(), _stream(x.device))
     return out, index
@@ -687,7 +694,7 @@ def adaptive_stats(x: torch.Tensor) -> dict:
     taken, chunks re-run sequentially, and whether the exact sequential chain ran instead."""
     x = x.reshape(-1)
     n = x.numel()
-    ws = workspace(x.device, _lib.size("flc_adaptive_workspace_size", n), "adaptive")
+    ws = workspace(x.device, _ws_size(x.device, "flc_adaptive_workspace_size", n), "adaptive")
     st = torch.empty(4, dtype=torch.int32, device=x.device)
     call("flc_adaptive_stats", _p(ws), ws.numel(), n, _p(st), _stream(x.device))
     s = [int(v) for v in st.cpu()]
@@ -975,7 +982,7 @@ def _dev_f64(x: torch.Tensor, name: str = "x") -> torch.Tensor:
 
 
 def _ws64(x: torch.Tensor, k: int = 0) -> torch.Tensor:
-    return workspace(x.device, _lib.size("flc_f64_workspace_size", x.numel(), int(k)), "f64")
+    return workspace(x.device, _ws_size(x.device, "flc_f64_workspace_size", x.numel(), int(k)), "f64")
 
 
 def copy_f64(x: torch.Tensor) -> torch.Tensor:

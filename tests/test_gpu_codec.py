@@ -222,6 +222,19 @@ def test_quant_encode_auto_equals_the_separate_calls(p, kind, levels, rows, d):
     assert torch.equal(pkt.codes, pkt3.codes) and gc.same_bits(out3.cpu().numpy(), ref_out.cpu().numpy())
 
 
+def test_raw_stream_handle_is_the_current_stream():
+    """codec._stream (torch's raw current-stream accessor) names the stream torch.cuda.current_stream names: the
+    default stream, a side stream under `with torch.cuda.stream`, a device given without an index."""
+    codec = _codec()
+    d = torch.device("cuda", 0)
+    assert codec._stream(d) == torch.cuda.current_stream(d).cuda_stream
+    s = torch.cuda.Stream(d)
+    with torch.cuda.stream(s):
+        assert codec._stream(d) == s.cuda_stream
+        assert codec._stream(torch.device("cuda")) == s.cuda_stream
+    assert codec._stream(torch.device("cuda")) == torch.cuda.current_stream().cuda_stream
+
+
 def test_quant_one_launch_interleaved_shapes_share_the_exchange_words():
     """The one-launch quantizer's exchange words are tagged per call and polled per row: shapes with different grids
     and row layouts interleaved on one workspace (a word left by a larger grid must never pass for this call's), each
