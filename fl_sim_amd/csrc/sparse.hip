@@ -123,16 +123,6 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave_kernel(const int* __
 
 // One-wave decode, NT tiles of 1024 outputs per wave (adjacent: one NT x 4 KB piece), every load chain
 // of the NT tiles in flight together.
-// The decode's 16-B output stores go past the XCD's L2 (sc1: written through to the memory side), so the kernel
-// ends without dirty L2 lines to write back: configs[2]'s 25 M step 69.4 -> 67.7 us, the 1 GiB step unchanged (same-box
-// A/B, profiles/r05/r05zq_store_ab.txt; non-temporal stores made the 1 GiB step 13 us slower).  The compiler does not
-// see these stores: nothing in the kernel reads `out` after them.
-__device__ __forceinline__ void out_store(float* p, float4 v) {
-  typedef float f32x4n __attribute__((ext_vector_type(4)));
-  const f32x4n w = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
-}
-
 template <int MODE, int NT>
 __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* __restrict__ idx,
                                                                     const float* __restrict__ val,
@@ -193,7 +183,7 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
     float4 v = tile4[q];
     if (e + 4 <= n) {
       if (weight != 1.0f) v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
-      out_store(out + e, v);
+      *reinterpret_cast<float4*>(out + e) = v;
     } else {
       const float vv[4] = {v.x, v.y, v.z, v.w};
       for (int c = 0; c < 4 && e + c < n; ++c) out[e + c] = weight != 1.0f ? weight * vv[c] : vv[c];
