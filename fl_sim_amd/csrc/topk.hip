@@ -65,6 +65,9 @@ constexpr int kSampTop = kSample / 64 * kTopPer;  // ... 4096 keys, 4 per encode
 constexpr int kHistBits = 11;
 constexpr int kHistBins = 1 << kHistBits;
 constexpr int kHistStride = kHistBins + 64;   // bins, [kHistBins] above-the-range count, [+1] max key
+// copies of the round-0 histogram: block b adds into copy b % kHistCopies (slot 0, then slots kMaxSlots ..), so each
+// bin's word takes G / kHistCopies of the G blocks' atomics instead of all of them; readers sum the copies
+constexpr int kHistCopies = 8;
 constexpr int kMaxSlots = 12;                 // histogram rounds per call (normal + fallback pass)
 constexpr int kEpochStride = 32;              // exchanges per call < 32
 constexpr int kMaxBlocks = 1024;              // <= kET (per-block words are read one per thread)
@@ -97,7 +100,7 @@ constexpr size_t al256(size_t v) { return (v + 255) / 256 * 256; }
 constexpr size_t kOffSt = 0;
 constexpr size_t kOffFlags = al256(kOffSt + 128);
 constexpr size_t kOffHist = al256(kOffFlags + (size_t)kMaxBlocks * kFlagStride * 4);
-constexpr size_t kOffAcc = kOffHist + (size_t)kMaxSlots * kHistStride * 4;  // contiguous with hist (zeroed together)
+constexpr size_t kOffAcc = kOffHist + (size_t)(kMaxSlots + kHistCopies - 1) * kHistStride * 4;  // contiguous with hist (zeroed together)
 constexpr size_t kOffBlk = al256(kOffAcc + 64);
 constexpr size_t kOffStamps = al256(kOffBlk + (size_t)kMaxBlocks * 8);
 constexpr size_t kOffBlkT = al256(kOffStamps + 128);   // [kMaxBlocks][4] per-block times (diagnostic build)
@@ -106,7 +109,7 @@ constexpr size_t kOffSampTop = al256(kOffSample + (size_t)kSample * 4);
 constexpr size_t kOffInbin = al256(kOffSampTop + (size_t)kSampTop * 4);
 constexpr size_t kOffBlkC = al256(kOffInbin + (size_t)kMaxBlocks * kInbin * 4);
 constexpr size_t kOffStage = al256(kOffBlkC + (size_t)kMaxBlocks * 4);  // + G * kCap * 8 (keys, then indices)
-static_assert(kOffAcc % 8 == 0, "acc words are 64-bit");
+static_assert(kOffAcc % 8 == 0 && kOffHist % 8 == 0 && (kHistStride * 4) % 8 == 0, "acc / total words are 64-bit");
 static_assert(sizeof(EncState) <= 128, "state block");
 
 // A batched call (flc_stacked_encode_batch) runs one independent select per client in one launch: client g owns
@@ -222,7 +225,7 @@ EncWs carve_enc(void* ws, int64_t n, int64_t k, int cus, size_t* need) {
   *need = kOffStage + vb;
   return w;
 }
-constexpr int kZeroWords = kMaxSlots * kHistStride + 16;  // hist + acc, as 32-bit words
+constexpr int kZeroWords = (kMaxSlots + kHistCopies - 1) * kHistStride + 16;  // hist + acc, as 32-bit words
 
 // ------------------------------------------------------------------------------------------------
 // helpers
@@ -887,6 +890,15 @@ struct SelState {
   long long need;
 };
 
+// copy c of the round-0 histogram
+__device__ __forceinline__ unsigned* hist_copy(const EncWs& w, int c) {
+  return w.hist() + (size_t)(c == 0 ? 0 : kMaxSlots + c - 1) * kHistStride;
+}
+// copy c's share of the candidate total (64-bit, after the above count and the max key)
+__device__ __forceinline__ unsigned long long* hist_total(const EncWs& w, int c) {
+  return reinterpret_cast<unsigned long long*>(hist_copy(w, c) + kHistBins + 2);
+}
+
 // after the exchange of round slot r: the summed histogram, its above-the-range count and max key (and,
 // for round 0, the candidate total) read into LDS in one batch of coherent loads (one round trip)
 __device__ __forceinline__ void load_hist(const EncWs& w, int r, unsigned* s_ghist, unsigned long long* s_ex,
@@ -895,11 +907,39 @@ __device__ __forceinline__ void load_hist(const EncWs& w, int r, unsigned* s_ghi
   unsigned* h = w.hist() + (size_t)r * kHistStride;
   const int tid = threadIdx.x;
   unsigned v[BPT];
-#pragma unroll
-  for (int i = 0; i < BPT; ++i) v[i] = ld_mem(&h[tid + i * kET]);
   unsigned long long e = 0;
-  if (tid < 2) e = ld_mem(&h[kHistBins + tid]);  // above count, max key
-  else if (tid == 2 && with_total) e = ld_mem64(&w.acc()[0]);
+  if (r == 0) {  // round 0: the sum of the copies (all loads issued together)
+    unsigned u[kHistCopies][BPT];
+#pragma unroll
+    for (int c = 0; c < kHistCopies; ++c)
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) u[c][i] = ld_mem(&hist_copy(w, c)[tid + i * kET]);
+    unsigned long long x[kHistCopies];
+    if (tid < 2) {  // above count (summed), max key (the largest)
+#pragma unroll
+      for (int c = 0; c < kHistCopies; ++c) x[c] = ld_mem(&hist_copy(w, c)[kHistBins + tid]);
+    } else if (tid == 2 && with_total) {  // the candidate total (summed)
+#pragma unroll
+      for (int c = 0; c < kHistCopies; ++c) x[c] = ld_mem64(hist_total(w, c));
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      v[i] = 0u;
+#pragma unroll
+      for (int c = 0; c < kHistCopies; ++c) v[i] += u[c][i];
+    }
+    if (tid < 3) {
+      unsigned long long a = 0u;
+#pragma unroll
+      for (int c = 0; c < kHistCopies; ++c) a = tid != 1 ? a + x[c] : (x[c] > a ? x[c] : a);
+      e = tid == 2 && !with_total ? 0ull : a;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) v[i] = ld_mem(&h[tid + i * kET]);
+    if (tid < 2) e = ld_mem(&h[kHistBins + tid]);  // above count, max key
+    else if (tid == 2 && with_total) e = ld_mem64(hist_total(w, 0));  // (never: only round 0 has a total)
+  }
 #pragma unroll
   for (int i = 0; i < BPT; ++i) s_ghist[tid + i * kET] = v[i];
   if (tid < 3) s_ex[tid] = e;
@@ -1287,7 +1327,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
       di[q] = si[q];
     }
   }
-  unsigned* h = w.hist();
+  unsigned* h = hist_copy(w, w.bid % kHistCopies);
   for (int i = tid; i < kHistBins; i += kET)
     if (s_hist[i]) atomicAdd(&h[i], s_hist[i]);
   const unsigned long long ab = block_sum<unsigned long long, kENW>((unsigned long long)fc.above, s_red);
@@ -1299,7 +1339,7 @@ __device__ __forceinline__ FilterOut filter_phase(const Src& x, int64_t n, const
     for (int i = 0; i < kENW; ++i) m = s_mx[i] > m ? s_mx[i] : m;
     if (ab) atomicAdd(&h[kHistBins], (unsigned)ab);
     atomicMax(&h[kHistBins + 1], m);
-    atomicAdd(&w.acc()[0], (unsigned long long)C_b);
+    atomicAdd(hist_total(w, w.bid % kHistCopies), (unsigned long long)C_b);
     if (STAGE) w.blk_c()[w.bid] = C_b;
   }
   STAMP(4);
