@@ -448,6 +448,7 @@ constexpr int kDigits = 8;          // 8-bit digits of a 64-bit key, most signif
 constexpr int kSample64 = 16384;    // sample keys
 constexpr int kSampleDigits = 3;    // the band's ends keep the sample keys' top 24 bits
 constexpr int kBand = 2048;         // band histogram bins
+constexpr int kBandCopies = 8;      // copies of the band histogram: block b adds into copy b % 8 (fewer atomics per word)
 constexpr int kBinCap = 16384;      // keys of the K-th largest's bin the gather's list holds
 constexpr int kGT = 1024;           // threads of the sample, gather and fallback blocks
 constexpr int kGNW = kGT / kWave;
@@ -471,7 +472,7 @@ struct Sel64 {
   long long ithr;                     // the kept ties: index >= ithr
   unsigned long long flags[kMaxG64];  // grid barriers (zeroed by the prep kernel: targets 1, 2, ... in each call)
   unsigned long long pab[kMaxG64];    // per block: keys >= t_hi in its chunks + kOvf if a segment overflowed
-  unsigned hist[kBand];               // the band histogram
+  unsigned hist[kBandCopies][kBand];  // the band histogram, in copies (their sum is the histogram)
   unsigned fhist[2 * kDigits][256];   // the fallback's digit histograms: key digits, then tie-index digits
   unsigned long long bkey[kBinCap];   // the K-th largest's bin: keys (less the bin's base) and their indices
   long long bidx[kBinCap];
@@ -585,9 +586,9 @@ __global__ __launch_bounds__(kT) void sel64_prep_kernel(const double* __restrict
                                                         Sel64* __restrict__ st) {
   const int tid = threadIdx.x;
   STAMP64(blockIdx.x == 0, 0);
+  for (int i = (int)blockIdx.x * kT + tid; i < kBandCopies * kBand; i += (int)gridDim.x * kT) (&st->hist[0][0])[i] = 0u;
   if (blockIdx.x == 0) {
     for (int i = tid; i < 2 * kDigits * 256; i += kT) (&st->fhist[0][0])[i] = 0u;
-    for (int i = tid; i < kBand; i += kT) st->hist[i] = 0u;
     for (int i = tid; i < kMaxG64; i += kT) st->flags[i] = 0ull;
     if (tid == 0) {
       st->fb = 0;
@@ -1008,7 +1009,7 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
     const unsigned long long ab_blk =
         block_sum<unsigned long long, kGNW>((unsigned long long)above, reinterpret_cast<unsigned long long*>(s_scan));
     for (int i = tid; i < kBand; i += kGT)
-      if (L.hb[0][i]) atomicAdd(&st->hist[i], L.hb[0][i]);
+      if (L.hb[0][i]) atomicAdd(&st->hist[blockIdx.x % kBandCopies][i], L.hb[0][i]);
     if (tid == 0) st_sc1(&st->pab[blockIdx.x], ab_blk + (L.ovf ? kOvf : 0ull));
     STAMP64(blockIdx.x == 0, 7);
 #ifdef FLC_SELECT_STAMPS
@@ -1016,14 +1017,27 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
 #endif
     grid_sync64(st, ++target, spin_lim);
     STAMP64(blockIdx.x == 0, 8);
-    // 3. the bin of the K-th largest (every block the same)
+    // 3. the bin of the K-th largest (every block the same); the thread's two bins of every copy are loaded together
+    // with the above counts
+    const int ja = kBand - 1 - 2 * tid, jb = kBand - 2 - 2 * tid;  // (pick_band's two bins of thread tid)
+    unsigned hca[kBandCopies], hcb[kBandCopies];
+#pragma unroll
+    for (int c = 0; c < kBandCopies; ++c) {
+      hca[c] = ld_sc1(&st->hist[c][ja]);
+      hcb[c] = ld_sc1(&st->hist[c][jb]);
+    }
     unsigned long long ab = 0ull;
     for (int s = tid; s < G; s += kGT) ab += ld_sc1(&st->pab[s]);
+    long long ha = 0, hb = 0;
+#pragma unroll
+    for (int c = 0; c < kBandCopies; ++c) {
+      ha += hca[c];
+      hb += hcb[c];
+    }
     ab = block_sum<unsigned long long, kGNW>(ab, reinterpret_cast<unsigned long long*>(s_scan));
     const bool ovf = ab >= kOvf;
     // (the K-th largest's rank among the band keys: k less the keys above the band)
-    pick_band([&](int j) { return (long long)ld_sc1(&st->hist[j]); }, k - (long long)(ab & (kOvf - 1ull)), s_scan,
-              s_bin);
+    pick_band([&](int j) { return j == ja ? ha : hb; }, k - (long long)(ab & (kOvf - 1ull)), s_scan, s_bin);
     const long long bin = s_bin[0], rem0 = s_bin[1], cnt0 = s_bin[2];
     band = !ovf && bin >= 0 && cnt0 <= kBinCap;  // bin < 0: the sample's ceiling was too low or its floor too high
     STAMP64(blockIdx.x == 0, 10);
