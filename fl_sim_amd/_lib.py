@@ -118,6 +118,11 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_int64, c_void_p, c_void_p, c_int, c_int64, c_int64, c_int, c_int, c_void_p, c_void_p],
     ),
+    "flc_fedopt_fold_records": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float,
+         c_int, c_double, c_double, c_double, c_void_p],
+    ),
     "flc_comm_id_bytes": (c_size_t, []),
     "flc_comm_rccl_origin": (c_char_p, []),
     "flc_comm_unique_id": (c_int, [c_void_p]),
@@ -169,9 +174,12 @@ SIGNATURES = {
     "flc_fedopt_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
     "flc_model_fold": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
                                c_int, c_double, c_double, c_double, c_void_p]),
+    "flc_avg_and_gradients": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                      c_int, c_float, c_void_p]),
     "flc_model_fold_server": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                                       c_int, c_float, c_double, c_void_p]),
     "flc_delta_flatten": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "flc_delta_count_nonzero_at": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
     "flc_feddr_combine": (
         c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_int, c_float, c_void_p]
     ),

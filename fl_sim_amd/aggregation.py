@@ -31,7 +31,7 @@ from typing import Iterable, List, Mapping, Optional, Sequence
 
 import torch
 
-from . import _lib, codec, hoststage
+from . import _lib, codec, compressed, hoststage
 
 
 def _params(ps) -> List[torch.Tensor]:
@@ -203,6 +203,86 @@ def update_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Ma
     return grads
 
 
+def _pair_fold(dev: torch.device, params: Sequence[torch.Tensor], messages: Sequence[Mapping], wp: Sequence[float],
+               wg: Sequence[float], inertia: float):
+    """flc_avg_and_gradients on ``dev``: the parameters folded in place, the gradients into one new flat buffer.
+    Returns (gradient views, the flat buffer), or None (nothing launched) when a tensor is not a contiguous fp32
+    tensor of ``dev``."""
+    import ctypes
+
+    ok = lambda t: t.is_cuda and t.device == dev and t.dtype is torch.float32 and t.is_contiguous()  # noqa: E731
+    if not all(ok(p) for p in params):
+        return None
+    T = len(params)
+    psrc = [[_on(t, dev) for t in m["parameters"]] for m in messages]
+    gsrc = [[_on(t, dev) for t in m["gradients"]] for m in messages]
+    if any(len(r) != T or not all(ok(t) and t.numel() == p.numel() for t, p in zip(r, params))
+           for r in psrc + gsrc):
+        return None
+    flat = torch.empty(max(sum(p.numel() for p in params), 1), dtype=torch.float32, device=dev)
+    grads, off = [], 0
+    for p in params:
+        grads.append(flat[off:off + p.numel()].view(p.shape))
+        off += p.numel()
+    P = ctypes.c_void_p
+    n = len(messages)
+    _lib.call("flc_avg_and_gradients", (P * T)(*[p.data_ptr() for p in params]),
+              (P * T)(*[g.data_ptr() for g in grads]),
+              (P * (n * T))(*[t.data_ptr() for r in psrc for t in r]),
+              (P * (n * T))(*[t.data_ptr() for r in gsrc for t in r]),
+              (ctypes.c_float * n)(*wp), (ctypes.c_float * n)(*wg), n, (ctypes.c_int64 * T)(*[p.numel() for p in params]),
+              T, float(inertia), codec._stream(dev))
+    return grads, flat
+
+
+def avg_parameters_and_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Mapping],
+                                 size_aware: bool = False, inertia: float = 0.0) -> Optional[List[torch.Tensor]]:
+    """``avg_parameters(size_aware, inertia)`` then ``update_gradients()`` (nodes.py:1134-1180) over the same messages
+    in ONE launch (flc_avg_and_gradients) — the update of the variance-reduced servers (fedprox/_fedprox.py:163-167,
+    fedpd/_fedpd.py:197-202, proxskip/_proxskip.py:212-216, pfedmac/_pfedmac.py:158-162).  Bit-identical to the two
+    calls; a host-resident model is staged once (its messages and parameters in; the parameters and, in one copy, the
+    gradients out).  Sets ``.grad`` of each parameter as update_gradients does and returns the gradients."""
+    assert 0.0 <= inertia < 1.0, "`inertia` should be in [0, 1)"
+    if len(messages) == 0:
+        return None
+    assert all(["gradients" in m for m in messages]), "some clients have not sent gradients yet"
+    mps = list(model_params)
+    total = sum([m["train_samples"] for m in messages])
+    wp = [(m["train_samples"] / total if size_aware else 1 / len(messages)) * (1 - inertia) for m in messages]
+    wg = [m["train_samples"] / total for m in messages]
+    n = len(messages)
+    if hoststage.is_host(mps):
+        with hoststage.staged([mps], [True], [True], [m["parameters"] for m in messages]
+                              + [m["gradients"] for m in messages]) as ((dps,), dm):
+            dmsgs = [{"parameters": dm[i], "gradients": dm[n + i], "train_samples": m["train_samples"]}
+                     for i, m in enumerate(messages)]
+            dev = dps[0].device
+            r = _pair_fold(dev, dps, dmsgs, wp, wg, inertia)
+            if r is None:  # (a model the fused launch does not take: the two calls)
+                avg_parameters(dps, dmsgs, size_aware, inertia)
+                dg = _gradients_on(dev, dmsgs)
+                flat = torch.cat([g.reshape(-1) for g in dg])
+            else:
+                dg, flat = r
+            host = torch.empty(flat.numel(), dtype=flat.dtype, pin_memory=True)
+            host.copy_(flat, non_blocking=True)  # one D2H copy, drained by the staging's synchronisation
+        grads, off = [], 0
+        for g in dg:
+            grads.append(host[off:off + g.numel()].view(g.shape))
+            off += g.numel()
+    else:
+        ps = _params(mps)
+        r = _pair_fold(ps[0].device, ps, messages, wp, wg, inertia) if ps and ps[0].is_cuda else None
+        if r is None:
+            avg_parameters(mps, messages, size_aware, inertia)
+            return update_gradients(mps, messages)
+        grads = r[0]
+    for mp, g in zip(mps, grads):
+        if isinstance(mp, torch.Tensor):
+            mp.grad = g
+    return grads
+
+
 def fedopt_update(model_params: Sequence[torch.Tensor], delta_parameters: Sequence[torch.Tensor],
                   v_parameters: Optional[Sequence[torch.Tensor]], messages: Sequence[Mapping], optimizer: str,
                   lr: float, betas: Sequence[float], tau: float) -> None:
@@ -213,14 +293,24 @@ def fedopt_update(model_params: Sequence[torch.Tensor], delta_parameters: Sequen
     alpha = (1 - betas[0]) / len(messages) if len(messages) else 0.0
     model_params, delta_parameters = list(model_params), list(delta_parameters)
     vps = None if (v_parameters is None or opt == "avg") else list(v_parameters)
+    recs = compressed.stacked_round(messages)  # a round of packed stacked records (the codec's call site)
     if hoststage.is_host(model_params):
         groups = [model_params, delta_parameters] + ([vps] if vps is not None else [])
         n = len(groups)
-        with hoststage.staged(groups, [True] * n, [True] * n, [m["delta_parameters"] for m in messages]) as (dg, dm):
+        msgs = [[d.record] for d in recs] if recs is not None else [m["delta_parameters"] for m in messages]
+        with hoststage.staged(groups, [True] * n, [True] * n, msgs) as (dg, dm):
+            if recs is not None and compressed.fold_records(
+                    recs, [alpha] * len(recs), dg[1], _params(dg[0]), dg[2] if vps is not None else None, betas[0],
+                    opt if vps is not None else "avg", lr, betas[1], tau):
+                return
             fedopt_update(dg[0], dg[1], dg[2] if vps is not None else None,
-                          [{"delta_parameters": d} for d in dm], optimizer, lr, betas, tau)
+                          [{"delta_parameters": m["delta_parameters"] if recs is not None else d}
+                           for m, d in zip(messages, dm)], optimizer, lr, betas, tau)
         return
     ps = _params(model_params)
+    if recs is not None and compressed.fold_records(recs, [alpha] * len(recs), delta_parameters, ps, vps, betas[0],
+                                                    opt if vps is not None else "avg", lr, betas[1], tau):
+        return  # every record decoded, folded and the optimizer step applied in one pass
     if _fold(delta_parameters, messages, [alpha] * len(messages), 0, betas[0], key="delta_parameters",
              theta=ps, v=vps, opt=opt if vps is not None else "avg", lr=lr, beta2=betas[1], tau=tau):
         return  # the delta average and the optimizer step of every tensor in one launch
@@ -442,14 +532,58 @@ class AggregationMixin:
         update_gradients(list(self.model.parameters()), self._received_messages)
 
 
+class VRUpdateMixin:
+    """Device ``update()`` for the reference's variance-reduced servers, whose update is ``avg_parameters`` then, with
+    ``config.vr``, ``update_gradients``: FedProxServer (fedprox/_fedprox.py:163-167), ProxSkipServer
+    (proxskip/_proxskip.py:212-216), FedPDServer (fedpd/_fedpd.py:197-202, which also records the round's client ids)
+    and pFedMacServer (pfedmac/_pfedmac.py:158-162, inertia 1 - beta: set ``vr_inertia_from_beta = True``).  With
+    ``vr`` the two run as ONE launch (:func:`avg_parameters_and_gradients`), on a device- or host-resident model."""
+
+    vr_inertia_from_beta = False
+    record_communicated_clients = False
+
+    def update(self) -> None:
+        if self.record_communicated_clients:  # fedpd/_fedpd.py:198
+            self._communicated_clients = [m["client_id"] for m in self._received_messages]
+        inertia = 1 - self.config.beta if self.vr_inertia_from_beta else 0.0
+        keys = ["parameters"] + (["gradients"] if self.config.vr else [])
+        _adopt([list(self.model.parameters())], [m[k] for m in self._received_messages for k in keys])
+        if self.config.vr:
+            avg_parameters_and_gradients(list(self.model.parameters()), self._received_messages, inertia=inertia)
+        else:
+            avg_parameters(list(self.model.parameters()), self._received_messages, inertia=inertia)
+
+
+class FedProxUpdateMixin(VRUpdateMixin):
+    """fedprox/_fedprox.py:163-167."""
+
+
+class ProxSkipUpdateMixin(VRUpdateMixin):
+    """proxskip/_proxskip.py:212-216."""
+
+
+class FedPDUpdateMixin(VRUpdateMixin):
+    """fedpd/_fedpd.py:197-202."""
+
+    record_communicated_clients = True
+
+
+class pFedMacUpdateMixin(VRUpdateMixin):  # noqa: N801 (the reference's class name: pFedMacServer)
+    """pfedmac/_pfedmac.py:158-162."""
+
+    vr_inertia_from_beta = True
+
+
 class FedOptUpdateMixin:
     """Device ``update()`` for the reference's ``FedOptServer`` family (_fedopt.py:196-240), for a server model on a
     HIP device or in host memory."""
 
     def update(self) -> None:
         adaptive = self.v_parameters is not None and self.config.optimizer.lower() != "avg"
+        recs = compressed.stacked_round(self._received_messages)  # (compressed messages: the fold reads the records)
         _adopt([list(self.model.parameters()), self.delta_parameters, self.v_parameters if adaptive else None],
-               [m["delta_parameters"] for m in self._received_messages])
+               [[d.record] for d in recs] if recs is not None
+               else [m["delta_parameters"] for m in self._received_messages])
         fedopt_update(list(self.model.parameters()), self.delta_parameters, self.v_parameters,
                       self._received_messages, self.config.optimizer, self.config.lr, self.config.betas,
                       self.config.tau)

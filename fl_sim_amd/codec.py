@@ -572,10 +572,12 @@ def stacked_encode_delta_batch(local_params: Sequence[Sequence[torch.Tensor]], g
 
 
 def stacked_encode_delta(local_params: Sequence[torch.Tensor], global_params: Sequence[torch.Tensor], k: int,
-                         levels: int = 127, seed: int = 0, counter: int = 0) -> StackedPacket:
+                         levels: int = 127, seed: int = 0, counter: int = 0,
+                         wire: Optional[torch.Tensor] = None) -> StackedPacket:
     """The stacked encode of the client delta ``cat([l - g for l, g in zip(local, global)])`` with the delta formed in
     the encoder's read pass (flc_stacked_encode_delta): the flat delta is never written.  Same packet as
-    ``stacked_encode(delta_flatten(local, global), ...)``."""
+    ``stacked_encode(delta_flatten(local, global), ...)``.  ``wire``: a packed wire record to write into (the packet's
+    tensors are then views of it, see :func:`wire_packet`)."""
     import ctypes
 
     ls = [t if (t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 4 == 0) else t.contiguous().float()
@@ -593,10 +595,16 @@ def stacked_encode_delta(local_params: Sequence[torch.Tensor], global_params: Se
     lp = (ctypes.c_void_p * m)(*[t.data_ptr() for t in ls])
     gp = (ctypes.c_void_p * m)(*[t.data_ptr() for t in gs])
     sz = (ctypes.c_int64 * m)(*[t.numel() for t in ls])
-    idx = torch.empty(k, dtype=torch.int32, device=dev)
-    codes = torch.empty(max(k, 16), dtype=torch.uint8, device=dev)
-    norm = torch.empty(1, dtype=torch.float32, device=dev)
-    tiles = _tiles(n, dev)
+    if wire is not None:
+        if wire.device != dev:
+            raise ValueError("the wire record must be on the tensors' device")
+        pk = wire_packet(wire, n, k, levels)
+        idx, codes, norm, tiles = pk.idx, pk.codes, pk.norm, pk.tiles
+    else:
+        idx = torch.empty(k, dtype=torch.int32, device=dev)
+        codes = torch.empty(max(k, 16), dtype=torch.uint8, device=dev)
+        norm = torch.empty(1, dtype=torch.float32, device=dev)
+        tiles = _tiles(n, dev)
     ws = workspace(dev, _ws_size(dev, "flc_stacked_encode_delta_workspace_size", n, k, m), "topk")
     call("flc_stacked_encode_delta", ctypes.cast(lp, ctypes.c_void_p), ctypes.cast(gp, ctypes.c_void_p),
          ctypes.cast(sz, ctypes.c_void_p), m, k, levels, seed, counter, _p(idx), _p(codes), _p(norm), _p(tiles), _p(ws),

@@ -105,6 +105,7 @@ class Compressor:
         self.__compressorName = compressorName
         self.__compressorType = CompressorType.IDENTICAL
         self.__w = 0.0
+        self._pending = None  # (device count, base, per): send statistics a compressed round left on the device
         self.total_input_components = 0
         self.really_need_to_send_components = 0
         self.last_input_advance = 0
@@ -186,7 +187,49 @@ class Compressor:
             return f"Adaptive Random [D={self.D}]"
         return "?"
 
+    # send statistics (compressors.py:40-43, 406-408).  A compressed client round in philox mode (compressed.py) leaves
+    # the dithering stage's count of nonzero inputs on the device instead of synchronising for it; it is folded into
+    # the counters the first time one of them is read, with the reference's arithmetic (base + nnz * per).
+    def _flush(self) -> None:
+        p = self.__dict__.get("_pending")
+        if p is not None:
+            self._pending = None
+            cnt, base, per = p
+            nnz = int(cnt.item())
+            send = base + nnz * per if nnz else base
+            self._last_send = send
+            self._really_send += send
+
+    @property
+    def last_need_to_send_advance(self):
+        self._flush()
+        return self._last_send
+
+    @last_need_to_send_advance.setter
+    def last_need_to_send_advance(self, v):
+        self._flush()
+        self._last_send = v
+
+    @property
+    def really_need_to_send_components(self):
+        self._flush()
+        return self._really_send
+
+    @really_need_to_send_components.setter
+    def really_need_to_send_components(self, v):
+        self._flush()
+        self._really_send = v
+
+    def _finish_pending(self, d: int, count, base, per) -> None:
+        """_finish with the send count still on the device (see _flush)."""
+        self._flush()
+        self.last_input_advance = d
+        self.total_input_components += d
+        self._last_send = base
+        self._pending = (count, base, per)  # (the advance is added to the total on flush)
+
     def resetStats(self):
+        self._pending = None
         self.total_input_components = 0
         self.really_need_to_send_components = 0
         self.last_input_advance = 0

@@ -253,28 +253,7 @@ struct ModelPack {
   int nt, ns;
 };
 
-template <int OPT>
-__device__ __forceinline__ void opt_step(float& th, float d, float* vp, float lr, float beta2, float omb, float nomb,
-                                         float tau) {
-  if (OPT == FLC_OPT_AVG) {
-    th = fmaf(lr, d, th);
-    return;
-  }
-  const float d2 = d * d;
-  float vi = *vp;
-  if (OPT == FLC_OPT_ADAGRAD) {
-    vi = vi + d2;
-  } else if (OPT == FLC_OPT_YOGI) {
-    const float diff = vi - d2;
-    const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : (diff == 0.f ? 0.f : diff));
-    vi = vi + (nomb * d2) * sg;
-  } else {
-    vi = fmaf(omb, d2, vi * beta2);
-  }
-  *vp = vi;
-  th = th + (lr * d) / (sqrtf(vi) + tau);
-}
-
+// opt_step: flc_device.hpp (shared with the compressed round's fold, wire.hip)
 template <int INIT, int OPT>  // OPT < 0: the fold only
 __global__ __launch_bounds__(kThreads) void model_fold_kernel(ModelPack p, float beta, float lr, float beta2, float omb,
                                                               float nomb, float tau) {
@@ -334,6 +313,73 @@ __global__ __launch_bounds__(kThreads) void model_fold_kernel(ModelPack p, float
     dst[e] = a;
     if (OPT >= 0) opt_step<OPT < 0 ? 0 : OPT>(p.theta[t][e], a, OPT > 0 ? p.v[t] + e : nullptr, lr, beta2, omb, nomb,
                                             tau);
+  }
+}
+
+// avg_parameters and update_gradients of one round in ONE launch (flc_avg_and_gradients): the variance-reduced
+// servers (fedprox/_fedprox.py:163-167, fedpd/_fedpd.py:197-202, proxskip/_proxskip.py:212-216,
+// pfedmac/_pfedmac.py:158-162) call the two back to back over the same messages.  Entry t of the pack is a parameter
+// (weights w, init 0: θ·inertia first, or 2: a chained launch continues) or a gradient (weights w2, init 1: from +0,
+// or 2); per element the same fmaf chain in message order as model_fold_kernel's fold.
+struct PairPack {
+  float* dst[kModelT];
+  const float* src[kMaxSrc][kModelT];
+  int64_t n[kModelT];
+  int blk0[kModelT + 1];
+  float w[kMaxSrc];
+  float w2[kMaxSrc];
+  unsigned vec;   // bit t: entry t's operands are 16-B aligned
+  unsigned grad;  // bit t: entry t is a gradient (weights w2)
+  int init[kModelT];
+  int nt, ns;
+};
+
+__global__ __launch_bounds__(kThreads) void pair_fold_kernel(PairPack p, float beta) {
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < p.nt && p.blk0[t + 1] <= b) ++t;  // uniform: <= kModelT steps
+  float* __restrict__ dst = p.dst[t];
+  const int64_t n = p.n[t];
+  const int64_t c0 = (int64_t)(b - p.blk0[t]) * kModelChunk;
+  const int64_t c1 = c0 + kModelChunk < n ? c0 + kModelChunk : n;
+  const int init = p.init[t];
+  const float* __restrict__ w = ((p.grad >> t) & 1u) ? p.w2 : p.w;
+  if ((p.vec >> t) & 1u) {
+    for (int64_t i = c0 + 4 * (int64_t)threadIdx.x; i < c1; i += 4 * kThreads) {
+      if (i + 4 > c1) {  // the tensor's n % 4 tail
+        for (int64_t e = i; e < c1; ++e) {
+          float a = init == 1 ? 0.0f : (init == 0 ? dst[e] * beta : dst[e]);
+          for (int m = 0; m < p.ns; ++m) a = fmaf(w[m], p.src[m][t][e], a);
+          dst[e] = a;
+        }
+        break;
+      }
+      float4 sv[kMaxSrc];
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m)
+        if (m < p.ns) sv[m] = *reinterpret_cast<const float4*>(p.src[m][t] + i);
+      float4 a;
+      if (init == 1) {
+        a = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        a = *reinterpret_cast<const float4*>(dst + i);
+        if (init == 0) a = make_float4(a.x * beta, a.y * beta, a.z * beta, a.w * beta);
+      }
+#pragma unroll
+      for (int m = 0; m < kMaxSrc; ++m) {
+        if (m < p.ns) {
+          const float wm = w[m];
+          a = make_float4(fmaf(wm, sv[m].x, a.x), fmaf(wm, sv[m].y, a.y), fmaf(wm, sv[m].z, a.z), fmaf(wm, sv[m].w, a.w));
+        }
+      }
+      *reinterpret_cast<float4*>(dst + i) = a;
+    }
+    return;
+  }
+  for (int64_t e = c0 + threadIdx.x; e < c1; e += kThreads) {
+    float a = init == 1 ? 0.0f : (init == 0 ? dst[e] * beta : dst[e]);
+    for (int m = 0; m < p.ns; ++m) a = fmaf(w[m], p.src[m][t][e], a);
+    dst[e] = a;
   }
 }
 
@@ -528,6 +574,63 @@ int flc_model_fold(float* const* dst, const float* const* srcs, const float* wei
     else { FLC_MF_OPT(2); }
 #undef FLC_MF_OPT
 #undef FLC_MF
+  }
+  return FLC_OK;
+}
+
+int flc_avg_and_gradients(float* const* params, float* const* grads, const float* const* param_srcs,
+                          const float* const* grad_srcs, const float* w_params, const float* w_grads, int n_src,
+                          const int64_t* sizes, int n_tensors, float inertia, void* stream) {
+  if (n_tensors < 0 || (n_tensors > 0 && (!params || !grads || !sizes)) || n_src < 1 ||
+      !param_srcs || !grad_srcs || !w_params || !w_grads)
+    return fail(FLC_EINVAL, "flc_avg_and_gradients: bad arguments");
+  hipStream_t st = as_stream(stream);
+  for (int t = 0; t < n_tensors; ++t) {
+    if (sizes[t] < 0) return fail(FLC_EINVAL, "flc_avg_and_gradients: negative size for tensor %d", t);
+    if (sizes[t] > 0 && (!params[t] || !grads[t]))
+      return fail(FLC_EINVAL, "flc_avg_and_gradients: null pointer for tensor %d", t);
+    for (int m = 0; m < n_src; ++m)
+      if (sizes[t] > 0 && (!param_srcs[(size_t)m * n_tensors + t] || !grad_srcs[(size_t)m * n_tensors + t]))
+        return fail(FLC_EINVAL, "flc_avg_and_gradients: null source %d of tensor %d", m, t);
+  }
+  // entries: parameter t, then gradient t, for every non-empty tensor; packed kModelT per launch; messages
+  // kMaxSrc per launch (a later chunk continues each chain from the stored partial result: init 2)
+  for (int m0 = 0; m0 < n_src; m0 += kMaxSrc) {
+    const int ns = std::min(kMaxSrc, n_src - m0);
+    int e = 0;  // entry index over 2 * n_tensors
+    while (e < 2 * n_tensors) {
+      PairPack p{};
+      p.ns = ns;
+      for (int m = 0; m < ns; ++m) {
+        p.w[m] = w_params[m0 + m];
+        p.w2[m] = w_grads[m0 + m];
+      }
+      int blocks = 0;
+      for (; e < 2 * n_tensors && p.nt < kModelT; ++e) {
+        const int t = e >> 1;
+        const bool g = e & 1;
+        if (sizes[t] == 0) continue;
+        const int i = p.nt++;
+        p.dst[i] = g ? grads[t] : params[t];
+        p.n[i] = sizes[t];
+        p.init[i] = m0 > 0 ? 2 : (g ? 1 : 0);
+        if (g) p.grad |= 1u << i;
+        bool vec = aligned16(p.dst[i]);
+        for (int m = 0; m < ns; ++m) {
+          const float* sp = (g ? grad_srcs : param_srcs)[(size_t)(m0 + m) * n_tensors + t];
+          p.src[m][i] = sp;
+          vec = vec && aligned16(sp);
+        }
+        if (vec) p.vec |= 1u << i;
+        p.blk0[i] = blocks;
+        const int64_t nb = cdiv(sizes[t], kModelChunk);
+        if (blocks + nb > 0x7fffffff) return fail(FLC_EINVAL, "flc_avg_and_gradients: too many elements");
+        blocks += (int)nb;
+      }
+      p.blk0[p.nt] = blocks;
+      if (blocks > 0)
+        FLC_LAUNCH("avg_and_gradients", pair_fold_kernel, dim3(blocks), dim3(kThreads), 0, st, p, inertia);
+    }
   }
   return FLC_OK;
 }

@@ -71,6 +71,27 @@ __global__ __launch_bounds__(kThreads) void delta_flatten_kernel(TensorPack p, f
   }
 }
 
+// The send statistics of the standard dithering stage of a compressed client delta (compressors.py:339-365 count
+// one entry per nonzero element of their input; here: the delta at the top-k's kept indices): thread j looks up the
+// tensor of idx[j] (a uniform walk over the pack's offsets) and forms the delta as delta_flatten does; one 64-bit
+// atomic add per wave of the ballot's population count.
+__global__ __launch_bounds__(kThreads) void delta_count_nonzero_kernel(TensorPack p, const int32_t* __restrict__ idx,
+                                                                      int64_t k, unsigned long long* __restrict__ count) {
+  const int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  bool nz = false;
+  if (j < k) {
+    const int64_t i = idx[j];
+    for (int t = 0; t < p.nt; ++t) {
+      if (i >= p.off[t] && i < p.off[t] + p.n[t]) {
+        const int64_t o = i - p.off[t];
+        nz = !(p.l[t][o] - p.g[t][o] == 0.0f);  // (a NaN delta counts, as `x[i] == 0.0` is false for it)
+      }
+    }
+  }
+  const unsigned long long b = __ballot(nz);
+  if ((threadIdx.x & (kWave - 1)) == 0 && b != 0ull) atomicAdd(count, (unsigned long long)__popcll(b));
+}
+
 }  // namespace
 }  // namespace flc
 
@@ -108,6 +129,35 @@ int flc_delta_flatten(const float* const* local, const float* const* global, con
     }
     p.blk0[p.nt] = blocks;
     if (blocks > 0) FLC_LAUNCH("delta_flatten", delta_flatten_kernel, dim3(blocks), dim3(kThreads), 0, st, p, out);
+  }
+  return FLC_OK;
+}
+
+int flc_delta_count_nonzero_at(const float* const* local, const float* const* global, const int64_t* sizes,
+                               int n_tensors, const int32_t* idx, int64_t k, int64_t* count, void* stream) {
+  if (n_tensors < 0 || (n_tensors > 0 && (!local || !global || !sizes)) || k < 0 || !count || (k > 0 && !idx))
+    return fail(FLC_EINVAL, "flc_delta_count_nonzero_at: bad arguments");
+  hipStream_t st = as_stream(stream);
+  FLC_CHECK_HIP(hipMemsetAsync(count, 0, sizeof(int64_t), st));
+  if (k == 0) return FLC_OK;
+  int64_t off = 0;
+  for (int t0 = 0; t0 < n_tensors; t0 += kMaxT) {
+    TensorPack p{};
+    for (int t = t0; t < std::min(n_tensors, t0 + kMaxT); ++t) {
+      if (sizes[t] < 0) return fail(FLC_EINVAL, "flc_delta_count_nonzero_at: negative size for tensor %d", t);
+      if (sizes[t] > 0 && (!local[t] || !global[t]))
+        return fail(FLC_EINVAL, "flc_delta_count_nonzero_at: null pointer for tensor %d", t);
+      if (sizes[t] == 0) continue;
+      const int i = p.nt++;
+      p.l[i] = local[t];
+      p.g[i] = global[t];
+      p.off[i] = off;
+      p.n[i] = sizes[t];
+      off += sizes[t];
+    }
+    if (p.nt > 0)
+      FLC_LAUNCH("delta_count_nonzero", delta_count_nonzero_kernel, dim3((unsigned)cdiv(k, kThreads)), dim3(kThreads), 0,
+                 st, p, idx, k, reinterpret_cast<unsigned long long*>(count));
   }
   return FLC_OK;
 }

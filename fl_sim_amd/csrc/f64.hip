@@ -1507,7 +1507,7 @@ int flc_topk_dense_f64(const double* x, int64_t n, int64_t k, double* out, void*
   {  // (grid-synchronised: one block per CU, all resident)
     Coresident co(st, dev);
     if (co.status()) return co.status();
-    FLC_LAUNCH("sel64_select", sel64_select_kernel, dim3((unsigned)cus), dim3(kGT), 0, st, x, n, (long long)k,
+    FLC_LAUNCH_CO(co, "sel64_select", sel64_select_kernel, dim3((unsigned)cus), dim3(kGT), 0, st, x, n, (long long)k,
                f.on ? f.S : 0, f.r_lo, f.r_hi, f.on ? f.segcap : 0, w.sel, w.seg, w.segi, w.counts, f.on ? nch : 0,
                force_timeout64() ? 0u : (1u << 22));
     const int rc = co.finish();

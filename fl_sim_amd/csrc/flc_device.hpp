@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/flcodec.h"
+
 namespace flc {
 
 constexpr int kWave = 64;
@@ -319,6 +321,32 @@ __device__ __forceinline__ float stacked_dequant(uint32_t code, int levels, doub
   if (!(nrm > 0.0f && nrm <= 3.402823466e38f)) return code == 0u ? 0.0f : __uint_as_float(0x7fc00000u);
   const float lv = (float)level_value<0>((int)(code & 127u), levels, step);
   return ((code >> 7) ? -lv : lv) * nrm;
+}
+
+// The element-wise tail of FedOptServer.update (_fedopt.py:213-237) on one folded delta value d: the v update of the
+// server optimiser, then the model step, each rounded where the reference's torch CPU ops round (add_(alpha) is one
+// fma; mul_, pow(2), sqrt and the additions one rounding each; nothing else contracted: -ffp-contract=off).
+// omb = fp32(1 - beta2), nomb = fp32(-(1 - beta2)) as torch casts the Python scalars.
+template <int OPT>
+__device__ __forceinline__ void opt_step(float& th, float d, float* vp, float lr, float beta2, float omb, float nomb,
+                                         float tau) {
+  if (OPT == FLC_OPT_AVG) {
+    th = fmaf(lr, d, th);
+    return;
+  }
+  const float d2 = d * d;
+  float vi = *vp;
+  if (OPT == FLC_OPT_ADAGRAD) {
+    vi = vi + d2;
+  } else if (OPT == FLC_OPT_YOGI) {
+    const float diff = vi - d2;
+    const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : (diff == 0.f ? 0.f : diff));
+    vi = vi + (nomb * d2) * sg;
+  } else {
+    vi = fmaf(omb, d2, vi * beta2);
+  }
+  *vp = vi;
+  th = th + (lr * d) / (sqrtf(vi) + tau);
 }
 
 }  // namespace flc

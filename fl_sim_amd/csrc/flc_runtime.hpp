@@ -1,6 +1,7 @@
 // flc_runtime.hpp — host-side plumbing shared by the C-ABI entry points: error reporting, launch
 // checking, and the kernel-duration probe bench.py reads for its live roofline figure.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,16 +33,21 @@ int device_cus(int dev);                         // compute units of a device (c
 int current_cus(int* dev_out);                   // ... of the calling thread's current device
 int stream_cus(hipStream_t st, int* dev_out);    // ... of the stream's device (the current one for the null stream)
 
+// The chaining event is bound to the persistent kernel's own dispatch (hipExtLaunchKernel's stop event, FLC_LAUNCH_CO)
+// instead of a separate hipEventRecord after it: a marker packet behind each persistent launch had cost the next
+// kernel ~4 us of dispatch gap (profiles/r05/r05zo_gate_ab.txt).
 class Coresident {  // scoped: construct before the persistent launch(es) on `st`, finish() after them
  public:
   Coresident(hipStream_t st, int dev);
   ~Coresident();
   int status() const { return rc_; }
+  hipEvent_t stop_event() const;  // the event a persistent launch carries as its stop event (null: none needed)
+  void bound() { bound_ = stop_event() != nullptr; }
   int finish();  // records the chaining event when several streams are in use; returns FLC_OK or the error
  private:
   hipStream_t st_;
   int dev_, rc_ = 0;
-  bool gated_ = false, locked_ = false;
+  bool gated_ = false, locked_ = false, bound_ = false;
 };
 
 // workspace carving: every region 256-byte aligned
@@ -68,6 +74,17 @@ struct Carver {
     flc::probe_after(name, stream);                                               \
     hipError_t e_ = hipGetLastError();                                            \
     if (e_ != hipSuccess) return flc::hip_fail(e_, name);                         \
+  } while (0)
+
+// a persistent launch inside a Coresident scope `co`: the gate's chaining event (if any) is the kernel's stop event
+#define FLC_LAUNCH_CO(co, name, kernel, grid, block, shmem, stream, ...)                                  \
+  do {                                                                                                \
+    flc::probe_before(name, stream);                                                                  \
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, nullptr, (co).stop_event(), 0, __VA_ARGS__); \
+    flc::probe_after(name, stream);                                                                   \
+    hipError_t e_ = hipGetLastError();                                                                \
+    if (e_ != hipSuccess) return flc::hip_fail(e_, name);                                             \
+    (co).bound();                                                                                     \
   } while (0)
 
 #define FLC_CHECK_HIP(expr)                                                       \

@@ -903,10 +903,10 @@ int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p,
       Coresident co(st, dev);
       if (co.status()) return co.status();
       if (gpt == 2)
-        FLC_LAUNCH(fname, (quant_fused_kernel<KIND, BITS, DEC, 2>), dim3(grid), dim3(kFT), 0, st, x, n, d, levels, step,
+        FLC_LAUNCH_CO(co, fname, (quant_fused_kernel<KIND, BITS, DEC, 2>), dim3(grid), dim3(kFT), 0, st, x, n, d, levels, step,
                    norms, seed, counter, codes, nz, out, w, ep, cal);
       else
-        FLC_LAUNCH(fname, (quant_fused_kernel<KIND, BITS, DEC, 4>), dim3(grid), dim3(kFT), 0, st, x, n, d, levels, step,
+        FLC_LAUNCH_CO(co, fname, (quant_fused_kernel<KIND, BITS, DEC, 4>), dim3(grid), dim3(kFT), 0, st, x, n, d, levels, step,
                    norms, seed, counter, codes, nz, out, w, ep, cal);
       return co.finish();
     }

@@ -146,7 +146,7 @@ Coresident::Coresident(hipStream_t st, int dev) : st_(st), dev_(dev < 0 || dev >
       return;
     }
     e = hipDeviceSynchronize();
-    if (e == hipSuccess && !gt.last[dev_]) e = hipEventCreateWithFlags(&gt.last[dev_], hipEventDisableTiming);
+    if (e == hipSuccess && !gt.last[dev_]) e = hipEventCreate(&gt.last[dev_]);  // (a kernel's stop event)
     const hipError_t e2 = cur != dev_ ? hipSetDevice(cur) : hipSuccess;
     if (e != hipSuccess || e2 != hipSuccess) {
       rc_ = hip_fail(e != hipSuccess ? e : e2, "draining the gate's device");
@@ -158,12 +158,20 @@ Coresident::Coresident(hipStream_t st, int dev) : st_(st), dev_(dev < 0 || dev >
     rc_ = hip_fail(e, "hipStreamWaitEvent");
 }
 
+hipEvent_t Coresident::stop_event() const {
+  return (rc_ == 0 && gated_ && gate().multi[dev_]) ? gate().last[dev_] : nullptr;
+}
+
 int Coresident::finish() {
   Gate& gt = gate();
   if (rc_ == 0 && gated_ && gt.multi[dev_]) {
-    hipError_t e = hipEventRecord(gt.last[dev_], st_);
-    if (e != hipSuccess) rc_ = hip_fail(e, "hipEventRecord");
-    else gt.recorded[dev_] = true;
+    if (bound_) {  // the last persistent launch carried the event (FLC_LAUNCH_CO)
+      gt.recorded[dev_] = true;
+    } else {
+      hipError_t e = hipEventRecord(gt.last[dev_], st_);
+      if (e != hipSuccess) rc_ = hip_fail(e, "hipEventRecord");
+      else gt.recorded[dev_] = true;
+    }
   }
   if (locked_) {
     locked_ = false;

@@ -2151,13 +2151,13 @@ int launch_topk(const Src& x, int64_t n, int64_t k, void* ws, size_t ws_bytes, h
   if (co.status()) return co.status();
   const double step = levels > 0 ? 1.0 / (double)levels : 0.0;
   if (split)
-    FLC_LAUNCH(STACKED ? "stacked_select" : "topk_select", (topk_select_kernel<STACKED, false, Src>), dim3((unsigned)g.G),
+    FLC_LAUNCH_CO(co, STACKED ? "stacked_select" : "topk_select", (topk_select_kernel<STACKED, false, Src>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
-               tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
+               tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, (const BatchEntry*)nullptr);
   else
-    FLC_LAUNCH(STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true, Src>), dim3((unsigned)g.G),
+    FLC_LAUNCH_CO(co, STACKED ? "stacked_encode" : "topk_encode", (topk_select_kernel<STACKED, true, Src>), dim3((unsigned)g.G),
                dim3(kET), 0, st, x, n, (long long)k, w, idx, val, codes, norm, levels, step, seed, counter,
-               tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all);
+               tiles, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, (const BatchEntry*)nullptr);
   return co.finish();
 }
 
@@ -2389,7 +2389,7 @@ int launch_topk_batch_chunks(const Src& proto, const BatchEntry* tab, int C, con
       FLC_LAUNCH("topk_sample_batch", topk_sample_batch_kernel<Src>, dim3((unsigned)(cn * per)), dim3(256), 0, st,
                  proto, t, n, ss.S, w, per);
     }
-    FLC_LAUNCH(STACKED ? "stacked_encode_batch" : "topk_encode_batch", (topk_select_kernel<STACKED, true, Src, true>),
+    FLC_LAUNCH_CO(co, STACKED ? "stacked_encode_batch" : "topk_encode_batch", (topk_select_kernel<STACKED, true, Src, true>),
                dim3((unsigned)(cn * bg.g.G)),
                dim3(kET), 0, st, proto, n, (long long)k, w, nullptr, nullptr, nullptr, nullptr, levels, step, 0ull,
                counter, nullptr, ss.S, ss.rank_lo, ss.rank_hi, ss.take_all, t);

@@ -40,8 +40,8 @@ struct WireLayout {
   long long norm, idx, codes, tiles;
 };
 struct FoldArgs {
+  const uint8_t* rec[kMaxWires];  // the c-th client's record in fold order
   float w[kMaxWires];
-  int slot[kMaxWires];  // record index (in units of the stride) of the c-th client in fold order
 };
 
 WireLayout wire_layout(int64_t n, int64_t k, size_t* total) {
@@ -63,35 +63,154 @@ __device__ __forceinline__ float skip_clients(float a, unsigned from, unsigned t
   return (__float_as_uint(a) == 0x80000000u && (pos & lowmask(to) & ~lowmask(from)) != 0ull) ? 0.0f : a;
 }
 
-template <bool SPARSE>
-__global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t* __restrict__ wires, int64_t stride,
-                                                                   WireLayout L, FoldArgs a, int nw, int levels,
-                                                                   double step, int64_t n, int acc_in,
-                                                                   float* __restrict__ out, unsigned k) {
+// Where a tile's accumulator comes from and where it goes.  Lane `lane` owns float4 groups q = lane + 64 u (u < 4)
+// of the tile starting at flat element t0.
+struct FlatIO {  // one flat vector: out = fold (from +0, or from out itself)
+  float* out;
+  int64_t n;
+  int acc_in;
+  __device__ __forceinline__ void load(int64_t t0, int lane, float4 acc[4]) const {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (acc_in) {
+        if (e + 4 <= n) {
+          v = *reinterpret_cast<const float4*>(out + e);
+        } else {
+          if (e < n) v.x = out[e];
+          if (e + 1 < n) v.y = out[e + 1];
+          if (e + 2 < n) v.z = out[e + 2];
+        }
+      }
+      acc[u] = v;
+    }
+  }
+  __device__ __forceinline__ void store(int64_t t0, int lane, const float4 acc[4]) const {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
+      if (e + 4 <= n) {
+        *reinterpret_cast<float4*>(out + e) = acc[u];
+      } else {
+        if (e < n) out[e] = acc[u].x;
+        if (e + 1 < n) out[e + 1] = acc[u].y;
+        if (e + 2 < n) out[e + 2] = acc[u].z;
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ float& comp(float4& v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
+
+// A server's model as the fold's accumulator (flc_fedopt_fold_records): the flat element e of the records is
+// element e - start[t] of tensor t (the concatenation order of the client's flattened delta).  load: a = δ (· β0
+// when `scale`: FedOptServer.update's mul_(betas[0]) first); store: δ = a, then, with OPT >= 0, the server
+// optimiser's step on θ (and v) from a — _fedopt.py:202-237 in one pass.  The tile's tensors are walked with a
+// uniform index (a tile usually lies inside one tensor); a float4 group inside one 16-B aligned tensor moves as one.
+constexpr int kRoundT = 16;  // tensors per launch (kernel-argument budget)
+struct ModelTab {
+  float* delta[kRoundT];
+  float* theta[kRoundT];
+  float* v[kRoundT];
+  int64_t start[kRoundT + 1];  // flat offsets; start[nt] = end of the launch's range
+  int nt;
+  unsigned vec;  // bit t: tensor t's operands 16-B aligned and start[t] % 4 == 0
+  int scale;
+  float beta0, lr, beta2, omb, nomb, tau;
+};
+template <int OPT>  // OPT < 0: the fold only (δ written, no step)
+struct ModelIO {
+  ModelTab m;
+  __device__ __forceinline__ int first_tensor(int64_t t0) const {
+    int t = 0;
+    while (t + 1 < m.nt && m.start[t + 1] <= t0) ++t;
+    return t;
+  }
+  __device__ __forceinline__ void load(int64_t t0, int lane, float4 acc[4]) const {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t = first_tensor(t0); t < m.nt && m.start[t] < t0 + FLC_TILE; ++t) {
+      const int64_t s0 = m.start[t], s1 = m.start[t + 1];
+      const float* __restrict__ d = m.delta[t];
+      const bool vec = (m.vec >> t) & 1u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
+        if (vec && e >= s0 && e + 4 <= s1) {
+          float4 x = *reinterpret_cast<const float4*>(d + (e - s0));
+          if (m.scale) x = make_float4(x.x * m.beta0, x.y * m.beta0, x.z * m.beta0, x.w * m.beta0);
+          acc[u] = x;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (e + j >= s0 && e + j < s1) {
+              const float x = d[e + j - s0];
+              comp(acc[u], j) = m.scale ? x * m.beta0 : x;
+            }
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void store(int64_t t0, int lane, float4 acc[4]) const {
+    for (int t = first_tensor(t0); t < m.nt && m.start[t] < t0 + FLC_TILE; ++t) {
+      const int64_t s0 = m.start[t], s1 = m.start[t + 1];
+      float* __restrict__ d = m.delta[t];
+      float* __restrict__ th = m.theta[t];
+      float* __restrict__ vv = m.v[t];
+      const bool vec = (m.vec >> t) & 1u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
+        if (vec && e >= s0 && e + 4 <= s1) {
+          const int64_t o = e - s0;
+          *reinterpret_cast<float4*>(d + o) = acc[u];
+          if (OPT >= 0) {
+            float4 tv = *reinterpret_cast<const float4*>(th + o);
+            float4 vq = OPT > 0 ? *reinterpret_cast<const float4*>(vv + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+            opt_step<OPT < 0 ? 0 : OPT>(tv.x, acc[u].x, &vq.x, m.lr, m.beta2, m.omb, m.nomb, m.tau);
+            opt_step<OPT < 0 ? 0 : OPT>(tv.y, acc[u].y, &vq.y, m.lr, m.beta2, m.omb, m.nomb, m.tau);
+            opt_step<OPT < 0 ? 0 : OPT>(tv.z, acc[u].z, &vq.z, m.lr, m.beta2, m.omb, m.nomb, m.tau);
+            opt_step<OPT < 0 ? 0 : OPT>(tv.w, acc[u].w, &vq.w, m.lr, m.beta2, m.omb, m.nomb, m.tau);
+            *reinterpret_cast<float4*>(th + o) = tv;
+            if (OPT > 0) *reinterpret_cast<float4*>(vv + o) = vq;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (e + j >= s0 && e + j < s1) {
+              const int64_t o = e + j - s0;
+              const float a = comp(acc[u], j);
+              d[o] = a;
+              if (OPT >= 0) {
+                float vi = OPT > 0 ? vv[o] : 0.f;
+                opt_step<OPT < 0 ? 0 : OPT>(th[o], a, &vi, m.lr, m.beta2, m.omb, m.nomb, m.tau);
+                if (OPT > 0) vv[o] = vi;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+};
+
+template <bool SPARSE, class IO>
+__global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(FoldArgs a, WireLayout L, int nw, int levels,
+                                                                   double step, int64_t tile0, IO io, unsigned k) {
   __shared__ __attribute__((aligned(16))) float s_tile[FLC_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t s_last[SPARSE ? FLC_TILE : 4];  // sparse: last writer + 1 (0: none)
   float4* tile4 = reinterpret_cast<float4*>(s_tile);
   const int lane = threadIdx.x;
-  const int64_t t = blockIdx.x;
+  const int64_t t = tile0 + blockIdx.x;
   const int64_t t0 = t * FLC_TILE;
   // the tile's slice of the accumulator: lane owns float4 q = lane + 64 u
   float4 acc[4];
+  io.load(t0, lane, acc);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (acc_in) {
-      if (e + 4 <= n) {
-        v = *reinterpret_cast<const float4*>(out + e);
-      } else {
-        if (e < n) v.x = out[e];
-        if (e + 1 < n) v.y = out[e + 1];
-        if (e + 2 < n) v.z = out[e + 2];
-      }
-    }
-    acc[u] = v;
     // dense: a zero tile per client; sparse: the accumulator itself lives in the LDS tile
-    tile4[lane + u * kWave] = SPARSE ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    tile4[lane + u * kWave] = SPARSE ? acc[u] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (SPARSE) reinterpret_cast<unsigned*>(s_last)[lane + u * kWave] = 0u;
   }
   // client `lane`'s record, entry range in this tile and norm (lanes >= nw: empty)
@@ -99,7 +218,7 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
   unsigned lo = 0, cnt = 0;
   float nrm = 0.0f, wl = 0.0f;
   if (lane < nw) {
-    rec = wires + (int64_t)a.slot[lane] * stride;
+    rec = a.rec[lane];
     wl = a.w[lane];
     const unsigned* tiles = reinterpret_cast<const unsigned*>(rec + L.tiles);
     // (clamped to the record's k entries: a malformed or unwritten tile pointer never reads past the record)
@@ -258,17 +377,7 @@ __global__ __launch_bounds__(kWave) void stacked_fold_wires_kernel(const uint8_t
       acc[u].w = skip_clients(acc[u].w, lb >> 24, 64u, pos);
     }
   }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int64_t e = t0 + 4 * (int64_t)(lane + u * kWave);
-    if (e + 4 <= n) {
-      *reinterpret_cast<float4*>(out + e) = acc[u];
-    } else {
-      if (e < n) out[e] = acc[u].x;
-      if (e + 1 < n) out[e + 1] = acc[u].y;
-      if (e + 2 < n) out[e + 2] = acc[u].z;
-    }
-  }
+  io.store(t0, lane, acc);
 }
 
 }  // namespace
@@ -318,16 +427,101 @@ int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slo
     FoldArgs a;
     for (int c = 0; c < kMaxWires; ++c) {
       a.w[c] = c < nw ? weights[c0 + c] : 0.0f;
-      a.slot[c] = c < nw ? slots[c0 + c] : 0;
+      a.rec[c] = static_cast<const uint8_t*>(wires) + (c < nw ? (int64_t)slots[c0 + c] * stride : 0);
     }
-    const int acc_in = (c0 > 0 || accumulate) ? 1 : 0;
+    const FlatIO io{out, n, (c0 > 0 || accumulate) ? 1 : 0};
     if (sparse)
-      FLC_LAUNCH("stacked_fold_wires", stacked_fold_wires_kernel<true>, dim3((unsigned)ntiles), dim3(kWave), 0, st,
-                 static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, acc_in, out, (unsigned)k);
+      FLC_LAUNCH("stacked_fold_wires", (stacked_fold_wires_kernel<true, FlatIO>), dim3((unsigned)ntiles), dim3(kWave), 0,
+                 st, a, L, nw, levels, step, (int64_t)0, io, (unsigned)k);
     else
-      FLC_LAUNCH("stacked_fold_wires", stacked_fold_wires_kernel<false>, dim3((unsigned)ntiles), dim3(kWave), 0, st,
-                 static_cast<const uint8_t*>(wires), stride, L, a, nw, levels, step, n, acc_in, out, (unsigned)k);
+      FLC_LAUNCH("stacked_fold_wires", (stacked_fold_wires_kernel<false, FlatIO>), dim3((unsigned)ntiles), dim3(kWave),
+                 0, st, a, L, nw, levels, step, (int64_t)0, io, (unsigned)k);
   }
+  return FLC_OK;
+}
+
+int flc_fedopt_fold_records(const void* const* records, const float* weights, int n_records, int64_t n, int64_t k,
+                            int levels, float* const* delta, float* const* theta, float* const* v,
+                            const int64_t* sizes, int n_tensors, float beta0, int opt, double lr, double beta2,
+                            double tau, void* stream) {
+  if (n_records < 0 || (n_records > 0 && (!records || !weights)) || n <= 0 || k < 0 || n_tensors < 1 || !delta ||
+      !sizes)
+    return fail(FLC_EINVAL, "flc_fedopt_fold_records: bad arguments");
+  if (n >= (1ll << 31) || k >= (1ll << 31)) return fail(FLC_EINVAL, "flc_fedopt_fold_records: n and k must be < 2^31");
+  if (levels < 1 || levels > 127) return fail(FLC_EINVAL, "flc_fedopt_fold_records: levels must be in [1, 127]");
+  const bool step_on = theta != nullptr;
+  if (step_on && opt != FLC_OPT_AVG && opt != FLC_OPT_ADAGRAD && opt != FLC_OPT_YOGI && opt != FLC_OPT_ADAM)
+    return fail(FLC_EINVAL, "flc_fedopt_fold_records: unknown optimiser %d", opt);
+  if (step_on && opt != FLC_OPT_AVG && !v)
+    return fail(FLC_EINVAL, "flc_fedopt_fold_records: v required for adaptive optimisers");
+  int64_t total = 0;
+  for (int t = 0; t < n_tensors; ++t) {
+    if (sizes[t] < 0) return fail(FLC_EINVAL, "flc_fedopt_fold_records: negative size for tensor %d", t);
+    if (sizes[t] > 0 && (!delta[t] || (step_on && !theta[t]) || (step_on && opt != FLC_OPT_AVG && !v[t])))
+      return fail(FLC_EINVAL, "flc_fedopt_fold_records: null pointer for tensor %d", t);
+    total += sizes[t];
+  }
+  if (total != n)
+    return fail(FLC_EINVAL, "flc_fedopt_fold_records: the tensors hold %lld elements, the records %lld",
+                (long long)total, (long long)n);
+  for (int c = 0; c < n_records; ++c)
+    if (!records[c] || !aligned16(records[c]))
+      return fail(FLC_EINVAL, "flc_fedopt_fold_records: record %d is null or not 16-B aligned", c);
+  size_t need = 0;
+  const WireLayout L = wire_layout(n, k, &need);
+  hipStream_t st = as_stream(stream);
+  const double step = 1.0 / (double)levels;
+  const float omb = (float)(1.0 - beta2), nomb = (float)(-(1.0 - beta2));
+  // record chunks in order (the chain continues from the stored δ, the step after the last chunk only); within a
+  // chunk, one launch per group of <= kRoundT tensors over the tiles their flat range touches
+  int c0 = 0;
+  do {
+    const int nw = std::min(kMaxWires, n_records - c0);
+    const bool last = c0 + nw >= n_records;
+    FoldArgs a;
+    for (int c = 0; c < kMaxWires; ++c) {
+      a.w[c] = c < nw ? weights[c0 + c] : 0.0f;
+      a.rec[c] = static_cast<const uint8_t*>(c < nw ? records[c0 + c] : nullptr);
+    }
+    int64_t off = 0;
+    int t = 0;
+    while (t < n_tensors) {
+      ModelTab m{};
+      m.scale = c0 == 0;
+      m.beta0 = beta0;
+      m.lr = (float)lr;
+      m.beta2 = (float)beta2;
+      m.omb = omb;
+      m.nomb = nomb;
+      m.tau = (float)tau;
+      for (; t < n_tensors && m.nt < kRoundT; ++t) {
+        if (sizes[t] == 0) continue;
+        const int i = m.nt++;
+        m.delta[i] = delta[t];
+        m.theta[i] = step_on ? theta[t] : nullptr;
+        m.v[i] = (step_on && opt != FLC_OPT_AVG) ? v[t] : nullptr;
+        m.start[i] = off;
+        const bool vec = off % 4 == 0 && aligned16(m.delta[i]) && (!m.theta[i] || aligned16(m.theta[i])) &&
+                         (!m.v[i] || aligned16(m.v[i]));
+        if (vec) m.vec |= 1u << i;
+        off += sizes[t];
+      }
+      if (m.nt == 0) break;
+      m.start[m.nt] = off;
+      const int64_t tile_lo = m.start[0] / FLC_TILE, tile_hi = cdiv(off, (int64_t)FLC_TILE);
+      const dim3 grid((unsigned)(tile_hi - tile_lo));
+#define FLC_FR(O) \
+  FLC_LAUNCH("fedopt_fold_records", (stacked_fold_wires_kernel<false, ModelIO<O>>), grid, dim3(kWave), 0, st, a, L, nw, \
+             levels, step, tile_lo, ModelIO<O>{m}, (unsigned)k)
+      if (!step_on || !last) FLC_FR(-1);
+      else if (opt == FLC_OPT_AVG) FLC_FR(FLC_OPT_AVG);
+      else if (opt == FLC_OPT_ADAGRAD) FLC_FR(FLC_OPT_ADAGRAD);
+      else if (opt == FLC_OPT_YOGI) FLC_FR(FLC_OPT_YOGI);
+      else FLC_FR(FLC_OPT_ADAM);
+#undef FLC_FR
+    }
+    c0 += nw;
+  } while (c0 < n_records);
   return FLC_OK;
 }
 

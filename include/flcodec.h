@@ -206,6 +206,22 @@ size_t flc_stacked_wire_layout(int64_t n, int64_t k, int64_t* offsets);
  * the number of GPUs. */
 int flc_stacked_fold_wires(const void* wires, int64_t stride, const int32_t* slots, const float* weights,
                            int n_wires, int64_t n, int64_t k, int levels, int accumulate, float* out, void* stream);
+/* A compressed FedOpt round's server update in ONE pass (replaces FedOptServer.update, _fedopt.py:196-240, when each
+ * client message carries its delta as a packed stacked record — the codec's call site, fl_sim_amd/compressed.py):
+ * over the flat concatenation of the model's tensors (element e of the records = element e - offset_t of tensor t,
+ * the order FedOptClient.communicate's delta list flattens in),
+ *   a = delta * beta0;  for c = 0 .. n_records-1:  a = fmaf(weights[c], decode(records[c]), a);  delta = a;
+ *   then, if theta != NULL, the optimiser's step on theta (and v): avg theta = fmaf(lr, a, theta); adagrad / yogi /
+ *   adam as flc_model_fold (every rounding where torch's CPU ops round).
+ * Bit-identical to decoding every record densely (flc_stacked_decode_tiled) and running flc_model_fold with
+ * init_mode 0 and the step.  records: HOST array of n_records device pointers to records of the
+ * flc_stacked_wire_layout(n, k) layout (16-B aligned; any device memory the stream's device can read, e.g. each client's
+ * own); delta / theta / v: HOST arrays of n_tensors device pointers (v only for adaptive optimisers; pinned host
+ * memory mapped into the device's address space works too), sizes summing to n.  theta == NULL: the fold alone. */
+int flc_fedopt_fold_records(const void* const* records, const float* weights, int n_records, int64_t n, int64_t k,
+                            int levels, float* const* delta, float* const* theta, float* const* v,
+                            const int64_t* sizes, int n_tensors, float beta0, int opt, double lr, double beta2,
+                            double tau, void* stream);
 
 /* ------------------------------------------------------------------ multi-GPU exchange (RCCL over xGMI)
  * For callers outside torch; one process per GPU.  RCCL is the NCCL API on ROCm, looked
@@ -358,6 +374,12 @@ int flc_f64_status(void* ws, uint64_t* err_out, int reset, void* stream);
  * HOST arrays (of device pointers / element counts); empty tensors are allowed. */
 int flc_delta_flatten(const float* const* local, const float* const* global, const int64_t* sizes, int n_tensors,
                       float* out, void* stream);
+/* the number of nonzero deltas local - global (as flc_delta_flatten forms them; NaN counts) at the k flat indices idx
+ * of the concatenation — the count a standard-dithering stage's send statistics take from its input (compressors.py
+ * 339-365: one entry per nonzero element) when the delta itself is never formed (flc_stacked_encode_delta).  count: one
+ * device int64, written stream-ordered. */
+int flc_delta_count_nonzero_at(const float* const* local, const float* const* global, const int64_t* sizes,
+                               int n_tensors, const int32_t* idx, int64_t k, int64_t* count, void* stream);
 
 /* ------------------------------------------------------------------ aggregation
  * weighted sum of client tensors into dst, in message order, one fmaf per message per element:
@@ -378,6 +400,17 @@ int flc_weighted_sum(const float* const* srcs, const float* weights, int n_src, 
 int flc_model_fold(float* const* dst, const float* const* srcs, const float* weights, int n_src, const int64_t* sizes,
                    int n_tensors, int init_mode, float beta, float* const* theta, float* const* v, int opt, double lr,
                    double beta2, double tau, void* stream);
+/* avg_parameters (nodes.py:1134-1163) and update_gradients (nodes.py:1165-1180) of one round in ONE launch — what
+ * the variance-reduced servers run back to back (fedprox/_fedprox.py:163-167, fedpd/_fedpd.py:197-202,
+ * proxskip/_proxskip.py:212-216, pfedmac/_pfedmac.py:158-162):
+ *   params[t] = params[t] * inertia, then fmaf(w_params[m], param_srcs[m][t], .) for m in order;
+ *   grads[t]  = +0, then fmaf(w_grads[m], grad_srcs[m][t], .) for m in order;
+ * bit-identical to flc_model_fold(init 0, beta = inertia) of the parameters followed by flc_model_fold(init 1) of the
+ * gradients.  param_srcs / grad_srcs: HOST arrays [n_src][n_tensors] of device pointers; params / grads / sizes HOST
+ * arrays of n_tensors; more than 16 messages chain launches (each continuing the stored partial results). */
+int flc_avg_and_gradients(float* const* params, float* const* grads, const float* const* param_srcs,
+                          const float* const* grad_srcs, const float* w_params, const float* w_grads, int n_src,
+                          const int64_t* sizes, int n_tensors, float inertia, void* stream);
 /* FedDyn's and pFedMe's server updates on a whole model, one pass per <= 16 tensors and <= 16 messages
  * (theta = the model, aux = the per-element second state; srcs[m * n_tensors + t] = message m's tensor t):
  *   FLC_SRV_FEDDYN (feddyn/_feddyn.py:172-184): h = aux, for each message in order h = fmaf(c, fl(src - theta0), h)
