@@ -296,6 +296,16 @@ def cpu_configs(threads: int) -> dict:
         w8 = [100 * (i + 1) / 3600 for i in range(8)]
         per, reps = _time_reps(lambda: torch_ref.round_fold([x3] * 8, w8, 250_000, LEVELS, g), 4.0, 2, warm=False)
         res["config3_round_8x25M"] = {"ms": round(per * 1e3, 3), "reps": reps}
+        # the codec's call site on the CPU (oracle/round_ref.py: the reference's own composition restated — the client
+        # delta, TopK 1 % then standard dithering s = 10 on the host with random.random() uniforms, the FedAvg update)
+        from oracle import round_ref
+
+        th = [torch.randn(sh, generator=g) * 0.1 for sh in CONFIG0_SHAPES]
+        locs = [[t + torch.randn(t.shape, generator=g) * 1e-2 for t in th] for _ in range(10)]
+        dl0 = [torch.zeros(sh) for sh in CONFIG0_SHAPES]
+        per, reps = _time_reps(lambda: round_ref.fedopt_round("stacked10", [t.clone() for t in th], dl0, None, locs,
+                                                              [100] * 10, "avg", 1.0, (0, 1), 1.0), 2.0, 3)
+        res["config0_compressed_round_stacked"] = {"ms": round(per * 1e3, 3), "reps": reps}
     finally:
         torch.set_num_threads(threads0)
     res["threads"] = threads
@@ -308,6 +318,121 @@ def traffic_from_profiles():
         with open(p) as f:
             return json.load(f)
     return {}
+
+
+def compressed_round_extra(dev, world: int, th0) -> dict:
+    """The codec at its call site (fl_sim_amd/compressed.py): one configs[0] round — 10 clients (cnn_femmist_tiny on
+    the device, nodes.py:706-713) each send their delta (FedOptClient.communicate, _fedopt.py:295-308) through the
+    stacked pipeline (TopK 1 %, then standard dithering s = 127, p = inf, of the kept values; philox) as a packed wire
+    record; the FedAvg server (FedOptUpdateMixin) folds the records with the server step in one
+    flc_fedopt_fold_records pass.  Timed per round: the 10 communicates and the update, the server model on the device
+    and in host memory (the reference's placement, nodes.py:606: host to host, synchronised); beside it the same
+    round with uncompressed messages (the plain delta, the dense fold)."""
+    import types
+
+    from fl_sim_amd import Compressor
+    from fl_sim_amd.aggregation import FedOptUpdateMixin
+    from fl_sim_amd.compressed import CompressedFedOptClientMixin
+
+    class _Client(CompressedFedOptClientMixin):
+        pass
+
+    class _Server(FedOptUpdateMixin):
+        pass
+
+    d0, n0 = sum(int(np.prod(s)) for s in CONFIG0_SHAPES), 10
+    g = torch.Generator(device=dev).manual_seed(321)
+    clients = []
+    for i in range(n0):
+        c = _Client()
+        c.client_id, c._metrics = i, {}
+        c.train_loader = types.SimpleNamespace(dataset=range(100 * (i + 1)))
+        c.model = torch.nn.Module()
+        for j, t in enumerate(th0):
+            c.model.register_parameter(f"p{j}", torch.nn.Parameter(t + torch.randn(t.shape, generator=g, device=dev) * 1e-2))
+        c._cached_parameters = [t.clone() for t in th0]
+        clients.append(c)
+
+    def pipeline(i):
+        tk = Compressor(rng="philox", seed=i)
+        tk.makeTopKCompressor(d0 // 100, d0)
+        nc = Compressor("norm")
+        nc.makeIdenticalCompressor()
+        sd = Compressor(rng="philox", seed=i, extended_levels=True)
+        sd.makeStandardDitheringFP32(LEVELS, nc, np.inf)
+        return [tk, sd]
+
+    line = {"model": "cnn_femmist_tiny (8 tensors, 417,482 params) x 10 clients, FedAvg",
+            "codec": "TopK 1 % -> standard dithering s = 127 (p = inf) of the kept values, philox"}
+    for comp in (True, False):
+        for c in clients:
+            c.compressors = pipeline(c.client_id) if comp else []
+        for where in ("device", "host"):
+            s = _Server()
+            s.model = torch.nn.Module()
+            for j, t in enumerate(th0):
+                s.model.register_parameter(f"p{j}", torch.nn.Parameter(t.clone() if where == "device" else t.cpu()))
+            s.delta_parameters = [torch.zeros_like(p) for p in s.model.parameters()]
+            s.v_parameters = None
+            s.config = types.SimpleNamespace(optimizer="avg", lr=1, betas=(0, 1), tau=1)
+
+            def round_():
+                s._received_messages = []
+                for c in clients:
+                    c.communicate(s)
+                s.update()
+
+            ms, _ = timed(round_, 20, 5, world)
+            key = ("compressed" if comp else "uncompressed") + f"_server_{where}"
+            line[key + "_us_per_round"] = round(max_over_ranks(ms, world) * 1e3, 1)
+            if comp and where == "device":
+                s._received_messages = []
+                clients[0].communicate(s)
+                line["wire_bytes_per_client"] = s._received_messages[0]["delta_parameters"].nbytes
+                line["dense_bytes_per_client"] = 4 * d0
+    line["note"] = ("per round: 10 client communicates (delta formed inside the encoder's read, flc_stacked_encode_delta "
+                    "into a record) + the server update (flc_fedopt_fold_records: every record decoded and folded in "
+                    "message order, the FedAvg step fused); host: the server model adopted into pinned memory and "
+                    "updated in place (zero-copy); uncompressed: the plain delta and the dense model fold")
+    return line
+
+
+def vr_update_extra(dev, world: int, th0) -> dict:
+    """The variance-reduced servers' update (FedProx, fedprox/_fedprox.py:163-167; FedPD, ProxSkip, pFedMac alike):
+    avg_parameters then update_gradients over 10 clients of configs[0]'s model, as one flc_avg_and_gradients launch
+    (VRUpdateMixin) against the two calls (AggregationMixin), on the reference's host-resident server and on the
+    device.  Algorithmic bytes: 2 n + 2 tensors of 4 D read (parameters, gradients, θ) and 2 written (θ, grads)."""
+    import types
+
+    from fl_sim_amd.aggregation import AggregationMixin, FedProxUpdateMixin
+
+    class _Fused(FedProxUpdateMixin):
+        pass
+
+    class _TwoCalls(AggregationMixin):
+        def update(self):  # fedprox/_fedprox.py:163-167 over the mixin's two methods
+            self.avg_parameters()
+            if self.config.vr:
+                self.update_gradients()
+
+    g = torch.Generator(device=dev).manual_seed(77)
+    msgs = [{"client_id": i, "train_samples": 100 * (i + 1),
+             "parameters": [t + torch.randn(t.shape, generator=g, device=dev) * 1e-3 for t in th0],
+             "gradients": [torch.randn(t.shape, generator=g, device=dev) * 1e-3 for t in th0]} for i in range(10)]
+    d0 = sum(t.numel() for t in th0)
+    line = {"model": "cnn_femmist_tiny x 10 clients, vr = True",
+            "algorithmic_bytes": (2 * 10 + 1) * 4 * d0 + 2 * 4 * d0}
+    for cls, name in ((_Fused, "fused"), (_TwoCalls, "two_calls")):
+        for where in ("device", "host"):
+            s = cls()
+            s.model = torch.nn.Module()
+            for j, t in enumerate(th0):
+                s.model.register_parameter(f"p{j}", torch.nn.Parameter(t.clone() if where == "device" else t.cpu()))
+            s.config = types.SimpleNamespace(vr=True)
+            s._received_messages = msgs
+            ms, _ = timed(s.update, 30, 5, world)
+            line[f"{name}_{where}_us"] = round(max_over_ranks(ms, world) * 1e3, 1)
+    return line
 
 
 def aggregation_extras(dev, world: int, rank: int) -> dict:
@@ -397,6 +522,8 @@ def aggregation_extras(dev, world: int, rank: int) -> dict:
                            "(n + 2) * 4 * D: the n messages and theta read, theta written (the saved model never leaves "
                            "the registers)")
     out["aggregation_config0_feddyn_pfedme"] = sl
+    out["compressed_round_config0"] = compressed_round_extra(dev, world, th0)
+    out["vr_update_config0"] = vr_update_extra(dev, world, th0)
     del th0, dl0, v0, msgs0
     # 8 x 25 M: distinct sources (a repeated source would be served from the caches)
     n8 = 25_000_000
@@ -899,7 +1026,8 @@ def main():
                         ("config0_fedavg_10x417482", "aggregation_config0_host_server"),
                         ("config1_quant8_10x417482", "config2_quant8_10x417482"),
                         ("config2_topk1pct_25M", "config3_topk1pct_25M"),
-                        ("config3_round_8x25M", "config4_codec_plus_rccl_reduce_25M")):
+                        ("config3_round_8x25M", "config4_codec_plus_rccl_reduce_25M"),
+                        ("config0_compressed_round_stacked", "compressed_round_config0")):
             if ck in extra and key in cpu["configs"]:
                 extra[ck]["cpu_torch"] = dict(cpu["configs"][key], threads=cpu["configs"]["threads"])
 

@@ -466,12 +466,41 @@ def feddyn_update(model_params: Sequence[torch.Tensor], h_params: Sequence[torch
         except TypeError:
             pass  # messages elsewhere: moved below
     srcs = [[_on(t, dev) for t in m["parameters"]] for m in messages]
-    if len(srcs) <= cap:
-        codec.model_fold_server(ps, h_params, srcs, w, "feddyn", True, 0, 0.0, alpha)
-        return
-    for c0 in range(0, len(srcs), cap):
-        codec.model_fold_server(ps, h_params, srcs[c0:c0 + cap], w[c0:c0 + cap], "feddyn", False, 0, 0.0, alpha)
+    if _srv_ok([ps, h_params] + srcs):
+        if len(srcs) <= cap:
+            codec.model_fold_server(ps, h_params, srcs, w, "feddyn", True, 0, 0.0, alpha)
+            return
+        for c0 in range(0, len(srcs), cap):
+            codec.model_fold_server(ps, h_params, srcs[c0:c0 + cap], w[c0:c0 + cap], "feddyn", False, 0, 0.0, alpha)
+    else:  # (a float64, non-contiguous or spread model) per-tensor launches
+        for j, (p, h) in enumerate(zip(ps, h_params)):
+            for m in messages:  # h = fmaf(alpha, fl(p_m - θ), h) in message order, θ still the old model
+                d = _on(m["parameters"][j], p.device).clone().contiguous()
+                _weighted_sum_any(d, [p], [-1.0], 2)  # fmaf(-1, θ, p_m) = fl(p_m - θ)
+                _weighted_sum_any(h, [d], [alpha], 2)
     avg_parameters(ps, [{"parameters": s_, "train_samples": m["train_samples"]} for s_, m in zip(srcs, messages)])
+
+
+def _srv_ok(groups) -> bool:
+    """Every tensor of every group a contiguous fp32 tensor on the first one's device, sized as the first group
+    (what flc_model_fold_server takes)."""
+    if not groups or not groups[0]:
+        return False
+    dev = groups[0][0].device
+    sizes = [t.numel() for t in groups[0]]
+    return dev.type == "cuda" and all(
+        len(g) == len(sizes) and all(t.device == dev and t.dtype is torch.float32 and t.is_contiguous()
+                                     and t.numel() == k for t, k in zip(g, sizes)) for g in groups)
+
+
+def _weighted_sum_any(dst: torch.Tensor, srcs, weights, init_mode: int, beta: float = 0.0) -> None:
+    """codec.weighted_sum on a destination of any layout (a non-contiguous one through a contiguous copy)."""
+    if dst.is_contiguous():
+        codec.weighted_sum(dst, [_on(s_, dst.device) for s_ in srcs], weights, init_mode, beta)
+        return
+    tmp = dst.contiguous()
+    codec.weighted_sum(tmp, [_on(s_, dst.device) for s_ in srcs], weights, init_mode, beta)
+    dst.copy_(tmp)
 
 
 def pfedme_update(model_params: Sequence[torch.Tensor], messages: Sequence[Mapping], beta: float) -> None:
@@ -495,13 +524,19 @@ def pfedme_update(model_params: Sequence[torch.Tensor], messages: Sequence[Mappi
         except TypeError:
             pass  # messages elsewhere: moved below
     srcs = [[_on(t, dev) for t in m["parameters"]] for m in messages]
-    if len(srcs) <= codec.MODEL_FOLD_MAX_SRC:
-        # (no message: avg_parameters returns before its mul_(inertia): the blend of θ with itself, init 2)
-        codec.model_fold_server(ps, ps, srcs, w, "pfedme", True, 0 if srcs else 2, 0.0, beta)
-        return
-    saved = [p.detach().clone() for p in ps]
-    avg_parameters(ps, [{"parameters": s_, "train_samples": m["train_samples"]} for s_, m in zip(srcs, messages)])
-    codec.model_fold_server(ps, saved, [], [], "pfedme", False, 2, 0.0, beta)
+    if _srv_ok([ps] + srcs):
+        if len(srcs) <= codec.MODEL_FOLD_MAX_SRC:
+            # (no message: avg_parameters returns before its mul_(inertia): the blend of θ with itself, init 2)
+            codec.model_fold_server(ps, ps, srcs, w, "pfedme", True, 0 if srcs else 2, 0.0, beta)
+            return
+        saved = [p.detach().clone() for p in ps]
+        avg_parameters(ps, [{"parameters": s_, "train_samples": m["train_samples"]} for s_, m in zip(srcs, messages)])
+        codec.model_fold_server(ps, saved, [], [], "pfedme", False, 2, 0.0, beta)
+    else:  # (a float64, non-contiguous or spread model) per-tensor launches
+        saved = [p.detach().clone() for p in ps]
+        avg_parameters(ps, [{"parameters": m["parameters"], "train_samples": m["train_samples"]} for m in messages])
+        for p, pre in zip(ps, saved):  # θ = fmaf(1 - β, θ_prev, fl(θ · β)): mul_(beta).add_(prev, alpha=1 - beta)
+            _weighted_sum_any(p, [pre], [1 - beta], 0, beta)
 
 
 def _adopt(groups, messages_tensors=()) -> None:

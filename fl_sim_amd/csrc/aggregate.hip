@@ -434,7 +434,9 @@ __global__ __launch_bounds__(kThreads) void server_fold_kernel(ModelPack p, floa
       for (int m = 0; m < kMaxSrc; ++m)
         if (m < p.ns) sv[m] = *reinterpret_cast<const float4*>(p.src[m][t] + i);
       const float4 t0 = *reinterpret_cast<const float4*>(dst + i);
-      float4 x = *reinterpret_cast<const float4*>(aux + i);  // FedDyn: h; pFedMe !FOLD: the saved θ0
+      // FedDyn: h; pFedMe !FOLD: the saved θ0.  pFedMe's FOLD form never reads aux (its caller passes θ itself there,
+      // which the __restrict__ qualifiers would make undefined to load)
+      float4 x = (KIND == 1 || !FOLD) ? *reinterpret_cast<const float4*>(aux + i) : make_float4(0.f, 0.f, 0.f, 0.f);
       float4 a = t0;
       if (KIND == 1) {
 #pragma unroll

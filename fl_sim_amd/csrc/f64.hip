@@ -454,6 +454,9 @@ constexpr int kGT = 1024;           // threads of the sample, gather and fallbac
 constexpr int kGNW = kGT / kWave;
 constexpr int kMaxG64 = 1024;       // blocks of the grid-synchronised select (one flag each)
 constexpr int kSampleBlocks = 64;   // blocks loading the sample
+// the prep kernel writes the compact sample exactly when its grid covers the whole sample (gridDim.x * kT == kSample64)
+// and the select reads it whenever S == kSample64: the two conditions agree only while this holds
+static_assert(kSampleBlocks * kT == kSample64, "the compact sample's writer and reader disagree");
 constexpr int kMaxCPB = 2048;       // chunks per select block (more: the band is off, the passes over x run)
 constexpr unsigned long long kOvf = 1ull << 44;  // (n < 2^44)
 static_assert(kBand == 2 * kGT, "gather: two band bins per thread");

@@ -25,6 +25,18 @@ __device__ __forceinline__ void st_stream(float* p, float4 v) {
   __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
 }
 
+// 16-B store written through past the XCD's L2 (sc1: the line is not left dirty in L2 for the kernel's end to write
+// back).  No builtin sets sc1 on a 16-B store, so it is inline asm — and the compiler cannot see that the asm is a VMEM
+// store of more than 8 bytes, after which gfx940+ needs 2 wait states before a VALU may overwrite the store's data
+// VGPRs.  It schedules nothing for that, so the asm carries them itself (s_nop 1).  Without them the round-5 quantizer
+// variant stored two data dwords already overwritten by the next store's address (profiles/r06/r06c_asm_store_hazard.txt).
+// Waits the compiler counts (vmcnt) stay correct: an extra outstanding store only makes a counted wait for earlier
+// loads, which return in order, wait as long or longer.
+__device__ __forceinline__ void st_wt(float* p, float4 v) {
+  const f32x4 w = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+}
+
 // ------------------------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11).  Counter = (group_lo, group_hi, ctr_lo, ctr_hi), key = seed.
 // One call yields four 32-bit words; element e of a vector uses word (e & 3) of group e >> 2, so the

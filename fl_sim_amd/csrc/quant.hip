@@ -884,7 +884,12 @@ int launch_auto(const float* x, int64_t rows, int64_t d, int levels, int norm_p,
   const int64_t nb1 = cdiv(n, (int64_t)kGroup * kThreads);
   long long* nz = reinterpret_cast<long long*>(nnz);
   const char* name = DEC ? "quant_encode_decode" : "quant_encode";
-  if (norm_p == FLC_NORM_INF && !getenv("FLC_QUANT_TWO_LAUNCH")) {
+  // Under stream capture the two-launch path: the one-launch encode's exchange tag is made on the host per call, and
+  // a captured graph replays the same tag, so a word left by the previous replay (right tag, stale row maximum) would
+  // pass the check; the co-residency gate is off under capture as well.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  FLC_CHECK_HIP(hipStreamIsCapturing(st, &cap));
+  if (norm_p == FLC_NORM_INF && cap == hipStreamCaptureStatusNone && !getenv("FLC_QUANT_TWO_LAUNCH")) {
     // one launch when the batch fits one 1024-thread block per CU with at most two rows per block (configs[1])
     int dev = 0;
     const int cus = std::min(stream_cus(st, &dev), kMaxFused);

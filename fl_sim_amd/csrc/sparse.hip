@@ -22,6 +22,10 @@
 #include "flc_device.hpp"
 #include "flc_runtime.hpp"
 
+#ifndef FLC_DECODE_WT
+#define FLC_DECODE_WT 0  // the dense decode's output stores written through (st_wt): A/B switch
+#endif
+
 namespace flc {
 namespace {
 
@@ -183,7 +187,11 @@ __global__ __launch_bounds__(kWave) void sparse_decode_wave2_kernel(const int* _
     float4 v = tile4[q];
     if (e + 4 <= n) {
       if (weight != 1.0f) v = make_float4(weight * v.x, weight * v.y, weight * v.z, weight * v.w);
+#if FLC_DECODE_WT
+      st_wt(out + e, v);
+#else
       *reinterpret_cast<float4*>(out + e) = v;
+#endif
     } else {
       const float vv[4] = {v.x, v.y, v.z, v.w};
       for (int c = 0; c < 4 && e + c < n; ++c) out[e + c] = weight != 1.0f ? weight * vv[c] : vv[c];

@@ -455,3 +455,49 @@ def test_model_fold_server_misaligned_and_odd_tensors_equal_the_oracle():
             agg_ref.pfedme_update(params, msgs, 0.3)
             aggregation.pfedme_update(views, _msgs_dev(msgs, "parameters"), 0.3)
         assert gc.same_bits(_flat(views), _flat(params)), kind
+
+
+def _mixed_model(seed):
+    """A model the one-launch server folds do not take: a float64 tensor and a non-contiguous (transposed) fp32 one
+    beside plain fp32 tensors (the reference updates any model)."""
+    g = torch.Generator().manual_seed(seed)
+    a = torch.randn(7, 5, generator=g) * 0.1
+    b = (torch.randn(6, 4, generator=g) * 0.1).double()
+    c = (torch.randn(3, 9, generator=g) * 0.1).t()  # non-contiguous
+    d = torch.randn(11, generator=g) * 0.1
+    return [a, b, c, d]
+
+
+def _mixed_msgs(params, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [{"client_id": i, "train_samples": 10 * (i + 1), "metrics": {},
+             "parameters": [p + (torch.randn(p.shape, generator=g) * 1e-3).to(p.dtype) for p in params]}
+            for i in range(n)]
+
+
+@pytest.mark.parametrize("n_msgs", [3, 20])
+def test_feddyn_and_pfedme_take_any_model(n_msgs):
+    """FedDyn / pFedMe on a float64 + non-contiguous model fall back to per-tensor launches (the one-launch
+    server fold takes contiguous fp32 only), bit for bit with the oracle's restatement of the reference's update."""
+    from fl_sim_amd import aggregation
+
+    params = _mixed_model(1)
+    msgs = _mixed_msgs(params, n_msgs, 2)
+    g = torch.Generator().manual_seed(3)
+    hs = [(torch.randn(p.shape, generator=g) * 1e-3).to(p.dtype) for p in params]
+    # FedDyn
+    exp_p, exp_h = [p.clone() for p in params], [h.clone() for h in hs]
+    agg_ref.feddyn_update(exp_p, exp_h, msgs, 0.01, 20)
+    got_p = [p.cuda() if i != 2 else p.cuda().t().contiguous().t() for i, p in enumerate(params)]
+    assert not got_p[2].is_contiguous()
+    got_h = [h.cuda() for h in hs]
+    aggregation.feddyn_update(got_p, got_h, _msgs_dev(msgs, "parameters"), 0.01, 20)
+    for x, y in zip(got_p + got_h, exp_p + exp_h):
+        assert x.dtype == y.dtype and x.cpu().contiguous().numpy().tobytes() == y.contiguous().numpy().tobytes()
+    # pFedMe
+    exp_p = [p.clone() for p in params]
+    agg_ref.pfedme_update(exp_p, msgs, 0.7)
+    got_p = [p.cuda() if i != 2 else p.cuda().t().contiguous().t() for i, p in enumerate(params)]
+    aggregation.pfedme_update(got_p, _msgs_dev(msgs, "parameters"), 0.7)
+    for x, y in zip(got_p, exp_p):
+        assert x.dtype == y.dtype and x.cpu().contiguous().numpy().tobytes() == y.contiguous().numpy().tobytes()

@@ -138,12 +138,35 @@ def test_compressed_round_matches_reference(codec, opt, tag, server):
         assert all(m["delta_parameters"].kind == "stacked" and m["delta_parameters"].nbytes < D for m in msgs)
     s.update()
     assert all(m["delta_parameters"]._flat is None for m in msgs) or codec != "stacked10"  # (never decoded densely)
-    assert _same(rec, "theta", list(s.model.parameters()))
-    assert _same(rec, "delta", s.delta_parameters)
-    if s.v_parameters is not None:
-        assert _same(rec, "v", s.v_parameters)
+    assert _same(rec, "delta", s.delta_parameters)  # the fold: bit for bit, every optimiser
+    if opt == "avg":
+        assert _same(rec, "theta", list(s.model.parameters()))
+    else:
+        _check_adaptive_tail(codec, opt, tag, shapes, s)
     if server == "host":
         assert all(p.is_cpu for p in s.model.parameters())
+
+
+def _check_adaptive_tail(codec, opt, tag, shapes, s):
+    """The adaptive optimisers' tail against the oracle's round (oracle/round_ref.py, pinned to the same fixture on
+    CPU by tests/test_oracle_round.py), with the tolerance of test_gpu_aggregation.test_fedopt_update_matches_reference:
+    torch's CPU scalar tail loop may contract v's update to an fma (v: 1 ulp) and its vectorised sqrt is not correctly
+    rounded (θ: 1e-6 of the update + 1 ulp), where the kernels round every step as IEEE prescribes."""
+    from oracle import round_ref
+
+    theta, delta, v, locals_, sizes = round_inputs(shapes, opt)
+    theta0 = _flat(theta)
+    cfg = ROUND_OPTS[opt]
+    gc.seed_all(round_seed(codec, opt, tag))
+    round_ref.fedopt_round(codec, theta, delta, v, locals_, sizes, opt, cfg["lr"], cfg["betas"], cfg["tau"])
+    assert gc.same_bits(_flat(s.delta_parameters), _flat(delta))
+    exp_v, got_v = _flat(v), _flat(s.v_parameters)
+    ulp_v = np.abs(exp_v.view(np.int32).astype(np.int64) - got_v.view(np.int32).astype(np.int64))
+    assert ulp_v.max() <= 1 and (ulp_v > 0).mean() < 0.01
+    exp_t, got_t = _flat(theta), _flat(list(s.model.parameters()))
+    upd = np.abs(exp_t.astype(np.float64) - theta0)
+    err = np.abs(exp_t.astype(np.float64) - got_t.astype(np.float64))
+    assert np.all(err <= 1e-6 * upd + np.spacing(np.abs(exp_t)))
 
 
 def test_compressed_delta_reads_as_the_decoded_tensors():
@@ -262,9 +285,15 @@ def test_stacked_round_philox_matches_oracle():
         assert c.compressors[0].last_need_to_send_advance == K
     s.update()
     cfg = ROUND_OPTS["adam"]
+    theta0 = _flat(theta)
     agg_ref.fedopt_update(theta, delta, v, msgs, "adam", cfg["lr"], cfg["betas"], cfg["tau"])
-    for got, exp in ((list(s.model.parameters()), theta), (s.delta_parameters, delta), (s.v_parameters, v)):
-        assert gc.same_bits(_flat(got), _flat(exp))
+    assert gc.same_bits(_flat(s.delta_parameters), _flat(delta))
+    exp_v, got_v = _flat(v), _flat(s.v_parameters)  # (adaptive tail tolerance: see _check_adaptive_tail)
+    ulp_v = np.abs(exp_v.view(np.int32).astype(np.int64) - got_v.view(np.int32).astype(np.int64))
+    assert ulp_v.max() <= 1 and (ulp_v > 0).mean() < 0.01
+    exp_t, got_t = _flat(theta), _flat(list(s.model.parameters()))
+    err = np.abs(exp_t.astype(np.float64) - got_t.astype(np.float64))
+    assert np.all(err <= 1e-6 * np.abs(exp_t.astype(np.float64) - theta0) + np.spacing(np.abs(exp_t)))
 
 
 def test_fold_records_rejects_bad_arguments():
