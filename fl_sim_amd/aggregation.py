@@ -121,8 +121,8 @@ def add_parameters(server_params: Iterable[torch.Tensor], params: Iterable[torch
     sps = _params(sps)
     if _fold(sps, [ps], [ratio], 2):
         return
-    for sp, p in zip(sps, ps):
-        codec.weighted_sum(sp, [_on(p, sp.device)], [ratio], init_mode=2)
+    for sp, p in zip(sps, ps):  # (a float64, non-contiguous or spread model) per-tensor launches
+        _weighted_sum_any(sp, [p], [ratio], 2)
 
 
 def avg_parameters(server_params: Sequence[torch.Tensor], messages: Sequence[Mapping], size_aware: bool = False,
@@ -143,9 +143,8 @@ def avg_parameters(server_params: Sequence[torch.Tensor], messages: Sequence[Map
     ]
     if _fold(_params(sps), messages, ratios, 0, inertia, key=key):
         return
-    for j, sp in enumerate(_params(sps)):
-        srcs = [_on(m[key][j], sp.device) for m in messages]
-        codec.weighted_sum(sp, srcs, ratios, init_mode=0, beta=inertia)
+    for j, sp in enumerate(_params(sps)):  # (a float64, non-contiguous or spread model) per-tensor launches
+        _weighted_sum_any(sp, [m[key][j] for m in messages], ratios, 0, inertia)
 
 
 def _gradients_on(dev: torch.device, messages: Sequence[Mapping]) -> List[torch.Tensor]:
@@ -210,6 +209,20 @@ def _pair_fold(dev: torch.device, params: Sequence[torch.Tensor], messages: Sequ
     tensor of ``dev``."""
     import ctypes
 
+    fast = codec._pypair()
+    if fast is not None:
+        # one C call: every tensor checked in place (no per-tensor Python attribute reads, no ctypes tables); a
+        # TypeError (a tensor the launch does not take) leaves everything untouched, as does None below
+        flat = torch.empty(max(sum(p.numel() for p in params), 1), dtype=torch.float32, device=dev)
+        grads, off = [], 0
+        for p in params:
+            grads.append(flat[off:off + p.numel()].view(p.shape))
+            off += p.numel()
+        try:
+            fast(params, grads, messages, wp, wg, float(inertia))  # (on the current stream of the model's device)
+            return grads, flat
+        except TypeError:
+            pass  # (messages on another device: moved below, as _on does)
     ok = lambda t: t.is_cuda and t.device == dev and t.dtype is torch.float32 and t.is_contiguous()  # noqa: E731
     if not all(ok(p) for p in params):
         return None
@@ -315,12 +328,11 @@ def fedopt_update(model_params: Sequence[torch.Tensor], delta_parameters: Sequen
              theta=ps, v=vps, opt=opt if vps is not None else "avg", lr=lr, beta2=betas[1], tau=tau):
         return  # the delta average and the optimizer step of every tensor in one launch
     for j, dp in enumerate(delta_parameters):
-        srcs = [_on(m["delta_parameters"][j], dp.device) for m in messages]
-        codec.weighted_sum(dp, srcs, [alpha] * len(srcs), init_mode=0, beta=betas[0])
+        _weighted_sum_any(dp, [m["delta_parameters"][j] for m in messages], [alpha] * len(messages), 0, betas[0])
     ps = _params(model_params)
     for j, (sp, dp) in enumerate(zip(ps, delta_parameters)):
         vp = None if (v_parameters is None or opt == "avg") else v_parameters[j]
-        codec.fedopt_step(sp, dp, vp, opt if vp is not None else "avg", lr, betas[1], tau)
+        _contig_call(codec.fedopt_step, sp, dp, vp, opt if vp is not None else "avg", lr, betas[1], tau)
 
 
 def scaffold_update(model_params: Sequence[torch.Tensor], control_variates: Sequence[torch.Tensor],
@@ -343,12 +355,10 @@ def scaffold_update(model_params: Sequence[torch.Tensor], control_variates: Sequ
     ps, cvs = _params(model_params), list(control_variates)
     if not _fold(ps, messages, [ratio_p] * len(messages), 2, key="parameters_delta"):
         for j, sp in enumerate(ps):
-            codec.weighted_sum(sp, [_on(m["parameters_delta"][j], sp.device) for m in messages],
-                               [ratio_p] * len(messages), init_mode=2)
+            _weighted_sum_any(sp, [m["parameters_delta"][j] for m in messages], [ratio_p] * len(messages), 2)
     if not _fold(cvs, messages, [ratio_c] * len(messages), 2, key="control_variates_delta"):
         for j, cv in enumerate(cvs):
-            codec.weighted_sum(cv, [_on(m["control_variates_delta"][j], cv.device) for m in messages],
-                               [ratio_c] * len(messages), init_mode=2)
+            _weighted_sum_any(cv, [m["control_variates_delta"][j] for m in messages], [ratio_c] * len(messages), 2)
 
 
 def ifca_update(cluster_centers: Mapping[int, dict], messages: Sequence[Mapping], num_clusters: int) -> None:
@@ -374,11 +384,10 @@ def ifca_update(cluster_centers: Mapping[int, dict], messages: Sequence[Mapping]
         if hoststage.is_host(center):
             with hoststage.staged([center], [True], [True], [m["delta_parameters"] for m in ms]) as ((dc,), dm):
                 for j, p in enumerate(dc):
-                    codec.weighted_sum(p, [d[j] for d in dm], [1 / sizes[c]] * len(ms), init_mode=2)
+                    _weighted_sum_any(p, [d[j] for d in dm], [1 / sizes[c]] * len(ms), 2)
             continue
         for j, p in enumerate(_params(center)):
-            codec.weighted_sum(p, [_on(m["delta_parameters"][j], p.device) for m in ms], [1 / sizes[c]] * len(ms),
-                               init_mode=2)
+            _weighted_sum_any(p, [m["delta_parameters"][j] for m in ms], [1 / sizes[c]] * len(ms), 2)
     for m in messages:
         cluster_centers[m["cluster_id"]]["client_ids"].append(m["client_id"])
 
@@ -416,7 +425,7 @@ def feddr_update(model_params: Sequence[torch.Tensor], y_params: Sequence[torch.
     total = sum([m["train_samples"] for m in messages])
     weights = [m["train_samples"] / total for m in messages]
     for j, xt in enumerate(x_til_params):
-        codec.weighted_sum(xt, [_on(m["x_hat_delta"][j], xt.device) for m in messages], weights, init_mode=2)
+        _weighted_sum_any(xt, [m["x_hat_delta"][j] for m in messages], weights, 2)
     cx, cy = coeff / eta, 1 / (num_clients + 1)
     if kind == "l1":
         prox, pc = _lib.FLC_PROX_L1, coeff
@@ -426,7 +435,7 @@ def feddr_update(model_params: Sequence[torch.Tensor], y_params: Sequence[torch.
         prox, pc = _lib.FLC_PROX_NONE, 0.0
     ps = _params(model_params)
     for sp, yp, xt in zip(ps, y_params, x_til_params):
-        codec.feddr_combine(sp, yp, xt, alpha, cx, cy, prox, pc)
+        _contig_call(codec.feddr_combine, sp, yp, xt, alpha, cx, cy, prox, pc)
     if kind == "l2":
         sq = 0.0
         for sp in ps:
@@ -435,7 +444,7 @@ def feddr_update(model_params: Sequence[torch.Tensor], y_params: Sequence[torch.
         norm = coeff * math.sqrt(sq)
         f = max(0, 1 - coeff / norm)
         for sp in ps:
-            codec.weighted_sum(sp, [], [], init_mode=0, beta=f)
+            _weighted_sum_any(sp, [], [], 0, f)
 
 
 def feddyn_update(model_params: Sequence[torch.Tensor], h_params: Sequence[torch.Tensor], messages: Sequence[Mapping],
@@ -491,6 +500,16 @@ def _srv_ok(groups) -> bool:
     return dev.type == "cuda" and all(
         len(g) == len(sizes) and all(t.device == dev and t.dtype is torch.float32 and t.is_contiguous()
                                      and t.numel() == k for t, k in zip(g, sizes)) for g in groups)
+
+
+def _contig_call(fn, *ts, **kw) -> None:
+    """fn(*ts, **kw) on contiguous stand-ins of non-contiguous tensors (an in-place kernel's operands), copied back
+    afterwards; other arguments pass through."""
+    cs = [t.contiguous() if isinstance(t, torch.Tensor) else t for t in ts]
+    fn(*cs, **kw)
+    for t, c in zip(ts, cs):
+        if c is not t:
+            t.copy_(c)
 
 
 def _weighted_sum_any(dst: torch.Tensor, srcs, weights, init_mode: int, beta: float = 0.0) -> None:

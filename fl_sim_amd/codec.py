@@ -818,6 +818,22 @@ def _pysrv():
     return _PYSRV[0]
 
 
+_PYPAIR: list = []
+
+
+def _pypair():
+    """fl_sim_amd._flcfold.avg_and_gradients (csrc/pyfold.cpp: flc_avg_and_gradients on Python lists of tensors and
+    message mappings) when built, else None."""
+    if not _PYPAIR:
+        try:
+            from . import _flcfold
+
+            _PYPAIR.append(_flcfold.avg_and_gradients)
+        except (ImportError, AttributeError):
+            _PYPAIR.append(None)
+    return _PYPAIR[0]
+
+
 def model_fold_server(theta: Sequence[torch.Tensor], aux: Sequence[torch.Tensor],
                       srcs: Sequence[Sequence[torch.Tensor]], weights: Sequence[float], kind: str, fold: bool = True,
                       init_mode: int = 0, inertia: float = 0.0, c: float = 0.0) -> None:

@@ -43,15 +43,20 @@ from ._lib import FLC_NORM_INF, FLC_Q_STANDARD_DITHER
 from .compressors import Compressor, CompressorType
 
 
+_MSG_CLS: list = []
+
+
 def client_message_class():
     """The reference's ``ClientMessage`` (nodes.py:1537-1557) when ``fl_sim`` is importable (``Server._update``
-    asserts the type, nodes.py:767-770), else a dict subclass with the same constructor."""
-    try:
-        from fl_sim.nodes import ClientMessage as ref_cls  # type: ignore
-
-        return ref_cls
-    except Exception:  # fl_sim absent (or its dependencies: torch_ecg, ...)
-        return ClientMessage
+    asserts the type, nodes.py:767-770), else a dict subclass with the same constructor.  Looked up once per process
+    (a failing import costs ~80 us, and ``communicate`` runs once per client per round)."""
+    if not _MSG_CLS:
+        try:
+            from fl_sim.nodes import ClientMessage as ref_cls  # type: ignore
+        except Exception:  # fl_sim absent (or its dependencies: torch_ecg, ...)
+            ref_cls = ClientMessage
+        _MSG_CLS.append(ref_cls)
+    return _MSG_CLS[0]
 
 
 class ClientMessage(dict):

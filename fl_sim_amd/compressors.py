@@ -188,17 +188,24 @@ class Compressor:
         return "?"
 
     # send statistics (compressors.py:40-43, 406-408).  A compressed client round in philox mode (compressed.py) leaves
-    # the dithering stage's count of nonzero inputs on the device instead of synchronising for it; it is folded into
-    # the counters the first time one of them is read, with the reference's arithmetic (base + nnz * per).
+    # the dithering stage's count of nonzero inputs on the device instead of synchronising for it; the counts of up to
+    # 64 calls wait there and are folded into the counters, in call order with the reference's arithmetic
+    # (base + nnz * per per call), the first time one of them is read (one device-to-host copy for all of them).
+    _kMaxPending = 64
+
     def _flush(self) -> None:
         p = self.__dict__.get("_pending")
-        if p is not None:
+        if p:
             self._pending = None
-            cnt, base, per = p
-            nnz = int(cnt.item())
-            send = base + nnz * per if nnz else base
-            self._last_send = send
-            self._really_send += send
+            cs = [c for c, _, _ in p]
+            if len(cs) > 1 and all(c.device == cs[0].device for c in cs):
+                nnzs = [int(v) for v in torch.cat([c.reshape(-1) for c in cs]).tolist()]
+            else:
+                nnzs = [int(c.item()) for c in cs]
+            for (_, base, per), nnz in zip(p, nnzs):
+                send = base + nnz * per if nnz else base
+                self._last_send = send
+                self._really_send += send
 
     @property
     def last_need_to_send_advance(self):
@@ -222,11 +229,14 @@ class Compressor:
 
     def _finish_pending(self, d: int, count, base, per) -> None:
         """_finish with the send count still on the device (see _flush)."""
-        self._flush()
+        pend = self.__dict__.get("_pending") or []
+        if len(pend) >= self._kMaxPending:
+            self._flush()
+            pend = []
         self.last_input_advance = d
         self.total_input_components += d
-        self._last_send = base
-        self._pending = (count, base, per)  # (the advance is added to the total on flush)
+        pend.append((count, base, per))  # (the advances are added to the totals on flush)
+        self._pending = pend
 
     def resetStats(self):
         self._pending = None

@@ -247,6 +247,93 @@ PyObject* server_fold(PyObject*, PyObject* args) {
   return done((Py_INCREF(Py_None), Py_None));
 }
 
+// avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia): flc_avg_and_gradients (avg_parameters then
+// update_gradients over the same messages, nodes.py:1134-1180) on Python lists: `params` folded in place, `grads` (one
+// per parameter, same sizes) written from +0; every message a mapping with "parameters" and "gradients".  The same
+// checks and errors as model_fold; any number of messages (the C call chains them).
+PyObject* avg_and_gradients(PyObject*, PyObject* args) {
+  PyObject *params, *grads, *msgs, *wpar, *wgrd;
+  double inertia;
+  if (!PyArg_ParseTuple(args, "OOOOOd", &params, &grads, &msgs, &wpar, &wgrd, &inertia)) return nullptr;
+  std::vector<PyObject*> keep;
+  auto done = [&](PyObject* r) {
+    for (PyObject* o : keep) Py_XDECREF(o);
+    return r;
+  };
+  PyObject* seqs[5] = {params, grads, msgs, wpar, wgrd};
+  PyObject* f[5];
+  for (int i = 0; i < 5; ++i) {
+    f[i] = PySequence_Fast(seqs[i], "avg_and_gradients takes sequences");
+    if (!f[i]) return done(nullptr);
+    keep.push_back(f[i]);
+  }
+  const Py_ssize_t nt = PySequence_Fast_GET_SIZE(f[0]), ns = PySequence_Fast_GET_SIZE(f[2]);
+  if (PySequence_Fast_GET_SIZE(f[1]) != nt) return done(value_error("one gradient buffer per parameter"));
+  if (PySequence_Fast_GET_SIZE(f[3]) != ns || PySequence_Fast_GET_SIZE(f[4]) != ns)
+    return done(value_error("one weight of each kind per message"));
+  if (ns == 0) return done(value_error("avg_and_gradients needs at least one message"));
+  if (nt == 0) return done((Py_INCREF(Py_None), Py_None));
+  int dev = -1;
+  std::vector<float*> pp(nt), gp(nt);
+  std::vector<int64_t> sz(nt);
+  PyObject** pi = PySequence_Fast_ITEMS(f[0]);
+  PyObject** gi = PySequence_Fast_ITEMS(f[1]);
+  for (Py_ssize_t t = 0; t < nt; ++t) {
+    const at::Tensor* a = usable(pi[t], &dev);
+    if (!a) return done(type_error("model tensors must be contiguous fp32 HIP tensors on one device"));
+    pp[t] = a->data_ptr<float>();
+    sz[t] = a->numel();
+    const at::Tensor* b = usable(gi[t], &dev);
+    if (!b) return done(type_error("gradient buffers must be contiguous fp32 HIP tensors on the model's device"));
+    if (b->numel() != sz[t]) return done(value_error("gradient buffers must match the model tensors' sizes"));
+    gp[t] = b->data_ptr<float>();
+  }
+  std::vector<const float*> ps((size_t)ns * nt), gs((size_t)ns * nt);
+  std::vector<float> wp(ns), wg(ns);
+  PyObject** mi = PySequence_Fast_ITEMS(f[2]);
+  PyObject** wpi = PySequence_Fast_ITEMS(f[3]);
+  PyObject** wgi = PySequence_Fast_ITEMS(f[4]);
+  static PyObject* const keys[2] = {PyUnicode_InternFromString("parameters"), PyUnicode_InternFromString("gradients")};
+  for (Py_ssize_t m = 0; m < ns; ++m) {
+    const double a = PyFloat_AsDouble(wpi[m]), b = PyFloat_AsDouble(wgi[m]);
+    if (PyErr_Occurred()) return done(nullptr);
+    wp[m] = (float)a;
+    wg[m] = (float)b;
+    for (int k = 0; k < 2; ++k) {
+      PyObject* v = PyObject_GetItem(mi[m], keys[k]);
+      if (!v) return done(nullptr);
+      keep.push_back(v);
+      PyObject* fv = PySequence_Fast(v, "a message's parameters / gradients are sequences of tensors");
+      if (!fv) return done(nullptr);
+      keep.push_back(fv);
+      if (PySequence_Fast_GET_SIZE(fv) != nt) return done(value_error("every message has one tensor per model tensor"));
+      PyObject** it = PySequence_Fast_ITEMS(fv);
+      std::vector<const float*>& out = k == 0 ? ps : gs;
+      for (Py_ssize_t t = 0; t < nt; ++t) {
+        const at::Tensor* s = usable(it[t], &dev);
+        if (!s) return done(type_error("message tensors must be contiguous fp32 HIP tensors on the model's device"));
+        if (s->numel() != sz[t]) return done(value_error("message tensors must match the model tensors' sizes"));
+        out[(size_t)m * nt + t] = s->data_ptr<float>();
+      }
+    }
+  }
+  void* st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+  int rc = FLC_OK;
+  Py_BEGIN_ALLOW_THREADS
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  rc = flc_avg_and_gradients(pp.data(), gp.data(), ps.data(), gs.data(), wp.data(), wg.data(), (int)ns, sz.data(),
+                             (int)nt, (float)inertia, st);
+  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  Py_END_ALLOW_THREADS
+  if (rc != FLC_OK) {
+    PyErr_Format(PyExc_RuntimeError, "flc_avg_and_gradients failed with status %d: %s", rc, flc_last_error());
+    return done(nullptr);
+  }
+  return done((Py_INCREF(Py_None), Py_None));
+}
+
 void release_storage(void* ctx) { delete static_cast<c10::Storage*>(ctx); }
 
 // alias(host_tensor, device_index) -> tensor on cuda:device_index over the same bytes (see the header)
@@ -280,6 +367,9 @@ PyMethodDef kMethods[] = {
     {"server_fold", server_fold, METH_VARARGS,
      "server_fold(theta, aux, msgs, key, weights, kind, fold, init_mode, inertia, c): flc_model_fold_server (FedDyn / "
      "pFedMe) on Python lists of HIP tensors, at most 16 messages, on the current stream of the model's device"},
+    {"avg_and_gradients", avg_and_gradients, METH_VARARGS,
+     "avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia): flc_avg_and_gradients on Python lists of HIP "
+     "tensors (messages: mappings with 'parameters' and 'gradients'), on the current stream of the model's device"},
     {"alias", alias, METH_VARARGS,
      "alias(host_tensor, device_index): a HIP-device tensor over a pinned host tensor's memory (zero-copy)"},
     {nullptr, nullptr, 0, nullptr}};

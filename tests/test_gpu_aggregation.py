@@ -501,3 +501,79 @@ def test_feddyn_and_pfedme_take_any_model(n_msgs):
     aggregation.pfedme_update(got_p, _msgs_dev(msgs, "parameters"), 0.7)
     for x, y in zip(got_p, exp_p):
         assert x.dtype == y.dtype and x.cpu().contiguous().numpy().tobytes() == y.contiguous().numpy().tobytes()
+
+
+def _same_any(got, exp):
+    return all(x.dtype == y.dtype and x.cpu().contiguous().numpy().tobytes() == y.contiguous().numpy().tobytes()
+               for x, y in zip(got, exp))
+
+
+def _noncontig(params):
+    out = [p.cuda() if i != 2 else p.cuda().t().contiguous().t() for i, p in enumerate(params)]
+    assert not out[2].is_contiguous()
+    return out
+
+
+@pytest.mark.parametrize("n_msgs", [3, 20])
+@pytest.mark.parametrize("opt", ["avg", "adam"])
+def test_fedopt_takes_any_model(opt, n_msgs):
+    """FedOptServer.update (_fedopt.py:196-240) on a float64 + non-contiguous model: the per-tensor fallback (the delta
+    fold and the optimizer step through contiguous stand-ins), bit for bit with the oracle."""
+    from fl_sim_amd import aggregation
+
+    params = _mixed_model(4)
+    g = torch.Generator().manual_seed(5)
+    msgs = [{"train_samples": 10, "delta_parameters": [(torch.randn(p.shape, generator=g) * 1e-3).to(p.dtype)
+                                                       for p in params]} for _ in range(n_msgs)]
+    dls = [(torch.randn(p.shape, generator=g) * 1e-4).to(p.dtype) for p in params]
+    vs = [(torch.rand(p.shape, generator=g) * 1e-4 + 1e-6).to(p.dtype) for p in params] if opt == "adam" else None
+    betas = (0.9, 0.99) if opt == "adam" else (0.0, 1.0)
+    exp_p, exp_d = [p.clone() for p in params], [d.clone() for d in dls]
+    exp_v = [v.clone() for v in vs] if vs is not None else None
+    agg_ref.fedopt_update(exp_p, exp_d, exp_v, msgs, opt, 0.5, betas, 1e-3)
+    got_p, got_d = _noncontig(params), _noncontig(dls)
+    got_v = _noncontig(vs) if vs is not None else None
+    aggregation.fedopt_update(got_p, got_d, got_v, _msgs_dev(msgs, "delta_parameters"), opt, 0.5, betas, 1e-3)
+    assert _same_any(got_d, exp_d)
+    if vs is not None:
+        assert _same_any(got_v, exp_v)
+        # theta + lr * d / (sqrt(v) + tau) with IEEE (correctly rounded) sqrt: torch's CPU float32 sqrt (vectorised, Sleef)
+        # is not correctly rounded in ~0.6 % of cases, and at lr = 0.5 a 1-ulp denominator shows in theta (DESIGN.md §7)
+        exp_p = []
+        for p, d, v in zip(params, exp_d, exp_v):
+            if p.dtype == torch.float32:
+                den = np.sqrt(v.numpy()) + np.float32(1e-3)
+                exp_p.append(torch.from_numpy(p.numpy() + (np.float32(0.5) * d.numpy()) / den))
+            else:
+                exp_p.append(p + (0.5 * d) / (v.sqrt() + 1e-3))
+    assert _same_any(got_p, exp_p)
+
+
+@pytest.mark.parametrize("n_msgs", [3, 20])
+def test_avg_add_scaffold_take_any_model(n_msgs):
+    """avg_parameters with inertia, add_parameters (nodes.py:1116-1163) and SCAFFOLD's update (_scaffold.py:160-167)
+    on a float64 + non-contiguous model: per-tensor launches, bit for bit with the oracle."""
+    from fl_sim_amd import aggregation
+
+    params = _mixed_model(6)
+    msgs = _mixed_msgs(params, n_msgs, 7)
+    exp = [p.clone() for p in params]
+    agg_ref.avg_parameters(exp, msgs, size_aware=True, inertia=0.25)
+    got = _noncontig(params)
+    aggregation.avg_parameters(got, _msgs_dev(msgs, "parameters"), size_aware=True, inertia=0.25)
+    assert _same_any(got, exp)
+    exp = [p.clone() for p in params]
+    agg_ref.add_parameters(exp, msgs[0]["parameters"], 0.3)
+    got = _noncontig(params)
+    aggregation.add_parameters(got, [t.cuda() for t in msgs[0]["parameters"]], 0.3)
+    assert _same_any(got, exp)
+    g = torch.Generator().manual_seed(8)
+    smsgs = [{"parameters_delta": [(torch.randn(p.shape, generator=g) * 1e-3).to(p.dtype) for p in params],
+              "control_variates_delta": [(torch.randn(p.shape, generator=g) * 1e-3).to(p.dtype) for p in params]}
+             for _ in range(n_msgs)]
+    cvs = [(torch.randn(p.shape, generator=g) * 1e-3).to(p.dtype) for p in params]
+    exp_p, exp_c = [p.clone() for p in params], [c.clone() for c in cvs]
+    agg_ref.scaffold_update(exp_p, exp_c, smsgs, 0.1, 30)
+    got_p, got_c = _noncontig(params), _noncontig(cvs)
+    aggregation.scaffold_update(got_p, got_c, [{k: [t.cuda() for t in v] for k, v in m.items()} for m in smsgs], 0.1, 30)
+    assert _same_any(got_p, exp_p) and _same_any(got_c, exp_c)
