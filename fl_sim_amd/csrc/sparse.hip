@@ -23,7 +23,7 @@
 #include "flc_runtime.hpp"
 
 #ifndef FLC_DECODE_WT
-#define FLC_DECODE_WT 0  // the dense decode's output stores written through (st_wt): A/B switch
+#define FLC_DECODE_WT 1  // the dense decode's output stores written through (st_wt; 0: plain stores, the A/B switch)
 #endif
 
 namespace flc {

@@ -79,3 +79,18 @@ def test_pending_send_statistics_fold_in_on_read():
     c._finish_pending(100, torch.tensor([0]), 1, 5.0 / 32.0)
     c.resetStats()
     assert c.really_need_to_send_components == 0 and c.last_need_to_send_advance == 0
+
+
+def test_pending_send_statistics_of_many_calls_fold_in_call_order():
+    """Counts of several philox-mode calls wait together (read back in one copy, at most 64 at a time) and fold in
+    call by call: the totals and the last call's advance equal those of the calls finished one at a time."""
+    per = 5.0 / 32.0
+    counts = [7, 0, 3, 11, 0, 2] + list(range(70))
+    a, b = _std(10, np.inf), _std(10, np.inf)
+    for cnt in counts:
+        a._finish_pending(100, torch.tensor([cnt]), 1, per)
+        b._finish(100, 1 + cnt * per if cnt else 1)
+    assert len(a.__dict__.get("_pending") or []) <= 64
+    assert a.total_input_components == b.total_input_components
+    assert a.really_need_to_send_components == b.really_need_to_send_components
+    assert a.last_need_to_send_advance == b.last_need_to_send_advance

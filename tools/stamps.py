@@ -14,8 +14,8 @@ import torch
 
 from fl_sim_amd import codec
 
-STAMP_OFF = 175616  # byte offset of EncWs.stamps in the top-k workspace (topk.hip: kOffStamps)
-BLKT_OFF = 175872   # kOffBlkT
+STAMP_OFF = 234752  # byte offset of EncWs.stamps in the top-k workspace (topk.hip: kOffStamps, 8 histogram copies)
+BLKT_OFF = 235008   # kOffBlkT
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 268_435_456
 k = n // 100
 seed = int(os.environ.get("SEED", "1"))  # bench.py's headline delta: SEED=1234
@@ -30,6 +30,8 @@ elif os.environ.get("BATCH"):  # the batched encode of 100 clients x 1 M: client
     gen = torch.Generator(device="cuda").manual_seed(seed + 2)
     xs = [torch.randn(1_000_000, device="cuda", generator=gen) * 1e-3 for _ in range(int(os.environ["BATCH"]))]
     encode = lambda it: codec.stacked_encode_batch(xs, 10_000, 127, seeds=list(range(len(xs))), counter=it)  # noqa: E731
+elif os.environ.get("PLAIN"):  # the plain top-k select (configs[2]'s TopK compressor path)
+    encode = lambda it: codec.topk_encode(x, k, with_tiles=True)  # noqa: E731
 else:
     encode = lambda it: codec.stacked_encode(x, k, 127, 1, it)
 names = ["keys", "sample-sel", "filter", "post+stage+flush", "boundary", "load", "pick0", "inbin", "x1", "list", "local", "sums", "counts", "decide", "write+tiles"]
@@ -49,6 +51,12 @@ for it in range(int(os.environ.get("ITERS", "12"))):
             parts.append(f"{names[i - 1]} {(t[i] - prev) * 10 / 1000:.1f}")
             prev = t[i]
     print(" | ".join(parts), f"| total {(max(t[14], t[15]) - t[0]) * 10 / 1000:.1f} us")
+    wrow = ws[BLKT_OFF + 768 * 32:BLKT_OFF + 800 * 32].cpu().numpy().view(np.uint64).astype(np.int64).reshape(32, 4)[:, 0]
+    if wrow[16] > 0 and t[8] > 0:  # the speculative compaction's per-wave stamps (block 0), from stamp 8 (lists published)
+        rel = lambda v: round(float(v - t[8]) * 10 / 1000, 1) if v > 0 else None  # noqa: E731
+        print("  spec: workers start", rel(wrow[16]), "end per wave", [rel(v) for v in wrow[1:16]],
+              "| wave 0: meta", rel(wrow[17]), "keys", rel(wrow[19]), "T", rel(wrow[20]), "counts", rel(wrow[21]))
+        ws[BLKT_OFF + 768 * 32:BLKT_OFF + 800 * 32].zero_()
     ws[STAMP_OFF:STAMP_OFF + 16 * 8].zero_()
     if os.environ.get("XCD_EVERY"):  # per-call mean pass duration per XCD (blockIdx % 8), and the max block
         bt = ws[BLKT_OFF:BLKT_OFF + 256 * 32].cpu().numpy().view(np.uint64).astype(np.int64).reshape(256, 4)
