@@ -834,6 +834,22 @@ def _pypair():
     return _PYPAIR[0]
 
 
+_PYDELTA: list = []
+
+
+def _pydelta():
+    """fl_sim_amd._flcfold.stacked_delta_record (csrc/pyfold.cpp: the delta-fused stacked encode into a wire record and
+    the send count, one C call on Python lists of tensors) when built, else None."""
+    if not _PYDELTA:
+        try:
+            from . import _flcfold
+
+            _PYDELTA.append(_flcfold.stacked_delta_record)
+        except (ImportError, AttributeError):
+            _PYDELTA.append(None)
+    return _PYDELTA[0]
+
+
 def model_fold_server(theta: Sequence[torch.Tensor], aux: Sequence[torch.Tensor],
                       srcs: Sequence[Sequence[torch.Tensor]], weights: Sequence[float], kind: str, fold: bool = True,
                       init_mode: int = 0, inertia: float = 0.0, c: float = 0.0) -> None:

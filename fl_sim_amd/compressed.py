@@ -152,7 +152,7 @@ def _norm_stage_send(sd: Compressor, norm: torch.Tensor) -> float:
     """The norm compressor's pass over the one-element norm vector (compressors.py:334-337) and the send count it
     contributes; an identical norm compressor (the reference's usual one) is advanced without reading the norm back."""
     nc = sd.vectorNormCompressor
-    if isinstance(nc, Compressor) and nc.compressorType == CompressorType.IDENTICAL:
+    if _identical(nc):
         nc._finish(1, 1)
     else:
         nc.compressVector(np.array([np.float32(norm.item())]))
@@ -165,24 +165,60 @@ def compress_delta(local: Sequence[torch.Tensor], cached: Sequence[torch.Tensor]
     RNG stream and send statistics advance as its own ``compressVector`` call would advance them."""
     local = list(local)
     dev = local[0].device if local[0].is_cuda else torch.device("cuda", torch.cuda.current_device())
-    ls, gs = _fp32_on(local, dev), _fp32_on(cached, dev)
     shapes = [t.shape for t in local]
-    n = sum(t.numel() for t in ls)
+    n = sum(t.numel() for t in local)
     pipe = stacked_pipeline(compressors)
+    seed_ctr = None
+    if pipe is not None and 0 < pipe[0] < n and compressors[1].rng_mode == "philox":
+        # the common case in one C call, the tensors as they are (model parameters on the device): the record and the
+        # send count made by _flcfold.stacked_delta_record; a tensor it does not take (host-resident, not fp32 or not
+        # contiguous) falls through to the converted call below with the same Philox (seed, counter)
+        seed_ctr = compressors[1].philox.next()
+        r = _stacked_fast(local, cached, shapes, n, pipe[0], pipe[1], compressors[0], compressors[1], dev, seed_ctr)
+        if r is not None:
+            return r
+    ls, gs = _fp32_on(local, dev), _fp32_on(cached, dev)
     if pipe is not None and 0 < pipe[0] < n:
-        return _stacked(ls, gs, shapes, n, pipe[0], pipe[1], compressors[0], compressors[1], dev)
+        return _stacked(ls, gs, shapes, n, pipe[0], pipe[1], compressors[0], compressors[1], dev, seed_ctr)
     out = codec.delta_flatten(ls, gs)
     for comp in compressors:  # the drop-in compressors on the device, in order
         out = comp.compressVector(out)
     return CompressedDelta(shapes, dev, n, flat=out)
 
 
-def _stacked(ls, gs, shapes, n: int, K: int, s: int, tk: Compressor, sd: Compressor, dev) -> CompressedDelta:
+def _stacked_fast(local, cached, shapes, n: int, K: int, s: int, tk: Compressor, sd: Compressor, dev,
+                  seed_ctr) -> Optional[CompressedDelta]:
+    """The philox-mode stacked message in one C call (None: the extension is absent or a tensor needs converting)."""
+    fast = codec._pydelta()
+    if fast is None:
+        return None
+    stride, _ = codec.stacked_wire_layout(n, K)
+    rec = torch.empty(stride, dtype=torch.uint8, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    ws = codec.workspace(dev, codec._ws_size(dev, "flc_stacked_encode_delta_workspace_size", n, K, len(local)), "topk")
+    try:
+        fast(local, cached, K, s, seed_ctr[0], seed_ctr[1], rec, cnt, ws)
+    except TypeError:
+        return None  # (nothing launched)
+    codec._after_encode(dev)
+    tk._finish(n, tk.K)
+    nc = sd.vectorNormCompressor
+    base = _norm_stage_send(sd, None if _identical(nc) else codec.wire_packet(rec, n, K, s).norm)
+    sd._finish_pending(n, cnt, base, (1.0 + np.ceil(math.log2(sd.s))) / 32.0)  # compressors.py:365
+    return CompressedDelta(shapes, dev, n, record=rec, k=K, levels=s)
+
+
+def _identical(nc) -> bool:
+    return isinstance(nc, Compressor) and nc.compressorType == CompressorType.IDENTICAL
+
+
+def _stacked(ls, gs, shapes, n: int, K: int, s: int, tk: Compressor, sd: Compressor, dev,
+             seed_ctr=None) -> CompressedDelta:
     stride, _ = codec.stacked_wire_layout(n, K)
     rec = torch.empty(stride, dtype=torch.uint8, device=dev)
     pk = codec.wire_packet(rec, n, K, s)
     per = (1.0 + np.ceil(math.log2(sd.s))) / 32.0  # compressors.py:365
-    seed, ctr = sd.philox.next()
+    seed, ctr = seed_ctr if seed_ctr is not None else sd.philox.next()
     if sd.rng_mode == "philox":
         # the delta formed inside the encoder's read; the dithering stage's nonzero count stays on the device
         codec.stacked_encode_delta(ls, gs, K, s, seed, ctr, wire=rec)

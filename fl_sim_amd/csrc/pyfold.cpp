@@ -1,7 +1,9 @@
 // pyfold.cpp — `fl_sim_amd._flcfold.model_fold`: the server's whole-model fold (flc_model_fold) called straight from
 // Python lists of tensors, for the per-round host path of FedOptServer.update / avg_parameters / add_parameters /
 // update_gradients (_fedopt.py:196-240, nodes.py:1116-1180); `server_fold`, the same for FedDyn's and pFedMe's server
-// updates (flc_model_fold_server).
+// updates (flc_model_fold_server); `avg_and_gradients`, the variance-reduced servers' avg_parameters + update_gradients
+// (flc_avg_and_gradients); `stacked_delta_record`, a client's compressed message (flc_stacked_encode_delta into a wire
+// record + flc_delta_count_nonzero_at).
 //
 // At configs[0] (cnn_femmist_tiny: 8 tensors, 10 clients) the kernel takes ~9 us, but going through the dispatcher
 // (torch.ops.flcodec.model_fold_) cost ~14 us of host time: every tensor of the 96 in the call is boxed into an IValue
@@ -334,6 +336,99 @@ PyObject* avg_and_gradients(PyObject*, PyObject* args) {
   return done((Py_INCREF(Py_None), Py_None));
 }
 
+// a contiguous HIP tensor of `dt` on device `dev` (-1: any, returned); nullptr if not one
+const at::Tensor* usable_as(PyObject* o, at::ScalarType dt, int* dev) {
+  if (!THPVariable_Check(o)) return nullptr;
+  const at::Tensor& t = THPVariable_Unpack(o);
+  if (!t.is_cuda() || t.scalar_type() != dt || !t.is_contiguous()) return nullptr;
+  const int d = t.get_device();
+  if (*dev < 0) *dev = d;
+  else if (d != *dev) return nullptr;
+  return &t;
+}
+
+// stacked_delta_record(local, global, k, levels, seed, counter, record, count, ws): FedOptClient.communicate's delta
+// (_fedopt.py:295-308) through the stacked pipeline in one C call — flc_stacked_encode_delta of cat(local - global)
+// into the packed wire record `record` (a contiguous uint8 HIP tensor of at least flc_stacked_wire_layout(n, k) bytes,
+// 16-B aligned; the delta is formed in the encoder's read), then, with `count` (an int64 HIP tensor), the dithering
+// stage's send count (flc_delta_count_nonzero_at over the kept entries).  `ws`: the encoder's workspace (uint8).  The
+// same checks as model_fold: TypeError for a tensor the encoder does not take (the caller converts and retries),
+// ValueError for sizes.
+PyObject* stacked_delta_record(PyObject*, PyObject* args) {
+  PyObject *loc, *glo, *record, *count, *wso;
+  long long k;
+  int levels;
+  unsigned long long seed, counter;
+  if (!PyArg_ParseTuple(args, "OOLiKKOOO", &loc, &glo, &k, &levels, &seed, &counter, &record, &count, &wso))
+    return nullptr;
+  std::vector<PyObject*> keep;
+  auto done = [&](PyObject* r) {
+    for (PyObject* o : keep) Py_XDECREF(o);
+    return r;
+  };
+  PyObject* fl = PySequence_Fast(loc, "local must be a sequence of tensors");
+  if (!fl) return nullptr;
+  keep.push_back(fl);
+  PyObject* fg = PySequence_Fast(glo, "global must be a sequence of tensors");
+  if (!fg) return done(nullptr);
+  keep.push_back(fg);
+  const Py_ssize_t m = PySequence_Fast_GET_SIZE(fl);
+  if (m < 1 || PySequence_Fast_GET_SIZE(fg) != m) return done(value_error("one global tensor per local tensor, at least one"));
+  int dev = -1;
+  std::vector<const float*> lp(m), gp(m);
+  std::vector<int64_t> sz(m);
+  PyObject** li = PySequence_Fast_ITEMS(fl);
+  PyObject** gi = PySequence_Fast_ITEMS(fg);
+  int64_t n = 0;
+  for (Py_ssize_t t = 0; t < m; ++t) {
+    const at::Tensor* a = usable(li[t], &dev);
+    const at::Tensor* b = usable(gi[t], &dev);
+    if (!a || !b) return done(type_error("local / global tensors must be contiguous fp32 HIP tensors on one device"));
+    if (a->numel() != b->numel()) return done(value_error("local and global tensors must have matching sizes"));
+    lp[t] = a->data_ptr<float>();
+    gp[t] = b->data_ptr<float>();
+    sz[t] = a->numel();
+    n += sz[t];
+  }
+  const at::Tensor* rec = usable_as(record, at::kByte, &dev);
+  if (!rec) return done(type_error("the record must be a contiguous uint8 HIP tensor on the tensors' device"));
+  int64_t off[4] = {0, 0, 0, 0};  // norm, idx, codes, tiles
+  const size_t stride = flc_stacked_wire_layout(n, k, off);
+  uint8_t* rp = rec->data_ptr<uint8_t>();
+  if (stride == 0 || (size_t)rec->numel() < stride || reinterpret_cast<uintptr_t>(rp) % 16 != 0)
+    return done(value_error("the record is smaller than the wire layout or not 16-B aligned"));
+  int64_t* cp = nullptr;
+  if (count != Py_None) {
+    const at::Tensor* c = usable_as(count, at::kLong, &dev);
+    if (!c || c->numel() < 1) return done(type_error("count must be an int64 HIP tensor on the tensors' device"));
+    cp = c->data_ptr<int64_t>();
+  }
+  const at::Tensor* ws = usable_as(wso, at::kByte, &dev);
+  if (!ws) return done(type_error("ws must be a contiguous uint8 HIP tensor on the tensors' device"));
+  void* st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+  int32_t* idx = reinterpret_cast<int32_t*>(rp + off[1]);
+  int rc = FLC_OK;
+  const char* what = "flc_stacked_encode_delta";
+  Py_BEGIN_ALLOW_THREADS
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  rc = flc_stacked_encode_delta(lp.data(), gp.data(), sz.data(), (int)m, k, levels, seed, counter, idx, rp + off[2],
+                                reinterpret_cast<float*>(rp + off[0]), reinterpret_cast<uint32_t*>(rp + off[3]),
+                                ws->data_ptr(), (size_t)ws->numel(), st);
+  if (rc == FLC_OK && cp) {
+    what = "flc_delta_count_nonzero_at";
+    rc = flc_delta_count_nonzero_at(lp.data(), gp.data(), sz.data(), (int)m, idx, k, cp, st);
+  }
+  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  Py_END_ALLOW_THREADS
+  if (rc != FLC_OK) {
+    PyErr_Format(PyExc_RuntimeError, "%s failed with status %d: %s", what, rc, flc_last_error());
+    return done(nullptr);
+  }
+  return done((Py_INCREF(Py_None), Py_None));
+}
+
 void release_storage(void* ctx) { delete static_cast<c10::Storage*>(ctx); }
 
 // alias(host_tensor, device_index) -> tensor on cuda:device_index over the same bytes (see the header)
@@ -370,6 +465,9 @@ PyMethodDef kMethods[] = {
     {"avg_and_gradients", avg_and_gradients, METH_VARARGS,
      "avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia): flc_avg_and_gradients on Python lists of HIP "
      "tensors (messages: mappings with 'parameters' and 'gradients'), on the current stream of the model's device"},
+    {"stacked_delta_record", stacked_delta_record, METH_VARARGS,
+     "stacked_delta_record(local, global, k, levels, seed, counter, record, count, ws): flc_stacked_encode_delta into a "
+     "packed wire record (+ flc_delta_count_nonzero_at into count) on the current stream of the tensors' device"},
     {"alias", alias, METH_VARARGS,
      "alias(host_tensor, device_index): a HIP-device tensor over a pinned host tensor's memory (zero-copy)"},
     {nullptr, nullptr, 0, nullptr}};

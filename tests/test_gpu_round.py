@@ -316,3 +316,39 @@ def test_fold_records_rejects_bad_arguments():
         _lib.call("flc_fedopt_fold_records", (P * 1)(rec.data_ptr()), (ctypes.c_float * 1)(1.0), 1, n, k, 127,
                   (P * 1)(d.data_ptr()), (P * 1)(d.data_ptr()), None, (ctypes.c_int64 * 1)(n), 1, 0.0, 3, 1.0, 0.0,
                   0.0, None)
+
+
+def test_stacked_message_fast_path_equals_the_converted_path():
+    """Philox mode: the one-C-call message (_flcfold.stacked_delta_record on the parameters as they are) and the
+    converted path (a client whose parameters live on the host, or are non-contiguous / float64: the tensors copied to
+    contiguous fp32 device tensors first) give the same record, the same send statistics and the same Philox stream."""
+    from fl_sim_amd import codec
+    from fl_sim_amd.compressed import compress_delta
+
+    assert codec._pydelta() is not None, "the _flcfold extension must be built"
+    g = torch.Generator().manual_seed(11)
+    shapes = [(16, 1, 5, 5), (16,), (256, 37), (10,)]
+    glob = [torch.randn(sh, generator=g) for sh in shapes]
+    loc = [t + torch.randn(t.shape, generator=g) * 1e-2 for t in glob]
+    D = sum(t.numel() for t in glob)
+    forms = {
+        "device": ([t.cuda() for t in loc], [t.cuda() for t in glob]),
+        "host": (loc, [t.cuda() for t in glob]),
+        "noncontig": ([t.cuda() if i != 2 else t.cuda().t().contiguous().t() for i, t in enumerate(loc)],
+                      [t.cuda() for t in glob]),
+        "float64": ([t.double().cuda() for t in loc], [t.cuda() for t in glob]),
+    }
+    recs, stats = {}, {}
+    for name, (ls, gs) in forms.items():
+        comps = make_compressors("stacked10", D, rng="philox", seed=5)
+        d = compress_delta(ls, gs, comps)
+        pk = codec.wire_packet(d.record, D, d.k, d.levels)  # (the fields: a record's padding is never written)
+        recs[name] = np.concatenate([pk.norm.cpu().numpy().view(np.uint8), pk.idx.cpu().numpy().view(np.uint8),
+                                     pk.codes[:d.k].cpu().numpy(), pk.tiles.cpu().numpy().view(np.uint8)])
+        stats[name] = (comps[0].total_input_components, comps[0].really_need_to_send_components,
+                       comps[1].total_input_components, comps[1].really_need_to_send_components,
+                       comps[1].last_need_to_send_advance, comps[1].philox.counter)
+    assert not forms["noncontig"][0][2].is_contiguous()
+    for name in ("host", "noncontig", "float64"):  # (the float64 copies of fp32 values convert back exactly)
+        assert np.array_equal(recs[name], recs["device"]), name
+        assert stats[name] == stats["device"], name
