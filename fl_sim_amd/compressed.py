@@ -194,7 +194,7 @@ def _stacked_fast(local, cached, shapes, n: int, K: int, s: int, tk: Compressor,
         return None
     stride, _ = codec.stacked_wire_layout(n, K)
     rec = torch.empty(stride, dtype=torch.uint8, device=dev)
-    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    cnt = sd._count_slot(dev)
     ws = codec.workspace(dev, codec._ws_size(dev, "flc_stacked_encode_delta_workspace_size", n, K, len(local)), "topk")
     try:
         fast(local, cached, K, s, seed_ctr[0], seed_ctr[1], rec, cnt, ws)
@@ -222,7 +222,7 @@ def _stacked(ls, gs, shapes, n: int, K: int, s: int, tk: Compressor, sd: Compres
     if sd.rng_mode == "philox":
         # the delta formed inside the encoder's read; the dithering stage's nonzero count stays on the device
         codec.stacked_encode_delta(ls, gs, K, s, seed, ctr, wire=rec)
-        cnt = torch.empty(1, dtype=torch.int64, device=dev)
+        cnt = sd._count_slot(dev)
         _lib.call("flc_delta_count_nonzero_at", _ptrs(ls), _ptrs(gs),
                   (ctypes.c_int64 * len(ls))(*[t.numel() for t in ls]), len(ls), pk.idx.data_ptr(), K,
                   cnt.data_ptr(), codec._stream(dev))

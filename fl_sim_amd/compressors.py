@@ -190,15 +190,33 @@ class Compressor:
     # send statistics (compressors.py:40-43, 406-408).  A compressed client round in philox mode (compressed.py) leaves
     # the dithering stage's count of nonzero inputs on the device instead of synchronising for it; the counts of up to
     # 64 calls wait there and are folded into the counters, in call order with the reference's arithmetic
-    # (base + nnz * per per call), the first time one of them is read (one device-to-host copy for all of them).
+    # (base + nnz * per per call), the first time one of them is read (one device-to-host copy for all of them).  The
+    # counts are written into consecutive slots of one device slab per compressor (_count_slot), so the fold reads
+    # them with a single copy of the slab's prefix.
     _kMaxPending = 64
+
+    def _count_slot(self, dev) -> torch.Tensor:
+        """The one-element int64 device slot for the next pending send count (see _finish_pending)."""
+        pend = self.__dict__.get("_pending") or []
+        slab = self.__dict__.get("_slab")
+        if len(pend) >= self._kMaxPending or (slab is not None and slab.device != dev):
+            self._flush()  # (reads the slab back, so its slots are free again)
+            pend = []
+        if slab is None or slab.device != dev:
+            slab = torch.empty(self._kMaxPending, dtype=torch.int64, device=dev)
+            self._slab = slab
+        return slab[len(pend):len(pend) + 1]
 
     def _flush(self) -> None:
         p = self.__dict__.get("_pending")
         if p:
             self._pending = None
             cs = [c for c, _, _ in p]
-            if len(cs) > 1 and all(c.device == cs[0].device for c in cs):
+            slab = self.__dict__.get("_slab")
+            if slab is not None and all(c.device == slab.device and c.data_ptr() == slab.data_ptr() + 8 * i
+                                        for i, c in enumerate(cs)):
+                nnzs = [int(v) for v in slab[:len(cs)].tolist()]  # the counts in their slots, in call order
+            elif len(cs) > 1 and all(c.device == cs[0].device for c in cs):
                 nnzs = [int(v) for v in torch.cat([c.reshape(-1) for c in cs]).tolist()]
             else:
                 nnzs = [int(c.item()) for c in cs]

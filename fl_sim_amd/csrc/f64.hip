@@ -1054,7 +1054,9 @@ __global__ __launch_bounds__(kGT) void sel64_select_kernel(const double* __restr
         for (int i0 = 0; i0 < c; i0 += kWave) {  // (wave-uniform bounds)
           const int i = i0 + lane;
           const unsigned long long key = i < c ? order_key64(__longlong_as_double((long long)sc[i])) : 0ull;
-          const bool in = i < c && key >= lo_b && key - lo_b < wb;
+          // (and below t_hi: the band's top bin may reach past the ceiling — its width need not be a multiple of the
+          // bin width — and the keys above the ceiling were counted apart, in `above`, not in the bin)
+          const bool in = i < c && key >= lo_b && key - lo_b < wb && key < t_hi;
           const unsigned long long m = __ballot(in);
           if (m == 0ull) continue;
           const unsigned p = wave_append(&st->nbin, in, m);

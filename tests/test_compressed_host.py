@@ -94,3 +94,26 @@ def test_pending_send_statistics_of_many_calls_fold_in_call_order():
     assert a.total_input_components == b.total_input_components
     assert a.really_need_to_send_components == b.really_need_to_send_components
     assert a.last_need_to_send_advance == b.last_need_to_send_advance
+
+
+def test_pending_counts_in_slab_slots_fold_in_call_order():
+    """The counts written into the compressor's slab slots (_count_slot, as compressed.py's philox path writes them)
+    fold in exactly as counts finished one at a time, across slab refills; a slot handed out but never finished (a
+    call that fell through to another path) is handed out again."""
+    per = 5.0 / 32.0
+    cpu = torch.device("cpu")
+    counts = [7, 0, 3] + list(range(140))
+    a, b = _std(10, np.inf), _std(10, np.inf)
+    for i, cnt in enumerate(counts):
+        slot = a._count_slot(cpu)
+        if i == 5:
+            assert a._count_slot(cpu).data_ptr() == slot.data_ptr()  # (unfinished: the same slot again)
+        slot.fill_(cnt)
+        a._finish_pending(100, slot, 1, per)
+        b._finish(100, 1 + cnt * per if cnt else 1)
+        if i == 70:
+            assert a.last_need_to_send_advance == b.last_need_to_send_advance  # a read mid-slab frees the slots
+    assert len(a.__dict__.get("_pending") or []) <= 64
+    assert a.total_input_components == b.total_input_components
+    assert a.really_need_to_send_components == b.really_need_to_send_components
+    assert a.last_need_to_send_advance == b.last_need_to_send_advance

@@ -236,6 +236,35 @@ def test_f64_topk_filter_fallbacks():
     assert g64.same_bits(codec.topk_dense_f64(torch.from_numpy(z).to(DEV), K).cpu().numpy(), exp)
 
 
+def test_f64_topk_band_top_bin_past_the_ceiling():
+    """The band's top histogram bin can reach past the ceiling t_hi (the band's width need not be a multiple of the
+    bin width); the keys above the ceiling were counted apart and must not enter the K-th largest's bin list.  Built
+    around the sample (positions (j + 0.5) n / S): at k = 10 % the ceiling's sample rank is 1460 and the floor's 1817
+    (f64.hip filt64), so 1459 sampled A = 1.5 + 2^-12, 350 B = 1.5 and 100 C = 0.75 put the ceiling just above B (its
+    24-bit key prefix + 1, where A's keys start) and the floor on C: a band 4097 prefix units wide, binned by 4, whose
+    top bin holds B (the K-th largest's, 10,000 ties) and A (100,000 keys above the ceiling).  Before the fix the
+    list took A's keys too and T came out wrong."""
+    from fl_sim_amd import codec
+
+    n, S = 1 << 20, 16384
+    spos = ((np.arange(S) + 0.5) * n / S).astype(np.int64)
+    g = np.random.default_rng(11)
+    x = g.random(n) * 0.1
+    A, B, C = 1.5 + 2.0 ** -12, 1.5, 0.75
+    x[spos[:1459]] = A
+    x[spos[1459:1809]] = B
+    x[spos[1809:1909]] = C
+    free = g.permutation(np.setdiff1d(np.arange(n), spos))
+    na, nb = 100_000 - 1459, 10_000 - 350
+    x[free[:na]] = A
+    x[free[na:na + nb]] = B
+    K = n // 10  # 100,000 A < K <= 110,000 A + B: the K-th largest is a B
+    exp, _ = ref.topk(x, K)
+    got = codec.topk_dense_f64(torch.from_numpy(x).to(DEV), K).cpu().numpy()
+    assert g64.same_bits(got, exp)
+    assert sum(codec.topk_status_all().values()) == 0
+
+
 @pytest.mark.parametrize("n_ties", [3, 5000, 16384, 16385, 100_000])
 def test_f64_topk_ties_of_the_kth_value(n_ties):
     """The K-th largest value repeated n_ties times at random positions, k cutting through the ties: the band's bin

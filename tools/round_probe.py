@@ -79,6 +79,27 @@ def main():
         torch.cuda.synchronize()
         tot = (time.perf_counter() - t0) / 20
         print(f"{name}: host enqueue {host * 1e6:.1f} us, synchronised {tot * 1e6:.1f} us")
+    # amortised over 64 rounds with every client's send statistics read at the end (the pending counts folded in):
+    # the slab slots against one fresh count tensor per call (the torch.cat read-back)
+    def rounds64():
+        for _ in range(64):
+            round_()
+        for c in clients:
+            c.compressors[1].really_need_to_send_components
+
+    slot = Compressor._count_slot
+    for name, fn in (("slab", slot), ("per-call tensors", lambda self, dev: torch.empty(1, dtype=torch.int64,
+                                                                                          device=dev)),
+                     ("slab", slot)):
+        Compressor._count_slot = fn
+        rounds64()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            rounds64()
+        torch.cuda.synchronize()
+        print(f"64 rounds + statistics read, {name}: {(time.perf_counter() - t0) / 192 * 1e6:.1f} us per round")
+    Compressor._count_slot = slot
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(20):
