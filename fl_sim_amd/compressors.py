@@ -205,10 +205,23 @@ class Compressor:
         if slab is None or slab.device != dev:
             slab = torch.empty(self._kMaxPending, dtype=torch.int64, device=dev)
             self._slab = slab
+        if slab.is_cuda:  # the streams the slots are written on (the read-back waits for each)
+            ws = self.__dict__.get("_slab_streams") or []
+            cs = torch.cuda.current_stream(slab.device)
+            if cs not in ws:
+                self._slab_streams = ws + [cs]
         return slab[len(pend):len(pend) + 1]
 
     def _flush(self) -> None:
         p = self.__dict__.get("_pending")
+        ws = self.__dict__.get("_slab_streams")
+        if ws:
+            self._slab_streams = None
+            if p:  # counts written on another stream than the one reading them back: order the read after them
+                cur = torch.cuda.current_stream(ws[0].device)
+                for w in ws:
+                    if w != cur:
+                        cur.wait_stream(w)
         if p:
             self._pending = None
             cs = [c for c, _, _ in p]

@@ -352,3 +352,35 @@ def test_stacked_message_fast_path_equals_the_converted_path():
     for name in ("host", "noncontig", "float64"):  # (the float64 copies of fp32 values convert back exactly)
         assert np.array_equal(recs[name], recs["device"]), name
         assert stats[name] == stats["device"], name
+
+
+def test_pending_send_counts_written_on_side_streams_read_on_another():
+    """Philox-mode messages made on side streams (their send counts left in the compressor's device slab) and the
+    statistics read on the default stream: the read-back waits for the streams that wrote the counts, so the totals
+    equal those of the same messages made on the default stream."""
+    from fl_sim_amd.compressed import compress_delta
+
+    g = torch.Generator().manual_seed(12)
+    shapes = [(64, 3, 3), (4096,), (300, 77)]
+    glob = [torch.randn(sh, generator=g).cuda() for sh in shapes]
+    locs = [[t + torch.randn(t.shape, generator=g).cuda() * 1e-2 for t in glob] for _ in range(6)]
+    D = sum(t.numel() for t in glob)
+
+    def run(streams):
+        comps = make_compressors("stacked10", D, rng="philox", seed=9)
+        for i, ls in enumerate(locs):
+            s = streams[i % len(streams)] if streams else None
+            if s is None:
+                compress_delta(ls, glob, comps)
+            else:
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    big = torch.empty(1 << 26, device="cuda")  # (a long fill ahead of the count on that stream)
+                    big.fill_(1.0)
+                    compress_delta(ls, glob, comps)
+        return (comps[1].total_input_components, comps[1].really_need_to_send_components,
+                comps[1].last_need_to_send_advance)
+
+    ref = run(None)
+    got = run([torch.cuda.Stream(), torch.cuda.Stream()])
+    assert got == ref
