@@ -196,8 +196,8 @@ def update_gradients(model_params: Sequence[torch.Tensor], messages: Sequence[Ma
                 g = torch.empty(g0s[j].shape, dtype=g0s[j].dtype, device=d)
                 codec.weighted_sum(g, [_on(m["gradients"][j], d) for m in messages], weights, init_mode=1)
                 grads.append(g)
-    for mp, g in zip(model_params, grads):
-        if isinstance(mp, torch.Tensor) and mp.requires_grad:
+    for mp, g in zip(model_params, grads):  # (every parameter, frozen ones too: nodes.py:1171-1172 sets them all)
+        if isinstance(mp, torch.Tensor):
             mp.grad = g
     return grads
 
@@ -284,6 +284,14 @@ def avg_parameters_and_gradients(model_params: Sequence[torch.Tensor], messages:
             grads.append(host[off:off + g.numel()].view(g.shape))
             off += g.numel()
     else:
+        fast = codec._pypair()
+        if fast is not None and mps and isinstance(mps[0], torch.Tensor) and mps[0].is_cuda:
+            # one C call: the fold, the gradients' buffer and views, and every parameter's `.grad`; a TypeError (a
+            # tensor the launch does not take, or messages elsewhere) leaves everything untouched
+            try:
+                return fast(mps, None, messages, wp, wg, float(inertia), True)[0]
+            except TypeError:
+                pass
         ps = _params(mps)
         r = _pair_fold(ps[0].device, ps, messages, wp, wg, inertia) if ps and ps[0].is_cuda else None
         if r is None:
@@ -600,12 +608,15 @@ class VRUpdateMixin:
         if self.record_communicated_clients:  # fedpd/_fedpd.py:198
             self._communicated_clients = [m["client_id"] for m in self._received_messages]
         inertia = 1 - self.config.beta if self.vr_inertia_from_beta else 0.0
-        keys = ["parameters"] + (["gradients"] if self.config.vr else [])
-        _adopt([list(self.model.parameters())], [m[k] for m in self._received_messages for k in keys])
+        mps = list(self.model.parameters())
+        if hoststage.is_host(mps):
+            keys = ["parameters"] + (["gradients"] if self.config.vr else [])
+            _adopt([mps], [m[k] for m in self._received_messages for k in keys])
+            mps = list(self.model.parameters())  # (the adopted tensors)
         if self.config.vr:
-            avg_parameters_and_gradients(list(self.model.parameters()), self._received_messages, inertia=inertia)
+            avg_parameters_and_gradients(mps, self._received_messages, inertia=inertia)
         else:
-            avg_parameters(list(self.model.parameters()), self._received_messages, inertia=inertia)
+            avg_parameters(mps, self._received_messages, inertia=inertia)
 
 
 class FedProxUpdateMixin(VRUpdateMixin):

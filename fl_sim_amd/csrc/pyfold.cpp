@@ -249,20 +249,26 @@ PyObject* server_fold(PyObject*, PyObject* args) {
   return done((Py_INCREF(Py_None), Py_None));
 }
 
-// avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia): flc_avg_and_gradients (avg_parameters then
-// update_gradients over the same messages, nodes.py:1134-1180) on Python lists: `params` folded in place, `grads` (one
-// per parameter, same sizes) written from +0; every message a mapping with "parameters" and "gradients".  The same
-// checks and errors as model_fold; any number of messages (the C call chains them).
+// avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia[, set_grad]): flc_avg_and_gradients
+// (avg_parameters then update_gradients over the same messages, nodes.py:1134-1180) on Python lists: `params` folded
+// in place, `grads` (one per parameter, same sizes) written from +0; every message a mapping with "parameters" and
+// "gradients".  `grads` None: the gradients go into one new flat fp32 buffer on the model's device, returned as
+// (list of per-parameter views, flat buffer), and with `set_grad` each parameter's `.grad` is set to its view (as
+// update_gradients' `mp.grad = ...`) — the per-update Python work of the device-resident variance-reduced servers
+// (views, `.grad` setters) done here.  The same checks and errors as model_fold, all before anything is allocated or
+// launched; any number of messages (the C call chains them).
 PyObject* avg_and_gradients(PyObject*, PyObject* args) {
   PyObject *params, *grads, *msgs, *wpar, *wgrd;
   double inertia;
-  if (!PyArg_ParseTuple(args, "OOOOOd", &params, &grads, &msgs, &wpar, &wgrd, &inertia)) return nullptr;
+  int set_grad = 0;
+  if (!PyArg_ParseTuple(args, "OOOOOd|p", &params, &grads, &msgs, &wpar, &wgrd, &inertia, &set_grad)) return nullptr;
   std::vector<PyObject*> keep;
   auto done = [&](PyObject* r) {
     for (PyObject* o : keep) Py_XDECREF(o);
     return r;
   };
-  PyObject* seqs[5] = {params, grads, msgs, wpar, wgrd};
+  const bool alloc = grads == Py_None;
+  PyObject* seqs[5] = {params, alloc ? params : grads, msgs, wpar, wgrd};
   PyObject* f[5];
   for (int i = 0; i < 5; ++i) {
     f[i] = PySequence_Fast(seqs[i], "avg_and_gradients takes sequences");
@@ -278,13 +284,16 @@ PyObject* avg_and_gradients(PyObject*, PyObject* args) {
   int dev = -1;
   std::vector<float*> pp(nt), gp(nt);
   std::vector<int64_t> sz(nt);
+  std::vector<const at::Tensor*> pt(nt);
   PyObject** pi = PySequence_Fast_ITEMS(f[0]);
   PyObject** gi = PySequence_Fast_ITEMS(f[1]);
   for (Py_ssize_t t = 0; t < nt; ++t) {
     const at::Tensor* a = usable(pi[t], &dev);
     if (!a) return done(type_error("model tensors must be contiguous fp32 HIP tensors on one device"));
+    pt[t] = a;
     pp[t] = a->data_ptr<float>();
     sz[t] = a->numel();
+    if (alloc) continue;
     const at::Tensor* b = usable(gi[t], &dev);
     if (!b) return done(type_error("gradient buffers must be contiguous fp32 HIP tensors on the model's device"));
     if (b->numel() != sz[t]) return done(value_error("gradient buffers must match the model tensors' sizes"));
@@ -319,6 +328,26 @@ PyObject* avg_and_gradients(PyObject*, PyObject* args) {
       }
     }
   }
+  // (every tensor checked: the gradient buffer, when asked for, is allocated now)
+  at::Tensor flat;
+  std::vector<at::Tensor> gv;
+  if (alloc) {
+    int64_t total = 0;
+    for (Py_ssize_t t = 0; t < nt; ++t) total += sz[t];
+    try {
+      flat = at::empty({total > 0 ? total : 1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
+    } catch (const std::exception& e) {
+      PyErr_SetString(PyExc_RuntimeError, e.what());
+      return done(nullptr);
+    }
+    gv.reserve(nt);
+    int64_t off = 0;
+    for (Py_ssize_t t = 0; t < nt; ++t) {
+      gv.push_back(flat.narrow(0, off, sz[t]).view(pt[t]->sizes()));
+      gp[t] = flat.data_ptr<float>() + off;
+      off += sz[t];
+    }
+  }
   void* st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
   int rc = FLC_OK;
   Py_BEGIN_ALLOW_THREADS
@@ -333,7 +362,24 @@ PyObject* avg_and_gradients(PyObject*, PyObject* args) {
     PyErr_Format(PyExc_RuntimeError, "flc_avg_and_gradients failed with status %d: %s", rc, flc_last_error());
     return done(nullptr);
   }
-  return done((Py_INCREF(Py_None), Py_None));
+  if (!alloc) return done((Py_INCREF(Py_None), Py_None));
+  PyObject* lst = PyList_New(nt);
+  if (!lst) return done(nullptr);
+  for (Py_ssize_t t = 0; t < nt; ++t) {
+    if (set_grad) pt[t]->mutable_grad() = gv[t];  // (update_gradients' `mp.grad = ...`: same device, dtype, sizes)
+    PyObject* w = THPVariable_Wrap(gv[t]);
+    if (!w) {
+      Py_DECREF(lst);
+      return done(nullptr);
+    }
+    PyList_SET_ITEM(lst, t, w);
+  }
+  PyObject* fl = THPVariable_Wrap(flat);
+  if (!fl) {
+    Py_DECREF(lst);
+    return done(nullptr);
+  }
+  return done(Py_BuildValue("(NN)", lst, fl));
 }
 
 // a contiguous HIP tensor of `dt` on device `dev` (-1: any, returned); nullptr if not one
@@ -463,7 +509,8 @@ PyMethodDef kMethods[] = {
      "server_fold(theta, aux, msgs, key, weights, kind, fold, init_mode, inertia, c): flc_model_fold_server (FedDyn / "
      "pFedMe) on Python lists of HIP tensors, at most 16 messages, on the current stream of the model's device"},
     {"avg_and_gradients", avg_and_gradients, METH_VARARGS,
-     "avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia): flc_avg_and_gradients on Python lists of HIP "
+     "avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia[, set_grad]): flc_avg_and_gradients on Python "
+     "lists of HIP "
      "tensors (messages: mappings with 'parameters' and 'gradients'), on the current stream of the model's device"},
     {"stacked_delta_record", stacked_delta_record, METH_VARARGS,
      "stacked_delta_record(local, global, k, levels, seed, counter, record, count, ws): flc_stacked_encode_delta into a "

@@ -84,3 +84,27 @@ def test_avg_parameters_and_gradients_equals_the_two_calls(size_aware, inertia):
     gb = agg.update_gradients(b, msgs)
     for x, y in zip(a + ga, b + gb):
         assert gc.same_bits(x.cpu().numpy(), y.cpu().numpy())
+
+
+@pytest.mark.parametrize("kind", ["parameter", "tensor"])
+def test_avg_parameters_and_gradients_one_call_sets_grad(kind):
+    """Everything on the device: the one C call (the fold, the gradients' flat buffer and per-parameter views, every
+    `.grad` set in C++) against avg_parameters then update_gradients, on nn.Parameters and on plain tensors."""
+    from fl_sim_amd import aggregation as agg
+
+    g = torch.Generator().manual_seed(6)
+    shapes = [(16, 1, 5, 5), (16,), (256, 37), (10,)]
+    th = [torch.randn(s, generator=g).cuda() for s in shapes]
+    msgs = [{"parameters": [t + torch.randn(t.shape, generator=g).cuda() * 1e-2 for t in th],
+             "gradients": [torch.randn(t.shape, generator=g).cuda() for t in th], "train_samples": 7 * (i + 2)}
+            for i in range(12)]
+    make = (lambda t: torch.nn.Parameter(t.clone())) if kind == "parameter" else (lambda t: t.clone())
+    a, b = [make(t) for t in th], [make(t) for t in th]
+    ga = agg.avg_parameters_and_gradients(a, msgs, True, 0.2)
+    agg.avg_parameters(b, msgs, True, 0.2)
+    gb = agg.update_gradients(b, msgs)
+    for j, (x, y) in enumerate(zip(a, b)):
+        assert gc.same_bits(x.detach().cpu().numpy(), y.detach().cpu().numpy()), j
+        assert x.grad is not None and x.grad.shape == shapes[j] and x.grad.data_ptr() == ga[j].data_ptr()
+        assert gc.same_bits(x.grad.cpu().numpy(), y.grad.cpu().numpy()) and gc.same_bits(ga[j].cpu().numpy(),
+                                                                                           gb[j].cpu().numpy())
