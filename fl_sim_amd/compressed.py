@@ -315,8 +315,8 @@ class CompressedFedOptClientMixin:
     round of stacked records in one pass (or any reference server, which reads the message's delta unchanged)."""
 
     def communicate(self, target) -> None:
-        local = [p.detach() for p in self.model.parameters()]
-        delta = compress_delta(local, self._cached_parameters, _compressors_of(self))
+        # (the parameters as they are: the codec only reads them, and every converting path detaches first)
+        delta = compress_delta(list(self.model.parameters()), self._cached_parameters, _compressors_of(self))
         target._received_messages.append(
             client_message_class()(
                 **{
