@@ -180,6 +180,7 @@ SIGNATURES = {
                                       c_int, c_float, c_double, c_void_p]),
     "flc_delta_flatten": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "flc_delta_count_nonzero_at": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p]),
+    "flc_count_nonzero_at_batch": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "flc_feddr_combine": (
         c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_int, c_float, c_void_p]
     ),

@@ -835,6 +835,33 @@ def _pypair():
 
 
 _PYDELTA: list = []
+_PYFLAT: list = []
+_PYBATCH: list = []
+
+
+def _pyflat():
+    """fl_sim_amd._flcfold.delta_flat (a new flat delta, flc_delta_flatten, one C call) when built, else None."""
+    if not _PYFLAT:
+        try:
+            from . import _flcfold
+
+            _PYFLAT.append(_flcfold.delta_flat)
+        except (ImportError, AttributeError):
+            _PYFLAT.append(None)
+    return _PYFLAT[0]
+
+
+def _pybatch():
+    """fl_sim_amd._flcfold.stacked_records_batch (the batched stacked encode into a record block and the batched
+    send counts, one C call) when built, else None."""
+    if not _PYBATCH:
+        try:
+            from . import _flcfold
+
+            _PYBATCH.append(_flcfold.stacked_records_batch)
+        except (ImportError, AttributeError):
+            _PYBATCH.append(None)
+    return _PYBATCH[0]
 
 
 def _pydelta():

@@ -33,6 +33,7 @@ from __future__ import annotations
 import collections.abc as _abc
 import ctypes
 import math
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -77,14 +78,22 @@ class CompressedDelta(_abc.Sequence):
     a list of delta tensors reads it unchanged."""
 
     def __init__(self, shapes: Sequence[torch.Size], device: torch.device, n: int, *, record=None, k: int = 0,
-                 levels: int = 0, flat: Optional[torch.Tensor] = None):
+                 levels: int = 0, flat: Optional[torch.Tensor] = None, batch: Optional["_Batch"] = None):
         self.shapes = [torch.Size(s) for s in shapes]
         self.device = device
         self.n = int(n)
-        self.record, self.k, self.levels = record, int(k), int(levels)
-        self.kind = "stacked" if record is not None else "dense"
+        self._record, self.k, self.levels = record, int(k), int(levels)
+        self._batch = batch  # (a deferred encode: the record is made by the batch's launch on first access)
+        self.kind = "stacked" if record is not None or batch is not None else "dense"
         self._flat = flat
         self._views: Optional[List[torch.Tensor]] = None
+
+    @property
+    def record(self) -> Optional[torch.Tensor]:
+        """The packed wire record (stacked), or None (dense)."""
+        if self._batch is not None:
+            self._batch.run()
+        return self._record
 
     @property
     def nbytes(self) -> int:
@@ -174,6 +183,10 @@ def compress_delta(local: Sequence[torch.Tensor], cached: Sequence[torch.Tensor]
         # send count made by _flcfold.stacked_delta_record; a tensor it does not take (host-resident, not fp32 or not
         # contiguous) falls through to the converted call below with the same Philox (seed, counter)
         seed_ctr = compressors[1].philox.next()
+        if DEFER_ENCODE and n <= _DEFER_MAX_N and _identical(compressors[1].vectorNormCompressor):
+            r = _deferred(local, cached, shapes, n, pipe[0], pipe[1], compressors[0], compressors[1], dev, seed_ctr)
+            if r is not None:
+                return r
         r = _stacked_fast(local, cached, shapes, n, pipe[0], pipe[1], compressors[0], compressors[1], dev, seed_ctr)
         if r is not None:
             return r
@@ -184,6 +197,100 @@ def compress_delta(local: Sequence[torch.Tensor], cached: Sequence[torch.Tensor]
     for comp in compressors:  # the drop-in compressors on the device, in order
         out = comp.compressVector(out)
     return CompressedDelta(shapes, dev, n, flat=out)
+
+
+# Deferred encodes (philox mode, the stacked pipeline, an identical norm compressor, models up to 16 M parameters).
+# A model-sized encode is all fixed latency on the GPU — ~44 us per message at configs[0] (417,482 parameters), most of
+# it the persistent select's grid exchanges — so a round's messages are encoded together: `communicate` flattens the
+# client's delta (a snapshot: the model may change before the encode runs) and fixes its Philox (seed, counter) and
+# send-count slot, and the first access to any of the round's records — or to a statistic of their compressors —
+# encodes them all in one launch (flc_stacked_encode_batch: each client's select on its share of the CUs, records
+# bit-identical to the per-message encodes) and counts their dithering stages' nonzero inputs in one more
+# (flc_count_nonzero_at_batch).  FLC_DEFER_ENCODE=0 encodes every message when it is made (the one-C-call form).
+DEFER_ENCODE = os.environ.get("FLC_DEFER_ENCODE", "1") != "0"
+_DEFER_MAX_N = 1 << 24
+_DEFER_MAX_PENDING = 64
+
+
+class _Batch:
+    """The waiting messages of one (device, n, k, levels, counter)."""
+
+    def __init__(self, key):
+        self.key = key
+        self.items = []  # (CompressedDelta, flat delta, seed, count slot, dithering compressor, stream)
+
+    def run(self) -> None:
+        if _PENDING.get(self.key) is self:
+            del _PENDING[self.key]
+        items, self.items = self.items, []
+        if not items:
+            return
+        di, n, k, levels, counter = self.key
+        dev = torch.device("cuda", di)
+        with torch.cuda.device(dev):
+            cur = torch.cuda.current_stream(dev)
+            for st in {it[5] for it in items}:  # (the deltas were flattened on these streams)
+                if st != cur:
+                    cur.wait_stream(st)
+            stride, off = codec.stacked_wire_layout(n, k)
+            C = len(items)
+            recs = torch.empty(C, stride, dtype=torch.uint8, device=dev)
+            flats = [it[1] for it in items]
+            fast = codec._pybatch()
+            if fast is not None:  # both launches in one C call
+                ws = codec.workspace(dev, codec._ws_size(dev, "flc_stacked_encode_batch_workspace_size", n, k, C),
+                                     "topk_batch")
+                fast(flats, [it[2] for it in items], counter, k, levels, recs, [it[3] for it in items], ws)
+            else:
+                codec.stacked_encode_batch(flats, k, levels, seeds=[it[2] for it in items], counter=counter,
+                                           wires=recs)
+                P = ctypes.c_void_p * C
+                _lib.call("flc_count_nonzero_at_batch", P(*[f.data_ptr() for f in flats]),
+                          P(*[recs[c].data_ptr() + off["idx"] for c in range(C)]), C, n, k,
+                          P(*[it[3].data_ptr() for it in items]), codec._stream(dev))
+            codec._after_encode(dev)
+            for (d, flat, _, _, sd, st), r in zip(items, recs.unbind(0)):
+                if st != cur:
+                    flat.record_stream(cur)
+                sd._note_slab_stream(cur)  # (the count was written on this stream)
+                d._record, d._batch = r, None
+
+
+_PENDING: dict = {}
+
+
+def _run_pending() -> None:
+    """Every deferred encode now (before a compressor's pending send counts are read)."""
+    for b in list(_PENDING.values()):
+        b.run()
+
+
+Compressor._before_read = staticmethod(_run_pending)
+
+
+def _deferred(local, cached, shapes, n: int, K: int, s: int, tk: Compressor, sd: Compressor, dev,
+              seed_ctr) -> Optional[CompressedDelta]:
+    snap = codec._pyflat()
+    try:
+        flat = snap(local, cached) if snap is not None else codec.delta_flatten(local, cached)
+    except TypeError:  # (host-resident, non-contiguous or non-fp32 tensors: converted first)
+        flat = codec.delta_flatten(_fp32_on(local, dev), _fp32_on(cached, dev))
+    if flat.device != dev:
+        return None
+    st = torch.cuda.current_stream(dev)
+    cnt = sd._count_slot(dev, st)  # (before the batch is looked up: a full slab is read back, running the batches)
+    key = (dev.index, n, K, s, seed_ctr[1])
+    b = _PENDING.get(key)
+    if b is None:
+        b = _PENDING[key] = _Batch(key)
+    d = CompressedDelta(shapes, dev, n, k=K, levels=s, batch=b)
+    b.items.append((d, flat, seed_ctr[0], cnt, sd, st))
+    tk._finish(n, tk.K)
+    base = _norm_stage_send(sd, None)
+    sd._finish_pending(n, cnt, base, (1.0 + np.ceil(math.log2(sd.s))) / 32.0)  # compressors.py:365
+    if len(b.items) >= _DEFER_MAX_PENDING:
+        b.run()
+    return d
 
 
 def _stacked_fast(local, cached, shapes, n: int, K: int, s: int, tk: Compressor, sd: Compressor, dev,

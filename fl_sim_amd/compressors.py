@@ -195,8 +195,9 @@ class Compressor:
     # them with a single copy of the slab's prefix.
     _kMaxPending = 64
 
-    def _count_slot(self, dev) -> torch.Tensor:
-        """The one-element int64 device slot for the next pending send count (see _finish_pending)."""
+    def _count_slot(self, dev, stream=None) -> torch.Tensor:
+        """The one-element int64 device slot for the next pending send count (see _finish_pending); ``stream``: the
+        current stream of ``dev`` when the caller has it."""
         pend = self.__dict__.get("_pending") or []
         slab = self.__dict__.get("_slab")
         if len(pend) >= self._kMaxPending or (slab is not None and slab.device != dev):
@@ -206,14 +207,20 @@ class Compressor:
             slab = torch.empty(self._kMaxPending, dtype=torch.int64, device=dev)
             self._slab = slab
         if slab.is_cuda:  # the streams the slots are written on (the read-back waits for each)
-            ws = self.__dict__.get("_slab_streams") or []
-            cs = torch.cuda.current_stream(slab.device)
-            if cs not in ws:
-                self._slab_streams = ws + [cs]
+            self._note_slab_stream(stream if stream is not None else torch.cuda.current_stream(slab.device))
         return slab[len(pend):len(pend) + 1]
+
+    _before_read = None  # compressed.py: runs the deferred encodes, which write their pending counts
+
+    def _note_slab_stream(self, st) -> None:
+        ws = self.__dict__.get("_slab_streams") or []
+        if st not in ws:
+            self._slab_streams = ws + [st]
 
     def _flush(self) -> None:
         p = self.__dict__.get("_pending")
+        if p and Compressor._before_read is not None:
+            Compressor._before_read()
         ws = self.__dict__.get("_slab_streams")
         if ws:
             self._slab_streams = None
@@ -270,6 +277,8 @@ class Compressor:
         self._pending = pend
 
     def resetStats(self):
+        if self.__dict__.get("_pending") and Compressor._before_read is not None:
+            Compressor._before_read()  # (deferred encodes write their counts before the slots are handed out again)
         self._pending = None
         self.total_input_components = 0
         self.really_need_to_send_components = 0

@@ -92,12 +92,58 @@ __global__ __launch_bounds__(kThreads) void delta_count_nonzero_kernel(TensorPac
   if ((threadIdx.x & (kWave - 1)) == 0 && b != 0ull) atomicAdd(count, (unsigned long long)__popcll(b));
 }
 
+// The same count for a round's clients at once (flc_count_nonzero_at_batch: the deferred compressed messages of
+// compressed.py, whose deltas were flattened when the messages were made): client c = blockIdx.y counts the nonzero
+// x_c[idx_c[j]]; the counts are zeroed by a one-wave launch ahead of it (stream-ordered).
+constexpr int kMaxCount = 32;  // clients per launch (kernel-argument budget)
+struct CountPack {
+  const float* x[kMaxCount];
+  const int32_t* idx[kMaxCount];
+  unsigned long long* out[kMaxCount];
+  int nc;
+};
+
+__global__ __launch_bounds__(kWave) void zero_counts_kernel(CountPack p) {
+  if ((int)threadIdx.x < p.nc) *p.out[threadIdx.x] = 0ull;
+}
+
+__global__ __launch_bounds__(kThreads) void count_nonzero_at_batch_kernel(CountPack p, int64_t k) {
+  const int c = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool nz = j < k && !(p.x[c][p.idx[c][j]] == 0.0f);  // (a NaN counts, as for the fused form)
+  const unsigned long long b = __ballot(nz);
+  if ((threadIdx.x & (kWave - 1)) == 0 && b != 0ull) atomicAdd(p.out[c], (unsigned long long)__popcll(b));
+}
+
 }  // namespace
 }  // namespace flc
 
 using namespace flc;
 
 extern "C" {
+
+int flc_count_nonzero_at_batch(const float* const* xs, const int32_t* const* idx, int n_clients, int64_t n,
+                               int64_t k, int64_t* const* counts, void* stream) {
+  if (n_clients < 0 || (n_clients > 0 && (!xs || !idx || !counts)) || n <= 0 || k < 0 || k > n)
+    return fail(FLC_EINVAL, "flc_count_nonzero_at_batch: bad arguments");
+  hipStream_t st = as_stream(stream);
+  for (int c0 = 0; c0 < n_clients; c0 += kMaxCount) {
+    CountPack p{};
+    p.nc = std::min(n_clients - c0, kMaxCount);
+    for (int c = 0; c < p.nc; ++c) {
+      if (!xs[c0 + c] || !counts[c0 + c] || (k > 0 && !idx[c0 + c]))
+        return fail(FLC_EINVAL, "flc_count_nonzero_at_batch: null pointer for client %d", c0 + c);
+      p.x[c] = xs[c0 + c];
+      p.idx[c] = idx[c0 + c];
+      p.out[c] = reinterpret_cast<unsigned long long*>(counts[c0 + c]);
+    }
+    FLC_LAUNCH("zero_counts", zero_counts_kernel, dim3(1), dim3(kWave), 0, st, p);
+    if (k > 0)
+      FLC_LAUNCH("count_nonzero_at_batch", count_nonzero_at_batch_kernel,
+                 dim3((unsigned)cdiv(k, kThreads), (unsigned)p.nc), dim3(kThreads), 0, st, p, k);
+  }
+  return FLC_OK;
+}
 
 int flc_delta_flatten(const float* const* local, const float* const* global, const int64_t* sizes, int n_tensors,
                       float* out, void* stream) {

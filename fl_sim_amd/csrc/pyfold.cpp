@@ -475,6 +475,158 @@ PyObject* stacked_delta_record(PyObject*, PyObject* args) {
   return done((Py_INCREF(Py_None), Py_None));
 }
 
+// delta_flat(local, global): a new flat fp32 tensor = cat(local_t - global_t) (flc_delta_flatten) on the tensors'
+// device — the deferred compressed message's snapshot of its delta (compressed.py).  TypeError (nothing allocated)
+// for a tensor that is not a contiguous fp32 HIP tensor of one device.
+PyObject* delta_flat(PyObject*, PyObject* args) {
+  PyObject *loc, *glo;
+  if (!PyArg_ParseTuple(args, "OO", &loc, &glo)) return nullptr;
+  std::vector<PyObject*> keep;
+  auto done = [&](PyObject* r) {
+    for (PyObject* o : keep) Py_XDECREF(o);
+    return r;
+  };
+  PyObject* fl = PySequence_Fast(loc, "local must be a sequence of tensors");
+  if (!fl) return nullptr;
+  keep.push_back(fl);
+  PyObject* fg = PySequence_Fast(glo, "global must be a sequence of tensors");
+  if (!fg) return done(nullptr);
+  keep.push_back(fg);
+  const Py_ssize_t m = PySequence_Fast_GET_SIZE(fl);
+  if (m < 1 || PySequence_Fast_GET_SIZE(fg) != m) return done(value_error("one global tensor per local tensor, at least one"));
+  int dev = -1;
+  std::vector<const float*> lp(m), gp(m);
+  std::vector<int64_t> sz(m);
+  PyObject** li = PySequence_Fast_ITEMS(fl);
+  PyObject** gi = PySequence_Fast_ITEMS(fg);
+  int64_t n = 0;
+  for (Py_ssize_t t = 0; t < m; ++t) {
+    const at::Tensor* a = usable(li[t], &dev);
+    const at::Tensor* b = usable(gi[t], &dev);
+    if (!a || !b) return done(type_error("local / global tensors must be contiguous fp32 HIP tensors on one device"));
+    if (a->numel() != b->numel()) return done(value_error("local and global tensors must have matching sizes"));
+    lp[t] = a->data_ptr<float>();
+    gp[t] = b->data_ptr<float>();
+    sz[t] = a->numel();
+    n += sz[t];
+  }
+  at::Tensor out;
+  try {
+    out = at::empty({n > 0 ? n : 1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return done(nullptr);
+  }
+  if (n == 0) out = out.narrow(0, 0, 0);
+  void* st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+  int rc = FLC_OK;
+  float* op = out.data_ptr<float>();
+  Py_BEGIN_ALLOW_THREADS
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  rc = flc_delta_flatten(lp.data(), gp.data(), sz.data(), (int)m, op, st);
+  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  Py_END_ALLOW_THREADS
+  if (rc != FLC_OK) {
+    PyErr_Format(PyExc_RuntimeError, "flc_delta_flatten failed with status %d: %s", rc, flc_last_error());
+    return done(nullptr);
+  }
+  return done(THPVariable_Wrap(out));
+}
+
+// stacked_records_batch(flats, seeds, counter, k, levels, records, counts, ws): the deferred messages of a round in
+// one C call — flc_stacked_encode_batch of the flat deltas into rows of the [C, >= stride] record block (row c equals
+// client c's one-message record), then flc_count_nonzero_at_batch of each delta at its kept indices into counts[c].
+PyObject* stacked_records_batch(PyObject*, PyObject* args) {
+  PyObject *flats, *seeds, *recs, *counts, *wso;
+  unsigned long long counter;
+  long long k;
+  int levels;
+  if (!PyArg_ParseTuple(args, "OOKLiOOO", &flats, &seeds, &counter, &k, &levels, &recs, &counts, &wso)) return nullptr;
+  std::vector<PyObject*> keep;
+  auto done = [&](PyObject* r) {
+    for (PyObject* o : keep) Py_XDECREF(o);
+    return r;
+  };
+  PyObject* seqs[3] = {flats, seeds, counts};
+  PyObject* f[3];
+  for (int i = 0; i < 3; ++i) {
+    f[i] = PySequence_Fast(seqs[i], "stacked_records_batch takes sequences");
+    if (!f[i]) return done(nullptr);
+    keep.push_back(f[i]);
+  }
+  const Py_ssize_t C = PySequence_Fast_GET_SIZE(f[0]);
+  if (C < 1 || PySequence_Fast_GET_SIZE(f[1]) != C || PySequence_Fast_GET_SIZE(f[2]) != C)
+    return done(value_error("one seed and one count per client, at least one client"));
+  int dev = -1;
+  int64_t n = -1;
+  std::vector<const float*> xp(C);
+  std::vector<uint64_t> sd(C);
+  std::vector<int64_t*> cp(C);
+  PyObject** xi = PySequence_Fast_ITEMS(f[0]);
+  PyObject** si = PySequence_Fast_ITEMS(f[1]);
+  PyObject** ci = PySequence_Fast_ITEMS(f[2]);
+  for (Py_ssize_t c = 0; c < C; ++c) {
+    const at::Tensor* x = usable(xi[c], &dev);
+    if (!x) return done(type_error("flat deltas must be contiguous fp32 HIP tensors on one device"));
+    if (n < 0) n = x->numel();
+    if (x->numel() != n) return done(value_error("flat deltas must all have one size"));
+    xp[c] = x->data_ptr<float>();
+    sd[c] = (uint64_t)PyLong_AsUnsignedLongLongMask(si[c]);
+    if (PyErr_Occurred()) return done(nullptr);
+    const at::Tensor* ct = usable_as(ci[c], at::kLong, &dev);
+    if (!ct || ct->numel() < 1) return done(type_error("counts must be int64 HIP tensors on the deltas' device"));
+    cp[c] = ct->data_ptr<int64_t>();
+  }
+  int64_t off[4] = {0, 0, 0, 0};  // norm, idx, codes, tiles
+  const size_t stride = flc_stacked_wire_layout(n, k, off);
+  if (stride == 0) return done(value_error("bad wire shape"));
+  if (!THPVariable_Check(recs)) return done(type_error("records must be a uint8 HIP tensor"));
+  const at::Tensor& rb = THPVariable_Unpack(recs);
+  if (!rb.is_cuda() || rb.get_device() != dev || rb.scalar_type() != at::kByte || rb.dim() != 2 || !rb.is_contiguous() ||
+      rb.size(0) != C || rb.size(1) < (int64_t)stride || rb.size(1) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(rb.data_ptr()) % 16 != 0)
+    return done(value_error("records must be a contiguous [clients, >= stride] uint8 block (16-B rows) on the device"));
+  const at::Tensor* ws = usable_as(wso, at::kByte, &dev);
+  if (!ws) return done(type_error("ws must be a contiguous uint8 HIP tensor on the deltas' device"));
+  uint8_t* base = rb.data_ptr<uint8_t>();
+  const int64_t rs = rb.size(1);
+  std::vector<int32_t*> ip(C);
+  std::vector<uint8_t*> kp(C);
+  std::vector<float*> np(C);
+  std::vector<uint32_t*> tp(C);
+  std::vector<const int32_t*> cip(C);
+  for (Py_ssize_t c = 0; c < C; ++c) {
+    uint8_t* r = base + c * rs;
+    np[c] = reinterpret_cast<float*>(r + off[0]);
+    ip[c] = reinterpret_cast<int32_t*>(r + off[1]);
+    cip[c] = ip[c];
+    kp[c] = r + off[2];
+    tp[c] = reinterpret_cast<uint32_t*>(r + off[3]);
+  }
+  void* st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+  int rc = FLC_OK;
+  const char* what = "flc_stacked_encode_batch";
+  Py_BEGIN_ALLOW_THREADS
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  rc = flc_stacked_encode_batch(xp.data(), (int)C, n, k, levels, sd.data(), counter, ip.data(), kp.data(), np.data(),
+                                tp.data(), ws->data_ptr(), (size_t)ws->numel(), st);
+  if (rc == FLC_OK) {
+    what = "flc_count_nonzero_at_batch";
+    rc = flc_count_nonzero_at_batch(xp.data(), cip.data(), (int)C, n, k, cp.data(), st);
+  }
+  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  Py_END_ALLOW_THREADS
+  if (rc != FLC_OK) {
+    PyErr_Format(PyExc_RuntimeError, "%s failed with status %d: %s", what, rc, flc_last_error());
+    return done(nullptr);
+  }
+  return done((Py_INCREF(Py_None), Py_None));
+}
+
 void release_storage(void* ctx) { delete static_cast<c10::Storage*>(ctx); }
 
 // alias(host_tensor, device_index) -> tensor on cuda:device_index over the same bytes (see the header)
@@ -512,6 +664,11 @@ PyMethodDef kMethods[] = {
      "avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia[, set_grad]): flc_avg_and_gradients on Python "
      "lists of HIP "
      "tensors (messages: mappings with 'parameters' and 'gradients'), on the current stream of the model's device"},
+    {"delta_flat", delta_flat, METH_VARARGS,
+     "delta_flat(local, global): a new flat fp32 tensor cat(local - global) (flc_delta_flatten) on the tensors' device"},
+    {"stacked_records_batch", stacked_records_batch, METH_VARARGS,
+     "stacked_records_batch(flats, seeds, counter, k, levels, records, counts, ws): flc_stacked_encode_batch into the "
+     "rows of a record block, then flc_count_nonzero_at_batch into counts"},
     {"stacked_delta_record", stacked_delta_record, METH_VARARGS,
      "stacked_delta_record(local, global, k, levels, seed, counter, record, count, ws): flc_stacked_encode_delta into a "
      "packed wire record (+ flc_delta_count_nonzero_at into count) on the current stream of the tensors' device"},

@@ -384,3 +384,54 @@ def test_pending_send_counts_written_on_side_streams_read_on_another():
     ref = run(None)
     got = run([torch.cuda.Stream(), torch.cuda.Stream()])
     assert got == ref
+
+
+def _record_fields(d):
+    from fl_sim_amd import codec
+
+    pk = codec.wire_packet(d.record, d.n, d.k, d.levels)  # (the fields: a record's padding is never written)
+    return np.concatenate([pk.norm.cpu().numpy().view(np.uint8), pk.idx.cpu().numpy().view(np.uint8),
+                           pk.codes[:d.k].cpu().numpy(), pk.tiles.cpu().numpy().view(np.uint8)])
+
+
+@pytest.mark.parametrize("n_msgs", [1, 7, 70])
+def test_deferred_round_encode_equals_the_immediate_encodes(n_msgs, monkeypatch):
+    """Deferred philox messages (each delta flattened when the message is made, the round's encodes in one batched
+    launch on first access) against the one-C-call encode per message: the same records, the same send statistics
+    and Philox streams — with every client's model changed in place right after its message was made (the snapshot),
+    two counters in one round (two batches), a statistic read mid-round (the batches run), a resetStats, and 70
+    messages (a batch runs itself at 64)."""
+    from fl_sim_amd import compressed
+
+    g = torch.Generator().manual_seed(13)
+    shapes = [(16, 1, 5, 5), (16,), (256, 37), (10,)]
+    glob = [torch.randn(sh, generator=g).cuda() for sh in shapes]
+    D = sum(t.numel() for t in glob)
+    locs = [[t + torch.randn(t.shape, generator=g).cuda() * 1e-2 for t in glob] for _ in range(n_msgs)]
+
+    def run(defer):
+        monkeypatch.setattr(compressed, "DEFER_ENCODE", defer)
+        comps = [make_compressors("stacked10", D, rng="philox", seed=100 + i) for i in range(n_msgs)]
+        for i in range(0, n_msgs, 3):  # (every third client's dithering stream one call ahead: a second counter)
+            comps[i][1].philox.next()
+        ls = [[t.clone() for t in loc] for loc in locs]
+        ds, seen = [], []
+        for i in range(n_msgs):
+            ds.append(compressed.compress_delta(ls[i], glob, comps[i]))
+            for t in ls[i]:
+                t.add_(1.0)  # (the model moves on: the message keeps the delta it was made from)
+            if i == n_msgs // 2:
+                seen.append(comps[0][1].really_need_to_send_components)  # (a read mid-round)
+            if i == 2:
+                comps[1][1].resetStats()
+        recs = [_record_fields(d) for d in ds]
+        stats = [(c[0].total_input_components, c[1].total_input_components, c[1].really_need_to_send_components,
+                  c[1].last_need_to_send_advance, c[1].philox.counter) for c in comps]
+        return recs, stats, seen
+
+    ra, sa, ma = run(True)
+    assert not compressed._PENDING
+    rb, sb, mb = run(False)
+    for i, (x, y) in enumerate(zip(ra, rb)):
+        assert np.array_equal(x, y), i
+    assert sa == sb and ma == mb

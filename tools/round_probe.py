@@ -88,7 +88,7 @@ def main():
             c.compressors[1].really_need_to_send_components
 
     slot = Compressor._count_slot
-    for name, fn in (("slab", slot), ("per-call tensors", lambda self, dev: torch.empty(1, dtype=torch.int64,
+    for name, fn in (("slab", slot), ("per-call tensors", lambda self, dev, *a: torch.empty(1, dtype=torch.int64,
                                                                                           device=dev)),
                      ("slab", slot)):
         Compressor._count_slot = fn
