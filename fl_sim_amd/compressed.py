@@ -225,6 +225,14 @@ class _Batch:
         items, self.items = self.items, []
         if not items:
             return
+        try:
+            self._encode(items)
+        except BaseException:
+            self.items = items + self.items  # (left pending: the next access tries again and raises again)
+            _PENDING.setdefault(self.key, self)
+            raise
+
+    def _encode(self, items) -> None:
         di, n, k, levels, counter = self.key
         dev = torch.device("cuda", di)
         with torch.cuda.device(dev):
