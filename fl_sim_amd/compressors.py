@@ -113,6 +113,15 @@ class Compressor:
         self.rng_mode = rng
         self.philox = _rng.PhiloxStream(seed)
 
+    def __getstate__(self):
+        """Copies and pickles carry the folded send statistics: the counts still pending on the device are read back
+        (running any deferred encode that writes them) and the per-process device slab is left behind."""
+        self._flush()
+        d = self.__dict__.copy()
+        for key in ("_slab", "_slab_streams"):
+            d.pop(key, None)
+        return d
+
     # ------------------------------------------------------------------ properties (compressors.py:58-132)
     @property
     def compressorName(self):

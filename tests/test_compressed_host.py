@@ -117,3 +117,29 @@ def test_pending_counts_in_slab_slots_fold_in_call_order():
     assert a.total_input_components == b.total_input_components
     assert a.really_need_to_send_components == b.really_need_to_send_components
     assert a.last_need_to_send_advance == b.last_need_to_send_advance
+
+
+def test_copies_and_pickles_carry_the_pending_send_statistics():
+    """A compressor with send counts still pending in its slab: a deep copy and a pickle round trip hold the folded
+    statistics (and no slab); the original keeps working."""
+    import copy
+    import pickle
+
+    per = 5.0 / 32.0
+    cpu = torch.device("cpu")
+    a, b = _std(10, np.inf), _std(10, np.inf)
+    for cnt in (4, 0, 9):
+        slot = a._count_slot(cpu)
+        slot.fill_(cnt)
+        a._finish_pending(100, slot, 1, per)
+        b._finish(100, 1 + cnt * per if cnt else 1)
+    for c in (copy.deepcopy(a), pickle.loads(pickle.dumps(a))):
+        assert "_slab" not in c.__dict__ and not c.__dict__.get("_pending")
+        assert c.really_need_to_send_components == b.really_need_to_send_components
+        assert c.last_need_to_send_advance == b.last_need_to_send_advance
+        assert c.total_input_components == b.total_input_components
+    slot = a._count_slot(cpu)
+    slot.fill_(2)
+    a._finish_pending(100, slot, 1, per)
+    b._finish(100, 1 + 2 * per)
+    assert a.really_need_to_send_components == b.really_need_to_send_components
