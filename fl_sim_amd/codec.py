@@ -837,6 +837,19 @@ def _pypair():
 _PYDELTA: list = []
 _PYFLAT: list = []
 _PYBATCH: list = []
+_PYRECS: list = []
+
+
+def _pyrecs():
+    """fl_sim_amd._flcfold.fold_records (flc_fedopt_fold_records on Python lists, one C call) when built, else None."""
+    if not _PYRECS:
+        try:
+            from . import _flcfold
+
+            _PYRECS.append(_flcfold.fold_records)
+        except (ImportError, AttributeError):
+            _PYRECS.append(None)
+    return _PYRECS[0]
 
 
 def _pyflat():

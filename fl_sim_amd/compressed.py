@@ -392,6 +392,16 @@ def fold_records(deltas: Sequence[CompressedDelta], weights: Sequence[float], de
     ``flc_fedopt_fold_records`` pass.  False (nothing launched) when the server tensors are not contiguous fp32 tensors
     of one HIP device holding the records' element count (the caller then takes the dense path)."""
     dps = list(delta_params)
+    d0 = deltas[0]
+    fast = codec._pyrecs()
+    if fast is not None and dps:
+        try:  # one C call: every tensor checked in place; TypeError: nothing launched, the checks below decide
+            fast([d.record for d in deltas], [float(w) for w in weights], d0.n, d0.k, d0.levels, dps,
+                 None if theta is None else list(theta), None if v is None else list(v), float(beta0),
+                 _lib.FLC_OPT[opt], float(lr), float(beta2), float(tau))
+            return True
+        except TypeError:
+            pass
     if not dps or not all(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype is torch.float32 and t.is_contiguous()
                           for t in dps):
         return False

@@ -627,6 +627,97 @@ PyObject* stacked_records_batch(PyObject*, PyObject* args) {
   return done((Py_INCREF(Py_None), Py_None));
 }
 
+// fold_records(records, weights, n, k, levels, delta, theta, v, beta0, opt, lr, beta2, tau): the server update of a
+// round of stacked records (flc_fedopt_fold_records) on Python lists.  TypeError (nothing launched) when a tensor is
+// not what the pass takes — the server tensors contiguous fp32 HIP tensors of one device summing to n, the records
+// 16-B aligned uint8 tensors of at least the wire layout's bytes on that device — so the caller can take its other
+// path; theta / v None: the fold alone / no second moment.
+PyObject* fold_records(PyObject*, PyObject* args) {
+  PyObject *recs, *weights, *delta, *theta, *v;
+  long long n, k;
+  int levels, opt;
+  double beta0, lr, beta2, tau;
+  if (!PyArg_ParseTuple(args, "OOLLiOOOdiddd", &recs, &weights, &n, &k, &levels, &delta, &theta, &v, &beta0, &opt, &lr,
+                        &beta2, &tau))
+    return nullptr;
+  std::vector<PyObject*> keep;
+  auto done = [&](PyObject* r) {
+    for (PyObject* o : keep) Py_XDECREF(o);
+    return r;
+  };
+  PyObject* seqs[3] = {recs, weights, delta};
+  PyObject* f[3];
+  for (int i = 0; i < 3; ++i) {
+    f[i] = PySequence_Fast(seqs[i], "fold_records takes sequences");
+    if (!f[i]) return done(nullptr);
+    keep.push_back(f[i]);
+  }
+  const Py_ssize_t nr = PySequence_Fast_GET_SIZE(f[0]), nt = PySequence_Fast_GET_SIZE(f[2]);
+  if (PySequence_Fast_GET_SIZE(f[1]) != nr) return done(value_error("one weight per record"));
+  if (nr < 1 || nt < 1) return done(type_error("fold_records needs records and server tensors"));
+  int dev = -1;
+  std::vector<float*> dp(nt), tp, vp;
+  std::vector<int64_t> sz(nt);
+  int64_t total = 0;
+  PyObject** di = PySequence_Fast_ITEMS(f[2]);
+  for (Py_ssize_t t = 0; t < nt; ++t) {
+    const at::Tensor* a = usable(di[t], &dev);
+    if (!a) return done(type_error("server tensors must be contiguous fp32 HIP tensors on one device"));
+    dp[t] = a->data_ptr<float>();
+    sz[t] = a->numel();
+    total += sz[t];
+  }
+  if (total != n) return done(type_error("the server tensors do not hold the records' element count"));
+  for (int which = 0; which < 2; ++which) {
+    PyObject* src = which == 0 ? theta : v;
+    if (src == Py_None) continue;
+    PyObject* fs = PySequence_Fast(src, "theta / v must be sequences of tensors");
+    if (!fs) return done(nullptr);
+    keep.push_back(fs);
+    if (PySequence_Fast_GET_SIZE(fs) != nt) return done(type_error("theta / v need one tensor per server tensor"));
+    std::vector<float*>& out = which == 0 ? tp : vp;
+    out.resize(nt);
+    PyObject** it = PySequence_Fast_ITEMS(fs);
+    for (Py_ssize_t t = 0; t < nt; ++t) {
+      const at::Tensor* a = usable(it[t], &dev);
+      if (!a || a->numel() != sz[t]) return done(type_error("theta / v must match the server tensors"));
+      out[t] = a->data_ptr<float>();
+    }
+  }
+  int64_t off[4];
+  const size_t stride = flc_stacked_wire_layout(n, k, off);
+  if (stride == 0) return done(value_error("bad wire shape"));
+  std::vector<const void*> rp(nr);
+  std::vector<float> w(nr);
+  PyObject** ri = PySequence_Fast_ITEMS(f[0]);
+  PyObject** wi = PySequence_Fast_ITEMS(f[1]);
+  for (Py_ssize_t c = 0; c < nr; ++c) {
+    const at::Tensor* r = usable_as(ri[c], at::kByte, &dev);
+    if (!r || (size_t)r->numel() < stride || reinterpret_cast<uintptr_t>(r->data_ptr()) % 16 != 0)
+      return done(type_error("records must be 16-B aligned uint8 HIP tensors of the wire layout on the server's device"));
+    rp[c] = r->data_ptr();
+    const double wd = PyFloat_AsDouble(wi[c]);
+    if (wd == -1.0 && PyErr_Occurred()) return done(nullptr);
+    w[c] = (float)wd;
+  }
+  void* st = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+  int rc = FLC_OK;
+  Py_BEGIN_ALLOW_THREADS
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  rc = flc_fedopt_fold_records(rp.data(), w.data(), (int)nr, n, k, levels, dp.data(), tp.empty() ? nullptr : tp.data(),
+                               vp.empty() ? nullptr : vp.data(), sz.data(), (int)nt, (float)beta0, opt, lr, beta2, tau,
+                               st);
+  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  Py_END_ALLOW_THREADS
+  if (rc != FLC_OK) {
+    PyErr_Format(PyExc_RuntimeError, "flc_fedopt_fold_records failed with status %d: %s", rc, flc_last_error());
+    return done(nullptr);
+  }
+  return done((Py_INCREF(Py_None), Py_None));
+}
+
 void release_storage(void* ctx) { delete static_cast<c10::Storage*>(ctx); }
 
 // alias(host_tensor, device_index) -> tensor on cuda:device_index over the same bytes (see the header)
@@ -664,6 +755,9 @@ PyMethodDef kMethods[] = {
      "avg_and_gradients(params, grads, msgs, w_params, w_grads, inertia[, set_grad]): flc_avg_and_gradients on Python "
      "lists of HIP "
      "tensors (messages: mappings with 'parameters' and 'gradients'), on the current stream of the model's device"},
+    {"fold_records", fold_records, METH_VARARGS,
+     "fold_records(records, weights, n, k, levels, delta, theta, v, beta0, opt, lr, beta2, tau): "
+     "flc_fedopt_fold_records on Python lists"},
     {"delta_flat", delta_flat, METH_VARARGS,
      "delta_flat(local, global): a new flat fp32 tensor cat(local - global) (flc_delta_flatten) on the tensors' device"},
     {"stacked_records_batch", stacked_records_batch, METH_VARARGS,

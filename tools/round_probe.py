@@ -79,6 +79,20 @@ def main():
         torch.cuda.synchronize()
         tot = (time.perf_counter() - t0) / 20
         print(f"{name}: host enqueue {host * 1e6:.1f} us, synchronised {tot * 1e6:.1f} us")
+    # the server update alone (its messages made and drained first): host time, and synchronised
+    hu, su = [], []
+    for i in range(25):
+        comm_only()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.update()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        if i >= 5:
+            hu.append(t1 - t0)
+            su.append(t2 - t0)
+    print(f"server update alone: host {np.median(hu) * 1e6:.1f} us, synchronised {np.median(su) * 1e6:.1f} us")
     # amortised over 64 rounds with every client's send statistics read at the end (the pending counts folded in):
     # the slab slots against one fresh count tensor per call (the torch.cat read-back)
     def rounds64():
