@@ -328,10 +328,11 @@ def fedopt_update(model_params: Sequence[torch.Tensor], delta_parameters: Sequen
                           [{"delta_parameters": m["delta_parameters"] if recs is not None else d}
                            for m, d in zip(messages, dm)], optimizer, lr, betas, tau)
         return
-    ps = _params(model_params)
-    if recs is not None and compressed.fold_records(recs, [alpha] * len(recs), delta_parameters, ps, vps, betas[0],
-                                                    opt if vps is not None else "avg", lr, betas[1], tau):
+    # (the parameters as they are for the one-pass fold: its kernels write θ in place, outside autograd)
+    if recs is not None and compressed.fold_records(recs, [alpha] * len(recs), delta_parameters, model_params, vps,
+                                                    betas[0], opt if vps is not None else "avg", lr, betas[1], tau):
         return  # every record decoded, folded and the optimizer step applied in one pass
+    ps = _params(model_params)
     if _fold(delta_parameters, messages, [alpha] * len(messages), 0, betas[0], key="delta_parameters",
              theta=ps, v=vps, opt=opt if vps is not None else "avg", lr=lr, beta2=betas[1], tau=tau):
         return  # the delta average and the optimizer step of every tensor in one launch

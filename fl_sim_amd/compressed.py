@@ -217,7 +217,7 @@ class _Batch:
 
     def __init__(self, key):
         self.key = key
-        self.items = []  # (CompressedDelta, flat delta, seed, count slot, dithering compressor, stream)
+        self.items = []  # (CompressedDelta, flat delta, seed, count slot, dithering compressor, stream, its handle)
 
     def run(self) -> None:
         if _PENDING.get(self.key) is self:
@@ -237,9 +237,9 @@ class _Batch:
         dev = torch.device("cuda", di)
         with torch.cuda.device(dev):
             cur = torch.cuda.current_stream(dev)
-            for st in {it[5] for it in items}:  # (the deltas were flattened on these streams)
-                if st != cur:
-                    cur.wait_stream(st)
+            ch = cur.cuda_stream
+            for st in {it[6]: it[5] for it in items if it[6] != ch}.values():  # (deltas flattened on other streams)
+                cur.wait_stream(st)
             stride, off = codec.stacked_wire_layout(n, k)
             C = len(items)
             recs = torch.empty(C, stride, dtype=torch.uint8, device=dev)
@@ -257,10 +257,10 @@ class _Batch:
                           P(*[recs[c].data_ptr() + off["idx"] for c in range(C)]), C, n, k,
                           P(*[it[3].data_ptr() for it in items]), codec._stream(dev))
             codec._after_encode(dev)
-            for (d, flat, _, _, sd, st), r in zip(items, recs.unbind(0)):
-                if st != cur:
+            for (d, flat, _, _, sd, _, sh), r in zip(items, recs.unbind(0)):
+                if sh != ch:
                     flat.record_stream(cur)
-                sd._note_slab_stream(cur)  # (the count was written on this stream)
+                    sd._note_slab_stream(cur)  # (the count was written on this stream, not the slot's own)
                 d._record, d._batch = r, None
 
 
@@ -292,7 +292,7 @@ def _deferred(local, cached, shapes, n: int, K: int, s: int, tk: Compressor, sd:
     if b is None:
         b = _PENDING[key] = _Batch(key)
     d = CompressedDelta(shapes, dev, n, k=K, levels=s, batch=b)
-    b.items.append((d, flat, seed_ctr[0], cnt, sd, st))
+    b.items.append((d, flat, seed_ctr[0], cnt, sd, st, st.cuda_stream))
     tk._finish(n, tk.K)
     base = _norm_stage_send(sd, None)
     sd._finish_pending(n, cnt, base, (1.0 + np.ceil(math.log2(sd.s))) / 32.0)  # compressors.py:365
