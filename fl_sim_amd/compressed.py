@@ -190,10 +190,21 @@ def compress_delta(local: Sequence[torch.Tensor], cached: Sequence[torch.Tensor]
         r = _stacked_fast(local, cached, shapes, n, pipe[0], pipe[1], compressors[0], compressors[1], dev, seed_ctr)
         if r is not None:
             return r
-    ls, gs = _fp32_on(local, dev), _fp32_on(cached, dev)
-    if pipe is not None and 0 < pipe[0] < n:
-        return _stacked(ls, gs, shapes, n, pipe[0], pipe[1], compressors[0], compressors[1], dev, seed_ctr)
-    out = codec.delta_flatten(ls, gs)
+    out = None
+    if pipe is None or not 0 < pipe[0] < n:
+        snap = codec._pyflat()
+        if snap is not None:
+            try:  # the flat delta in one C call (the tensors as they are: contiguous fp32 on one device)
+                out = snap(local, cached)
+            except TypeError:
+                pass
+            if out is not None and out.device != dev:
+                out = None
+    if out is None:
+        ls, gs = _fp32_on(local, dev), _fp32_on(cached, dev)
+        if pipe is not None and 0 < pipe[0] < n:
+            return _stacked(ls, gs, shapes, n, pipe[0], pipe[1], compressors[0], compressors[1], dev, seed_ctr)
+        out = codec.delta_flatten(ls, gs)
     for comp in compressors:  # the drop-in compressors on the device, in order
         out = comp.compressVector(out)
     return CompressedDelta(shapes, dev, n, flat=out)
