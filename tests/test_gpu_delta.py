@@ -147,3 +147,29 @@ def test_stacked_encode_delta_1gib_in_64_tensors():
     assert _same_packet(a, b)
     del flat, local, cached
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n_clients,k", [(1, 0), (5, 777), (40, 3000)])
+def test_count_nonzero_at_batch_matches_numpy(n_clients, k):
+    """flc_count_nonzero_at_batch (the deferred compressed messages' send counts) against numpy: per client the nonzero
+    entries of x at k indices, NaN counted, -0.0 not, more clients than one launch takes (32)."""
+    import ctypes
+
+    from fl_sim_amd import _lib, codec
+
+    n = 50_001
+    g = np.random.default_rng(n_clients + k)
+    xs, idxs, exp = [], [], []
+    for c in range(n_clients):
+        x = np.where(g.random(n) < 0.3, 0.0, g.standard_normal(n)).astype(np.float32)
+        x[g.random(n) < 0.01] = np.nan
+        x[g.random(n) < 0.05] = -0.0
+        idx = np.sort(g.choice(n, k, replace=False)).astype(np.int32)
+        xs.append(torch.from_numpy(x).cuda())
+        idxs.append(torch.from_numpy(idx).cuda())
+        exp.append(int(np.count_nonzero(~(x[idx] == 0.0))))
+    counts = [torch.full((1,), -7, dtype=torch.int64, device="cuda") for _ in range(n_clients)]
+    P = ctypes.c_void_p * n_clients
+    _lib.call("flc_count_nonzero_at_batch", P(*[x.data_ptr() for x in xs]), P(*[i.data_ptr() for i in idxs]),
+              n_clients, n, k, P(*[c.data_ptr() for c in counts]), codec._stream(xs[0].device))
+    assert [int(c.item()) for c in counts] == exp
