@@ -258,8 +258,7 @@ template <int INIT, int OPT>  // OPT < 0: the fold only
 __global__ __launch_bounds__(kThreads) void model_fold_kernel(ModelPack p, float beta, float lr, float beta2, float omb,
                                                               float nomb, float tau) {
   const int b = blockIdx.x;
-  int t = 0;
-  while (t + 1 < p.nt && p.blk0[t + 1] <= b) ++t;  // uniform: <= kModelT steps
+  const int t = pack_entry<kModelT>(p.blk0, p.nt, b);  // (uniform)
   float* __restrict__ dst = p.dst[t];
   const int64_t n = p.n[t];
   const int64_t c0 = (int64_t)(b - p.blk0[t]) * kModelChunk;
@@ -336,8 +335,7 @@ struct PairPack {
 
 __global__ __launch_bounds__(kThreads) void pair_fold_kernel(PairPack p, float beta) {
   const int b = blockIdx.x;
-  int t = 0;
-  while (t + 1 < p.nt && p.blk0[t + 1] <= b) ++t;  // uniform: <= kModelT steps
+  const int t = pack_entry<kModelT>(p.blk0, p.nt, b);  // (uniform)
   float* __restrict__ dst = p.dst[t];
   const int64_t n = p.n[t];
   const int64_t c0 = (int64_t)(b - p.blk0[t]) * kModelChunk;
@@ -415,8 +413,7 @@ __device__ __forceinline__ float server_elem(float th0, float* __restrict__ aux,
 template <int KIND, bool FOLD, int INIT>
 __global__ __launch_bounds__(kThreads) void server_fold_kernel(ModelPack p, float beta, float c, float c2) {
   const int b = blockIdx.x;
-  int t = 0;
-  while (t + 1 < p.nt && p.blk0[t + 1] <= b) ++t;  // uniform: <= kModelT steps
+  const int t = pack_entry<kModelT>(p.blk0, p.nt, b);  // (uniform)
   float* __restrict__ dst = p.dst[t];
   float* __restrict__ aux = p.theta[t];
   const int64_t n = p.n[t];

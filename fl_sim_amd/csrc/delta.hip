@@ -35,8 +35,7 @@ struct TensorPack {
 
 __global__ __launch_bounds__(kThreads) void delta_flatten_kernel(TensorPack p, float* __restrict__ out) {
   const int b = blockIdx.x;
-  int t = 0;
-  while (t + 1 < p.nt && p.blk0[t + 1] <= b) ++t;  // uniform: <= kMaxT steps
+  const int t = pack_entry<kMaxT>(p.blk0, p.nt, b);  // (uniform)
   const float* __restrict__ l = p.l[t];
   const float* __restrict__ g = p.g[t];
   float* __restrict__ o = out + p.off[t];

@@ -243,6 +243,24 @@ __device__ __forceinline__ void acquire_agent() {
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// The entry of a kernel-argument pack that holds block b, from the entries' first blocks blk0[0..N] (non-decreasing,
+// blk0[0] = 0; entries past nt ignored): every compare reads blk0 at a static offset, so its scalar loads issue together
+// (one round trip), where a `while (blk0[t + 1] <= b) ++t` walk waits for one dependent load per entry it passes.
+#ifndef FLC_PACK_SEARCH_STATIC
+#define FLC_PACK_SEARCH_STATIC 1
+#endif
+template <int N>
+__device__ __forceinline__ int pack_entry(const int (&blk0)[N + 1], int nt, int b) {
+  int t = 0;
+#if FLC_PACK_SEARCH_STATIC
+#pragma unroll
+  for (int i = 1; i < N; ++i) t += (i < nt && blk0[i] <= b) ? 1 : 0;
+#else
+  while (t + 1 < nt && blk0[t + 1] <= b) ++t;
+#endif
+  return t;
+}
+
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope fence + s_barrier, and
 // on gfx950 that fence waits for vmcnt(0): every global load and store the wave has in flight.  Kernels
 // that keep prefetched loads (or fire-and-forget stores) in flight across a barrier use this instead:
