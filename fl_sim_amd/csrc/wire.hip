@@ -124,7 +124,12 @@ struct ModelIO {
   ModelTab m;
   __device__ __forceinline__ int first_tensor(int64_t t0) const {
     int t = 0;
+#if FLC_PACK_SEARCH_STATIC  // (static offsets: the scalar loads of start issue together, flc_device.hpp pack_entry)
+#pragma unroll
+    for (int i = 1; i < kRoundT; ++i) t += (i < m.nt && m.start[i] <= t0) ? 1 : 0;
+#else
     while (t + 1 < m.nt && m.start[t + 1] <= t0) ++t;
+#endif
     return t;
   }
   __device__ __forceinline__ void load(int64_t t0, int lane, float4 acc[4]) const {
