@@ -221,6 +221,7 @@ def compress_delta(local: Sequence[torch.Tensor], cached: Sequence[torch.Tensor]
 DEFER_ENCODE = os.environ.get("FLC_DEFER_ENCODE", "1") != "0"
 _DEFER_MAX_N = 1 << 24
 _DEFER_MAX_PENDING = 64
+_DEFER_MAX_BATCHES = 16
 
 
 class _Batch:
@@ -309,6 +310,8 @@ def _deferred(local, cached, shapes, n: int, K: int, s: int, tk: Compressor, sd:
     sd._finish_pending(n, cnt, base, (1.0 + np.ceil(math.log2(sd.s))) / 32.0)  # compressors.py:365
     if len(b.items) >= _DEFER_MAX_PENDING:
         b.run()
+    elif len(_PENDING) > _DEFER_MAX_BATCHES:  # (messages nobody reads: the waiting deltas stay bounded)
+        _run_pending()
     return d
 
 

@@ -435,3 +435,32 @@ def test_deferred_round_encode_equals_the_immediate_encodes(n_msgs, monkeypatch)
     for i, (x, y) in enumerate(zip(ra, rb)):
         assert np.array_equal(x, y), i
     assert sa == sb and ma == mb
+
+
+def test_deferred_messages_of_many_counters_stay_bounded(monkeypatch):
+    """Messages nobody reads, each of its own Philox counter (a batch each): past 16 waiting batches they are encoded,
+    and every record and statistic still equals the immediate encodes'."""
+    from fl_sim_amd import compressed
+
+    g = torch.Generator().manual_seed(14)
+    shapes = [(64, 9), (300,)]
+    glob = [torch.randn(sh, generator=g).cuda() for sh in shapes]
+    D = sum(t.numel() for t in glob)
+    locs = [[t + torch.randn(t.shape, generator=g).cuda() * 1e-2 for t in glob] for _ in range(20)]
+
+    def run(defer):
+        monkeypatch.setattr(compressed, "DEFER_ENCODE", defer)
+        comps = [make_compressors("stacked10", D, rng="philox", seed=7 + i) for i in range(20)]
+        ds = []
+        for i, c in enumerate(comps):
+            for _ in range(i):
+                c[1].philox.next()
+            ds.append(compressed.compress_delta(locs[i], glob, c))
+            if defer:
+                assert len(compressed._PENDING) <= compressed._DEFER_MAX_BATCHES + 1
+        return [_record_fields(d) for d in ds], [(c[1].really_need_to_send_components, c[1].philox.counter)
+                                                  for c in comps]
+
+    ra, sa = run(True)
+    rb, sb = run(False)
+    assert all(np.array_equal(x, y) for x, y in zip(ra, rb)) and sa == sb
