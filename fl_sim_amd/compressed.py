@@ -95,6 +95,14 @@ class CompressedDelta(_abc.Sequence):
             self._batch.run()
         return self._record
 
+    def __getstate__(self):
+        """A copied or pickled message carries its record (a deferred encode runs first)."""
+        if self._batch is not None:
+            self._batch.run()
+        d = self.__dict__.copy()
+        d["_batch"] = None
+        return d
+
     @property
     def nbytes(self) -> int:
         """Bytes the message carries for the delta (the wire record, or the dense fp32 vector)."""

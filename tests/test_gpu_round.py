@@ -464,3 +464,24 @@ def test_deferred_messages_of_many_counters_stay_bounded(monkeypatch):
     ra, sa = run(True)
     rb, sb = run(False)
     assert all(np.array_equal(x, y) for x, y in zip(ra, rb)) and sa == sb
+
+
+def test_deferred_message_pickles_with_its_record():
+    """A deferred message copied or pickled before anything read it carries the record its encode makes."""
+    import copy
+    import pickle
+
+    from fl_sim_amd import compressed
+
+    g = torch.Generator().manual_seed(15)
+    glob = [torch.randn(4000, generator=g).cuda()]
+    loc = [glob[0] + torch.randn(4000, generator=g).cuda() * 1e-2]
+    comps = make_compressors("stacked10", 4000, rng="philox", seed=3)
+    d = compressed.compress_delta(loc, glob, comps)
+    assert d._batch is not None  # (deferred)
+    c = copy.deepcopy(d)
+    p = pickle.loads(pickle.dumps(d))
+    ref = _record_fields(d)
+    for x in (c, p):
+        assert x._batch is None and np.array_equal(_record_fields(x), ref)
+        assert torch.equal(torch.cat([t.reshape(-1) for t in x]).cpu(), torch.cat([t.reshape(-1) for t in d]).cpu())
