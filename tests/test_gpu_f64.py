@@ -265,6 +265,23 @@ def test_f64_topk_band_top_bin_past_the_ceiling():
     assert sum(codec.topk_status_all().values()) == 0
 
 
+@pytest.mark.parametrize("K", [150, 1000, 3000])
+def test_f64_topk_infinite_kth_value_below_nans(K):
+    """Small k (no ceiling from the sample: the NaN keys, the largest, are counted above the band) with the K-th
+    largest among +inf ties near the band's top: the NaNs are kept, then the highest-index +infs."""
+    from fl_sim_amd import codec
+
+    n = 1 << 20
+    g = np.random.default_rng(K)
+    x = g.standard_normal(n)
+    x[g.choice(n, 100, replace=False)] = np.nan
+    free = np.flatnonzero(~np.isnan(x))
+    x[g.choice(free, 5000, replace=False)] = np.inf
+    exp, _ = ref.topk(x, K)
+    got = codec.topk_dense_f64(torch.from_numpy(x).to(DEV), K).cpu().numpy()
+    assert g64.same_bits(got, exp)
+
+
 @pytest.mark.parametrize("n_ties", [3, 5000, 16384, 16385, 100_000])
 def test_f64_topk_ties_of_the_kth_value(n_ties):
     """The K-th largest value repeated n_ties times at random positions, k cutting through the ties: the band's bin
