@@ -380,9 +380,10 @@ int flc_delta_flatten(const float* const* local, const float* const* global, con
  * device int64, written stream-ordered. */
 int flc_delta_count_nonzero_at(const float* const* local, const float* const* global, const int64_t* sizes,
                                int n_tensors, const int32_t* idx, int64_t k, int64_t* count, void* stream);
-/* the same count for many clients whose deltas are already flat: counts[c] = the number of nonzero xs[c][idx[c][j]],
- * j < k (NaN counts), every x of n elements, every idx of k in-range indices (a stacked record's kept indices).  xs,
- * idx and counts are HOST arrays of device pointers; each count one device int64, written stream-ordered. */
+/* the same count (compressors.py:339-365, one send entry per nonzero dithering input) for many clients whose deltas
+ * are already flat — a round's deferred compressed messages: counts[c] = the number of nonzero xs[c][idx[c][j]], j < k
+ * (NaN counts), every x of n elements, every idx of k in-range indices (a stacked record's kept indices).  xs, idx
+ * and counts are HOST arrays of device pointers; each count one device int64, written stream-ordered. */
 int flc_count_nonzero_at_batch(const float* const* xs, const int32_t* const* idx, int n_clients, int64_t n,
                                int64_t k, int64_t* const* counts, void* stream);
 
